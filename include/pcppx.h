@@ -1,0 +1,151 @@
+/*
+ * pcppx.h — C ABI of the MI355X packet-dissection engine (drop-in boundary).
+ *
+ * This is the boundary that replaces the per-packet Packet++ parse path
+ *   RawPacket -> pcpp::Packet(RawPacket*, ...)          Packet++/src/Packet.cpp:202-209, :66-196
+ *   pcpp::hash5Tuple / pcpp::hash2Tuple                  Packet++/src/PacketUtils.cpp:139-245
+ *   IPv4 header checksum                                 Packet++/src/IPv4Layer.cpp:410-412
+ *   TcpLayer/UdpLayer::calculateChecksum(false)          Packet++/src/TcpLayer.cpp:271, UdpLayer.cpp:47
+ * with one batched call over many packets that sit in GPU memory (HBM).
+ *
+ * Conventions:
+ *   - every function returns 0 or a negative PCPPX_E* code; nothing throws across the ABI;
+ *   - the caller owns every buffer; records are arrays sized n (and n*max_layers);
+ *   - a context belongs to one host thread and one GPU; contexts are never shared.
+ *
+ * Records mirror what a pcpp::Packet exposes after parsing:
+ *   pcppx_layer   <-> Layer::getProtocol/getOsiModelLayer/getData()-raw/getHeaderLen/getDataLen
+ *                      (Packet++/header/Layer.h, ProtocolType.h:35-284)
+ *   pcppx_summary <-> Packet::isPacketOfType (proto_mask, Packet.cpp:614-640), hash5Tuple(false/true),
+ *                      hash2Tuple, the IPv4/L4 checksums.
+ * Packets for which the reference would build a layer outside this engine's scope (L7 dissectors, ARP,
+ * ICMP, PPPoE, ...) are flagged PCPPX_F_NEEDS_HOST_L7 / PCPPX_F_NEEDS_HOST_PROTO: their layer prefix is
+ * exact, and the host owns the rest.
+ */
+#ifndef PCPPX_H
+#define PCPPX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCPPX_ABI_VERSION 1
+#define PCPPX_MAX_LAYERS 16     /* fixed depth cap; deeper chains set PCPPX_F_DEPTH_OVERFLOW */
+#define PCPPX_MAX_CAPLEN 65535  /* larger packets are flagged PCPPX_F_OVERSIZE and not parsed */
+
+/* error codes */
+#define PCPPX_OK 0
+#define PCPPX_E_INVAL -1    /* bad argument (null pointer, n too large, max_layers > 16 ...) */
+#define PCPPX_E_NODEV -2    /* no HIP device / bad ordinal */
+#define PCPPX_E_HIP -3      /* a HIP runtime call failed */
+#define PCPPX_E_NOMEM -4    /* device or pinned allocation failed */
+#define PCPPX_E_LINKTYPE -5 /* link type not handled by the device path */
+
+/* pcppx_summary.flags */
+#define PCPPX_F_NEEDS_HOST_L7 0x0001    /* an L4 payload would go to an L7 dissector (TcpLayer.cpp:372-491,
+                                           UdpLayer.cpp:103-178); chain stops at the L4 layer */
+#define PCPPX_F_NEEDS_HOST_PROTO 0x0002 /* an out-of-scope L2/L3 layer would be built (ARP, PPPoE, ICMP,
+                                           IGMP, IPSec, VRRP, ICMPv6, STP, WoL); chain stops before it */
+#define PCPPX_F_DEPTH_OVERFLOW 0x0004   /* more than max_layers layers; extra layers not written */
+#define PCPPX_F_OVERSIZE 0x0008         /* caplen > PCPPX_MAX_CAPLEN: not parsed */
+#define PCPPX_F_IP_CSUM 0x0010          /* ip_csum_* computed (an IPv4 layer exists and want_checksums) */
+#define PCPPX_F_IP_CSUM_OK 0x0020       /* ip_csum_calc == ip_csum_stored */
+#define PCPPX_F_L4_CSUM 0x0040          /* l4_csum_* computed (a TCP/UDP layer exists and want_checksums) */
+#define PCPPX_F_L4_CSUM_OK 0x0080       /* l4_csum_calc == l4_csum_stored */
+#define PCPPX_F_TRAILER 0x0100          /* last layer is a PacketTrailer (Packet.cpp:178-195) */
+#define PCPPX_F_BAD_DESC 0x0200         /* offsets[i] + caplens[i] > batch data_len: not parsed */
+#define PCPPX_F_NEEDS_HOST \
+	(PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC)
+
+/* One parsed layer, 8 bytes. */
+typedef struct pcppx_layer {
+	uint8_t proto;     /* pcpp::ProtocolType (ProtocolType.h:42-258) */
+	uint8_t osi;       /* pcpp::OsiModelLayer (ProtocolType.h:266-284) */
+	uint16_t offset;   /* Layer::getData() - RawPacket::getRawData() */
+	uint16_t hdr_len;  /* Layer::getHeaderLen() */
+	uint16_t data_len; /* Layer::getDataLen() */
+} pcppx_layer;
+
+/* Per-packet summary, 32 bytes. */
+typedef struct pcppx_summary {
+	uint32_t hash5;          /* pcpp::hash5Tuple(&packet, false) */
+	uint32_t hash5_dir;      /* pcpp::hash5Tuple(&packet, true) */
+	uint32_t hash2;          /* pcpp::hash2Tuple(&packet) */
+	uint16_t flags;          /* PCPPX_F_* */
+	uint8_t n_layers;        /* layers in the chain (capped at max_layers, see PCPPX_F_DEPTH_OVERFLOW) */
+	uint8_t l4_layer;        /* index of the layer hash5Tuple takes its ports from (last TCP, else last
+	                            UDP); 0xFF if none */
+	uint64_t proto_mask;     /* bit p set iff some layer has protocol p: Packet::isPacketOfType(p) */
+	uint16_t ip_csum_calc;   /* computeChecksum over the first IPv4 header, checksum field zeroed
+	                            (IPv4Layer.cpp:410-412) — the value computeCalculateFields would store */
+	uint16_t ip_csum_stored; /* be16 of the header's checksum field */
+	uint16_t l4_csum_calc;   /* {Tcp,Udp}Layer::calculateChecksum(false) of layer l4_layer */
+	uint16_t l4_csum_stored; /* be16 of that layer's checksum field */
+} pcppx_summary;
+
+/* A batch of packets: bytes of packet i are data[offsets[i] .. offsets[i] + caplens[i]).
+ * For the fast path packets should be stored back to back in ascending offset order (any order and
+ * gaps are legal; they only cost bandwidth). */
+typedef struct pcppx_batch {
+	const uint8_t* data;
+	const uint64_t* offsets;
+	const uint32_t* caplens;
+	uint64_t data_len; /* bytes addressable at data (bounds every packet) */
+	uint32_t n;
+	uint16_t linktype; /* pcpp::LinkLayerType (RawPacket.h:24-178) for every packet of the batch */
+	uint16_t reserved;
+} pcppx_batch;
+
+/* pcpp::PacketParseOptions (Packet++/header/Packet.h:17-37) plus output selection. */
+typedef struct pcppx_opts {
+	uint32_t parse_until_family; /* pcpp::ProtocolTypeFamily; 0 = UnknownProtocol (parse everything) */
+	uint8_t parse_until_osi;     /* pcpp::OsiModelLayer; 8 = OsiModelLayerUnknown */
+	uint8_t want_checksums;      /* compute IPv4 / L4 checksums */
+	uint8_t max_layers;          /* 0 = do not write layers; else layers stride per packet (1..16) */
+	uint8_t reserved;
+} pcppx_opts;
+
+/* Output arrays (same memory space as the batch for the _device call, host for the _host call). */
+typedef struct pcppx_records {
+	pcppx_summary* summary; /* n entries */
+	pcppx_layer* layers;    /* n * max_layers entries, or NULL when max_layers == 0 */
+} pcppx_records;
+
+typedef struct pcppx_ctx pcppx_ctx;
+
+/* library / device management */
+int pcppx_abi_version(void);
+const char* pcppx_strerror(int err);
+int pcppx_device_count(int* out);
+int pcppx_open(int device_ordinal, pcppx_ctx** out); /* one per host thread & GPU */
+void pcppx_close(pcppx_ctx* ctx);
+int pcppx_sync(pcppx_ctx* ctx);                      /* wait for everything queued on ctx's stream */
+void pcppx_default_opts(pcppx_opts* opts);           /* Packet(RawPacket*) defaults + checksums + 16 layers */
+
+/* Device-resident parse. batch and records hold device pointers; the kernels are queued on
+ * hip_stream (a hipStream_t; NULL = the context's own stream) and the call returns without waiting. */
+int pcppx_parse_batch_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
+                             pcppx_records* out, void* hip_stream);
+
+/* Host-to-host parse: batch and records hold host pointers. The context stages the bytes through pinned
+ * buffers in chunks, overlapping H2D copies, kernels and D2H copies; returns when out is filled. */
+int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
+                           pcppx_records* out);
+
+/* Per-flow counters keyed by hash5Tuple (Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:99-125).
+ * Device pointers: summary[n] from a previous parse, caplens[n]. The table is open-addressed with
+ * `capacity` slots (power of two); keys[i]==0 marks an empty slot — flow key 0 (non-5-tuple packets,
+ * PacketUtils.cpp:141-148) is counted in stats[0] (packets) / stats[1] (bytes) instead, and packets
+ * that found no free slot in stats[2]. Counts accumulate across calls. */
+int pcppx_flow_count_device(pcppx_ctx* ctx, const pcppx_summary* summary, const uint32_t* caplens,
+                            uint32_t n, uint32_t* keys, uint64_t* packets, uint64_t* bytes,
+                            uint32_t capacity, uint64_t* stats, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PCPPX_H */

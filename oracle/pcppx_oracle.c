@@ -1,0 +1,635 @@
+/*
+ * pcppx_oracle.c — TEST INFRASTRUCTURE ONLY: the parity checker, never the product path.
+ *
+ * A scalar, allocation-free C restatement of the reference Packet++ per-packet parse path
+ * (SURVEY.md §8a rows a1-a17). Every rule cites the reference file:line it restates (paths relative
+ * to the reference root). The output is the engine's record format (include/pcppx.h).
+ *
+ * Engine contract for layers this path does not dissect (restated identically by the HIP kernels):
+ *   - where the reference would hand an L4 payload to an L7 dissector (port/content triggers of
+ *     TcpLayer.cpp:372-491 and UdpLayer.cpp:103-178, incl. the SIP content heuristic
+ *     SipLayer.cpp:127-160) the chain stops after the TCP/UDP layer and PCPPX_F_NEEDS_HOST_L7 is set;
+ *   - where it would build an out-of-scope L2/L3 layer (ARP, PPPoE, WoL, ICMP, IGMP, AH, ESP, VRRP,
+ *     ICMPv6, STP, SLL/SLL2/NULL/NFLOG/C_HDLC first layers) the chain stops before it and
+ *     PCPPX_F_NEEDS_HOST_PROTO is set;
+ *   - no trailer is appended to a flagged chain; hashes and checksums are computed over the emitted chain.
+ * For unflagged packets every field equals the reference; for flagged packets the emitted layers are an
+ * exact prefix of the reference chain.
+ *
+ * Pinned against the real reference (oracle/_ref/libpcpp_ref.so) and committed golden records: see
+ * tests/test_oracle_vs_reference.py.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "pcppx_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* ---- ProtocolType ids (Packet++/header/ProtocolType.h:42-258) and OSI (:266-284) ---- */
+enum {
+	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14,
+	P_GREV0 = 15, P_GREV1 = 16, P_PPTP = 17, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44
+};
+
+enum kind { K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP,
+	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7 };
+
+static uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static uint32_t le32(const uint8_t* p)
+{
+	return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static uint16_t bswap16(uint16_t v) { return (uint16_t)((v >> 8) | (v << 8)); }
+
+/* ---- isDataValid restatements ---- */
+/* EthLayer::isDataValid, Packet++/src/EthLayer.cpp:100-117 */
+static int eth_valid(const uint8_t* p, uint32_t n) { return n >= 14 && be16(p + 12) >= 0x0600; }
+/* EthDot3Layer::isDataValid, Packet++/src/EthDot3Layer.cpp:38-54 */
+static int dot3_valid(const uint8_t* p, uint32_t n) { return n >= 14 && be16(p + 12) <= 0x05DC; }
+/* LLCLayer::isDataValid, Packet++/src/LLCLayer.cpp:49-52 */
+static int llc_valid(const uint8_t* p, uint32_t n) { return n >= 3 && !(p[0] == 0xFF && p[1] == 0xFF); }
+/* IPv4Layer::isDataValid, Packet++/header/IPv4Layer.h:626-630 (iphdr bitfields: IHL low nibble) */
+static int ipv4_valid(const uint8_t* p, uint32_t n) { return n >= 20 && (p[0] >> 4) == 4 && (p[0] & 0xF) >= 5; }
+/* IPv6Layer::isDataValid, Packet++/header/IPv6Layer.h:245-249 */
+static int ipv6_valid(const uint8_t* p, uint32_t n) { return n >= 40 && (p[0] >> 4) == 6; }
+/* TcpLayer::isDataValid, Packet++/header/TcpLayer.h:596-601 */
+static int tcp_valid(const uint8_t* p, uint32_t n) { return n >= 20 && (p[12] >> 4) >= 5 && n >= (uint32_t)(p[12] >> 4) * 4; }
+
+/* ---- L7 trigger sets (engine contract; reference dispatch chains cited) ---- */
+/* SSLLayer::isSSLPort, Packet++/header/SSLLayer.h:488-510 */
+static int ssl_port(uint16_t x)
+{
+	switch (x) {
+	case 443: case 261: case 448: case 465: case 563: case 614: case 636:
+	case 989: case 990: case 992: case 993: case 994: case 995: return 1;
+	default: return 0;
+	}
+}
+/* Ports gating TcpLayer::parseNextLayer's dispatch, Packet++/src/TcpLayer.cpp:372-491 */
+static int tcp_l7_port(uint16_t x)
+{
+	if (ssl_port(x)) return 1;
+	switch (x) {
+	case 80: case 8080:              /* HTTP, HttpLayer.h:74-77 */
+	case 5060: case 5061:            /* SIP, SipLayer.h:112-115 */
+	case 179:                        /* BGP, BgpLayer.h:65-68 */
+	case 22:                         /* SSH, SSHLayer.h:92-95 */
+	case 53: case 5353: case 5355:   /* DNS, DnsLayer.h:468-479 */
+	case 23:                         /* Telnet, TelnetLayer.h:276-279 */
+	case 21: case 20:                /* FTP / FTP-data, FtpLayer.h:24-34 */
+	case 13400: case 3496:           /* DoIP, DoIpLayer.h:666-670 */
+	case 30490:                      /* SOME/IP(-SD), SomeIpSdLayer.h:569-572 */
+	case 102:                        /* TPKT, TpktLayer.h:82-85 */
+	case 25: case 587:               /* SMTP, SmtpLayer.h:27-30 */
+	case 389:                        /* LDAP, LdapLayer.h:346-349 */
+	case 5432:                       /* Postgres, PostgresLayer.h:508-511 */
+	case 3306:                       /* MySQL, MySqlLayer.h:306-309 */
+	case 2123:                       /* GTPv2, GtpLayer.h:996-999 */
+	case 502:                        /* Modbus, ModbusLayer.h:99-102 */
+		return 1;
+	default: return 0;
+	}
+}
+/* Ports gating UdpLayer::parseNextLayer's dispatch, Packet++/src/UdpLayer.cpp:103-165 */
+static int udp_l7_port(uint16_t src, uint16_t dst)
+{
+	/* DhcpLayer::isDhcpPorts, DhcpLayer.h:784-788 */
+	if ((src == 68 && dst == 67) || (src == 67 && dst == 68) || (src == 67 && dst == 67)) return 1;
+	if (dst == 4789) return 1;                                  /* VXLAN (dst), VxlanLayer.h:119-122 */
+	if (dst == 0 || dst == 7 || dst == 9) return 1;             /* WoL (dst), WakeOnLanLayer.h:105-108 */
+	for (int k = 0; k < 2; ++k) {
+		uint16_t x = k ? dst : src;
+		switch (x) {
+		case 53: case 5353: case 5355:       /* DNS */
+		case 5060: case 5061:                /* SIP */
+		case 1812: case 1813: case 3799:     /* RADIUS, RadiusLayer.h:273-284 */
+		case 2152: case 2123:                /* GTPv1/v2, GtpLayer.h:386-389,996-999 */
+		case 546: case 547:                  /* DHCPv6, DhcpV6Layer.h:388-391 */
+		case 123:                            /* NTP, NtpLayer.h:531-534 */
+		case 13400: case 3496:               /* DoIP */
+		case 30490:                          /* SOME/IP */
+		case 51820:                          /* WireGuard, WireGuardLayer.h:67-70 */
+			return 1;
+		default: break;
+		}
+	}
+	return 0;
+}
+/* SipLayer::detectSipMessageType, Packet++/src/SipLayer.cpp:127-160 (pack4 at :19-25: bytes are
+ * sign-extended chars, so a byte >= 0x80 in positions 1..3 can never match an ASCII key) */
+static int sip_heuristic(const uint8_t* p, uint32_t n)
+{
+	static const char* keys[] = { "INVI", "ACK ", "BYE ", "CANC", "REGI", "PRAC", "OPTI", "SUBS",
+		                          "NOTI", "PUBL", "INFO", "REFE", "MESS", "UPDA", "SIP/" };
+	if (n < 4) return 0; /* with n == 3 the packed key's low byte is 0: no key matches */
+	for (unsigned k = 0; k < sizeof(keys) / sizeof(keys[0]); ++k)
+		if (memcmp(p, keys[k], 4) == 0) return 1;
+	return 0;
+}
+
+/* ---- computeChecksum, Packet++/src/PacketUtils.cpp:12-64 ---- */
+uint16_t pcppx_oracle_checksum(const uint8_t* const* bufs, const uint32_t* lens, int nbufs)
+{
+	uint32_t sum = 0;
+	for (int i = 0; i < nbufs; ++i) {
+		uint32_t local = 0;
+		for (uint32_t j = 0; j < lens[i] / 2; ++j) local += le16(bufs[i] + 2 * j);
+		if (lens[i] % 2) local += bufs[i][lens[i] - 1]; /* be16toh(lastByte << 8) on LE == lastByte */
+		while (local >> 16) local = (local & 0xFFFF) + (local >> 16);
+		sum += local;
+	}
+	while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+	uint16_t result = (uint16_t)~sum;
+	return bswap16(result); /* htobe16 */
+}
+
+/* ---- fnvHash (FNV-1 32), Packet++/src/PacketUtils.cpp:114-137 ---- */
+static uint32_t fnv_update(uint32_t h, const uint8_t* p, uint32_t n)
+{
+	for (uint32_t j = 0; j < n; ++j) { h *= 16777619u; h ^= p[j]; }
+	return h;
+}
+uint32_t pcppx_oracle_fnv1(const uint8_t* buf, uint32_t len) { return fnv_update(2166136261u, buf, len); }
+
+typedef struct {
+	uint8_t proto, osi;
+	uint32_t off, hdr, dlen;
+} lay;
+
+/* ProtocolTypeFamily membership, ProtocolType.h:293-298 + Layer.cpp:47-50 */
+static int family_member(uint32_t fam, uint8_t p)
+{
+	uint32_t q = p;
+	return p != 0 && (q == (fam & 0xff) || (q << 8) == (fam & 0xff00) || (q << 16) == (fam & 0xff0000) ||
+	                  (q << 24) == (fam & 0xff000000u));
+}
+
+/* Build layer `k` at [off, off+len) and report its next layer through nk, noff, nlen.
+ * Returns the layer descriptor. */
+static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int* nk, uint32_t* noff, uint32_t* nlen)
+{
+	const uint8_t* p = pkt + off;
+	lay L = { 0, 0, off, 0, len };
+	*nk = K_NONE;
+	uint32_t po, pl; /* payload of this layer */
+#define NEXT(K, O, N) do { *nk = (K); *noff = (O); *nlen = (N); } while (0)
+	switch (k) {
+	case K_ETH: /* EthLayer::parseNextLayer, Packet++/src/EthLayer.cpp:28-69 */
+		L.proto = P_ETH; L.osi = 2; L.hdr = 14;
+		if (len <= 14) break;
+		po = off + 14; pl = len - 14;
+		switch (be16(p + 12)) {
+		case 0x0800: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 0x86DD: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		case 0x8100: case 0x88A8: NEXT(pl >= 4 ? K_VLAN : K_PAYLOAD, po, pl); break;
+		case 0x8847: NEXT(pl >= 4 ? K_MPLS : K_PAYLOAD, po, pl); break;
+		case 0x0806: case 0x8864: case 0x8863: case 0x0842: NEXT(K_OUT, po, pl); break; /* ARP, PPPoE, WoL */
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	case K_DOT3: /* EthDot3Layer::parseNextLayer, Packet++/src/EthDot3Layer.cpp:22-30 */
+		L.proto = P_DOT3; L.osi = 2; L.hdr = 14;
+		if (len <= 14) break;
+		po = off + 14; pl = len - 14;
+		NEXT(llc_valid(pkt + po, pl) ? K_LLC : K_PAYLOAD, po, pl);
+		break;
+	case K_LLC: /* LLCLayer::parseNextLayer, Packet++/src/LLCLayer.cpp:24-41 */
+		L.proto = P_LLC; L.osi = 2; L.hdr = 3;
+		if (len <= 3) break;
+		po = off + 3; pl = len - 3;
+		if (p[0] == 0x42 && p[1] == 0x42) NEXT(K_OUT, po, pl); /* STP (or Payload): host */
+		else NEXT(K_PAYLOAD, po, pl);
+		break;
+	case K_VLAN: /* VlanLayer::parseNextLayer, Packet++/src/VlanLayer.cpp:59-119 */
+		L.proto = P_VLAN; L.osi = 2; L.hdr = 4;
+		if (len <= 4) break;
+		po = off + 4; pl = len - 4;
+		switch (be16(p + 2)) {
+		case 0x0800: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 0x86DD: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		case 0x8100: case 0x88A8: NEXT(K_VLAN, po, pl); break; /* unchecked */
+		case 0x8847: NEXT(K_MPLS, po, pl); break;              /* unchecked */
+		case 0x0806: case 0x8864: case 0x8863: NEXT(K_OUT, po, pl); break;
+		default:
+			if (be16(p + 2) < 1500) NEXT(llc_valid(pkt + po, pl) ? K_LLC : K_PAYLOAD, po, pl);
+			else NEXT(K_PAYLOAD, po, pl);
+			break;
+		}
+		break;
+	case K_MPLS: /* MplsLayer::parseNextLayer, Packet++/src/MplsLayer.cpp:101-128 */
+		L.proto = P_MPLS; L.osi = 3; L.hdr = 4;
+		if (len < 5) break;
+		po = off + 4; pl = len - 4;
+		if (!(p[2] & 1)) { NEXT(K_MPLS, po, pl); break; } /* not bottom-of-stack: unchecked */
+		switch (p[4] >> 4) {
+		case 4: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 6: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	case K_IPV4: { /* IPv4Layer: initLayerInPacket Packet++/src/IPv4Layer.cpp:180-197; parseNextLayer :245-370 */
+		L.proto = P_IPV4; L.osi = 3; L.hdr = (uint32_t)(p[0] & 0xF) * 4;
+		uint32_t tl = be16(p + 2);
+		if (tl < len && tl != 0) {
+			uint32_t hmin = L.hdr < len ? L.hdr : len;
+			L.dlen = tl > hmin ? tl : hmin;
+		}
+		if (L.dlen <= L.hdr || L.hdr == 0) break;
+		po = off + L.hdr; pl = L.dlen - L.hdr;
+		/* isFragment :415-418, getFragmentFlags/Offset :430-438 */
+		if ((p[6] & 0x20) || (((p[6] & 0x1F) << 8) | p[7]) != 0) { NEXT(K_PAYLOAD, po, pl); break; }
+		switch (p[9]) {
+		case 17: NEXT(pl >= 8 ? K_UDP : K_PAYLOAD, po, pl); break;
+		case 6: NEXT(tcp_valid(pkt + po, pl) ? K_TCP : K_PAYLOAD, po, pl); break;
+		case 4: /* IPLayer::getIPVersion, Packet++/src/IPLayer.cpp:5-25 */
+			switch (pkt[po] >> 4) {
+			case 4: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+			case 6: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+			default: NEXT(K_PAYLOAD, po, pl); break;
+			}
+			break;
+		case 47: /* GreLayer::getGREVersion, Packet++/src/GreLayer.cpp:23-36 */
+			if (pl < 4) NEXT(K_PAYLOAD, po, pl);
+			else if ((pkt[po + 1] & 7) == 0) NEXT(K_GRE0, po, pl);
+			else if ((pkt[po + 1] & 7) == 1) NEXT(pl >= 8 ? K_GRE1 : K_PAYLOAD, po, pl);
+			else NEXT(K_PAYLOAD, po, pl);
+			break;
+		case 41: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		case 1: case 2: case 51: case 50: case 112: NEXT(K_OUT, po, pl); break; /* ICMP IGMP AH ESP VRRP */
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	}
+	case K_IPV6: { /* IPv6Layer ctor Packet++/src/IPv6Layer.cpp:28-40; parseExtensions :79-147 */
+		L.proto = P_IPV6; L.osi = 3;
+		uint8_t nh = p[6];
+		uint32_t eo = 40, ext = 0;
+		int last_ext = -1;
+		while (eo <= len - 2) {
+			uint32_t el;
+			if (nh == 44 || nh == 0 || nh == 60 || nh == 43) el = 8u * ((uint32_t)p[eo + 1] + 1); /* IPv6Extensions.h:40-43 */
+			else if (nh == 51) el = 4u * ((uint32_t)p[eo + 1] + 2);                            /* IPv6Extensions.h:480-483 */
+			else break;
+			last_ext = nh;
+			nh = p[eo];
+			eo += el;
+			ext += el;
+		}
+		L.hdr = 40 + ext;
+		uint32_t total = (uint32_t)be16(p + 4) + L.hdr; /* payloadLength + getHeaderLen() */
+		if (total < len) L.dlen = total;
+		/* parseNextLayer :194-312 */
+		if (L.dlen <= L.hdr) break;
+		po = off + L.hdr; pl = L.dlen - L.hdr;
+		if (last_ext == 44) { NEXT(K_PAYLOAD, po, pl); break; }
+		switch (nh) {
+		case 17: NEXT(pl >= 8 ? K_UDP : K_PAYLOAD, po, pl); break;
+		case 6: NEXT(tcp_valid(pkt + po, pl) ? K_TCP : K_PAYLOAD, po, pl); break;
+		case 4:
+			switch (pkt[po] >> 4) {
+			case 4: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+			case 6: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+			default: NEXT(K_PAYLOAD, po, pl); break;
+			}
+			break;
+		case 47:
+			if (pl < 4) NEXT(K_PAYLOAD, po, pl);
+			else if ((pkt[po + 1] & 7) == 0) NEXT(K_GRE0, po, pl);
+			else if ((pkt[po + 1] & 7) == 1) NEXT(pl >= 8 ? K_GRE1 : K_PAYLOAD, po, pl);
+			else NEXT(K_PAYLOAD, po, pl);
+			break;
+		case 51: case 50: case 58: case 112: NEXT(K_OUT, po, pl); break; /* AH ESP ICMPv6 VRRP */
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	}
+	case K_GRE0:
+	case K_GRE1: { /* GreLayer::getHeaderLen :237-252, parseNextLayer :195-235; bitfields GreLayer.h:14-57 */
+		L.proto = k == K_GRE0 ? P_GREV0 : P_GREV1; L.osi = 3;
+		L.hdr = 4;
+		if ((p[0] & 0x80) || (p[0] & 0x40)) L.hdr += 4; /* checksum | routing */
+		if (p[0] & 0x20) L.hdr += 4;                    /* key */
+		if (p[0] & 0x10) L.hdr += 4;                    /* sequence */
+		if (p[1] & 0x80) L.hdr += 4;                    /* ack */
+		if (len <= L.hdr) break;
+		po = off + L.hdr; pl = len - L.hdr;
+		switch (be16(p + 2)) {
+		case 0x0800: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 0x86DD: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		case 0x8100: NEXT(K_VLAN, po, pl); break; /* unchecked */
+		case 0x8847: NEXT(K_MPLS, po, pl); break; /* unchecked */
+		case 0x880B: NEXT(pl >= 4 ? K_PPTP : K_PAYLOAD, po, pl); break;
+		case 0x6558:
+			if (eth_valid(pkt + po, pl)) NEXT(K_ETH, po, pl);
+			else NEXT(dot3_valid(pkt + po, pl) ? K_DOT3 : K_PAYLOAD, po, pl);
+			break;
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	}
+	case K_PPTP: /* PPP_PPTPLayer::parseNextLayer, Packet++/src/GreLayer.cpp:547-566 */
+		L.proto = P_PPTP; L.osi = 5; L.hdr = 4;
+		if (len <= 4) break;
+		po = off + 4; pl = len - 4;
+		switch (be16(p + 2)) {
+		case 0x21: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 0x57: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	case K_TCP: /* TcpLayer::getHeaderLen TcpLayer.h:565-568; parseNextLayer TcpLayer.cpp:360-492 */
+		L.proto = P_TCP; L.osi = 4; L.hdr = (uint32_t)(p[12] >> 4) * 4;
+		if (len <= L.hdr) break;
+		po = off + L.hdr; pl = len - L.hdr;
+		NEXT((tcp_l7_port(be16(p)) || tcp_l7_port(be16(p + 2))) ? K_L7 : K_PAYLOAD, po, pl);
+		break;
+	case K_UDP: /* UdpLayer::parseNextLayer, Packet++/src/UdpLayer.cpp:92-184 */
+		L.proto = P_UDP; L.osi = 4; L.hdr = 8;
+		if (len <= 8) break;
+		po = off + 8; pl = len - 8;
+		NEXT((udp_l7_port(be16(p), be16(p + 2)) || sip_heuristic(pkt + po, pl)) ? K_L7 : K_PAYLOAD, po, pl);
+		break;
+	case K_PAYLOAD: /* PayloadLayer: header = whole data, no next (PayloadLayer.h:61-81) */
+		L.proto = P_PAYLOAD; L.osi = 7; L.hdr = len;
+		break;
+	default: break;
+	}
+#undef NEXT
+	return L;
+}
+
+void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t linktype, const pcppx_opts* opts,
+                               pcppx_summary* sum, pcppx_layer* layers)
+{
+	memset(sum, 0, sizeof(*sum));
+	sum->l4_layer = 0xFF;
+	int cap = opts->max_layers ? opts->max_layers : PCPPX_MAX_LAYERS;
+	uint16_t flags = 0;
+	if (caplen > PCPPX_MAX_CAPLEN) { sum->flags = PCPPX_F_OVERSIZE; return; }
+	if (caplen == 0) return; /* createFirstLayer returns nullptr, Packet.cpp:829-831 */
+
+	/* first layer: Packet::createFirstLayer, Packet++/src/Packet.cpp:827-923 */
+	int k;
+	switch (linktype) {
+	case 1: /* LINKTYPE_ETHERNET */
+		k = eth_valid(pkt, caplen) ? K_ETH : dot3_valid(pkt, caplen) ? K_DOT3 : K_PAYLOAD;
+		break;
+	case 101: case 12: case 14: /* LINKTYPE_RAW, DLT_RAW1, DLT_RAW2 */
+		k = ((pkt[0] & 0xF0) == 0x40 && ipv4_valid(pkt, caplen)) ? K_IPV4
+		    : ((pkt[0] & 0xF0) == 0x60 && ipv6_valid(pkt, caplen)) ? K_IPV6 : K_PAYLOAD;
+		break;
+	case 228: k = ipv4_valid(pkt, caplen) ? K_IPV4 : K_PAYLOAD; break; /* LINKTYPE_IPV4 */
+	case 229: k = ipv6_valid(pkt, caplen) ? K_IPV6 : K_PAYLOAD; break; /* LINKTYPE_IPV6 */
+	case 0: case 113: case 276: case 239: case 104: /* NULL, SLL, SLL2, NFLOG, C_HDLC: host dissectors */
+		sum->flags = PCPPX_F_NEEDS_HOST_PROTO;
+		return;
+	default: k = K_PAYLOAD; break;
+	}
+
+	/* chain walk with the stop rules of Packet::parsePacket, Packet++/src/Packet.cpp:123-175 */
+	lay chain_first_ipv4 = { 0 }, chain_first_ipv6 = { 0 };
+	int have_ipv4 = 0, have_ipv6 = 0, l4_idx = -1, l4_is_tcp = 0, last_udp = -1, last_tcp = -1;
+	lay last_tcp_l = { 0 }, last_udp_l = { 0 }, prev_of_tcp = { 0 }, prev_of_udp = { 0 };
+	lay prev = { 0 }, last = { 0 };
+	int count = 0, found = 0, stopped_by_rule = 0;
+	uint64_t mask = 0;
+	uint32_t off = 0, len = caplen;
+	while (k != K_NONE) {
+		if (k == K_OUT) { flags |= PCPPX_F_NEEDS_HOST_PROTO; break; }
+		if (k == K_L7) { flags |= PCPPX_F_NEEDS_HOST_L7; break; }
+		int nk; uint32_t noff = 0, nlen = 0;
+		lay L = make_layer(pkt, k, off, len, &nk, &noff, &nlen);
+		int member = family_member(opts->parse_until_family, L.proto);
+		int fail = L.osi > opts->parse_until_osi;
+		if (!fail) {
+			if (opts->parse_until_family != 0 && member) found = 1;
+			if (found && !member) fail = 1;
+		}
+		if (fail) {
+			stopped_by_rule = 1;
+			if (count > 0) break; /* roll back the layer (Packet.cpp:170-175) */
+			nk = K_NONE;          /* the first layer is kept, but not parsed further */
+		}
+		/* record */
+		if (layers && count < cap) {
+			pcppx_layer* o = &layers[count];
+			o->proto = L.proto; o->osi = L.osi;
+			o->offset = (uint16_t)L.off; o->hdr_len = (uint16_t)L.hdr; o->data_len = (uint16_t)L.dlen;
+		}
+		mask |= (uint64_t)1 << L.proto;
+		if (L.proto == P_IPV4 && !have_ipv4) { have_ipv4 = 1; chain_first_ipv4 = L; }
+		if (L.proto == P_IPV6 && !have_ipv6) { have_ipv6 = 1; chain_first_ipv6 = L; }
+		if (L.proto == P_TCP) { last_tcp = count; last_tcp_l = L; prev_of_tcp = prev; }
+		if (L.proto == P_UDP) { last_udp = count; last_udp_l = L; prev_of_udp = prev; }
+		prev = L;
+		last = L;
+		++count;
+		k = nk; off = noff; len = nlen;
+	}
+	/* trailer: Packet.cpp:178-195 (only with no parse-until options, and not for flagged chains) */
+	if (count > 0 && opts->parse_until_family == 0 && opts->parse_until_osi == 8 && !stopped_by_rule &&
+	    !(flags & (PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_NEEDS_HOST_PROTO))) {
+		int64_t tl = (int64_t)caplen - ((int64_t)last.off + last.dlen);
+		if (tl > 0) {
+			if (layers && count < cap) {
+				pcppx_layer* o = &layers[count];
+				o->proto = P_TRAILER; o->osi = 2;
+				o->offset = (uint16_t)(last.off + last.dlen); o->hdr_len = (uint16_t)tl; o->data_len = (uint16_t)tl;
+			}
+			mask |= (uint64_t)1 << P_TRAILER;
+			++count;
+			flags |= PCPPX_F_TRAILER;
+		}
+	}
+	if (count > cap) flags |= PCPPX_F_DEPTH_OVERFLOW;
+	sum->n_layers = (uint8_t)(count > cap ? cap : count);
+	sum->proto_mask = mask;
+
+	/* l4 layer: getLayerOfType<TcpLayer>(true) else <UdpLayer>(true), PacketUtils.cpp:157-169 */
+	lay l4 = { 0 }, l4prev = { 0 };
+	if (last_tcp >= 0) { l4_idx = last_tcp; l4_is_tcp = 1; l4 = last_tcp_l; l4prev = prev_of_tcp; }
+	else if (last_udp >= 0) { l4_idx = last_udp; l4 = last_udp_l; l4prev = prev_of_udp; }
+	if (l4_idx >= 0 && l4_idx < 255) sum->l4_layer = (uint8_t)l4_idx;
+
+	/* hash5Tuple, PacketUtils.cpp:139-210 (ICMP never appears in an emitted chain: it is OUT) */
+	int has_ip = have_ipv4 || have_ipv6;
+	for (int dir = 0; dir < 2; ++dir) {
+		uint32_t h = 0;
+		if (has_ip && l4_idx >= 0) {
+			const uint8_t* lp = pkt + l4.off;
+			uint16_t sp = le16(lp), dp = le16(lp + 2); /* raw network-order values */
+			int s = 0;
+			if (!dir && dp < sp) s = 1;
+			const uint8_t* ports[2];
+			ports[0 + s] = lp; ports[1 - s] = lp + 2;
+			h = 2166136261u;
+			h = fnv_update(h, ports[0], 2);
+			h = fnv_update(h, ports[1], 2);
+			if (have_ipv4) {
+				const uint8_t* ip = pkt + chain_first_ipv4.off;
+				if (!dir && sp == dp && le32(ip + 16) < le32(ip + 12)) s = 1;
+				const uint8_t* a[2];
+				a[0 + s] = ip + 12; a[1 - s] = ip + 16;
+				h = fnv_update(h, a[0], 4);
+				h = fnv_update(h, a[1], 4);
+				h = fnv_update(h, ip + 9, 1);
+			} else {
+				const uint8_t* ip = pkt + chain_first_ipv6.off;
+				if (!dir && sp == dp && memcmp(ip + 24, ip + 8, 16) < 0) s = 1;
+				const uint8_t* a[2];
+				a[0 + s] = ip + 8; a[1 - s] = ip + 24;
+				h = fnv_update(h, a[0], 16);
+				h = fnv_update(h, a[1], 16);
+				h = fnv_update(h, ip + 6, 1);
+			}
+		}
+		if (dir) sum->hash5_dir = h; else sum->hash5 = h;
+	}
+	/* hash2Tuple, PacketUtils.cpp:212-245 */
+	if (have_ipv4) {
+		const uint8_t* ip = pkt + chain_first_ipv4.off;
+		int s = le32(ip + 16) < le32(ip + 12);
+		const uint8_t* a[2];
+		a[0 + s] = ip + 12; a[1 - s] = ip + 16;
+		uint32_t h = fnv_update(2166136261u, a[0], 4);
+		sum->hash2 = fnv_update(h, a[1], 4);
+	} else if (have_ipv6) {
+		const uint8_t* ip = pkt + chain_first_ipv6.off;
+		int s = memcmp(ip + 24, ip + 8, 16) < 0;
+		const uint8_t* a[2];
+		a[0 + s] = ip + 8; a[1 - s] = ip + 24;
+		uint32_t h = fnv_update(2166136261u, a[0], 16);
+		sum->hash2 = fnv_update(h, a[1], 16);
+	}
+
+	if (opts->want_checksums) {
+		if (have_ipv4) { /* IPv4Layer::computeCalculateFields, IPv4Layer.cpp:410-412 */
+			const uint8_t* ip = pkt + chain_first_ipv4.off;
+			uint32_t hl = (uint32_t)(ip[0] & 0xF) * 4;
+			if (hl > chain_first_ipv4.dlen) hl = chain_first_ipv4.dlen;
+			uint8_t hdr[60];
+			memcpy(hdr, ip, hl);
+			hdr[10] = hdr[11] = 0;
+			const uint8_t* b[1] = { hdr };
+			uint32_t n[1] = { hl };
+			sum->ip_csum_calc = pcppx_oracle_checksum(b, n, 1);
+			sum->ip_csum_stored = be16(ip + 10);
+			flags |= PCPPX_F_IP_CSUM;
+			if (sum->ip_csum_calc == sum->ip_csum_stored) flags |= PCPPX_F_IP_CSUM_OK;
+		}
+		if (l4_idx >= 0) {
+			/* {Tcp,Udp}Layer::calculateChecksum(false): TcpLayer.cpp:271-311, UdpLayer.cpp:47-90;
+			 * computePseudoHdrChecksum PacketUtils.cpp:66-112 */
+			const uint8_t* lp = pkt + l4.off;
+			uint32_t field = l4_is_tcp ? 16 : 6;
+			uint16_t res = 0;
+			if (l4prev.proto == P_IPV4 || l4prev.proto == P_IPV6) {
+				uint8_t* tmp = (uint8_t*)malloc(l4.dlen ? l4.dlen : 1);
+				memcpy(tmp, lp, l4.dlen);
+				tmp[field] = tmp[field + 1] = 0;
+				uint8_t proto = l4_is_tcp ? 6 : 17;
+				uint16_t ph[18];
+				uint32_t phlen;
+				const uint8_t* ip = pkt + l4prev.off;
+				if (l4prev.proto == P_IPV4) {
+					uint32_t src = le32(ip + 12), dst = le32(ip + 16);
+					ph[0] = (uint16_t)(src >> 16); ph[1] = (uint16_t)(src & 0xFFFF);
+					ph[2] = (uint16_t)(dst >> 16); ph[3] = (uint16_t)(dst & 0xFFFF);
+					ph[4] = bswap16((uint16_t)l4.dlen);
+					ph[5] = bswap16(proto);
+					phlen = 12;
+				} else {
+					memcpy(ph, ip + 8, 16);
+					memcpy(ph + 8, ip + 24, 16);
+					ph[16] = bswap16((uint16_t)l4.dlen);
+					ph[17] = bswap16(proto);
+					phlen = 36;
+				}
+				const uint8_t* b[2] = { tmp, (const uint8_t*)ph };
+				uint32_t n[2] = { l4.dlen, phlen };
+				res = pcppx_oracle_checksum(b, n, 2);
+				free(tmp);
+			}
+			if (!l4_is_tcp && res == 0) res = 0xFFFF;
+			sum->l4_csum_calc = res;
+			sum->l4_csum_stored = be16(lp + field);
+			flags |= PCPPX_F_L4_CSUM;
+			if (sum->l4_csum_calc == sum->l4_csum_stored) flags |= PCPPX_F_L4_CSUM_OK;
+		}
+	}
+	sum->flags = flags;
+}
+
+/* ---- batch drivers ---- */
+typedef struct {
+	const pcppx_batch* b;
+	const pcppx_opts* o;
+	pcppx_records* r;
+	int t, nt;
+	uint64_t acc;
+} job;
+
+static void* run_job(void* arg)
+{
+	job* j = (job*)arg;
+	uint64_t acc = 0;
+	int ml = j->o->max_layers;
+	for (uint32_t i = (uint32_t)j->t; i < j->b->n; i += (uint32_t)j->nt) {
+		pcppx_summary s;
+		pcppx_summary* sp = j->r ? &j->r->summary[i] : &s;
+		pcppx_layer scratch[PCPPX_MAX_LAYERS];
+		pcppx_layer* lp = (j->r && j->r->layers && ml) ? j->r->layers + (size_t)i * ml : (ml ? scratch : NULL);
+		if (j->b->offsets[i] + j->b->caplens[i] > j->b->data_len) {
+			memset(sp, 0, sizeof(*sp));
+			sp->l4_layer = 0xFF;
+			sp->flags = PCPPX_F_BAD_DESC;
+			continue;
+		}
+		pcppx_oracle_parse_packet(j->b->data + j->b->offsets[i], j->b->caplens[i], j->b->linktype, j->o, sp, lp);
+		acc += sp->hash5 + sp->hash5_dir + sp->hash2 + sp->l4_csum_calc + sp->ip_csum_calc + sp->n_layers;
+	}
+	j->acc = acc;
+	return NULL;
+}
+
+static int run_all(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, int threads, uint64_t* digest)
+{
+	if (threads < 1) threads = 1;
+	if (threads > 256) threads = 256;
+	job jobs[256];
+	pthread_t th[256];
+	for (int t = 0; t < threads; ++t) {
+		jobs[t].b = b; jobs[t].o = o; jobs[t].r = r; jobs[t].t = t; jobs[t].nt = threads; jobs[t].acc = 0;
+	}
+	if (threads == 1) run_job(&jobs[0]);
+	else {
+		for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, run_job, &jobs[t]);
+		for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+	}
+	if (digest) {
+		uint64_t d = 0;
+		for (int t = 0; t < threads; ++t) d += jobs[t].acc;
+		*digest = d;
+	}
+	return PCPPX_OK;
+}
+
+int pcppx_oracle_parse_batch(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, int threads)
+{
+	if (!b || !o || !r || !r->summary || o->max_layers > PCPPX_MAX_LAYERS) return PCPPX_E_INVAL;
+	return run_all(b, o, r, threads, NULL);
+}
+
+int pcppx_oracle_bench(const pcppx_batch* b, const pcppx_opts* o, int threads, double* seconds, uint64_t* digest)
+{
+	if (!b || !o || !seconds || o->max_layers > PCPPX_MAX_LAYERS) return PCPPX_E_INVAL;
+	struct timespec t0, t1;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	run_all(b, o, NULL, threads, digest);
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	*seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+	return PCPPX_OK;
+}

@@ -1,0 +1,243 @@
+// ref_harness.cpp — TEST INFRASTRUCTURE ONLY (part of oracle/).
+//
+// Our own harness around the *real* reference Packet++ (compiled from /root/reference sources by
+// oracle/Makefile into oracle/_ref/). It turns a pcppx_batch into pcppx records by driving the
+// reference API exactly as its own callers do:
+//   Packet(RawPacket*, false, parseUntil, parseUntilLayer)      Packet++/src/Packet.cpp:202-209
+//   layer walk: getProtocol/getOsiModelLayer/getData/getHeaderLen/getDataLen   Packet++/header/Layer.h
+//   hash5Tuple(&p, false|true), hash2Tuple(&p)                  Packet++/src/PacketUtils.cpp:139-245
+//   IPv4 header checksum as IPv4Layer::computeCalculateFields   Packet++/src/IPv4Layer.cpp:410-412
+//   TcpLayer/UdpLayer::calculateChecksum(false)                 TcpLayer.cpp:271-311, UdpLayer.cpp:47-90
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+// It never ships in the product path.
+
+#include "pcppx.h"
+
+#include "Packet.h"
+#include "RawPacket.h"
+#include "IPv4Layer.h"
+#include "IPv6Layer.h"
+#include "TcpLayer.h"
+#include "UdpLayer.h"
+#include "PacketUtils.h"
+#include "Logger.h"
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace
+{
+	uint16_t be16at(const uint8_t* p)
+	{
+		return static_cast<uint16_t>((p[0] << 8) | p[1]);
+	}
+
+	void fillRecord(pcpp::Packet& packet, const uint8_t* raw, const pcppx_opts* opts, pcppx_summary* sum,
+	                pcppx_layer* layers)
+	{
+		std::memset(sum, 0, sizeof(*sum));
+		sum->l4_layer = 0xFF;
+		int cap = opts->max_layers;
+		int idx = 0;
+		uint64_t mask = 0;
+		pcpp::Layer* last = nullptr;
+		for (pcpp::Layer* l = packet.getFirstLayer(); l != nullptr; l = l->getNextLayer(), ++idx)
+		{
+			mask |= (uint64_t)1 << (l->getProtocol() & 63);
+			if (layers != nullptr && idx < cap)
+			{
+				pcppx_layer& o = layers[idx];
+				o.proto = l->getProtocol();
+				o.osi = static_cast<uint8_t>(l->getOsiModelLayer());
+				o.offset = static_cast<uint16_t>(l->getData() - raw);
+				o.hdr_len = static_cast<uint16_t>(l->getHeaderLen());
+				o.data_len = static_cast<uint16_t>(l->getDataLen());
+			}
+			last = l;
+		}
+		uint16_t flags = 0;
+		int limit = cap > 0 ? cap : PCPPX_MAX_LAYERS;
+		if (idx > limit)
+			flags |= PCPPX_F_DEPTH_OVERFLOW;
+		sum->n_layers = static_cast<uint8_t>(idx > limit ? limit : idx);
+		sum->proto_mask = mask;
+		if (last != nullptr && last->getProtocol() == pcpp::PacketTrailer)
+			flags |= PCPPX_F_TRAILER;
+
+		sum->hash5 = pcpp::hash5Tuple(&packet, false);
+		sum->hash5_dir = pcpp::hash5Tuple(&packet, true);
+		sum->hash2 = pcpp::hash2Tuple(&packet);
+
+		// index of the layer hash5Tuple reads its ports from (PacketUtils.cpp:157-169)
+		pcpp::Layer* l4 = packet.getLayerOfType<pcpp::TcpLayer>(true);
+		if (l4 == nullptr)
+			l4 = packet.getLayerOfType<pcpp::UdpLayer>(true);
+		if (l4 != nullptr)
+		{
+			int i = 0;
+			for (pcpp::Layer* l = packet.getFirstLayer(); l != l4; l = l->getNextLayer())
+				++i;
+			sum->l4_layer = static_cast<uint8_t>(i);
+		}
+
+		if (opts->want_checksums)
+		{
+			pcpp::IPv4Layer* ip = packet.getLayerOfType<pcpp::IPv4Layer>();
+			if (ip != nullptr)
+			{
+				size_t hl = (std::min)(static_cast<size_t>(ip->getIPv4Header()->internetHeaderLength * 4),
+				                       ip->getDataLen());
+				std::vector<uint8_t> hdr(ip->getData(), ip->getData() + hl);
+				if (hl >= 12)
+				{
+					hdr[10] = 0;
+					hdr[11] = 0;
+				}
+				pcpp::ScalarBuffer<uint16_t> sb = { reinterpret_cast<uint16_t*>(hdr.data()), hl };
+				sum->ip_csum_calc = pcpp::computeChecksum(&sb, 1);
+				sum->ip_csum_stored = be16at(ip->getData() + 10);
+				flags |= PCPPX_F_IP_CSUM;
+				if (sum->ip_csum_calc == sum->ip_csum_stored)
+					flags |= PCPPX_F_IP_CSUM_OK;
+			}
+			if (l4 != nullptr)
+			{
+				if (l4->getProtocol() == pcpp::TCP)
+				{
+					sum->l4_csum_calc = static_cast<pcpp::TcpLayer*>(l4)->calculateChecksum(false);
+					sum->l4_csum_stored = be16at(l4->getData() + 16);
+				}
+				else
+				{
+					sum->l4_csum_calc = static_cast<pcpp::UdpLayer*>(l4)->calculateChecksum(false);
+					sum->l4_csum_stored = be16at(l4->getData() + 6);
+				}
+				flags |= PCPPX_F_L4_CSUM;
+				if (sum->l4_csum_calc == sum->l4_csum_stored)
+					flags |= PCPPX_F_L4_CSUM_OK;
+			}
+		}
+		sum->flags = flags;
+	}
+
+	struct Prepared
+	{
+		std::vector<uint8_t> bytes;  // private mutable copy: calculateChecksum zeroes+restores a field
+		std::vector<pcpp::RawPacket> raws;
+	};
+
+	void prepare(const pcppx_batch* b, Prepared& p)
+	{
+		uint64_t total = 0;
+		for (uint32_t i = 0; i < b->n; ++i)
+			total += b->caplens[i];
+		p.bytes.resize(total + 1);
+		p.raws.clear();
+		p.raws.reserve(b->n);
+		uint64_t pos = 0;
+		timeval ts{ 0, 0 };
+		for (uint32_t i = 0; i < b->n; ++i)
+		{
+			std::memcpy(p.bytes.data() + pos, b->data + b->offsets[i], b->caplens[i]);
+			p.raws.emplace_back(p.bytes.data() + pos, static_cast<int>(b->caplens[i]), ts, false,
+			                    static_cast<pcpp::LinkLayerType>(b->linktype));
+			pos += b->caplens[i];
+		}
+	}
+}  // namespace
+
+extern "C"
+{
+	// Parse a host batch with the reference Packet++ and fill host records.
+	int pcppx_ref_parse_batch(const pcppx_batch* b, const pcppx_opts* opts, pcppx_records* out)
+	{
+		if (b == nullptr || opts == nullptr || out == nullptr || out->summary == nullptr)
+			return PCPPX_E_INVAL;
+		pcpp::Logger::getInstance().suppressLogs();
+		Prepared p;
+		prepare(b, p);
+		for (uint32_t i = 0; i < b->n; ++i)
+		{
+			pcpp::Packet packet(&p.raws[i], false, opts->parse_until_family,
+			                    static_cast<pcpp::OsiModelLayer>(opts->parse_until_osi));
+			pcppx_layer* layers = (out->layers != nullptr && opts->max_layers > 0)
+			                          ? out->layers + static_cast<size_t>(i) * opts->max_layers
+			                          : nullptr;
+			fillRecord(packet, p.raws[i].getRawData(), opts, &out->summary[i], layers);
+		}
+		return PCPPX_OK;
+	}
+
+	// Timed CPU baseline: the reference parse (+hash5Tuple both directions, hash2Tuple, and the
+	// checksums when opts->want_checksums) over the batch, packets preloaded as RawPackets in the style
+	// of BM_PacketPureParsing (Examples/PcapPlusPlus-benchmark/benchmark-google.cpp:209-264), packet
+	// indices interleaved over `threads` threads. Returns seconds of the timed region.
+	int pcppx_ref_bench(const pcppx_batch* b, const pcppx_opts* opts, int threads, double* seconds,
+	                    uint64_t* digest)
+	{
+		if (b == nullptr || opts == nullptr || seconds == nullptr || threads < 1)
+			return PCPPX_E_INVAL;
+		pcpp::Logger::getInstance().suppressLogs();
+		Prepared p;
+		prepare(b, p);
+		std::vector<uint64_t> part(threads, 0);
+		auto work = [&](int t) {
+			uint64_t acc = 0;
+			for (uint32_t i = t; i < b->n; i += threads)
+			{
+				pcpp::Packet packet(&p.raws[i], false, opts->parse_until_family,
+				                    static_cast<pcpp::OsiModelLayer>(opts->parse_until_osi));
+				acc += pcpp::hash5Tuple(&packet, false);
+				acc += pcpp::hash5Tuple(&packet, true);
+				acc += pcpp::hash2Tuple(&packet);
+				if (opts->want_checksums)
+				{
+					pcpp::IPv4Layer* ip = packet.getLayerOfType<pcpp::IPv4Layer>();
+					if (ip != nullptr)
+					{
+						size_t hl = (std::min)(static_cast<size_t>(ip->getIPv4Header()->internetHeaderLength * 4),
+						                       ip->getDataLen());
+						uint8_t hdr[64];
+						std::memcpy(hdr, ip->getData(), hl);
+						hdr[10] = hdr[11] = 0;
+						pcpp::ScalarBuffer<uint16_t> sb = { reinterpret_cast<uint16_t*>(hdr), hl };
+						acc += pcpp::computeChecksum(&sb, 1);
+					}
+					pcpp::TcpLayer* tcp = packet.getLayerOfType<pcpp::TcpLayer>(true);
+					if (tcp != nullptr)
+						acc += tcp->calculateChecksum(false);
+					else
+					{
+						pcpp::UdpLayer* udp = packet.getLayerOfType<pcpp::UdpLayer>(true);
+						if (udp != nullptr)
+							acc += udp->calculateChecksum(false);
+					}
+				}
+			}
+			part[t] = acc;
+		};
+		auto t0 = std::chrono::steady_clock::now();
+		if (threads == 1)
+			work(0);
+		else
+		{
+			std::vector<std::thread> pool;
+			for (int t = 0; t < threads; ++t)
+				pool.emplace_back(work, t);
+			for (auto& th : pool)
+				th.join();
+		}
+		auto t1 = std::chrono::steady_clock::now();
+		*seconds = std::chrono::duration<double>(t1 - t0).count();
+		if (digest != nullptr)
+		{
+			uint64_t d = 0;
+			for (auto v : part)
+				d += v;
+			*digest = d;
+		}
+		return PCPPX_OK;
+	}
+}

@@ -1,0 +1,163 @@
+"""ctypes/numpy mirror of include/pcppx.h (the engine's C ABI) and the loader of libpcppx.so.
+
+The loader fails loudly when the HIP engine library is missing: there is no CPU fallback in the
+product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+ENGINE_SO = PKG_DIR / "libpcppx.so"
+
+ABI_VERSION = 1
+MAX_LAYERS = 16
+MAX_CAPLEN = 65535
+
+# error codes
+OK, E_INVAL, E_NODEV, E_HIP, E_NOMEM, E_LINKTYPE = 0, -1, -2, -3, -4, -5
+
+# summary flags
+F_NEEDS_HOST_L7 = 0x0001
+F_NEEDS_HOST_PROTO = 0x0002
+F_DEPTH_OVERFLOW = 0x0004
+F_OVERSIZE = 0x0008
+F_IP_CSUM = 0x0010
+F_IP_CSUM_OK = 0x0020
+F_L4_CSUM = 0x0040
+F_L4_CSUM_OK = 0x0080
+F_TRAILER = 0x0100
+F_BAD_DESC = 0x0200
+F_NEEDS_HOST = F_NEEDS_HOST_L7 | F_NEEDS_HOST_PROTO | F_OVERSIZE | F_BAD_DESC
+
+# pcpp::LinkLayerType values used here (Packet++/header/RawPacket.h:24-178)
+LINKTYPE_NULL = 0
+LINKTYPE_ETHERNET = 1
+LINKTYPE_DLT_RAW1 = 12
+LINKTYPE_DLT_RAW2 = 14
+LINKTYPE_RAW = 101
+LINKTYPE_LINUX_SLL = 113
+LINKTYPE_IPV4 = 228
+LINKTYPE_IPV6 = 229
+
+SUMMARY_DTYPE = np.dtype(
+    [
+        ("hash5", "<u4"),
+        ("hash5_dir", "<u4"),
+        ("hash2", "<u4"),
+        ("flags", "<u2"),
+        ("n_layers", "u1"),
+        ("l4_layer", "u1"),
+        ("proto_mask", "<u8"),
+        ("ip_csum_calc", "<u2"),
+        ("ip_csum_stored", "<u2"),
+        ("l4_csum_calc", "<u2"),
+        ("l4_csum_stored", "<u2"),
+    ]
+)
+LAYER_DTYPE = np.dtype(
+    [("proto", "u1"), ("osi", "u1"), ("offset", "<u2"), ("hdr_len", "<u2"), ("data_len", "<u2")]
+)
+assert SUMMARY_DTYPE.itemsize == 32 and LAYER_DTYPE.itemsize == 8
+
+
+class Batch(C.Structure):
+    _fields_ = [
+        ("data", C.c_void_p),
+        ("offsets", C.c_void_p),
+        ("caplens", C.c_void_p),
+        ("data_len", C.c_uint64),
+        ("n", C.c_uint32),
+        ("linktype", C.c_uint16),
+        ("reserved", C.c_uint16),
+    ]
+
+
+class Opts(C.Structure):
+    _fields_ = [
+        ("parse_until_family", C.c_uint32),
+        ("parse_until_osi", C.c_uint8),
+        ("want_checksums", C.c_uint8),
+        ("max_layers", C.c_uint8),
+        ("reserved", C.c_uint8),
+    ]
+
+
+class Records(C.Structure):
+    _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p)]
+
+
+def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checksums: bool = True,
+              max_layers: int = MAX_LAYERS) -> Opts:
+    """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection."""
+    if not 0 <= max_layers <= MAX_LAYERS:
+        raise ValueError(f"max_layers must be in [0, {MAX_LAYERS}]")
+    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, 0)
+
+
+def _declare(lib: C.CDLL) -> C.CDLL:
+    P = C.c_void_p
+    lib.pcppx_abi_version.restype = C.c_int
+    lib.pcppx_strerror.restype = C.c_char_p
+    lib.pcppx_strerror.argtypes = [C.c_int]
+    lib.pcppx_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.pcppx_open.argtypes = [C.c_int, C.POINTER(P)]
+    lib.pcppx_close.argtypes = [P]
+    lib.pcppx_close.restype = None
+    lib.pcppx_sync.argtypes = [P]
+    lib.pcppx_default_opts.argtypes = [C.POINTER(Opts)]
+    lib.pcppx_default_opts.restype = None
+    lib.pcppx_parse_batch_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records), P]
+    lib.pcppx_parse_batch_host.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records)]
+    lib.pcppx_flow_count_device.argtypes = [P, P, P, C.c_uint32, P, P, P, C.c_uint32, P, P]
+    for name in ("pcppx_device_count", "pcppx_open", "pcppx_sync", "pcppx_parse_batch_device",
+                 "pcppx_parse_batch_host", "pcppx_flow_count_device"):
+        getattr(lib, name).restype = C.c_int
+    return lib
+
+
+_ENGINE: C.CDLL | None = None
+
+# every symbol include/pcppx.h declares
+EXPORTED_SYMBOLS = (
+    "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_open", "pcppx_close",
+    "pcppx_sync", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
+    "pcppx_flow_count_device",
+)
+
+
+def load_engine() -> C.CDLL:
+    """Load the HIP engine (pcapplusplus_amd/libpcppx.so). Raises if it has not been built."""
+    global _ENGINE
+    if _ENGINE is None:
+        if not ENGINE_SO.exists():
+            raise RuntimeError(
+                f"HIP engine library {ENGINE_SO} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                " (or `make -C pcapplusplus_amd/csrc`). There is no CPU fallback.")
+        lib = _declare(C.CDLL(str(ENGINE_SO)))
+        if lib.pcppx_abi_version() != ABI_VERSION:
+            raise RuntimeError("libpcppx.so ABI version mismatch")
+        _ENGINE = lib
+    return _ENGINE
+
+
+def check(rc: int, what: str = "pcppx") -> None:
+    if rc != OK:
+        msg = load_engine().pcppx_strerror(rc).decode() if _ENGINE is not None else str(rc)
+        raise RuntimeError(f"{what} failed: {msg} ({rc})")
+
+
+def ptr(a) -> int:
+    """Data pointer of a numpy array or torch tensor."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+__all__ = [n for n in dir() if not n.startswith("_")]
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")

@@ -1,0 +1,322 @@
+// pcppx_capi.cpp — the C ABI of include/pcppx.h: contexts, argument checks, kernel launches and the
+// pinned, double-buffered host-to-host pipeline.
+//
+// One context = one GPU + one host thread (the DpdkExample-FilterTraffic model of one private worker
+// per core, AppWorkerThread.h:45-162, mapped to one worker per GPU). Nothing here touches packet bytes
+// on the CPU except the copy into pinned staging on the host path.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+
+#include "pcppx.h"
+#include "pcppx_internal.h"
+
+namespace
+{
+constexpr size_t kChunkBytes = 64u << 20;    // packet bytes per host-path chunk
+constexpr uint32_t kChunkPackets = 1u << 18;  // packets per host-path chunk
+
+struct Slot
+{
+	hipStream_t st = nullptr;
+	hipEvent_t done = nullptr;
+	uint8_t* h_data = nullptr;
+	uint64_t* h_off = nullptr;
+	uint32_t* h_cap = nullptr;
+	pcppx_summary* h_sum = nullptr;
+	pcppx_layer* h_lay = nullptr;
+	uint8_t* d_data = nullptr;
+	uint64_t* d_off = nullptr;
+	uint32_t* d_cap = nullptr;
+	pcppx_summary* d_sum = nullptr;
+	pcppx_layer* d_lay = nullptr;
+	bool busy = false;
+	uint32_t first = 0, count = 0, ml = 0;
+};
+}  // namespace
+
+struct pcppx_ctx
+{
+	int device = 0;
+	hipStream_t stream = nullptr;
+	bool host_ready = false;
+	Slot slots[2];
+};
+
+namespace
+{
+bool ok(hipError_t e)
+{
+	return e == hipSuccess;
+}
+
+int valid_opts(const pcppx_opts* o)
+{
+	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS)
+		return PCPPX_E_INVAL;
+	return PCPPX_OK;
+}
+
+void free_slot(Slot& s)
+{
+	if (s.st) (void)hipStreamDestroy(s.st);
+	if (s.done) (void)hipEventDestroy(s.done);
+	(void)hipHostFree(s.h_data);
+	(void)hipHostFree(s.h_off);
+	(void)hipHostFree(s.h_cap);
+	(void)hipHostFree(s.h_sum);
+	(void)hipHostFree(s.h_lay);
+	(void)hipFree(s.d_data);
+	(void)hipFree(s.d_off);
+	(void)hipFree(s.d_cap);
+	(void)hipFree(s.d_sum);
+	(void)hipFree(s.d_lay);
+	s = Slot();
+}
+
+int init_host_path(pcppx_ctx* c)
+{
+	if (c->host_ready)
+		return PCPPX_OK;
+	for (Slot& s : c->slots)
+	{
+		bool good = ok(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking)) && ok(hipEventCreate(&s.done)) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_data), kChunkBytes + 16)) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), kChunkPackets * sizeof(uint64_t))) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_cap), kChunkPackets * sizeof(uint32_t))) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_sum), kChunkPackets * sizeof(pcppx_summary))) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_lay),
+		                             (size_t)kChunkPackets * PCPPX_MAX_LAYERS * sizeof(pcppx_layer))) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_data), kChunkBytes + 16)) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), kChunkPackets * sizeof(uint64_t))) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_cap), kChunkPackets * sizeof(uint32_t))) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_sum), kChunkPackets * sizeof(pcppx_summary))) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_lay),
+		                         (size_t)kChunkPackets * PCPPX_MAX_LAYERS * sizeof(pcppx_layer)));
+		if (!good)
+		{
+			for (Slot& t : c->slots)
+				free_slot(t);
+			return PCPPX_E_NOMEM;
+		}
+	}
+	c->host_ready = true;
+	return PCPPX_OK;
+}
+
+// copy a finished chunk's records from pinned memory to the caller's arrays
+void drain(Slot& s, pcppx_records* out)
+{
+	std::memcpy(out->summary + s.first, s.h_sum, (size_t)s.count * sizeof(pcppx_summary));
+	if (s.ml && out->layers)
+		std::memcpy(out->layers + (size_t)s.first * s.ml, s.h_lay, (size_t)s.count * s.ml * sizeof(pcppx_layer));
+	s.busy = false;
+}
+}  // namespace
+
+extern "C"
+{
+	int pcppx_abi_version(void)
+	{
+		return PCPPX_ABI_VERSION;
+	}
+
+	const char* pcppx_strerror(int err)
+	{
+		switch (err)
+		{
+		case PCPPX_OK: return "ok";
+		case PCPPX_E_INVAL: return "invalid argument";
+		case PCPPX_E_NODEV: return "no such HIP device";
+		case PCPPX_E_HIP: return "HIP runtime error";
+		case PCPPX_E_NOMEM: return "out of device or pinned memory";
+		case PCPPX_E_LINKTYPE: return "link type not handled";
+		default: return "unknown error";
+		}
+	}
+
+	int pcppx_device_count(int* out)
+	{
+		if (out == nullptr)
+			return PCPPX_E_INVAL;
+		int n = 0;
+		if (!ok(hipGetDeviceCount(&n)))
+			n = 0;
+		*out = n;
+		return PCPPX_OK;
+	}
+
+	void pcppx_default_opts(pcppx_opts* o)
+	{
+		if (o == nullptr)
+			return;
+		o->parse_until_family = 0;  // UnknownProtocol
+		o->parse_until_osi = 8;     // OsiModelLayerUnknown
+		o->want_checksums = 1;
+		o->max_layers = PCPPX_MAX_LAYERS;
+		o->reserved = 0;
+	}
+
+	int pcppx_open(int device, pcppx_ctx** out)
+	{
+		if (out == nullptr)
+			return PCPPX_E_INVAL;
+		*out = nullptr;
+		int n = 0;
+		if (!ok(hipGetDeviceCount(&n)) || device < 0 || device >= n)
+			return PCPPX_E_NODEV;
+		if (!ok(hipSetDevice(device)))
+			return PCPPX_E_HIP;
+		pcppx_ctx* c = new (std::nothrow) pcppx_ctx();
+		if (c == nullptr)
+			return PCPPX_E_NOMEM;
+		c->device = device;
+		if (!ok(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)))
+		{
+			delete c;
+			return PCPPX_E_HIP;
+		}
+		*out = c;
+		return PCPPX_OK;
+	}
+
+	void pcppx_close(pcppx_ctx* c)
+	{
+		if (c == nullptr)
+			return;
+		(void)hipSetDevice(c->device);
+		(void)hipStreamSynchronize(c->stream);
+		for (Slot& s : c->slots)
+		{
+			if (s.st)
+				(void)hipStreamSynchronize(s.st);
+			free_slot(s);
+		}
+		(void)hipStreamDestroy(c->stream);
+		delete c;
+	}
+
+	int pcppx_sync(pcppx_ctx* c)
+	{
+		if (c == nullptr)
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)) || !ok(hipStreamSynchronize(c->stream)))
+			return PCPPX_E_HIP;
+		return PCPPX_OK;
+	}
+
+	int pcppx_parse_batch_device(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r,
+	                             void* hip_stream)
+	{
+		if (c == nullptr || b == nullptr || r == nullptr || valid_opts(o) != PCPPX_OK)
+			return PCPPX_E_INVAL;
+		if (b->n == 0)
+			return PCPPX_OK;
+		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || r->summary == nullptr ||
+		    (o->max_layers != 0 && r->layers == nullptr))
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+		return pcppx::launch_parse(b, o, r, st);
+	}
+
+	int pcppx_parse_batch_host(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r)
+	{
+		if (c == nullptr || b == nullptr || r == nullptr || valid_opts(o) != PCPPX_OK)
+			return PCPPX_E_INVAL;
+		if (b->n == 0)
+			return PCPPX_OK;
+		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || r->summary == nullptr ||
+		    (o->max_layers != 0 && r->layers == nullptr))
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		int rc = init_host_path(c);
+		if (rc != PCPPX_OK)
+			return rc;
+		const uint32_t ml = o->max_layers;
+		uint32_t i = 0, k = 0;
+		while (i < b->n)
+		{
+			Slot& s = c->slots[k & 1];
+			if (s.busy)
+			{
+				if (!ok(hipEventSynchronize(s.done)))
+					return PCPPX_E_HIP;
+				drain(s, r);
+			}
+			// gather packets [i, j) into pinned staging, rebasing offsets
+			size_t pos = 0;
+			uint32_t j = i;
+			while (j < b->n && j - i < kChunkPackets)
+			{
+				const uint64_t off = b->offsets[j];
+				const uint32_t cap = b->caplens[j];
+				const bool in_bounds = off + cap <= b->data_len && off + cap >= off;
+				const size_t take = in_bounds ? cap : 0;
+				if (pos + take > kChunkBytes && j > i)
+					break;
+				if (in_bounds && cap <= kChunkBytes)
+				{
+					std::memcpy(s.h_data + pos, b->data + off, cap);
+					s.h_off[j - i] = pos;
+					pos += cap;
+				}
+				else
+					s.h_off[j - i] = ~0ull >> 1;  // kernel flags PCPPX_F_BAD_DESC
+				s.h_cap[j - i] = cap;
+				++j;
+			}
+			const uint32_t cnt = j - i;
+			bool good = ok(hipMemcpyAsync(s.d_data, s.h_data, pos ? pos : 1, hipMemcpyHostToDevice, s.st)) &&
+			            ok(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint64_t), hipMemcpyHostToDevice, s.st)) &&
+			            ok(hipMemcpyAsync(s.d_cap, s.h_cap, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.st));
+			if (!good)
+				return PCPPX_E_HIP;
+			pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
+			pcppx_records dr{ s.d_sum, ml ? s.d_lay : nullptr };
+			rc = pcppx::launch_parse(&db, o, &dr, s.st);
+			if (rc != PCPPX_OK)
+				return rc;
+			good = ok(hipMemcpyAsync(s.h_sum, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
+			       (ml == 0 || ok(hipMemcpyAsync(s.h_lay, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer),
+			                                     hipMemcpyDeviceToHost, s.st))) &&
+			       ok(hipEventRecord(s.done, s.st));
+			if (!good)
+				return PCPPX_E_HIP;
+			s.busy = true;
+			s.first = i;
+			s.count = cnt;
+			s.ml = ml;
+			i = j;
+			++k;
+		}
+		for (Slot& s : c->slots)
+			if (s.busy)
+			{
+				if (!ok(hipEventSynchronize(s.done)))
+					return PCPPX_E_HIP;
+				drain(s, r);
+			}
+		return PCPPX_OK;
+	}
+
+	int pcppx_flow_count_device(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* caplens, uint32_t n,
+	                            uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity,
+	                            uint64_t* stats, void* hip_stream)
+	{
+		if (c == nullptr || capacity == 0 || (capacity & (capacity - 1)) != 0)
+			return PCPPX_E_INVAL;
+		if (n == 0)
+			return PCPPX_OK;
+		if (summary == nullptr || caplens == nullptr || keys == nullptr || packets == nullptr || bytes == nullptr ||
+		    stats == nullptr)
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+		return pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats, st);
+	}
+}

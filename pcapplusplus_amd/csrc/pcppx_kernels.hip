@@ -1,0 +1,758 @@
+// pcppx_kernels.hip — gfx950 kernels of the packet-dissection engine.
+//
+// One lane owns one packet. A 256-lane workgroup stages the first 128 bytes of each of its packets
+// from HBM into a private LDS slot (aligned 16-B loads), walks the packet's layer chain out of LDS
+// (the per-layer rules of Packet++: Packet.cpp:66-196 and each Layer::parseNextLayer), then
+//   - writes the layer records (8 B each) and a 32-B summary per packet,
+//   - computes hash5Tuple / hash2Tuple (FNV-1, PacketUtils.cpp:114-245) from the staged header bytes,
+//   - computes the IPv4 header and TCP/UDP pseudo-header checksums (PacketUtils.cpp:12-112) with the
+//     ones'-complement sum taken mod 65535 over aligned 16-B chunks: a chunk's little-endian word sum
+//     is byte-order independent up to a multiply by 256 (an odd start address), so each lane streams its
+//     L4 bytes with aligned dwordx4 loads and never shifts bytes.
+// Pure integer/byte work: no MFMA. The parse-side semantics are restated independently in
+// oracle/pcppx_oracle.c, which is the parity checker for everything here.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pcppx.h"
+#include "pcppx_internal.h"
+
+namespace pcppx
+{
+namespace
+{
+
+constexpr int kBlock = 256;
+constexpr int kSlotDw = 33;  // 32 dwords of staged bytes + 1 pad dword: consecutive lanes land on different banks
+constexpr int kStageChunks = 8;  // 8 x 16 B = 128 B staged per packet
+
+// ProtocolType ids (Packet++/header/ProtocolType.h:42-258)
+enum : uint32_t
+{
+	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_VLAN = 9, P_MPLS = 14, P_GREV0 = 15,
+	P_GREV1 = 16, P_PPTP = 17, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44
+};
+
+// next-layer kinds of the chain walk
+enum : uint32_t
+{
+	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
+	K_PAYLOAD, K_OUT, K_L7
+};
+
+// explicit address spaces: keep packet reads as global_load / ds_read, never flat
+typedef const __attribute__((address_space(1))) uint8_t* gptr8;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4* gptr16;
+typedef const __attribute__((address_space(3))) uint8_t* lptr8;
+typedef const __attribute__((address_space(3))) uint32_t* lptr32;
+typedef __attribute__((address_space(3))) uint32_t* lptr32w;
+
+struct Pkt
+{
+	gptr8 g;                   // packet start in global memory
+	lptr8 s;                   // LDS slot base (byte 0 of the aligned window)
+	uintptr_t a0;              // aligned window start address (g rounded down to 16)
+	uint32_t mis;              // g - a0
+	uint32_t lim;              // packet bytes available in LDS: [0, lim)
+	uint32_t nch;              // staged 16-B chunks
+};
+
+__device__ __forceinline__ uint4 ld16(uintptr_t a)
+{
+	u32x4 v = *reinterpret_cast<gptr16>(a);
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t rb(const Pkt& p, uint32_t j)
+{
+	if (j < p.lim)
+		return p.s[p.mis + j];
+	return p.g[j];
+}
+__device__ __forceinline__ uint32_t be16(const Pkt& p, uint32_t j)
+{
+	return (rb(p, j) << 8) | rb(p, j + 1);
+}
+__device__ __forceinline__ uint32_t le16(const Pkt& p, uint32_t j)
+{
+	return rb(p, j) | (rb(p, j + 1) << 8);
+}
+__device__ __forceinline__ uint32_t le32(const Pkt& p, uint32_t j)
+{
+	return rb(p, j) | (rb(p, j + 1) << 8) | (rb(p, j + 2) << 16) | (rb(p, j + 3) << 24);
+}
+
+// ---- validity predicates (isDataValid of each layer; cited in oracle/pcppx_oracle.c) ----
+__device__ __forceinline__ bool ipv4_ok(const Pkt& p, uint32_t o, uint32_t n)
+{
+	if (n < 20)
+		return false;
+	uint32_t b = rb(p, o);
+	return (b >> 4) == 4 && (b & 0xF) >= 5;
+}
+__device__ __forceinline__ bool ipv6_ok(const Pkt& p, uint32_t o, uint32_t n)
+{
+	return n >= 40 && (rb(p, o) >> 4) == 6;
+}
+__device__ __forceinline__ bool tcp_ok(const Pkt& p, uint32_t o, uint32_t n)
+{
+	if (n < 20)
+		return false;
+	uint32_t d = rb(p, o + 12) >> 4;
+	return d >= 5 && n >= d * 4;
+}
+__device__ __forceinline__ bool eth_ok(const Pkt& p, uint32_t o, uint32_t n)
+{
+	return n >= 14 && be16(p, o + 12) >= 0x0600;
+}
+__device__ __forceinline__ bool dot3_ok(const Pkt& p, uint32_t o, uint32_t n)
+{
+	return n >= 14 && be16(p, o + 12) <= 0x05DC;
+}
+__device__ __forceinline__ bool llc_ok(const Pkt& p, uint32_t o, uint32_t n)
+{
+	return n >= 3 && !(rb(p, o) == 0xFF && rb(p, o + 1) == 0xFF);
+}
+
+// L7 trigger ports (engine contract = oracle tcp_l7_port / udp_l7_port)
+__device__ __forceinline__ bool tcp_l7(uint32_t x)
+{
+	switch (x)
+	{
+	case 443: case 261: case 448: case 465: case 563: case 614: case 636: case 989: case 990: case 992:
+	case 993: case 994: case 995: case 80: case 8080: case 5060: case 5061: case 179: case 22: case 53:
+	case 5353: case 5355: case 23: case 21: case 20: case 13400: case 3496: case 30490: case 102: case 25:
+	case 587: case 389: case 5432: case 3306: case 2123: case 502:
+		return true;
+	default:
+		return false;
+	}
+}
+__device__ __forceinline__ bool udp_l7_one(uint32_t x)
+{
+	switch (x)
+	{
+	case 53: case 5353: case 5355: case 5060: case 5061: case 1812: case 1813: case 3799: case 2152:
+	case 2123: case 546: case 547: case 123: case 13400: case 3496: case 30490: case 51820:
+		return true;
+	default:
+		return false;
+	}
+}
+__device__ __forceinline__ bool udp_l7(uint32_t src, uint32_t dst)
+{
+	if ((src == 68 && dst == 67) || (src == 67 && dst == 68) || (src == 67 && dst == 67))
+		return true;
+	if (dst == 4789 || dst == 0 || dst == 7 || dst == 9)
+		return true;
+	return udp_l7_one(src) || udp_l7_one(dst);
+}
+// SipLayer::detectSipMessageType keys, big-endian packed ("INVI" = 0x494E5649 ...)
+__device__ __forceinline__ bool sip_key(uint32_t k)
+{
+	switch (k)
+	{
+	case 0x494E5649u: case 0x41434B20u: case 0x42594520u: case 0x43414E43u: case 0x52454749u:
+	case 0x50524143u: case 0x4F505449u: case 0x53554253u: case 0x4E4F5449u: case 0x5055424Cu:
+	case 0x494E464Fu: case 0x52454645u: case 0x4D455353u: case 0x55504441u: case 0x5349502Fu:
+		return true;
+	default:
+		return false;
+	}
+}
+
+__device__ __forceinline__ uint32_t fnv(uint32_t h, uint32_t b)
+{
+	return (h * 16777619u) ^ b;
+}
+
+// fold a u32 sum of 16-bit halves to its residue mod 65535 (0..65534)
+__device__ __forceinline__ uint32_t mod65535(uint32_t x)
+{
+	x = (x & 0xFFFF) + (x >> 16);
+	x = (x & 0xFFFF) + (x >> 16);
+	return x == 0xFFFF ? 0 : x;
+}
+
+__device__ __forceinline__ uint32_t halves(uint32_t v)
+{
+	return (v & 0xFFFF) + (v >> 16);
+}
+
+__device__ __forceinline__ uint32_t mask_dword(uint32_t v, uintptr_t b, uintptr_t lo, uintptr_t hi)
+{
+	// keep bytes of the dword at address b that fall in [lo, hi)
+	int64_t s = (int64_t)lo - (int64_t)b, e = (int64_t)hi - (int64_t)b;
+	s = s < 0 ? 0 : (s > 4 ? 4 : s);
+	e = e < 0 ? 0 : (e > 4 ? 4 : e);
+	if (e <= s)
+		return 0;
+	uint64_t m = ((1ull << (8 * e)) - 1) & ~((1ull << (8 * s)) - 1);
+	return v & (uint32_t)m;
+}
+
+__device__ __forceinline__ uint32_t chunk_sum(uint4 v, uintptr_t c, uintptr_t lo, uintptr_t hi)
+{
+	if (c < lo || c + 16 > hi)
+	{
+		v.x = mask_dword(v.x, c, lo, hi);
+		v.y = mask_dword(v.y, c + 4, lo, hi);
+		v.z = mask_dword(v.z, c + 8, lo, hi);
+		v.w = mask_dword(v.w, c + 12, lo, hi);
+	}
+	return halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
+}
+
+// Residue mod 65535 of the little-endian 16-bit word sum of packet bytes [lo, hi) taken as a stream
+// starting at lo (odd last byte zero-padded), i.e. computeChecksum's localSum before folding.
+__device__ uint32_t range_residue(const Pkt& p, uint32_t lo, uint32_t hi)
+{
+	if (hi <= lo)
+		return 0;
+	const uintptr_t alo = (uintptr_t)p.g + lo, ahi = (uintptr_t)p.g + hi;
+	uintptr_t c = alo & ~(uintptr_t)15;
+	uint32_t acc = 0;
+	// chunks still in the LDS window
+	for (; c < ahi; c += 16)
+	{
+		uint32_t ci = (uint32_t)((c - p.a0) >> 4);
+		if (ci >= p.nch)
+			break;
+		lptr32 w = reinterpret_cast<lptr32>(p.s) + ci * 4;
+		uint4 v = make_uint4(w[0], w[1], w[2], w[3]);
+		acc += chunk_sum(v, c, alo, ahi);
+	}
+	// the rest straight from HBM, 64 B per iteration
+	for (; c + 64 <= ahi; c += 64)
+	{
+		uint4 v0 = ld16(c), v1 = ld16(c + 16), v2 = ld16(c + 32), v3 = ld16(c + 48);
+		acc += chunk_sum(v0, c, alo, ahi) + chunk_sum(v1, c + 16, alo, ahi) + chunk_sum(v2, c + 32, alo, ahi) +
+		       chunk_sum(v3, c + 48, alo, ahi);
+	}
+	for (; c < ahi; c += 16)
+	{
+		uint4 v = ld16(c);
+		acc += chunk_sum(v, c, alo, ahi);
+	}
+	uint32_t r = mod65535(acc);
+	if (alo & 1)
+		r = (r * 256u) % 65535u;  // the stream's words are the memory words byte-swapped
+	return r;
+}
+
+// computeChecksum's final step over a total whose true sum is known to be non-zero:
+// fold -> [1, 0xFFFF] (0xFFFF iff residue 0), invert, htobe16
+__device__ __forceinline__ uint32_t finish_checksum(uint32_t residue)
+{
+	uint32_t folded = residue == 0 ? 0xFFFFu : residue;
+	uint32_t result = (~folded) & 0xFFFFu;
+	return ((result >> 8) | (result << 8)) & 0xFFFFu;
+}
+
+struct Params
+{
+	const uint8_t* data;
+	const uint64_t* offsets;
+	const uint32_t* caplens;
+	uint64_t data_len;
+	pcppx_summary* summary;
+	pcppx_layer* layers;
+	uint32_t n;
+	uint32_t family;
+	uint32_t until_osi;
+	uint32_t want_csum;
+	uint32_t max_layers;
+	uint32_t linktype;
+};
+
+__global__ __launch_bounds__(kBlock) void parse_kernel(Params prm)
+{
+	__shared__ uint32_t stage[kBlock * kSlotDw];
+
+	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+	if (i >= prm.n)
+		return;
+
+	uint4 s0 = make_uint4(0, 0xFF00u, 0, 0), s1 = make_uint4(0, 0, 0, 0);  // summary, l4_layer = 0xFF
+	pcppx_summary* sum_out = prm.summary + i;
+
+	const uint64_t off = prm.offsets[i];
+	const uint32_t cap = prm.caplens[i];
+	if (off + cap > prm.data_len || cap > PCPPX_MAX_CAPLEN || cap == 0)
+	{
+		uint32_t fl = cap == 0 ? 0 : (cap > PCPPX_MAX_CAPLEN ? PCPPX_F_OVERSIZE : PCPPX_F_BAD_DESC);
+		if (off + cap > prm.data_len)
+			fl = PCPPX_F_BAD_DESC;
+		s0.w = fl | 0xFF000000u;
+		reinterpret_cast<uint4*>(sum_out)[0] = s0;
+		reinterpret_cast<uint4*>(sum_out)[1] = s1;
+		return;
+	}
+
+	// ---- stage the first 128 B of the packet into this lane's LDS slot ----
+	Pkt p;
+	p.g = (gptr8)(prm.data + off);
+	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
+	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+	{
+		uint32_t need = (p.mis + cap + 15) >> 4;
+		p.nch = need < kStageChunks ? need : kStageChunks;
+		lptr32w slot = (lptr32w)(stage) + threadIdx.x * kSlotDw;
+
+		uint4 v[kStageChunks];
+#pragma unroll
+		for (int c = 0; c < kStageChunks; ++c)
+			if ((uint32_t)c < p.nch)
+				v[c] = ld16(p.a0 + 16 * c);
+#pragma unroll
+		for (int c = 0; c < kStageChunks; ++c)
+			if ((uint32_t)c < p.nch)
+			{
+				slot[4 * c + 0] = v[c].x;
+				slot[4 * c + 1] = v[c].y;
+				slot[4 * c + 2] = v[c].z;
+				slot[4 * c + 3] = v[c].w;
+			}
+		p.s = reinterpret_cast<lptr8>(slot);
+		uint32_t staged = 16 * p.nch - p.mis;
+		p.lim = staged < cap ? staged : cap;
+	}
+
+	// ---- first layer: Packet::createFirstLayer (Packet.cpp:827-923) ----
+	uint32_t flags = 0;
+	uint32_t k;
+	switch (prm.linktype)
+	{
+	case 1:
+		k = eth_ok(p, 0, cap) ? K_ETH : (dot3_ok(p, 0, cap) ? K_DOT3 : K_PAYLOAD);
+		break;
+	case 101: case 12: case 14:
+	{
+		uint32_t v = rb(p, 0) & 0xF0;
+		k = (v == 0x40 && ipv4_ok(p, 0, cap)) ? K_IPV4 : ((v == 0x60 && ipv6_ok(p, 0, cap)) ? K_IPV6 : K_PAYLOAD);
+		break;
+	}
+	case 228: k = ipv4_ok(p, 0, cap) ? K_IPV4 : K_PAYLOAD; break;
+	case 229: k = ipv6_ok(p, 0, cap) ? K_IPV6 : K_PAYLOAD; break;
+	case 0: case 113: case 276: case 239: case 104: k = K_OUT; break;
+	default: k = K_PAYLOAD; break;
+	}
+
+	// ---- chain walk (Packet::parsePacket loop + stop rules, Packet.cpp:123-175) ----
+	const uint32_t ml = prm.max_layers;
+	const uint32_t cap_layers = ml ? ml : PCPPX_MAX_LAYERS;
+	uint2* lay_out = prm.layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
+	uint32_t count = 0, found = 0, stopped = 0;
+	uint64_t mask = 0;
+	int32_t v4 = -1, v6 = -1;                        // offsets of the first IPv4 / IPv6 layers
+	uint32_t v4_dlen = 0;
+	int32_t tcp_i = -1, udp_i = -1;                  // indices of the last TCP / UDP layers
+	uint32_t tcp_off = 0, tcp_dlen = 0, tcp_pp = 0, tcp_po = 0;  // + previous layer proto/offset
+	uint32_t udp_off = 0, udp_dlen = 0, udp_pp = 0, udp_po = 0;
+	uint32_t prev_proto = 0, prev_off = 0;
+	uint32_t last_end = 0;
+	uint32_t o = 0, len = cap;
+
+	while (k != K_NONE)
+	{
+		if (k == K_OUT)
+		{
+			flags |= PCPPX_F_NEEDS_HOST_PROTO;
+			break;
+		}
+		if (k == K_L7)
+		{
+			flags |= PCPPX_F_NEEDS_HOST_L7;
+			break;
+		}
+		uint32_t proto = 0, osi = 0, hdr = 0, dlen = len;
+		uint32_t nk = K_NONE, po = 0, pl = 0;
+		switch (k)
+		{
+		case K_ETH:  // EthLayer::parseNextLayer, EthLayer.cpp:28-69
+		{
+			proto = P_ETH; osi = 2; hdr = 14;
+			if (len <= 14) break;
+			po = o + 14; pl = len - 14;
+			uint32_t et = be16(p, o + 12);
+			if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
+			else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+			else if (et == 0x8100 || et == 0x88A8) nk = pl >= 4 ? K_VLAN : K_PAYLOAD;
+			else if (et == 0x8847) nk = pl >= 4 ? K_MPLS : K_PAYLOAD;
+			else if (et == 0x0806 || et == 0x8864 || et == 0x8863 || et == 0x0842) nk = K_OUT;
+			else nk = K_PAYLOAD;
+			break;
+		}
+		case K_DOT3:  // EthDot3Layer::parseNextLayer, EthDot3Layer.cpp:22-30
+			proto = P_DOT3; osi = 2; hdr = 14;
+			if (len <= 14) break;
+			po = o + 14; pl = len - 14;
+			nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
+			break;
+		case K_LLC:  // LLCLayer::parseNextLayer, LLCLayer.cpp:24-41
+			proto = P_LLC; osi = 2; hdr = 3;
+			if (len <= 3) break;
+			po = o + 3; pl = len - 3;
+			nk = (rb(p, o) == 0x42 && rb(p, o + 1) == 0x42) ? K_OUT : K_PAYLOAD;
+			break;
+		case K_VLAN:  // VlanLayer::parseNextLayer, VlanLayer.cpp:59-119
+		{
+			proto = P_VLAN; osi = 2; hdr = 4;
+			if (len <= 4) break;
+			po = o + 4; pl = len - 4;
+			uint32_t et = be16(p, o + 2);
+			if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
+			else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+			else if (et == 0x8100 || et == 0x88A8) nk = K_VLAN;
+			else if (et == 0x8847) nk = K_MPLS;
+			else if (et == 0x0806 || et == 0x8864 || et == 0x8863) nk = K_OUT;
+			else if (et < 1500) nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
+			else nk = K_PAYLOAD;
+			break;
+		}
+		case K_MPLS:  // MplsLayer::parseNextLayer, MplsLayer.cpp:101-128
+		{
+			proto = P_MPLS; osi = 3; hdr = 4;
+			if (len < 5) break;
+			po = o + 4; pl = len - 4;
+			if (!(rb(p, o + 2) & 1)) { nk = K_MPLS; break; }
+			uint32_t nib = rb(p, o + 4) >> 4;
+			nk = nib == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+			              : (nib == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+			break;
+		}
+		case K_IPV4:  // IPv4Layer.cpp:180-197 (dataLen), :245-370 (next layer)
+		{
+			proto = P_IPV4; osi = 3;
+			uint32_t b0 = rb(p, o);
+			hdr = (b0 & 0xF) * 4;
+			uint32_t tl = be16(p, o + 2);
+			if (tl < len && tl != 0)
+			{
+				uint32_t hmin = hdr < len ? hdr : len;
+				dlen = tl > hmin ? tl : hmin;
+			}
+			if (dlen <= hdr) break;
+			po = o + hdr; pl = dlen - hdr;
+			uint32_t b6 = rb(p, o + 6), b7 = rb(p, o + 7);
+			if ((b6 & 0x20) || (((b6 & 0x1F) << 8) | b7) != 0) { nk = K_PAYLOAD; break; }
+			uint32_t ipp = rb(p, o + 9);
+			if (ipp == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
+			else if (ipp == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
+			else if (ipp == 4)
+			{
+				uint32_t ver = rb(p, po) >> 4;
+				nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+				              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+			}
+			else if (ipp == 47)
+			{
+				uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
+				nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
+			}
+			else if (ipp == 41) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+			else if (ipp == 1 || ipp == 2 || ipp == 51 || ipp == 50 || ipp == 112) nk = K_OUT;
+			else nk = K_PAYLOAD;
+			break;
+		}
+		case K_IPV6:  // IPv6Layer.cpp:28-40 (extensions + dataLen), :194-312 (next layer)
+		{
+			proto = P_IPV6; osi = 3;
+			uint32_t nh = rb(p, o + 6);
+			uint32_t eo = 40, ext = 0, last_ext = 0xFFFF;
+			while (eo <= len - 2)
+			{
+				uint32_t el;
+				if (nh == 44 || nh == 0 || nh == 60 || nh == 43) el = 8u * (rb(p, o + eo + 1) + 1);
+				else if (nh == 51) el = 4u * (rb(p, o + eo + 1) + 2);
+				else break;
+				last_ext = nh;
+				nh = rb(p, o + eo);
+				eo += el;
+				ext += el;
+			}
+			hdr = 40 + ext;
+			uint32_t total = be16(p, o + 4) + hdr;
+			if (total < len) dlen = total;
+			if (dlen <= hdr) break;
+			po = o + hdr; pl = dlen - hdr;
+			if (last_ext == 44) { nk = K_PAYLOAD; break; }
+			if (nh == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
+			else if (nh == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
+			else if (nh == 4)
+			{
+				uint32_t ver = rb(p, po) >> 4;
+				nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+				              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+			}
+			else if (nh == 47)
+			{
+				uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
+				nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
+			}
+			else if (nh == 51 || nh == 50 || nh == 58 || nh == 112) nk = K_OUT;
+			else nk = K_PAYLOAD;
+			break;
+		}
+		case K_GRE0:
+		case K_GRE1:  // GreLayer.cpp:195-252
+		{
+			proto = k == K_GRE0 ? P_GREV0 : P_GREV1; osi = 3;
+			uint32_t f0 = rb(p, o), f1 = rb(p, o + 1);
+			hdr = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
+			if (len <= hdr) break;
+			po = o + hdr; pl = len - hdr;
+			uint32_t et = be16(p, o + 2);
+			if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
+			else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+			else if (et == 0x8100) nk = K_VLAN;
+			else if (et == 0x8847) nk = K_MPLS;
+			else if (et == 0x880B) nk = pl >= 4 ? K_PPTP : K_PAYLOAD;
+			else if (et == 0x6558) nk = eth_ok(p, po, pl) ? K_ETH : (dot3_ok(p, po, pl) ? K_DOT3 : K_PAYLOAD);
+			else nk = K_PAYLOAD;
+			break;
+		}
+		case K_PPTP:  // PPP_PPTPLayer::parseNextLayer, GreLayer.cpp:547-566
+		{
+			proto = P_PPTP; osi = 5; hdr = 4;
+			if (len <= 4) break;
+			po = o + 4; pl = len - 4;
+			uint32_t pp = be16(p, o + 2);
+			nk = pp == 0x21 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+			                : (pp == 0x57 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+			break;
+		}
+		case K_TCP:  // TcpLayer.cpp:360-492
+			proto = P_TCP; osi = 4; hdr = (rb(p, o + 12) >> 4) * 4;
+			if (len <= hdr) break;
+			po = o + hdr; pl = len - hdr;
+			nk = (tcp_l7(be16(p, o)) || tcp_l7(be16(p, o + 2))) ? K_L7 : K_PAYLOAD;
+			break;
+		case K_UDP:  // UdpLayer.cpp:92-184
+		{
+			proto = P_UDP; osi = 4; hdr = 8;
+			if (len <= 8) break;
+			po = o + 8; pl = len - 8;
+			bool l7 = udp_l7(be16(p, o), be16(p, o + 2));
+			if (!l7 && pl >= 4)
+				l7 = sip_key((rb(p, po) << 24) | (rb(p, po + 1) << 16) | (rb(p, po + 2) << 8) | rb(p, po + 3));
+			nk = l7 ? K_L7 : K_PAYLOAD;
+			break;
+		}
+		default:  // K_PAYLOAD: PayloadLayer.h:61-81
+			proto = P_PAYLOAD; osi = 7; hdr = len;
+			break;
+		}
+
+		// stop rules (inclusive, then roll back one layer; the first layer is never rolled back)
+		bool member = prm.family != 0 &&
+		              (proto == (prm.family & 0xFF) || (proto << 8) == (prm.family & 0xFF00) ||
+		               (proto << 16) == (prm.family & 0xFF0000) || (proto << 24) == (prm.family & 0xFF000000u));
+		bool fail = osi > prm.until_osi;
+		if (!fail)
+		{
+			if (member) found = 1;
+			if (found && !member) fail = true;
+		}
+		if (fail)
+		{
+			stopped = 1;
+			if (count > 0) break;
+			nk = K_NONE;
+		}
+		if (lay_out && count < ml)
+			lay_out[count] = make_uint2(proto | (osi << 8) | (o << 16), (hdr & 0xFFFF) | (dlen << 16));
+		mask |= 1ull << proto;
+		if (proto == P_IPV4 && v4 < 0) { v4 = (int32_t)o; v4_dlen = dlen; }
+		if (proto == P_IPV6 && v6 < 0) v6 = (int32_t)o;
+		if (proto == P_TCP) { tcp_i = (int32_t)count; tcp_off = o; tcp_dlen = dlen; tcp_pp = prev_proto; tcp_po = prev_off; }
+		if (proto == P_UDP) { udp_i = (int32_t)count; udp_off = o; udp_dlen = dlen; udp_pp = prev_proto; udp_po = prev_off; }
+		prev_proto = proto;
+		prev_off = o;
+		last_end = o + dlen;
+		++count;
+		k = nk; o = po; len = pl;
+	}
+
+	// ---- trailer (Packet.cpp:178-195) ----
+	if (count > 0 && prm.family == 0 && prm.until_osi == 8 && !stopped &&
+	    !(flags & (PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_NEEDS_HOST_PROTO)) && last_end < cap)
+	{
+		uint32_t tl = cap - last_end;
+		if (lay_out && count < ml)
+			lay_out[count] = make_uint2(P_TRAILER | (2u << 8) | (last_end << 16), (tl & 0xFFFF) | (tl << 16));
+		mask |= 1ull << P_TRAILER;
+		++count;
+		flags |= PCPPX_F_TRAILER;
+	}
+	if (count > cap_layers) flags |= PCPPX_F_DEPTH_OVERFLOW;
+	const uint32_t n_layers = count > cap_layers ? cap_layers : count;
+
+	// ---- hash5Tuple / hash2Tuple (PacketUtils.cpp:139-245) ----
+	const bool is_tcp = tcp_i >= 0;
+	const int32_t l4i = is_tcp ? tcp_i : udp_i;
+	const uint32_t l4o = is_tcp ? tcp_off : udp_off;
+	const uint32_t l4dlen = is_tcp ? tcp_dlen : udp_dlen;
+	uint32_t h5 = 0, h5d = 0, h2 = 0;
+	const bool have_ip = v4 >= 0 || v6 >= 0;
+	const uint32_t ipo = v4 >= 0 ? (uint32_t)v4 : (uint32_t)v6;
+	const uint32_t alen = v4 >= 0 ? 4 : 16;
+	const uint32_t src_o = ipo + (v4 >= 0 ? 12 : 8), dst_o = ipo + (v4 >= 0 ? 16 : 24);
+	if (have_ip)
+	{
+		// address order: dst < src compared as host LE u32 (IPv4) or memcmp (IPv6)
+		int cmp = 0;
+		if (v4 >= 0)
+		{
+			uint32_t s = le32(p, src_o), d = le32(p, dst_o);
+			cmp = d < s ? -1 : (d > s ? 1 : 0);
+		}
+		else
+		{
+			for (uint32_t j = 0; j < 16 && cmp == 0; ++j)
+			{
+				uint32_t a = rb(p, dst_o + j), b = rb(p, src_o + j);
+				cmp = a < b ? -1 : (a > b ? 1 : 0);
+			}
+		}
+		const uint32_t a_o = cmp < 0 ? dst_o : src_o, b_o = cmp < 0 ? src_o : dst_o;
+		uint32_t h = 2166136261u;
+		for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, a_o + j));
+		for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, b_o + j));
+		h2 = h;
+		if (l4i >= 0)
+		{
+			const uint32_t sp = le16(p, l4o), dp = le16(p, l4o + 2);
+			const uint32_t ipproto = rb(p, ipo + (v4 >= 0 ? 9 : 6));
+			for (int dir = 0; dir < 2; ++dir)
+			{
+				bool swap = !dir && (dp < sp || (dp == sp && cmp < 0));
+				uint32_t x = fnv(fnv(2166136261u, swap ? (dp & 0xFF) : (sp & 0xFF)), swap ? (dp >> 8) : (sp >> 8));
+				x = fnv(fnv(x, swap ? (sp & 0xFF) : (dp & 0xFF)), swap ? (sp >> 8) : (dp >> 8));
+				const uint32_t f_o = swap ? dst_o : src_o, s_o = swap ? src_o : dst_o;
+				for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, f_o + j));
+				for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, s_o + j));
+				x = fnv(x, ipproto);
+				if (dir) h5d = x; else h5 = x;
+			}
+		}
+	}
+
+	// ---- checksums ----
+	uint32_t ipc = 0, ips = 0, l4c = 0, l4s = 0;
+	if (prm.want_csum)
+	{
+		if (v4 >= 0)  // IPv4Layer.cpp:410-412: computeChecksum(header with field zeroed, min(IHL*4, dataLen))
+		{
+			uint32_t hl = (rb(p, (uint32_t)v4) & 0xF) * 4;
+			if (hl > v4_dlen) hl = v4_dlen;
+			uint32_t r = range_residue(p, (uint32_t)v4, (uint32_t)v4 + hl);
+			ips = be16(p, (uint32_t)v4 + 10);
+			uint32_t fw = le16(p, (uint32_t)v4 + 10);  // field at even offset 10 of the stream
+			r = (r + 65535u - mod65535(fw)) % 65535u;
+			ipc = finish_checksum(r);
+			flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+		}
+		if (l4i >= 0)  // TcpLayer.cpp:271-311, UdpLayer.cpp:47-90, computePseudoHdrChecksum PacketUtils.cpp:66-112
+		{
+			const uint32_t field = is_tcp ? 16 : 6;
+			const uint32_t pp = is_tcp ? tcp_pp : udp_pp, ppo = is_tcp ? tcp_po : udp_po;
+			uint32_t res = 0;
+			if (pp == P_IPV4 || pp == P_IPV6)
+			{
+				uint32_t r = range_residue(p, l4o, l4o + l4dlen);
+				r = (r + 65535u - mod65535(le16(p, l4o + field))) % 65535u;
+				uint32_t ph = 0;
+				const uint32_t as = pp == P_IPV4 ? ppo + 12 : ppo + 8;
+				const uint32_t nw = pp == P_IPV4 ? 4 : 16;  // 16-bit words of src+dst
+				for (uint32_t j = 0; j < nw; ++j) ph += le16(p, as + 2 * j);
+				ph += ((l4dlen & 0xFF) << 8) | ((l4dlen >> 8) & 0xFF);  // htobe16(dataLen)
+				ph += (is_tcp ? 6u : 17u) << 8;                          // htobe16(protocol)
+				r = (r + mod65535(ph)) % 65535u;
+				res = finish_checksum(r);
+			}
+			if (!is_tcp && res == 0) res = 0xFFFF;
+			l4c = res;
+			l4s = be16(p, l4o + field);
+			flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
+		}
+	}
+
+	s0 = make_uint4(h5, h5d, h2, flags | (n_layers << 16) | ((l4i >= 0 ? (uint32_t)l4i : 0xFFu) << 24));
+	s1 = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), ipc | (ips << 16), l4c | (l4s << 16));
+	reinterpret_cast<uint4*>(sum_out)[0] = s0;
+	reinterpret_cast<uint4*>(sum_out)[1] = s1;
+}
+
+// ---- per-flow counters keyed by hash5Tuple (FilterTraffic's flow table, AppWorkerThread.h:99-125) ----
+__global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
+                                                            const uint32_t* __restrict__ caplens, uint32_t n,
+                                                            uint32_t* keys, unsigned long long* packets,
+                                                            unsigned long long* bytes, uint32_t capacity,
+                                                            unsigned long long* stats)
+{
+	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+	if (i >= n)
+		return;
+	const uint32_t key = sum[i].hash5;
+	const unsigned long long len = caplens[i];
+	if (key == 0)
+	{
+		atomicAdd(&stats[0], 1ull);
+		atomicAdd(&stats[1], len);
+		return;
+	}
+	const uint32_t m = capacity - 1;
+	uint32_t slot = (key * 0x9E3779B1u) & m;
+	for (uint32_t probe = 0; probe < capacity; ++probe)
+	{
+		uint32_t prev = atomicCAS(&keys[slot], 0u, key);
+		if (prev == 0u || prev == key)
+		{
+			atomicAdd(&packets[slot], 1ull);
+			atomicAdd(&bytes[slot], len);
+			return;
+		}
+		slot = (slot + 1) & m;
+	}
+	atomicAdd(&stats[2], 1ull);
+}
+
+}  // namespace
+
+int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream)
+{
+	if (b->n == 0)
+		return PCPPX_OK;
+	Params prm;
+	prm.data = b->data;
+	prm.offsets = b->offsets;
+	prm.caplens = b->caplens;
+	prm.data_len = b->data_len;
+	prm.summary = r->summary;
+	prm.layers = o->max_layers ? r->layers : nullptr;
+	prm.n = b->n;
+	prm.family = o->parse_until_family;
+	prm.until_osi = o->parse_until_osi;
+	prm.want_csum = o->want_checksums;
+	prm.max_layers = o->max_layers;
+	prm.linktype = b->linktype;
+	dim3 grid((b->n + kBlock - 1) / kBlock);
+	hipLaunchKernelGGL(parse_kernel, grid, dim3(kBlock), 0, stream, prm);
+	return hipGetLastError() == hipSuccess ? PCPPX_OK : PCPPX_E_HIP;
+}
+
+int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
+                      uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, hipStream_t stream)
+{
+	if (n == 0)
+		return PCPPX_OK;
+	dim3 grid((n + kBlock - 1) / kBlock);
+	hipLaunchKernelGGL(flow_count_kernel, grid, dim3(kBlock), 0, stream, sum, caplens, n, keys,
+	                   reinterpret_cast<unsigned long long*>(packets), reinterpret_cast<unsigned long long*>(bytes),
+	                   capacity, reinterpret_cast<unsigned long long*>(stats));
+	return hipGetLastError() == hipSuccess ? PCPPX_OK : PCPPX_E_HIP;
+}
+
+}  // namespace pcppx

@@ -1,0 +1,109 @@
+"""Engine handle: one pcppx context (one GPU, one host thread) over the C ABI of include/pcppx.h.
+
+Host batches (numpy) go through pcppx_parse_batch_host (pinned, double-buffered H2D -> kernel -> D2H);
+device batches (torch tensors resident in HBM) through pcppx_parse_batch_device on a HIP stream.
+There is no CPU fallback: a missing libpcppx.so or a missing GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .pcap import PacketBatch
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        self.lib = abi.load_engine()
+        self.ctx = C.c_void_p()
+        abi.check(self.lib.pcppx_open(device, C.byref(self.ctx)), "pcppx_open")
+        self.device = device
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.pcppx_close(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- host-resident batches ----
+    def parse_host(self, batch: PacketBatch, opts: abi.Opts | None = None):
+        """Parse a host batch; returns (summary[n], layers[n, max_layers]) numpy record arrays."""
+        opts = opts or abi.make_opts()
+        summary = np.zeros(batch.n, dtype=abi.SUMMARY_DTYPE)
+        layers = np.zeros(max(batch.n * opts.max_layers, 1), dtype=abi.LAYER_DTYPE)
+        rec = abi.Records(summary.ctypes.data, layers.ctypes.data if opts.max_layers else None)
+        b = batch.c_batch()
+        abi.check(self.lib.pcppx_parse_batch_host(self.ctx, C.byref(b), C.byref(opts), C.byref(rec)),
+                  "pcppx_parse_batch_host")
+        return summary, layers[: batch.n * opts.max_layers].reshape(batch.n, opts.max_layers)
+
+    # ---- device-resident batches (torch tensors on this GPU) ----
+    def parse_device(self, data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers=None,
+                     stream: int | None = None) -> None:
+        """Queue a parse of device tensors on `stream` (a hipStream_t handle, e.g.
+        torch.cuda.current_stream().cuda_stream). summary: uint8 tensor of n*32 bytes; layers: n*max_layers*8."""
+        b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
+        rec = abi.Records(abi.ptr(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None)
+        abi.check(self.lib.pcppx_parse_batch_device(self.ctx, C.byref(b), C.byref(opts), C.byref(rec),
+                                                    C.c_void_p(stream or 0)), "pcppx_parse_batch_device")
+
+    def flow_count_device(self, summary, caplens, n: int, keys, packets, bytes_, capacity: int, stats,
+                          stream: int | None = None) -> None:
+        abi.check(self.lib.pcppx_flow_count_device(self.ctx, abi.ptr(summary), abi.ptr(caplens), n, abi.ptr(keys),
+                                                   abi.ptr(packets), abi.ptr(bytes_), capacity, abi.ptr(stats),
+                                                   C.c_void_p(stream or 0)), "pcppx_flow_count_device")
+
+    def sync(self) -> None:
+        abi.check(self.lib.pcppx_sync(self.ctx), "pcppx_sync")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    abi.check(abi.load_engine().pcppx_device_count(C.byref(n)), "pcppx_device_count")
+    return n.value
+
+
+def to_device(batch: PacketBatch, device: str = "cuda:0"):
+    """Copy a host batch into HBM as torch tensors: (data u8, offsets i64-as-u64, caplens i32-as-u32)."""
+    import torch
+
+    data = torch.from_numpy(batch.data).to(device)
+    offsets = torch.from_numpy(batch.offsets.view(np.int64)).to(device)
+    caplens = torch.from_numpy(batch.caplens.view(np.int32)).to(device)
+    return data, offsets, caplens
+
+
+def records_from_device(summary_t, layers_t, n: int, max_layers: int):
+    s = summary_t.cpu().numpy().view(abi.SUMMARY_DTYPE)[:n]
+    if layers_t is None or max_layers == 0:
+        return s, np.zeros((n, 0), dtype=abi.LAYER_DTYPE)
+    lay = layers_t.cpu().numpy().view(abi.LAYER_DTYPE)[: n * max_layers].reshape(n, max_layers)
+    return s, lay
+
+
+def parse_on_device(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = None, device: str = "cuda:0"):
+    """Copy a host batch to HBM, run the device-resident parse, copy the records back."""
+    import torch
+
+    opts = opts or abi.make_opts()
+    data, offsets, caplens = to_device(batch, device)
+    n = batch.n
+    summary = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device=device)
+    layers = torch.zeros(max(n * opts.max_layers, 1) * 8, dtype=torch.uint8, device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, stream)
+    torch.cuda.synchronize(device)
+    return records_from_device(summary, layers, n, opts.max_layers)

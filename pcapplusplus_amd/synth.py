@@ -1,0 +1,295 @@
+"""Seeded synthetic packet batches for BASELINE.json's configs.
+
+Packets are generated per header template as 2-D arrays (vectorised numpy), with valid IPv4 and L4
+checksums, ports drawn outside the reference's L7 trigger sets (so Packet++ yields GenericPayload,
+TcpLayer.cpp:372-491 / UdpLayer.cpp:103-178), then laid back to back in a random interleaving order.
+
+  config 1: 10k Eth/IPv4/UDP, caplen uniform 64..1500, seed 1
+  config 2: 1M x 64 B Eth/IPv4/{TCP,UDP} 50/50, seed 2
+  config 3: 10M IMIX 64/512/1500 B at 7:4:1, 25% single VLAN, 70% IPv4 / 30% IPv6 (64 B: IPv6/UDP
+            without VLAN only), TCP/UDP 50/50, 1% corrupted checksums, seed 3
+  config 4: IMIX as config 3 with 5-tuples drawn Zipf(1.1) over a flow table, both directions, seed 4
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import abi
+from .pcap import PacketBatch
+
+# ports the reference routes to L7 dissectors (engine contract, oracle tcp_l7_port/udp_l7_port)
+TRIGGER_PORTS = np.array(sorted({
+    443, 261, 448, 465, 563, 614, 636, 989, 990, 992, 993, 994, 995, 80, 8080, 5060, 5061, 179, 22, 53,
+    5353, 5355, 23, 21, 20, 13400, 3496, 30490, 102, 25, 587, 389, 5432, 3306, 2123, 502, 67, 68, 4789, 0,
+    7, 9, 1812, 1813, 3799, 2152, 546, 547, 123, 51820}), dtype=np.int64)
+SIP_KEYS = [b"INVI", b"ACK ", b"BYE ", b"CANC", b"REGI", b"PRAC", b"OPTI", b"SUBS", b"NOTI", b"PUBL",
+            b"INFO", b"REFE", b"MESS", b"UPDA", b"SIP/"]
+
+IMIX_SIZES = (64, 512, 1500)
+IMIX_WEIGHTS = (7, 4, 1)
+
+
+def safe_ports(rng: np.random.Generator, n: int) -> np.ndarray:
+    p = rng.integers(1024, 65536, size=n, dtype=np.int64)
+    bad = np.isin(p, TRIGGER_PORTS)
+    while bad.any():
+        p[bad] = rng.integers(1024, 65536, size=int(bad.sum()), dtype=np.int64)
+        bad = np.isin(p, TRIGGER_PORTS)
+    return p.astype(np.uint16)
+
+
+def _be16(a: np.ndarray) -> np.ndarray:
+    a = a.astype(np.uint32)
+    return np.stack([(a >> 8) & 0xFF, a & 0xFF], axis=1).astype(np.uint8)
+
+
+def _le_word_sum(rows: np.ndarray) -> np.ndarray:
+    """Sum of little-endian 16-bit words of each row (odd length zero-padded), as uint64."""
+    n, w = rows.shape
+    if w % 2:
+        rows = np.concatenate([rows, np.zeros((n, 1), np.uint8)], axis=1)
+    return rows.view("<u2").sum(axis=1, dtype=np.uint64)
+
+
+def _fold_checksum(s: np.ndarray) -> np.ndarray:
+    """computeChecksum's fold + invert, as the 16-bit value stored big-endian in the header."""
+    s = s.astype(np.uint64)
+    while (s >> 16).any():
+        s = (s & 0xFFFF) + (s >> 16)
+    res = (~s) & 0xFFFF  # little-endian word sum, inverted: written back as LE bytes
+    return res.astype(np.uint16)
+
+
+def build_rows(rng: np.random.Generator, n: int, size: int, vlan: bool, ipv6: bool, tcp: bool,
+               tuples: dict | None = None) -> np.ndarray:
+    """n packets of `size` bytes: Eth [VLAN] IPv4|IPv6 TCP|UDP + random payload, valid checksums."""
+    l2 = 18 if vlan else 14
+    l3 = 40 if ipv6 else 20
+    l4 = 20 if tcp else 8
+    hlen = l2 + l3 + l4
+    if hlen > size:
+        raise ValueError("headers do not fit")
+    rows = np.frombuffer(rng.bytes(n * size), dtype=np.uint8).reshape(n, size).copy()
+    # Ethernet (EthLayer.h ether_header): dst, src, ethertype
+    et = 0x86DD if ipv6 else 0x0800
+    if vlan:
+        rows[:, 12:14] = _be16(np.full(n, 0x8100))
+        tci = rng.integers(1, 4095, size=n)
+        rows[:, 14:16] = _be16(tci)
+        rows[:, 16:18] = _be16(np.full(n, et))
+    else:
+        rows[:, 12:14] = _be16(np.full(n, et))
+    rows[:, 0] &= 0xFE  # unicast dst
+    ip = l2
+    l4o = l2 + l3
+    l4len = size - l4o
+    if tuples is not None:
+        src_ip, dst_ip, sport, dport = tuples["src"], tuples["dst"], tuples["sport"], tuples["dport"]
+    else:
+        src_ip = dst_ip = None
+        sport, dport = safe_ports(rng, n), safe_ports(rng, n)
+    proto = 6 if tcp else 17
+    if ipv6:
+        rows[:, ip] = 0x60 | (rows[:, ip] & 0x0F)
+        rows[:, ip + 4:ip + 6] = _be16(np.full(n, l4len))
+        rows[:, ip + 6] = proto
+        rows[:, ip + 7] = 64
+        if src_ip is not None:
+            rows[:, ip + 8:ip + 24] = src_ip
+            rows[:, ip + 24:ip + 40] = dst_ip
+    else:
+        rows[:, ip] = 0x45
+        rows[:, ip + 1] = 0
+        rows[:, ip + 2:ip + 4] = _be16(np.full(n, size - l2))
+        rows[:, ip + 6] = 0x40  # DF, offset 0
+        rows[:, ip + 7] = 0
+        rows[:, ip + 8] = 64
+        rows[:, ip + 9] = proto
+        rows[:, ip + 10:ip + 12] = 0
+        if src_ip is not None:
+            rows[:, ip + 12:ip + 16] = src_ip
+            rows[:, ip + 16:ip + 20] = dst_ip
+        c = _fold_checksum(_le_word_sum(rows[:, ip:ip + 20]))
+        rows[:, ip + 10] = (c & 0xFF).astype(np.uint8)
+        rows[:, ip + 11] = (c >> 8).astype(np.uint8)
+    rows[:, l4o:l4o + 2] = _be16(sport)
+    rows[:, l4o + 2:l4o + 4] = _be16(dport)
+    if tcp:
+        rows[:, l4o + 12] = 0x50
+        rows[:, l4o + 13] = 0x18
+        rows[:, l4o + 16:l4o + 18] = 0
+        rows[:, l4o + 18:l4o + 20] = 0
+        cs = l4o + 16
+    else:
+        rows[:, l4o + 4:l4o + 6] = _be16(np.full(n, l4len))
+        rows[:, l4o + 6:l4o + 8] = 0
+        cs = l4o + 6
+        # keep the UDP payload clear of the SIP content heuristic (SipLayer.cpp:127-160)
+        if size - l4o - 8 >= 4:
+            head = rows[:, l4o + 8:l4o + 12].copy().view(">u4").ravel()
+            keys = np.array([int.from_bytes(k, "big") for k in SIP_KEYS], dtype=np.uint32)
+            hit = np.isin(head, keys)
+            rows[hit, l4o + 8] ^= 0x80
+    # pseudo header (computePseudoHdrChecksum, PacketUtils.cpp:66-112)
+    s = _le_word_sum(rows[:, l4o:])
+    addr_lo, addr_hi = (ip + 8, ip + 40) if ipv6 else (ip + 12, ip + 20)
+    s += _le_word_sum(rows[:, addr_lo:addr_hi])
+    s += np.uint64(((l4len & 0xFF) << 8) | (l4len >> 8))
+    s += np.uint64(proto << 8)
+    c = _fold_checksum(s)
+    if not tcp:
+        c = np.where(c == 0, np.uint16(0xFFFF), c)
+    rows[:, cs] = (c & 0xFF).astype(np.uint8)
+    rows[:, cs + 1] = (c >> 8).astype(np.uint8)
+    return rows
+
+
+def _interleave(groups: list[tuple[np.ndarray, np.ndarray]], n: int, order_rng: np.random.Generator,
+                chunk_bytes: int = 1 << 26) -> PacketBatch:
+    """groups: (rows[n_g, size_g], packet indices[n_g]) -> back-to-back batch in index order."""
+    caps = np.zeros(n, dtype=np.uint32)
+    for rows, idx in groups:
+        caps[idx] = rows.shape[1]
+    offs = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        np.cumsum(caps[:-1], dtype=np.uint64, out=offs[1:])
+    total = int(offs[-1]) + int(caps[-1]) if n else 0
+    data = np.empty(total + 64, dtype=np.uint8)
+    data[total:] = 0
+    for rows, idx in groups:
+        size = rows.shape[1]
+        step = max(1, chunk_bytes // size)
+        col = np.arange(size, dtype=np.int64)
+        for a in range(0, len(idx), step):
+            d = offs[idx[a:a + step]].astype(np.int64)
+            data[(d[:, None] + col[None, :]).ravel()] = rows[a:a + step].ravel()
+    return PacketBatch(data, offs, caps, abi.LINKTYPE_ETHERNET)
+
+
+def _corrupt(batch: PacketBatch, rng: np.random.Generator, frac: float, info: dict) -> None:
+    """Flip checksum bytes of a fraction of packets (config 3's 1% corrupted checksums)."""
+    n = batch.n
+    k = int(n * frac)
+    if k == 0:
+        return
+    pick = rng.choice(n, size=k, replace=False)
+    half = pick[: k // 2]
+    rest = pick[k // 2:]
+    l4cs = info["l4_csum_off"]
+    ipcs = info["ip_csum_off"]
+    offs = batch.offsets.astype(np.int64)
+    batch.data[offs[half] + l4cs[half]] ^= 0x5A
+    v4 = rest[ipcs[rest] > 0]
+    batch.data[offs[v4] + ipcs[v4]] ^= 0xA5
+    batch.meta["corrupted"] = int(len(half) + len(v4))
+
+
+def imix(n: int, seed: int, vlan_frac: float = 0.25, v6_frac: float = 0.30, corrupt_frac: float = 0.01,
+         sizes=IMIX_SIZES, weights=IMIX_WEIGHTS, flows: int | None = None) -> PacketBatch:
+    """Config 3 (flows=None) / config 4 (flows=N: 5-tuples Zipf(1.1) over N flows, both directions)."""
+    rng = np.random.default_rng(seed)
+    w = np.array(weights, dtype=np.float64)
+    size_of = np.array(sizes)[rng.choice(len(sizes), size=n, p=w / w.sum())]
+    vlan = rng.random(n) < vlan_frac
+    v6 = rng.random(n) < v6_frac
+    tcp = rng.random(n) < 0.5
+    small = size_of < 14 + 4 + 40 + 20 + 2
+    # 64 B: IPv6 only as IPv6/UDP without VLAN (14+40+8 = 62 fits; 66/82 do not)
+    tcp = np.where(small & v6, False, tcp)
+    vlan = np.where(small & v6, False, vlan)
+    flow_id = dirn = None
+    if flows:
+        ranks = np.arange(1, flows + 1, dtype=np.float64)
+        pz = ranks ** -1.1
+        pz /= pz.sum()
+        flow_id = rng.choice(flows, size=n, p=pz)
+        dirn = rng.random(n) < 0.5
+        frng = np.random.default_rng(seed + 1000)
+        f_v6 = frng.random(flows) < v6_frac
+        f_tcp = frng.random(flows) < 0.5
+        f_src4 = frng.integers(0, 256, size=(flows, 4), dtype=np.uint8)
+        f_dst4 = frng.integers(0, 256, size=(flows, 4), dtype=np.uint8)
+        f_src6 = frng.integers(0, 256, size=(flows, 16), dtype=np.uint8)
+        f_dst6 = frng.integers(0, 256, size=(flows, 16), dtype=np.uint8)
+        f_sp, f_dp = safe_ports(frng, flows), safe_ports(frng, flows)
+        v6 = f_v6[flow_id]
+        tcp = f_tcp[flow_id]
+        tcp = np.where(small & v6, False, tcp)
+        vlan = np.where(small & v6, False, vlan)
+    groups = []
+    info_l4 = np.zeros(n, dtype=np.int64)
+    info_ip = np.zeros(n, dtype=np.int64)
+    for s in sizes:
+        for vl in (False, True):
+            for ip6 in (False, True):
+                for t in (False, True):
+                    idx = np.nonzero((size_of == s) & (vlan == vl) & (v6 == ip6) & (tcp == t))[0]
+                    if len(idx) == 0:
+                        continue
+                    tuples = None
+                    if flows:
+                        fid = flow_id[idx]
+                        fwd = ~dirn[idx]
+                        if ip6:
+                            a, b = f_src6[fid], f_dst6[fid]
+                        else:
+                            a, b = f_src4[fid], f_dst4[fid]
+                        src = np.where(fwd[:, None], a, b)
+                        dst = np.where(fwd[:, None], b, a)
+                        sp = np.where(fwd, f_sp[fid], f_dp[fid]).astype(np.uint16)
+                        dp = np.where(fwd, f_dp[fid], f_sp[fid]).astype(np.uint16)
+                        tuples = {"src": src, "dst": dst, "sport": sp, "dport": dp}
+                    grng = np.random.default_rng([seed, s, int(vl), int(ip6), int(t)])
+                    rows = build_rows(grng, len(idx), s, vl, ip6, t, tuples)
+                    groups.append((rows, idx))
+                    l2 = 18 if vl else 14
+                    l4o = l2 + (40 if ip6 else 20)
+                    info_l4[idx] = l4o + (16 if t else 6)
+                    info_ip[idx] = 0 if ip6 else l2 + 10
+    batch = _interleave(groups, n, rng)
+    del groups
+    if corrupt_frac:
+        _corrupt(batch, rng, corrupt_frac, {"l4_csum_off": info_l4, "ip_csum_off": info_ip})
+    batch.meta.update(config="imix", seed=seed, flows=flows)
+    if flows:
+        batch.meta["flow_id"] = flow_id
+    return batch
+
+
+def small64(n: int, seed: int = 2) -> PacketBatch:
+    """Config 2: n x 64 B Eth/IPv4/{TCP,UDP} 50/50, valid checksums."""
+    rng = np.random.default_rng(seed)
+    tcp = rng.random(n) < 0.5
+    groups = []
+    for t in (False, True):
+        idx = np.nonzero(tcp == t)[0]
+        if len(idx):
+            groups.append((build_rows(np.random.default_rng([seed, int(t)]), len(idx), 64, False, False, t), idx))
+    b = _interleave(groups, n, rng)
+    b.meta.update(config="64B", seed=seed)
+    return b
+
+
+def udp_uniform(n: int, seed: int = 1, lo: int = 64, hi: int = 1500) -> PacketBatch:
+    """Config 1: Eth/IPv4/UDP with caplen uniform in [lo, hi]."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(lo, hi + 1, size=n)
+    groups = []
+    for s in np.unique(sizes):
+        idx = np.nonzero(sizes == s)[0]
+        groups.append((build_rows(np.random.default_rng([seed, int(s)]), len(idx), int(s), False, False, False), idx))
+    b = _interleave(groups, n, rng)
+    b.meta.update(config="udp-uniform", seed=seed)
+    return b
+
+
+def config(cfg: int, n: int | None = None) -> PacketBatch:
+    if cfg == 1:
+        return udp_uniform(n or 10_000, 1)
+    if cfg == 2:
+        return small64(n or 1_000_000, 2)
+    if cfg == 3:
+        return imix(n or 10_000_000, 3)
+    if cfg == 4:
+        return imix(n or 12_500_000, 4, flows=1_000_000, corrupt_frac=0.0)
+    raise ValueError(f"unknown config {cfg}")

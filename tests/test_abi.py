@@ -1,0 +1,81 @@
+"""The C-ABI library loads (no GPU needed) and exports every function include/pcppx.h declares;
+record layouts of the header match the Python/numpy mirror."""
+from __future__ import annotations
+
+import ctypes as C
+import re
+import subprocess
+import tempfile
+from pathlib import Path
+
+import pytest
+
+from pcapplusplus_amd import abi
+
+HEADER = abi.REPO_DIR / "include" / "pcppx.h"
+
+
+def declared_functions() -> list[str]:
+    txt = HEADER.read_text()
+    return sorted(set(re.findall(r"^(?:int|void|const char\*)\s+(pcppx_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_expected_api():
+    assert declared_functions() == sorted(abi.EXPORTED_SYMBOLS)
+
+
+def test_engine_library_exports_every_symbol():
+    if not abi.ENGINE_SO.exists():
+        pytest.fail("libpcppx.so not built (run __graft_entry__.build())")
+    lib = C.CDLL(str(abi.ENGINE_SO))
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    lib.pcppx_abi_version.restype = C.c_int
+    assert lib.pcppx_abi_version() == abi.ABI_VERSION
+
+
+def test_engine_rejects_bad_arguments_without_gpu():
+    lib = abi.load_engine()
+    assert lib.pcppx_parse_batch_device(None, None, None, None, None) == abi.E_INVAL
+    assert lib.pcppx_parse_batch_host(None, None, None, None) == abi.E_INVAL
+    o = abi.Opts()
+    lib.pcppx_default_opts(C.byref(o))
+    assert (o.parse_until_family, o.parse_until_osi, o.want_checksums, o.max_layers) == (0, 8, 1, 16)
+    assert lib.pcppx_strerror(abi.E_INVAL) == b"invalid argument"
+
+
+def test_struct_layout_matches_header():
+    src = r"""
+    #include <stdio.h>
+    #include <stddef.h>
+    #include "pcppx.h"
+    #define F(T, f) printf(#T "." #f " %zu %zu\n", offsetof(T, f), sizeof(((T*)0)->f));
+    int main(void) {
+      printf("pcppx_summary %zu\npcppx_layer %zu\npcppx_batch %zu\npcppx_opts %zu\n", sizeof(pcppx_summary),
+             sizeof(pcppx_layer), sizeof(pcppx_batch), sizeof(pcppx_opts));
+      F(pcppx_summary, hash5) F(pcppx_summary, hash5_dir) F(pcppx_summary, hash2) F(pcppx_summary, flags)
+      F(pcppx_summary, n_layers) F(pcppx_summary, l4_layer) F(pcppx_summary, proto_mask)
+      F(pcppx_summary, ip_csum_calc) F(pcppx_summary, ip_csum_stored) F(pcppx_summary, l4_csum_calc)
+      F(pcppx_summary, l4_csum_stored)
+      F(pcppx_layer, proto) F(pcppx_layer, osi) F(pcppx_layer, offset) F(pcppx_layer, hdr_len) F(pcppx_layer, data_len)
+      return 0; }
+    """
+    with tempfile.TemporaryDirectory() as d:
+        c = Path(d) / "l.c"
+        c.write_text(src)
+        exe = Path(d) / "l"
+        subprocess.run(["gcc", "-I", str(HEADER.parent), str(c), "-o", str(exe)], check=True)
+        out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    sizes = dict(l.split() for l in out[:4])
+    assert int(sizes["pcppx_summary"]) == abi.SUMMARY_DTYPE.itemsize
+    assert int(sizes["pcppx_layer"]) == abi.LAYER_DTYPE.itemsize
+    assert int(sizes["pcppx_batch"]) == C.sizeof(abi.Batch)
+    assert int(sizes["pcppx_opts"]) == C.sizeof(abi.Opts)
+    for line in out[4:]:
+        if not line:
+            continue
+        name, off, size = line.split()
+        t, f = name.split(".")
+        dt = abi.SUMMARY_DTYPE if t == "pcppx_summary" else abi.LAYER_DTYPE
+        assert dt.fields[f][1] == int(off), name
+        assert dt.fields[f][0].itemsize == int(size), name

@@ -1,0 +1,142 @@
+"""HIP engine parity on an MI355X, through the C ABI (libpcppx.so).
+
+Bar: bit-exact. Every record field of the device path equals the C restatement (oracle/) on every
+packet, and equals the reference Packet++'s golden records under the engine contract (unflagged packets
+fully, flagged packets as an exact layer prefix). Full-size batches are checked through size-independent
+properties plus a sampled restatement comparison.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_files, load_golden
+from mutate import as_batch, crafted, mutate
+from pcapplusplus_amd import abi, synth
+from pcapplusplus_amd.engine import parse_on_device
+from pcapplusplus_amd.pcap import from_packets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.stem)
+def test_gpu_golden(engine, path):
+    batch, variants = load_golden(path)
+    for v, (opts, rsum, rlay) in variants.items():
+        gsum, glay = parse_on_device(engine, batch, opts)
+        osum, olay = oracle.oracle_parse(batch, opts)
+        oracle.compare_exact(gsum, glay, osum, olay)
+        oracle.compare_engine_to_reference(gsum, glay, rsum, rlay)
+
+
+@pytest.mark.parametrize("gaps", [False, True])
+def test_gpu_crafted_deep_stacks(engine, gaps):
+    b = as_batch(crafted(), gaps=gaps, seed=11)
+    for opts in (abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 3, True, 5),
+                 abi.make_opts(0, 8, True, 0), abi.make_opts(0, 8, False, 16)):
+        g = parse_on_device(engine, b, opts)
+        o = oracle.oracle_parse(b, opts)
+        oracle.compare_exact(g[0], g[1], o[0], o[1])
+        if oracle.ref_available():
+            r = oracle.ref_parse(b, opts)
+            oracle.compare_engine_to_reference(g[0], g[1], r[0], r[1])
+
+
+def test_gpu_mutations(engine):
+    seedb, _ = load_golden([p for p in golden_files() if p.stem == "pcap_lt1"][0])
+    pk = [seedb.packet(i) for i in range(seedb.n)]
+    b = as_batch(mutate(pk, 40000, 5), gaps=True, seed=5)
+    g = parse_on_device(engine, b)
+    o = oracle.oracle_parse(b, threads=8)
+    oracle.compare_exact(g[0], g[1], o[0], o[1])
+
+
+def test_gpu_edge_descriptors(engine):
+    pk = [b"", b"\x01", bytes(13), bytes(14), bytes(70000), bytes(60)]
+    b = from_packets(pk)
+    b.caplens[5] = 1 << 20  # beyond data_len
+    g = parse_on_device(engine, b)
+    o = oracle.oracle_parse(b)
+    oracle.compare_exact(g[0], g[1], o[0], o[1])
+    assert g[0]["flags"][4] == abi.F_OVERSIZE and g[0]["flags"][5] == abi.F_BAD_DESC
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 200_000), (3, 200_000), (4, 200_000)])
+def test_gpu_synthetic_configs(engine, cfg, n):
+    b = synth.config(cfg, n)
+    for opts in (abi.make_opts(), abi.make_opts(0, 8, False, 8)):
+        g = parse_on_device(engine, b, opts)
+        o = oracle.oracle_parse(b, opts, threads=8)
+        oracle.compare_exact(g[0], g[1], o[0], o[1])
+        assert not (g[0]["flags"] & abi.F_NEEDS_HOST).any()
+
+
+def test_gpu_host_path_matches_device_path(engine):
+    b = synth.config(3, 300_000)
+    opts = abi.make_opts(0, 8, True, 8)
+    h = engine.parse_host(b, opts)
+    d = parse_on_device(engine, b, opts)
+    oracle.compare_exact(h[0], h[1], d[0], d[1])
+
+
+def test_gpu_full_size_imix_properties(engine):
+    """Config 3 at its full 10M size: properties that hold independently of size, plus a sampled
+    bit-exact comparison against the restatement."""
+    n = 10_000_000
+    b = synth.config(3, n)
+    opts = abi.make_opts(0, 8, True, 8)
+    s, lay = parse_on_device(engine, b, opts)
+    fl = s["flags"]
+    assert not (fl & abi.F_NEEDS_HOST).any()
+    # every packet: Eth [VLAN] IP L4 Payload, no trailer (synthetic lengths are exact)
+    assert ((s["n_layers"] >= 5) & (s["n_layers"] <= 6)).all()
+    assert not (fl & abi.F_TRAILER).any()
+    # checksum verdicts: exactly the corrupted packets fail
+    bad = int(((fl & abi.F_L4_CSUM) != 0).sum() - ((fl & abi.F_L4_CSUM_OK) != 0).sum()) + \
+        int(((fl & abi.F_IP_CSUM) != 0).sum() - ((fl & abi.F_IP_CSUM_OK) != 0).sum())
+    assert bad == b.meta["corrupted"]
+    # last layer ends at caplen
+    last = lay[np.arange(n), s["n_layers"] - 1]
+    assert (last["offset"].astype(np.int64) + last["data_len"] == b.caplens).all()
+    # sampled bit-exact comparison with the restatement
+    rng = np.random.default_rng(0)
+    idx = np.sort(rng.choice(n, size=100_000, replace=False))
+    sub = from_packets([b.packet(int(i)) for i in idx])
+    o = oracle.oracle_parse(sub, opts, threads=8)
+    oracle.compare_exact(s[idx], lay[idx], o[0], o[1])
+
+
+def test_gpu_flow_hash_symmetry_and_flow_table(engine):
+    """Config 4 shape: both directions of a flow share hash5Tuple; the device flow table's per-flow
+    counters equal a host group-by over the same hashes (FilterTraffic's flow table)."""
+    import torch
+
+    b = synth.config(4, 500_000)
+    opts = abi.make_opts(0, 8, False, 0)
+    s, _ = parse_on_device(engine, b, opts)
+    fid = b.meta["flow_id"]
+    order = np.argsort(fid, kind="stable")
+    f_sorted, h_sorted = fid[order], s["hash5"][order]
+    same_flow = f_sorted[1:] == f_sorted[:-1]
+    assert (h_sorted[1:][same_flow] == h_sorted[:-1][same_flow]).all()
+    # device flow table
+    dev = "cuda:0"
+    summ = torch.from_numpy(s.view(np.uint8).copy()).to(dev)
+    caps = torch.from_numpy(b.caplens.view(np.int32)).to(dev)
+    cap = 1 << 21
+    keys = torch.zeros(cap, dtype=torch.int32, device=dev)
+    pk = torch.zeros(cap, dtype=torch.int64, device=dev)
+    by = torch.zeros(cap, dtype=torch.int64, device=dev)
+    st = torch.zeros(4, dtype=torch.int64, device=dev)
+    engine.flow_count_device(summ, caps, b.n, keys, pk, by, cap, st, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    k = keys.cpu().numpy().view(np.uint32)
+    used = k != 0
+    got = dict(zip(k[used].tolist(), zip(pk.cpu().numpy()[used].tolist(), by.cpu().numpy()[used].tolist())))
+    uniq, inv = np.unique(s["hash5"], return_inverse=True)
+    cnt = np.bincount(inv)
+    byt = np.bincount(inv, weights=b.caplens.astype(np.float64)).astype(np.int64)
+    want = {int(u): (int(c), int(y)) for u, c, y in zip(uniq, cnt, byt) if u != 0}
+    assert got == want
+    assert st.cpu().numpy()[2] == 0

@@ -1,0 +1,41 @@
+"""The restatement against the LIVE reference on adversarial inputs (mutations + crafted deep stacks).
+
+Needs oracle/_ref/libpcpp_ref.so (the reference compiled from /root/reference by oracle/Makefile);
+skipped where it was not built.
+"""
+from __future__ import annotations
+
+import pytest
+
+import oracle
+from conftest import golden_files, load_golden
+from mutate import as_batch, crafted, mutate
+from pcapplusplus_amd import abi
+
+pytestmark = pytest.mark.skipif(not oracle.ref_available(), reason="reference library not built")
+
+OPTS = [abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 3, True, 16),
+        abi.make_opts(0x203, 8, True, 4), abi.make_opts(0, 8, True, 0)]
+
+
+def _seed_packets():
+    batch, _ = load_golden([p for p in golden_files() if p.stem == "pcap_lt1"][0])
+    dat, _ = load_golden([p for p in golden_files() if p.stem == "dat_ethernet"][0])
+    return [batch.packet(i) for i in range(0, batch.n, 3)] + [dat.packet(i) for i in range(dat.n)]
+
+
+@pytest.mark.parametrize("opt_i", range(len(OPTS)))
+def test_crafted_stacks_vs_reference(opt_i):
+    b = as_batch(crafted())
+    rs, rl = oracle.ref_parse(b, OPTS[opt_i])
+    os_, ol = oracle.oracle_parse(b, OPTS[opt_i])
+    oracle.compare_engine_to_reference(os_, ol, rs, rl)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_mutations_vs_reference(seed):
+    b = as_batch(mutate(_seed_packets(), 6000, seed), gaps=True, seed=seed)
+    for opts in OPTS[:3]:
+        rs, rl = oracle.ref_parse(b, opts)
+        os_, ol = oracle.oracle_parse(b, opts)
+        oracle.compare_engine_to_reference(os_, ol, rs, rl)
