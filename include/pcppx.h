@@ -120,13 +120,16 @@ typedef struct pcppx_ctx pcppx_ctx;
 int pcppx_abi_version(void);
 const char* pcppx_strerror(int err);
 int pcppx_device_count(int* out);
+int pcppx_runtime_info(int device, char* buf, size_t len); /* HIP runtime/driver versions, device name */
 int pcppx_open(int device_ordinal, pcppx_ctx** out); /* one per host thread & GPU */
 void pcppx_close(pcppx_ctx* ctx);
 int pcppx_sync(pcppx_ctx* ctx);                      /* wait for everything queued on ctx's stream */
+void* pcppx_ctx_stream(pcppx_ctx* ctx);              /* the context's own hipStream_t */
 void pcppx_default_opts(pcppx_opts* opts);           /* Packet(RawPacket*) defaults + checksums + 16 layers */
 
 /* Device-resident parse. batch and records hold device pointers; the kernels are queued on
- * hip_stream (a hipStream_t; NULL = the context's own stream) and the call returns without waiting. */
+ * hip_stream (a hipStream_t; NULL = the null/default stream, as everywhere in HIP) and the call returns
+ * without waiting. pcppx_ctx_stream() gives the context's own non-blocking stream. */
 int pcppx_parse_batch_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
                              pcppx_records* out, void* hip_stream);
 

@@ -106,10 +106,14 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_strerror.restype = C.c_char_p
     lib.pcppx_strerror.argtypes = [C.c_int]
     lib.pcppx_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.pcppx_runtime_info.argtypes = [C.c_int, C.c_char_p, C.c_size_t]
+    lib.pcppx_runtime_info.restype = C.c_int
     lib.pcppx_open.argtypes = [C.c_int, C.POINTER(P)]
     lib.pcppx_close.argtypes = [P]
     lib.pcppx_close.restype = None
     lib.pcppx_sync.argtypes = [P]
+    lib.pcppx_ctx_stream.argtypes = [P]
+    lib.pcppx_ctx_stream.restype = P
     lib.pcppx_default_opts.argtypes = [C.POINTER(Opts)]
     lib.pcppx_default_opts.restype = None
     lib.pcppx_parse_batch_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records), P]
@@ -125,8 +129,8 @@ _ENGINE: C.CDLL | None = None
 
 # every symbol include/pcppx.h declares
 EXPORTED_SYMBOLS = (
-    "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_open", "pcppx_close",
-    "pcppx_sync", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
+    "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_runtime_info", "pcppx_open", "pcppx_close",
+    "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
     "pcppx_flow_count_device",
 )
 
@@ -139,11 +143,24 @@ def load_engine() -> C.CDLL:
             raise RuntimeError(
                 f"HIP engine library {ENGINE_SO} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`"
                 " (or `make -C pcapplusplus_amd/csrc`). There is no CPU fallback.")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7. Importing torch first makes
+        # the engine bind to that same runtime (matched by SONAME), so torch tensors/streams and the
+        # engine's kernels share one device context.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = _declare(C.CDLL(str(ENGINE_SO)))
         if lib.pcppx_abi_version() != ABI_VERSION:
             raise RuntimeError("libpcppx.so ABI version mismatch")
         _ENGINE = lib
     return _ENGINE
+
+
+def runtime_info(device: int = 0) -> str:
+    buf = C.create_string_buffer(256)
+    load_engine().pcppx_runtime_info(device, buf, 256)
+    return buf.value.decode()
 
 
 def check(rc: int, what: str = "pcppx") -> None:

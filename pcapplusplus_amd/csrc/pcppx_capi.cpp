@@ -6,6 +6,7 @@
 // on the CPU except the copy into pinned staging on the host path.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 #include <new>
 
@@ -136,6 +137,25 @@ extern "C"
 		}
 	}
 
+	int pcppx_runtime_info(int device, char* buf, size_t len)
+	{
+		if (buf == nullptr || len == 0)
+			return PCPPX_E_INVAL;
+		int rt = 0, drv = 0;
+		(void)hipRuntimeGetVersion(&rt);
+		(void)hipDriverGetVersion(&drv);
+		hipDeviceProp_t prop;
+		if (!ok(hipGetDeviceProperties(&prop, device)))
+		{
+			snprintf(buf, len, "hip runtime %d driver %d, device %d unavailable", rt, drv, device);
+			return PCPPX_E_NODEV;
+		}
+		snprintf(buf, len, "hip runtime %d driver %d, device %d: %s (%s), %d CUs, %.1f GiB", rt, drv, device,
+		         prop.name, prop.gcnArchName, prop.multiProcessorCount,
+		         (double)prop.totalGlobalMem / (1024.0 * 1024.0 * 1024.0));
+		return PCPPX_OK;
+	}
+
 	int pcppx_device_count(int* out)
 	{
 		if (out == nullptr)
@@ -197,6 +217,11 @@ extern "C"
 		delete c;
 	}
 
+	void* pcppx_ctx_stream(pcppx_ctx* c)
+	{
+		return c ? static_cast<void*>(c->stream) : nullptr;
+	}
+
 	int pcppx_sync(pcppx_ctx* c)
 	{
 		if (c == nullptr)
@@ -218,8 +243,7 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
-		hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-		return pcppx::launch_parse(b, o, r, st);
+		return pcppx::launch_parse(b, o, r, static_cast<hipStream_t>(hip_stream));
 	}
 
 	int pcppx_parse_batch_host(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r)
@@ -316,7 +340,7 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
-		hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-		return pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats, st);
+		return pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats,
+		                                static_cast<hipStream_t>(hip_stream));
 	}
 }

@@ -13,6 +13,8 @@
 // oracle/pcppx_oracle.c, which is the parity checker for everything here.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "pcppx.h"
 #include "pcppx_internal.h"
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(Params prm)
 	if (i >= prm.n)
 		return;
 
-	uint4 s0 = make_uint4(0, 0xFF00u, 0, 0), s1 = make_uint4(0, 0, 0, 0);  // summary, l4_layer = 0xFF
+	uint4 s0 = make_uint4(0, 0, 0, 0), s1 = make_uint4(0, 0, 0, 0);
 	pcppx_summary* sum_out = prm.summary + i;
 
 	const uint64_t off = prm.offsets[i];
@@ -721,6 +723,25 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 
 }  // namespace
 
+// Launch-error check; with PCPPX_SYNC_CHECK=1 in the environment every launch is also synchronised
+// and its execution status reported (debug aid: turns asynchronous faults into a named failure).
+int check_launch(const char* what, hipStream_t stream)
+{
+	static const bool sync_check = [] {
+		const char* e = getenv("PCPPX_SYNC_CHECK");
+		return e != nullptr && e[0] == '1';
+	}();
+	hipError_t e = hipGetLastError();
+	if (e == hipSuccess && sync_check)
+		e = hipStreamSynchronize(stream);
+	if (e != hipSuccess)
+	{
+		fprintf(stderr, "pcppx: %s failed: %s\n", what, hipGetErrorString(e));
+		return PCPPX_E_HIP;
+	}
+	return PCPPX_OK;
+}
+
 int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream)
 {
 	if (b->n == 0)
@@ -740,7 +761,7 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	prm.linktype = b->linktype;
 	dim3 grid((b->n + kBlock - 1) / kBlock);
 	hipLaunchKernelGGL(parse_kernel, grid, dim3(kBlock), 0, stream, prm);
-	return hipGetLastError() == hipSuccess ? PCPPX_OK : PCPPX_E_HIP;
+	return check_launch("parse_kernel", stream);
 }
 
 int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
@@ -752,7 +773,7 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 	hipLaunchKernelGGL(flow_count_kernel, grid, dim3(kBlock), 0, stream, sum, caplens, n, keys,
 	                   reinterpret_cast<unsigned long long*>(packets), reinterpret_cast<unsigned long long*>(bytes),
 	                   capacity, reinterpret_cast<unsigned long long*>(stats));
-	return hipGetLastError() == hipSuccess ? PCPPX_OK : PCPPX_E_HIP;
+	return check_launch("flow_count_kernel", stream);
 }
 
 }  // namespace pcppx

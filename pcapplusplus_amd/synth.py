@@ -214,7 +214,9 @@ def imix(n: int, seed: int, vlan_frac: float = 0.25, v6_frac: float = 0.30, corr
         f_sp, f_dp = safe_ports(frng, flows), safe_ports(frng, flows)
         v6 = f_v6[flow_id]
         tcp = f_tcp[flow_id]
-        tcp = np.where(small & v6, False, tcp)
+        # a flow keeps its protocol: 64 B cannot hold IPv6/TCP, so those packets become 512 B
+        size_of = np.where(small & v6 & tcp, sizes[1], size_of)
+        small = size_of < 14 + 4 + 40 + 20 + 2
         vlan = np.where(small & v6, False, vlan)
     groups = []
     info_l4 = np.zeros(n, dtype=np.int64)
