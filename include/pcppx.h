@@ -105,7 +105,8 @@ typedef struct pcppx_opts {
 	uint8_t parse_until_osi;     /* pcpp::OsiModelLayer; 8 = OsiModelLayerUnknown */
 	uint8_t want_checksums;      /* compute IPv4 / L4 checksums */
 	uint8_t max_layers;          /* 0 = do not write layers; else layers stride per packet (1..16) */
-	uint8_t reserved;
+	uint8_t variant;             /* kernel variant, for A/B measurement only: 0 = default (tile kernel),
+	                                1 = lane-per-packet kernel. Results are identical. */
 } pcppx_opts;
 
 /* Output arrays (same memory space as the batch for the _device call, host for the _host call). */

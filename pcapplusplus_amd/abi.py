@@ -84,7 +84,7 @@ class Opts(C.Structure):
         ("parse_until_osi", C.c_uint8),
         ("want_checksums", C.c_uint8),
         ("max_layers", C.c_uint8),
-        ("reserved", C.c_uint8),
+        ("variant", C.c_uint8),
     ]
 
 
@@ -93,11 +93,11 @@ class Records(C.Structure):
 
 
 def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checksums: bool = True,
-              max_layers: int = MAX_LAYERS) -> Opts:
+              max_layers: int = MAX_LAYERS, variant: int = 0) -> Opts:
     """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection."""
     if not 0 <= max_layers <= MAX_LAYERS:
         raise ValueError(f"max_layers must be in [0, {MAX_LAYERS}]")
-    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, 0)
+    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, variant)
 
 
 def _declare(lib: C.CDLL) -> C.CDLL:

@@ -175,7 +175,7 @@ extern "C"
 		o->parse_until_osi = 8;     // OsiModelLayerUnknown
 		o->want_checksums = 1;
 		o->max_layers = PCPPX_MAX_LAYERS;
-		o->reserved = 0;
+		o->variant = 0;
 	}
 
 	int pcppx_open(int device, pcppx_ctx** out)

@@ -252,6 +252,196 @@ __device__ __forceinline__ uint32_t finish_checksum(uint32_t residue)
 	return ((result >> 8) | (result << 8)) & 0xFFFFu;
 }
 
+// The next layer of the chain, as Layer::parseNextLayer of the layer of kind k at [o, o+len) computes
+// it. Outputs: the layer (proto, osi, hdr, dlen) and its successor (nk at [po, po+pl)).
+struct Step
+{
+	uint32_t proto, osi, hdr, dlen, nk, po, pl;
+};
+
+__device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o, uint32_t len)
+{
+	uint32_t proto = 0, osi = 0, hdr = 0, dlen = len;
+	uint32_t nk = K_NONE, po = 0, pl = 0;
+	switch (k)
+	{
+	case K_ETH:  // EthLayer::parseNextLayer, EthLayer.cpp:28-69
+	{
+		proto = P_ETH; osi = 2; hdr = 14;
+		if (len <= 14) break;
+		po = o + 14; pl = len - 14;
+		uint32_t et = be16(p, o + 12);
+		if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
+		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+		else if (et == 0x8100 || et == 0x88A8) nk = pl >= 4 ? K_VLAN : K_PAYLOAD;
+		else if (et == 0x8847) nk = pl >= 4 ? K_MPLS : K_PAYLOAD;
+		else if (et == 0x0806 || et == 0x8864 || et == 0x8863 || et == 0x0842) nk = K_OUT;
+		else nk = K_PAYLOAD;
+		break;
+	}
+	case K_DOT3:  // EthDot3Layer::parseNextLayer, EthDot3Layer.cpp:22-30
+		proto = P_DOT3; osi = 2; hdr = 14;
+		if (len <= 14) break;
+		po = o + 14; pl = len - 14;
+		nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
+		break;
+	case K_LLC:  // LLCLayer::parseNextLayer, LLCLayer.cpp:24-41
+		proto = P_LLC; osi = 2; hdr = 3;
+		if (len <= 3) break;
+		po = o + 3; pl = len - 3;
+		nk = (rb(p, o) == 0x42 && rb(p, o + 1) == 0x42) ? K_OUT : K_PAYLOAD;
+		break;
+	case K_VLAN:  // VlanLayer::parseNextLayer, VlanLayer.cpp:59-119
+	{
+		proto = P_VLAN; osi = 2; hdr = 4;
+		if (len <= 4) break;
+		po = o + 4; pl = len - 4;
+		uint32_t et = be16(p, o + 2);
+		if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
+		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+		else if (et == 0x8100 || et == 0x88A8) nk = K_VLAN;
+		else if (et == 0x8847) nk = K_MPLS;
+		else if (et == 0x0806 || et == 0x8864 || et == 0x8863) nk = K_OUT;
+		else if (et < 1500) nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
+		else nk = K_PAYLOAD;
+		break;
+	}
+	case K_MPLS:  // MplsLayer::parseNextLayer, MplsLayer.cpp:101-128
+	{
+		proto = P_MPLS; osi = 3; hdr = 4;
+		if (len < 5) break;
+		po = o + 4; pl = len - 4;
+		if (!(rb(p, o + 2) & 1)) { nk = K_MPLS; break; }
+		uint32_t nib = rb(p, o + 4) >> 4;
+		nk = nib == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+		              : (nib == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+		break;
+	}
+	case K_IPV4:  // IPv4Layer.cpp:180-197 (dataLen), :245-370 (next layer)
+	{
+		proto = P_IPV4; osi = 3;
+		uint32_t b0 = rb(p, o);
+		hdr = (b0 & 0xF) * 4;
+		uint32_t tl = be16(p, o + 2);
+		if (tl < len && tl != 0)
+		{
+			uint32_t hmin = hdr < len ? hdr : len;
+			dlen = tl > hmin ? tl : hmin;
+		}
+		if (dlen <= hdr) break;
+		po = o + hdr; pl = dlen - hdr;
+		uint32_t b6 = rb(p, o + 6), b7 = rb(p, o + 7);
+		if ((b6 & 0x20) || (((b6 & 0x1F) << 8) | b7) != 0) { nk = K_PAYLOAD; break; }
+		uint32_t ipp = rb(p, o + 9);
+		if (ipp == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
+		else if (ipp == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
+		else if (ipp == 4)
+		{
+			uint32_t ver = rb(p, po) >> 4;
+			nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+			              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+		}
+		else if (ipp == 47)
+		{
+			uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
+			nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
+		}
+		else if (ipp == 41) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+		else if (ipp == 1 || ipp == 2 || ipp == 51 || ipp == 50 || ipp == 112) nk = K_OUT;
+		else nk = K_PAYLOAD;
+		break;
+	}
+	case K_IPV6:  // IPv6Layer.cpp:28-40 (extensions + dataLen), :194-312 (next layer)
+	{
+		proto = P_IPV6; osi = 3;
+		uint32_t nh = rb(p, o + 6);
+		uint32_t eo = 40, ext = 0, last_ext = 0xFFFF;
+		while (eo <= len - 2)
+		{
+			uint32_t el;
+			if (nh == 44 || nh == 0 || nh == 60 || nh == 43) el = 8u * (rb(p, o + eo + 1) + 1);
+			else if (nh == 51) el = 4u * (rb(p, o + eo + 1) + 2);
+			else break;
+			last_ext = nh;
+			nh = rb(p, o + eo);
+			eo += el;
+			ext += el;
+		}
+		hdr = 40 + ext;
+		uint32_t total = be16(p, o + 4) + hdr;
+		if (total < len) dlen = total;
+		if (dlen <= hdr) break;
+		po = o + hdr; pl = dlen - hdr;
+		if (last_ext == 44) { nk = K_PAYLOAD; break; }
+		if (nh == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
+		else if (nh == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
+		else if (nh == 4)
+		{
+			uint32_t ver = rb(p, po) >> 4;
+			nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+			              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+		}
+		else if (nh == 47)
+		{
+			uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
+			nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
+		}
+		else if (nh == 51 || nh == 50 || nh == 58 || nh == 112) nk = K_OUT;
+		else nk = K_PAYLOAD;
+		break;
+	}
+	case K_GRE0:
+	case K_GRE1:  // GreLayer.cpp:195-252
+	{
+		proto = k == K_GRE0 ? P_GREV0 : P_GREV1; osi = 3;
+		uint32_t f0 = rb(p, o), f1 = rb(p, o + 1);
+		hdr = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
+		if (len <= hdr) break;
+		po = o + hdr; pl = len - hdr;
+		uint32_t et = be16(p, o + 2);
+		if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
+		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
+		else if (et == 0x8100) nk = K_VLAN;
+		else if (et == 0x8847) nk = K_MPLS;
+		else if (et == 0x880B) nk = pl >= 4 ? K_PPTP : K_PAYLOAD;
+		else if (et == 0x6558) nk = eth_ok(p, po, pl) ? K_ETH : (dot3_ok(p, po, pl) ? K_DOT3 : K_PAYLOAD);
+		else nk = K_PAYLOAD;
+		break;
+	}
+	case K_PPTP:  // PPP_PPTPLayer::parseNextLayer, GreLayer.cpp:547-566
+	{
+		proto = P_PPTP; osi = 5; hdr = 4;
+		if (len <= 4) break;
+		po = o + 4; pl = len - 4;
+		uint32_t pp = be16(p, o + 2);
+		nk = pp == 0x21 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
+		                : (pp == 0x57 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
+		break;
+	}
+	case K_TCP:  // TcpLayer.cpp:360-492
+		proto = P_TCP; osi = 4; hdr = (rb(p, o + 12) >> 4) * 4;
+		if (len <= hdr) break;
+		po = o + hdr; pl = len - hdr;
+		nk = (tcp_l7(be16(p, o)) || tcp_l7(be16(p, o + 2))) ? K_L7 : K_PAYLOAD;
+		break;
+	case K_UDP:  // UdpLayer.cpp:92-184
+	{
+		proto = P_UDP; osi = 4; hdr = 8;
+		if (len <= 8) break;
+		po = o + 8; pl = len - 8;
+		bool l7 = udp_l7(be16(p, o), be16(p, o + 2));
+		if (!l7 && pl >= 4)
+			l7 = sip_key((rb(p, po) << 24) | (rb(p, po + 1) << 16) | (rb(p, po + 2) << 8) | rb(p, po + 3));
+		nk = l7 ? K_L7 : K_PAYLOAD;
+		break;
+	}
+	default:  // K_PAYLOAD: PayloadLayer.h:61-81
+		proto = P_PAYLOAD; osi = 7; hdr = len;
+		break;
+	}
+	return Step{ proto, osi, hdr, dlen, nk, po, pl };
+}
+
 struct Params
 {
 	const uint8_t* data;
@@ -268,60 +458,23 @@ struct Params
 	uint32_t linktype;
 };
 
-__global__ __launch_bounds__(kBlock) void parse_kernel(Params prm)
+// Everything the summary needs after the chain walk.
+struct Walk
 {
-	__shared__ uint32_t stage[kBlock * kSlotDw];
+	uint32_t flags, n_layers;
+	uint64_t mask;
+	int32_t v4, v6;             // offsets of the first IPv4 / IPv6 layers (-1: none)
+	uint32_t v4_dlen;
+	int32_t l4i;                // hash5Tuple's port layer: last TCP, else last UDP (-1: none)
+	uint32_t l4o, l4dlen, l4pp, l4ppo;  // its offset, dataLen, and the previous layer's proto/offset
+	bool is_tcp;
+};
 
-	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-	if (i >= prm.n)
-		return;
-
-	uint4 s0 = make_uint4(0, 0, 0, 0), s1 = make_uint4(0, 0, 0, 0);
-	pcppx_summary* sum_out = prm.summary + i;
-
-	const uint64_t off = prm.offsets[i];
-	const uint32_t cap = prm.caplens[i];
-	if (off + cap > prm.data_len || cap > PCPPX_MAX_CAPLEN || cap == 0)
-	{
-		uint32_t fl = cap == 0 ? 0 : (cap > PCPPX_MAX_CAPLEN ? PCPPX_F_OVERSIZE : PCPPX_F_BAD_DESC);
-		if (off + cap > prm.data_len)
-			fl = PCPPX_F_BAD_DESC;
-		s0.w = fl | 0xFF000000u;
-		reinterpret_cast<uint4*>(sum_out)[0] = s0;
-		reinterpret_cast<uint4*>(sum_out)[1] = s1;
-		return;
-	}
-
-	// ---- stage the first 128 B of the packet into this lane's LDS slot ----
-	Pkt p;
-	p.g = (gptr8)(prm.data + off);
-	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
-	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
-	{
-		uint32_t need = (p.mis + cap + 15) >> 4;
-		p.nch = need < kStageChunks ? need : kStageChunks;
-		lptr32w slot = (lptr32w)(stage) + threadIdx.x * kSlotDw;
-
-		uint4 v[kStageChunks];
-#pragma unroll
-		for (int c = 0; c < kStageChunks; ++c)
-			if ((uint32_t)c < p.nch)
-				v[c] = ld16(p.a0 + 16 * c);
-#pragma unroll
-		for (int c = 0; c < kStageChunks; ++c)
-			if ((uint32_t)c < p.nch)
-			{
-				slot[4 * c + 0] = v[c].x;
-				slot[4 * c + 1] = v[c].y;
-				slot[4 * c + 2] = v[c].z;
-				slot[4 * c + 3] = v[c].w;
-			}
-		p.s = reinterpret_cast<lptr8>(slot);
-		uint32_t staged = 16 * p.nch - p.mis;
-		p.lim = staged < cap ? staged : cap;
-	}
-
-	// ---- first layer: Packet::createFirstLayer (Packet.cpp:827-923) ----
+// Packet::parsePacket (Packet.cpp:66-196): first layer by link type (createFirstLayer :827-923), the
+// parseNextLayer chain with the parse-until stop rules (:123-175), and the trailer (:178-195).
+// Layer records go straight to lay_out (uint2 per layer) when it is non-null.
+__device__ Walk walk_chain(const Pkt& p, uint32_t cap, const Params& prm, uint2* lay_out)
+{
 	uint32_t flags = 0;
 	uint32_t k;
 	switch (prm.linktype)
@@ -341,16 +494,14 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(Params prm)
 	default: k = K_PAYLOAD; break;
 	}
 
-	// ---- chain walk (Packet::parsePacket loop + stop rules, Packet.cpp:123-175) ----
 	const uint32_t ml = prm.max_layers;
 	const uint32_t cap_layers = ml ? ml : PCPPX_MAX_LAYERS;
-	uint2* lay_out = prm.layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 	uint32_t count = 0, found = 0, stopped = 0;
 	uint64_t mask = 0;
-	int32_t v4 = -1, v6 = -1;                        // offsets of the first IPv4 / IPv6 layers
+	int32_t v4 = -1, v6 = -1;
 	uint32_t v4_dlen = 0;
-	int32_t tcp_i = -1, udp_i = -1;                  // indices of the last TCP / UDP layers
-	uint32_t tcp_off = 0, tcp_dlen = 0, tcp_pp = 0, tcp_po = 0;  // + previous layer proto/offset
+	int32_t tcp_i = -1, udp_i = -1;
+	uint32_t tcp_off = 0, tcp_dlen = 0, tcp_pp = 0, tcp_po = 0;
 	uint32_t udp_off = 0, udp_dlen = 0, udp_pp = 0, udp_po = 0;
 	uint32_t prev_proto = 0, prev_off = 0;
 	uint32_t last_end = 0;
@@ -368,190 +519,14 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(Params prm)
 			flags |= PCPPX_F_NEEDS_HOST_L7;
 			break;
 		}
-		uint32_t proto = 0, osi = 0, hdr = 0, dlen = len;
-		uint32_t nk = K_NONE, po = 0, pl = 0;
-		switch (k)
-		{
-		case K_ETH:  // EthLayer::parseNextLayer, EthLayer.cpp:28-69
-		{
-			proto = P_ETH; osi = 2; hdr = 14;
-			if (len <= 14) break;
-			po = o + 14; pl = len - 14;
-			uint32_t et = be16(p, o + 12);
-			if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
-			else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-			else if (et == 0x8100 || et == 0x88A8) nk = pl >= 4 ? K_VLAN : K_PAYLOAD;
-			else if (et == 0x8847) nk = pl >= 4 ? K_MPLS : K_PAYLOAD;
-			else if (et == 0x0806 || et == 0x8864 || et == 0x8863 || et == 0x0842) nk = K_OUT;
-			else nk = K_PAYLOAD;
-			break;
-		}
-		case K_DOT3:  // EthDot3Layer::parseNextLayer, EthDot3Layer.cpp:22-30
-			proto = P_DOT3; osi = 2; hdr = 14;
-			if (len <= 14) break;
-			po = o + 14; pl = len - 14;
-			nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
-			break;
-		case K_LLC:  // LLCLayer::parseNextLayer, LLCLayer.cpp:24-41
-			proto = P_LLC; osi = 2; hdr = 3;
-			if (len <= 3) break;
-			po = o + 3; pl = len - 3;
-			nk = (rb(p, o) == 0x42 && rb(p, o + 1) == 0x42) ? K_OUT : K_PAYLOAD;
-			break;
-		case K_VLAN:  // VlanLayer::parseNextLayer, VlanLayer.cpp:59-119
-		{
-			proto = P_VLAN; osi = 2; hdr = 4;
-			if (len <= 4) break;
-			po = o + 4; pl = len - 4;
-			uint32_t et = be16(p, o + 2);
-			if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
-			else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-			else if (et == 0x8100 || et == 0x88A8) nk = K_VLAN;
-			else if (et == 0x8847) nk = K_MPLS;
-			else if (et == 0x0806 || et == 0x8864 || et == 0x8863) nk = K_OUT;
-			else if (et < 1500) nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
-			else nk = K_PAYLOAD;
-			break;
-		}
-		case K_MPLS:  // MplsLayer::parseNextLayer, MplsLayer.cpp:101-128
-		{
-			proto = P_MPLS; osi = 3; hdr = 4;
-			if (len < 5) break;
-			po = o + 4; pl = len - 4;
-			if (!(rb(p, o + 2) & 1)) { nk = K_MPLS; break; }
-			uint32_t nib = rb(p, o + 4) >> 4;
-			nk = nib == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-			              : (nib == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-			break;
-		}
-		case K_IPV4:  // IPv4Layer.cpp:180-197 (dataLen), :245-370 (next layer)
-		{
-			proto = P_IPV4; osi = 3;
-			uint32_t b0 = rb(p, o);
-			hdr = (b0 & 0xF) * 4;
-			uint32_t tl = be16(p, o + 2);
-			if (tl < len && tl != 0)
-			{
-				uint32_t hmin = hdr < len ? hdr : len;
-				dlen = tl > hmin ? tl : hmin;
-			}
-			if (dlen <= hdr) break;
-			po = o + hdr; pl = dlen - hdr;
-			uint32_t b6 = rb(p, o + 6), b7 = rb(p, o + 7);
-			if ((b6 & 0x20) || (((b6 & 0x1F) << 8) | b7) != 0) { nk = K_PAYLOAD; break; }
-			uint32_t ipp = rb(p, o + 9);
-			if (ipp == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
-			else if (ipp == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
-			else if (ipp == 4)
-			{
-				uint32_t ver = rb(p, po) >> 4;
-				nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-				              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-			}
-			else if (ipp == 47)
-			{
-				uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
-				nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
-			}
-			else if (ipp == 41) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-			else if (ipp == 1 || ipp == 2 || ipp == 51 || ipp == 50 || ipp == 112) nk = K_OUT;
-			else nk = K_PAYLOAD;
-			break;
-		}
-		case K_IPV6:  // IPv6Layer.cpp:28-40 (extensions + dataLen), :194-312 (next layer)
-		{
-			proto = P_IPV6; osi = 3;
-			uint32_t nh = rb(p, o + 6);
-			uint32_t eo = 40, ext = 0, last_ext = 0xFFFF;
-			while (eo <= len - 2)
-			{
-				uint32_t el;
-				if (nh == 44 || nh == 0 || nh == 60 || nh == 43) el = 8u * (rb(p, o + eo + 1) + 1);
-				else if (nh == 51) el = 4u * (rb(p, o + eo + 1) + 2);
-				else break;
-				last_ext = nh;
-				nh = rb(p, o + eo);
-				eo += el;
-				ext += el;
-			}
-			hdr = 40 + ext;
-			uint32_t total = be16(p, o + 4) + hdr;
-			if (total < len) dlen = total;
-			if (dlen <= hdr) break;
-			po = o + hdr; pl = dlen - hdr;
-			if (last_ext == 44) { nk = K_PAYLOAD; break; }
-			if (nh == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
-			else if (nh == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
-			else if (nh == 4)
-			{
-				uint32_t ver = rb(p, po) >> 4;
-				nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-				              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-			}
-			else if (nh == 47)
-			{
-				uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
-				nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
-			}
-			else if (nh == 51 || nh == 50 || nh == 58 || nh == 112) nk = K_OUT;
-			else nk = K_PAYLOAD;
-			break;
-		}
-		case K_GRE0:
-		case K_GRE1:  // GreLayer.cpp:195-252
-		{
-			proto = k == K_GRE0 ? P_GREV0 : P_GREV1; osi = 3;
-			uint32_t f0 = rb(p, o), f1 = rb(p, o + 1);
-			hdr = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
-			if (len <= hdr) break;
-			po = o + hdr; pl = len - hdr;
-			uint32_t et = be16(p, o + 2);
-			if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
-			else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-			else if (et == 0x8100) nk = K_VLAN;
-			else if (et == 0x8847) nk = K_MPLS;
-			else if (et == 0x880B) nk = pl >= 4 ? K_PPTP : K_PAYLOAD;
-			else if (et == 0x6558) nk = eth_ok(p, po, pl) ? K_ETH : (dot3_ok(p, po, pl) ? K_DOT3 : K_PAYLOAD);
-			else nk = K_PAYLOAD;
-			break;
-		}
-		case K_PPTP:  // PPP_PPTPLayer::parseNextLayer, GreLayer.cpp:547-566
-		{
-			proto = P_PPTP; osi = 5; hdr = 4;
-			if (len <= 4) break;
-			po = o + 4; pl = len - 4;
-			uint32_t pp = be16(p, o + 2);
-			nk = pp == 0x21 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-			                : (pp == 0x57 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-			break;
-		}
-		case K_TCP:  // TcpLayer.cpp:360-492
-			proto = P_TCP; osi = 4; hdr = (rb(p, o + 12) >> 4) * 4;
-			if (len <= hdr) break;
-			po = o + hdr; pl = len - hdr;
-			nk = (tcp_l7(be16(p, o)) || tcp_l7(be16(p, o + 2))) ? K_L7 : K_PAYLOAD;
-			break;
-		case K_UDP:  // UdpLayer.cpp:92-184
-		{
-			proto = P_UDP; osi = 4; hdr = 8;
-			if (len <= 8) break;
-			po = o + 8; pl = len - 8;
-			bool l7 = udp_l7(be16(p, o), be16(p, o + 2));
-			if (!l7 && pl >= 4)
-				l7 = sip_key((rb(p, po) << 24) | (rb(p, po + 1) << 16) | (rb(p, po + 2) << 8) | rb(p, po + 3));
-			nk = l7 ? K_L7 : K_PAYLOAD;
-			break;
-		}
-		default:  // K_PAYLOAD: PayloadLayer.h:61-81
-			proto = P_PAYLOAD; osi = 7; hdr = len;
-			break;
-		}
-
+		Step s = step_layer(p, k, o, len);
+		uint32_t nk = s.nk;
 		// stop rules (inclusive, then roll back one layer; the first layer is never rolled back)
+		const uint32_t proto = s.proto;
 		bool member = prm.family != 0 &&
 		              (proto == (prm.family & 0xFF) || (proto << 8) == (prm.family & 0xFF00) ||
 		               (proto << 16) == (prm.family & 0xFF0000) || (proto << 24) == (prm.family & 0xFF000000u));
-		bool fail = osi > prm.until_osi;
+		bool fail = s.osi > prm.until_osi;
 		if (!fail)
 		{
 			if (member) found = 1;
@@ -564,20 +539,19 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(Params prm)
 			nk = K_NONE;
 		}
 		if (lay_out && count < ml)
-			lay_out[count] = make_uint2(proto | (osi << 8) | (o << 16), (hdr & 0xFFFF) | (dlen << 16));
+			lay_out[count] = make_uint2(proto | (s.osi << 8) | (o << 16), (s.hdr & 0xFFFF) | (s.dlen << 16));
 		mask |= 1ull << proto;
-		if (proto == P_IPV4 && v4 < 0) { v4 = (int32_t)o; v4_dlen = dlen; }
+		if (proto == P_IPV4 && v4 < 0) { v4 = (int32_t)o; v4_dlen = s.dlen; }
 		if (proto == P_IPV6 && v6 < 0) v6 = (int32_t)o;
-		if (proto == P_TCP) { tcp_i = (int32_t)count; tcp_off = o; tcp_dlen = dlen; tcp_pp = prev_proto; tcp_po = prev_off; }
-		if (proto == P_UDP) { udp_i = (int32_t)count; udp_off = o; udp_dlen = dlen; udp_pp = prev_proto; udp_po = prev_off; }
+		if (proto == P_TCP) { tcp_i = (int32_t)count; tcp_off = o; tcp_dlen = s.dlen; tcp_pp = prev_proto; tcp_po = prev_off; }
+		if (proto == P_UDP) { udp_i = (int32_t)count; udp_off = o; udp_dlen = s.dlen; udp_pp = prev_proto; udp_po = prev_off; }
 		prev_proto = proto;
 		prev_off = o;
-		last_end = o + dlen;
+		last_end = o + s.dlen;
 		++count;
-		k = nk; o = po; len = pl;
+		k = nk; o = s.po; len = s.pl;
 	}
 
-	// ---- trailer (Packet.cpp:178-195) ----
 	if (count > 0 && prm.family == 0 && prm.until_osi == 8 && !stopped &&
 	    !(flags & (PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_NEEDS_HOST_PROTO)) && last_end < cap)
 	{
@@ -589,102 +563,720 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(Params prm)
 		flags |= PCPPX_F_TRAILER;
 	}
 	if (count > cap_layers) flags |= PCPPX_F_DEPTH_OVERFLOW;
-	const uint32_t n_layers = count > cap_layers ? cap_layers : count;
 
-	// ---- hash5Tuple / hash2Tuple (PacketUtils.cpp:139-245) ----
-	const bool is_tcp = tcp_i >= 0;
-	const int32_t l4i = is_tcp ? tcp_i : udp_i;
-	const uint32_t l4o = is_tcp ? tcp_off : udp_off;
-	const uint32_t l4dlen = is_tcp ? tcp_dlen : udp_dlen;
-	uint32_t h5 = 0, h5d = 0, h2 = 0;
-	const bool have_ip = v4 >= 0 || v6 >= 0;
-	const uint32_t ipo = v4 >= 0 ? (uint32_t)v4 : (uint32_t)v6;
-	const uint32_t alen = v4 >= 0 ? 4 : 16;
-	const uint32_t src_o = ipo + (v4 >= 0 ? 12 : 8), dst_o = ipo + (v4 >= 0 ? 16 : 24);
-	if (have_ip)
+	Walk w;
+	w.flags = flags;
+	w.n_layers = count > cap_layers ? cap_layers : count;
+	w.mask = mask;
+	w.v4 = v4;
+	w.v6 = v6;
+	w.v4_dlen = v4_dlen;
+	w.is_tcp = tcp_i >= 0;
+	w.l4i = w.is_tcp ? tcp_i : udp_i;
+	w.l4o = w.is_tcp ? tcp_off : udp_off;
+	w.l4dlen = w.is_tcp ? tcp_dlen : udp_dlen;
+	w.l4pp = w.is_tcp ? tcp_pp : udp_pp;
+	w.l4ppo = w.is_tcp ? tcp_po : udp_po;
+	return w;
+}
+
+// hash5Tuple (both directions) and hash2Tuple, PacketUtils.cpp:139-245
+__device__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
+{
+	h5 = h5d = h2 = 0;
+	if (w.v4 < 0 && w.v6 < 0)
+		return;
+	const bool v4 = w.v4 >= 0;
+	const uint32_t ipo = v4 ? (uint32_t)w.v4 : (uint32_t)w.v6;
+	const uint32_t alen = v4 ? 4 : 16;
+	const uint32_t src_o = ipo + (v4 ? 12 : 8), dst_o = ipo + (v4 ? 16 : 24);
+	// address order: dst < src compared as host LE u32 (IPv4) or memcmp (IPv6)
+	int cmp = 0;
+	if (v4)
 	{
-		// address order: dst < src compared as host LE u32 (IPv4) or memcmp (IPv6)
-		int cmp = 0;
-		if (v4 >= 0)
+		uint32_t s = le32(p, src_o), d = le32(p, dst_o);
+		cmp = d < s ? -1 : (d > s ? 1 : 0);
+	}
+	else
+	{
+		for (uint32_t j = 0; j < 16 && cmp == 0; ++j)
 		{
-			uint32_t s = le32(p, src_o), d = le32(p, dst_o);
-			cmp = d < s ? -1 : (d > s ? 1 : 0);
-		}
-		else
-		{
-			for (uint32_t j = 0; j < 16 && cmp == 0; ++j)
-			{
-				uint32_t a = rb(p, dst_o + j), b = rb(p, src_o + j);
-				cmp = a < b ? -1 : (a > b ? 1 : 0);
-			}
-		}
-		const uint32_t a_o = cmp < 0 ? dst_o : src_o, b_o = cmp < 0 ? src_o : dst_o;
-		uint32_t h = 2166136261u;
-		for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, a_o + j));
-		for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, b_o + j));
-		h2 = h;
-		if (l4i >= 0)
-		{
-			const uint32_t sp = le16(p, l4o), dp = le16(p, l4o + 2);
-			const uint32_t ipproto = rb(p, ipo + (v4 >= 0 ? 9 : 6));
-			for (int dir = 0; dir < 2; ++dir)
-			{
-				bool swap = !dir && (dp < sp || (dp == sp && cmp < 0));
-				uint32_t x = fnv(fnv(2166136261u, swap ? (dp & 0xFF) : (sp & 0xFF)), swap ? (dp >> 8) : (sp >> 8));
-				x = fnv(fnv(x, swap ? (sp & 0xFF) : (dp & 0xFF)), swap ? (sp >> 8) : (dp >> 8));
-				const uint32_t f_o = swap ? dst_o : src_o, s_o = swap ? src_o : dst_o;
-				for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, f_o + j));
-				for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, s_o + j));
-				x = fnv(x, ipproto);
-				if (dir) h5d = x; else h5 = x;
-			}
+			uint32_t a = rb(p, dst_o + j), b = rb(p, src_o + j);
+			cmp = a < b ? -1 : (a > b ? 1 : 0);
 		}
 	}
+	const uint32_t a_o = cmp < 0 ? dst_o : src_o, b_o = cmp < 0 ? src_o : dst_o;
+	uint32_t h = 2166136261u;
+	for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, a_o + j));
+	for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, b_o + j));
+	h2 = h;
+	if (w.l4i < 0)
+		return;
+	const uint32_t sp = le16(p, w.l4o), dp = le16(p, w.l4o + 2);
+	const uint32_t ipproto = rb(p, ipo + (v4 ? 9 : 6));
+	for (int dir = 0; dir < 2; ++dir)
+	{
+		bool swap = !dir && (dp < sp || (dp == sp && cmp < 0));
+		uint32_t x = fnv(fnv(2166136261u, swap ? (dp & 0xFF) : (sp & 0xFF)), swap ? (dp >> 8) : (sp >> 8));
+		x = fnv(fnv(x, swap ? (sp & 0xFF) : (dp & 0xFF)), swap ? (sp >> 8) : (dp >> 8));
+		const uint32_t f_o = swap ? dst_o : src_o, s_o = swap ? src_o : dst_o;
+		for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, f_o + j));
+		for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, s_o + j));
+		x = fnv(x, ipproto);
+		if (dir) h5d = x; else h5 = x;
+	}
+}
 
-	// ---- checksums ----
-	uint32_t ipc = 0, ips = 0, l4c = 0, l4s = 0;
+// IPv4 header checksum (IPv4Layer.cpp:410-412): computeChecksum over min(IHL*4, dataLen) header bytes
+// with the checksum field zeroed. Returns calc; *stored gets the field.
+__device__ uint32_t ipv4_checksum(const Pkt& p, const Walk& w, uint32_t* stored)
+{
+	const uint32_t o = (uint32_t)w.v4;
+	uint32_t hl = (rb(p, o) & 0xF) * 4;
+	if (hl > w.v4_dlen) hl = w.v4_dlen;
+	uint32_t r = range_residue(p, o, o + hl);
+	*stored = be16(p, o + 10);
+	r = (r + 65535u - mod65535(le16(p, o + 10))) % 65535u;  // field is stream word 5 (even offset)
+	return finish_checksum(r);
+}
+
+// {Tcp,Udp}Layer::calculateChecksum(false) (TcpLayer.cpp:271-311, UdpLayer.cpp:47-90) given the
+// residue of the L4 bytes as a stream: subtract the checksum field, add the pseudo header
+// (computePseudoHdrChecksum, PacketUtils.cpp:66-112), fold; UDP maps 0 to 0xFFFF.
+__device__ uint32_t l4_checksum(const Pkt& p, const Walk& w, uint32_t l4_residue, uint32_t* stored)
+{
+	const uint32_t field = w.is_tcp ? 16 : 6;
+	*stored = be16(p, w.l4o + field);
+	uint32_t res = 0;
+	if (w.l4pp == P_IPV4 || w.l4pp == P_IPV6)
+	{
+		uint32_t r = (l4_residue + 65535u - mod65535(le16(p, w.l4o + field))) % 65535u;
+		uint32_t ph = 0;
+		const uint32_t as = w.l4pp == P_IPV4 ? w.l4ppo + 12 : w.l4ppo + 8;
+		const uint32_t nw = w.l4pp == P_IPV4 ? 4 : 16;  // 16-bit words of src+dst
+		for (uint32_t j = 0; j < nw; ++j) ph += le16(p, as + 2 * j);
+		ph += ((w.l4dlen & 0xFF) << 8) | ((w.l4dlen >> 8) & 0xFF);  // htobe16(dataLen)
+		ph += (w.is_tcp ? 6u : 17u) << 8;                              // htobe16(protocol)
+		r = (r + mod65535(ph)) % 65535u;
+		res = finish_checksum(r);
+	}
+	if (!w.is_tcp && res == 0)
+		res = 0xFFFF;
+	return res;
+}
+
+__device__ __forceinline__ void write_summary(pcppx_summary* out, uint32_t h5, uint32_t h5d, uint32_t h2,
+                                              uint32_t flags, uint32_t n_layers, int32_t l4i, uint64_t mask,
+                                              uint32_t ipc, uint32_t ips, uint32_t l4c, uint32_t l4s)
+{
+	uint4 s0 = make_uint4(h5, h5d, h2, flags | (n_layers << 16) | ((l4i >= 0 ? (uint32_t)l4i : 0xFFu) << 24));
+	uint4 s1 = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), ipc | (ips << 16), l4c | (l4s << 16));
+	reinterpret_cast<uint4*>(out)[0] = s0;
+	reinterpret_cast<uint4*>(out)[1] = s1;
+}
+
+// descriptor checks shared by both kernels: returns 0 if the packet is parseable, else its flags
+__device__ __forceinline__ uint32_t desc_flags(uint64_t off, uint32_t cap, uint64_t data_len, bool* empty)
+{
+	*empty = false;
+	if (off + cap > data_len || off + cap < off)
+		return PCPPX_F_BAD_DESC;
+	if (cap > PCPPX_MAX_CAPLEN)
+		return PCPPX_F_OVERSIZE;
+	if (cap == 0)
+		*empty = true;
+	return 0;
+}
+
+// ================= lane kernel: one lane streams one whole packet (reference / fallback) =================
+__global__ __launch_bounds__(kBlock) void parse_lane_kernel(Params prm)
+{
+	__shared__ uint32_t stage[kBlock * kSlotDw];
+
+	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+	if (i >= prm.n)
+		return;
+	pcppx_summary* sum_out = prm.summary + i;
+	const uint64_t off = prm.offsets[i];
+	const uint32_t cap = prm.caplens[i];
+	bool empty;
+	uint32_t bad = desc_flags(off, cap, prm.data_len, &empty);
+	if (bad || empty)
+	{
+		write_summary(sum_out, 0, 0, 0, bad, 0, -1, 0, 0, 0, 0, 0);
+		return;
+	}
+
+	Pkt p;
+	p.g = (gptr8)(prm.data + off);
+	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
+	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+	{
+		uint32_t need = (p.mis + cap + 15) >> 4;
+		p.nch = need < kStageChunks ? need : kStageChunks;
+		lptr32w slot = (lptr32w)(stage) + threadIdx.x * kSlotDw;
+		uint4 v[kStageChunks];
+#pragma unroll
+		for (int c = 0; c < kStageChunks; ++c)
+			if ((uint32_t)c < p.nch)
+				v[c] = ld16(p.a0 + 16 * c);
+#pragma unroll
+		for (int c = 0; c < kStageChunks; ++c)
+			if ((uint32_t)c < p.nch)
+			{
+				slot[4 * c + 0] = v[c].x;
+				slot[4 * c + 1] = v[c].y;
+				slot[4 * c + 2] = v[c].z;
+				slot[4 * c + 3] = v[c].w;
+			}
+		p.s = reinterpret_cast<lptr8>(slot);
+		uint32_t staged = 16 * p.nch - p.mis;
+		p.lim = staged < cap ? staged : cap;
+	}
+
+	uint2* lay_out = prm.layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * prm.max_layers : nullptr;
+	Walk w = walk_chain(p, cap, prm, lay_out);
+	uint32_t h5, h5d, h2;
+	hashes(p, w, h5, h5d, h2);
+	uint32_t flags = w.flags, ipc = 0, ips = 0, l4c = 0, l4s = 0;
 	if (prm.want_csum)
 	{
-		if (v4 >= 0)  // IPv4Layer.cpp:410-412: computeChecksum(header with field zeroed, min(IHL*4, dataLen))
+		if (w.v4 >= 0)
 		{
-			uint32_t hl = (rb(p, (uint32_t)v4) & 0xF) * 4;
-			if (hl > v4_dlen) hl = v4_dlen;
-			uint32_t r = range_residue(p, (uint32_t)v4, (uint32_t)v4 + hl);
-			ips = be16(p, (uint32_t)v4 + 10);
-			uint32_t fw = le16(p, (uint32_t)v4 + 10);  // field at even offset 10 of the stream
-			r = (r + 65535u - mod65535(fw)) % 65535u;
-			ipc = finish_checksum(r);
+			ipc = ipv4_checksum(p, w, &ips);
 			flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
 		}
-		if (l4i >= 0)  // TcpLayer.cpp:271-311, UdpLayer.cpp:47-90, computePseudoHdrChecksum PacketUtils.cpp:66-112
+		if (w.l4i >= 0)
 		{
-			const uint32_t field = is_tcp ? 16 : 6;
-			const uint32_t pp = is_tcp ? tcp_pp : udp_pp, ppo = is_tcp ? tcp_po : udp_po;
-			uint32_t res = 0;
-			if (pp == P_IPV4 || pp == P_IPV6)
-			{
-				uint32_t r = range_residue(p, l4o, l4o + l4dlen);
-				r = (r + 65535u - mod65535(le16(p, l4o + field))) % 65535u;
-				uint32_t ph = 0;
-				const uint32_t as = pp == P_IPV4 ? ppo + 12 : ppo + 8;
-				const uint32_t nw = pp == P_IPV4 ? 4 : 16;  // 16-bit words of src+dst
-				for (uint32_t j = 0; j < nw; ++j) ph += le16(p, as + 2 * j);
-				ph += ((l4dlen & 0xFF) << 8) | ((l4dlen >> 8) & 0xFF);  // htobe16(dataLen)
-				ph += (is_tcp ? 6u : 17u) << 8;                          // htobe16(protocol)
-				r = (r + mod65535(ph)) % 65535u;
-				res = finish_checksum(r);
-			}
-			if (!is_tcp && res == 0) res = 0xFFFF;
-			l4c = res;
-			l4s = be16(p, l4o + field);
+			l4c = l4_checksum(p, w, range_residue(p, w.l4o, w.l4o + w.l4dlen), &l4s);
 			flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
 		}
 	}
+	write_summary(sum_out, h5, h5d, h2, flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
+}
 
-	s0 = make_uint4(h5, h5d, h2, flags | (n_layers << 16) | ((l4i >= 0 ? (uint32_t)l4i : 0xFFu) << 24));
-	s1 = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), ipc | (ips << 16), l4c | (l4s << 16));
-	reinterpret_cast<uint4*>(sum_out)[0] = s0;
-	reinterpret_cast<uint4*>(sum_out)[1] = s1;
+// ---------------- fast path for the common stacks (branch-free, dword LDS reads) ----------------
+//
+// Ethernet, up to two 802.1Q/802.1ad tags, IPv4 (any IHL, not a fragment) or IPv6 without extension
+// headers, then TCP or UDP, then Payload (or an L7 flag) and a trailer; no parse-until options. Every
+// byte it reads must sit in the LDS window; anything else (or any rule this path does not cover) makes
+// it report "not applicable" and the generic walk_chain() runs instead. Results are identical to
+// walk_chain() by construction: same rules, same records (checked bit-exactly by tests/).
+
+// bytes j..j+3 of the packet, little-endian, from the LDS window (caller guarantees j + 4 <= p.lim)
+__device__ __forceinline__ uint32_t lds_u32(const Pkt& p, uint32_t j)
+{
+	const uint32_t pos = p.mis + j;
+	lptr32 w = reinterpret_cast<lptr32>(p.s) + (pos >> 2);
+	return __builtin_amdgcn_alignbyte(w[1], w[0], pos & 3);
+}
+__device__ __forceinline__ uint32_t swap16(uint32_t v)
+{
+	return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF);
+}
+
+struct Fast
+{
+	uint32_t nv;        // VLAN tags
+	uint32_t ipo, iphdr, ipdlen, v6;
+	uint32_t l4o, l4hdr, l4dlen, tcp;
+	uint32_t payload;   // a Payload layer follows the L4 layer
+	uint32_t trailer;   // trailer length (0: none)
+	uint32_t l7;        // L4 payload would go to an L7 dissector
+};
+
+__device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Params& prm, Fast& f)
+{
+	bool ok = prm.linktype == 1 && prm.family == 0 && prm.until_osi == 8 && p.lim >= 20 && cap > 14;
+	// Ethernet (EthLayer.cpp:28-69, isDataValid :100-117)
+	uint32_t d = lds_u32(p, 12);
+	uint32_t et = swap16(d);
+	ok = ok && et >= 0x0600;
+	uint32_t o = 14, len = cap - 14, nv = 0;
+	// up to two VLAN tags (VlanLayer.cpp:59-119): each needs len > 4 so that a next layer follows
+#pragma unroll
+	for (int t = 0; t < 2; ++t)
+	{
+		const bool vl = (et == 0x8100 || et == 0x88A8) && len > 4 && o + 8 <= p.lim;
+		const uint32_t e2 = swap16(lds_u32(p, vl ? o : 0) >> 16);
+		et = vl ? e2 : et;
+		o = vl ? o + 4 : o;
+		len = vl ? len - 4 : len;
+		nv += vl ? 1 : 0;
+	}
+	const bool v4 = et == 0x0800, v6 = et == 0x86DD;
+	ok = ok && (v4 || v6) && o + 40 <= p.lim;  // both IP headers' fixed parts are read below
+	const uint32_t w0 = lds_u32(p, o);      // ver/ihl, tos, total length (v4) | ver/tc/flow (v6)
+	const uint32_t w1 = lds_u32(p, o + 4);  // id, frag (v4) | payload length, next header, hop limit (v6)
+	const uint32_t w2 = lds_u32(p, o + 8);  // ttl, protocol, checksum (v4)
+	const uint32_t b0 = w0 & 0xFF;
+	uint32_t hdr, dlen, proto;
+	if (v4)
+	{
+		// IPv4Layer::isDataValid (IPv4Layer.h:626-630), initLayerInPacket (IPv4Layer.cpp:180-197)
+		ok = ok && len >= 20 && (b0 >> 4) == 4 && (b0 & 0xF) >= 5;
+		hdr = (b0 & 0xF) * 4;
+		const uint32_t tl = swap16(w0 >> 16);
+		dlen = len;
+		if (tl < len && tl != 0)
+		{
+			const uint32_t hmin = hdr < len ? hdr : len;
+			dlen = tl > hmin ? tl : hmin;
+		}
+		const uint32_t b6 = (w1 >> 16) & 0xFF, b7 = w1 >> 24;
+		ok = ok && !((b6 & 0x20) || (((b6 & 0x1F) << 8) | b7) != 0);  // not a fragment (:415-438)
+		proto = (w2 >> 8) & 0xFF;
+	}
+	else
+	{
+		// IPv6Layer ctor (IPv6Layer.cpp:28-40): next header 6/17 means no extension walk
+		ok = ok && len >= 40 && (b0 >> 4) == 6;
+		hdr = 40;
+		const uint32_t total = swap16(w1) + 40;
+		dlen = total < len ? total : len;
+		proto = (w1 >> 16) & 0xFF;
+	}
+	ok = ok && (proto == 6 || proto == 17) && dlen > hdr;
+	const uint32_t l4o = o + hdr, pl = ok ? dlen - hdr : 0;
+	const bool tcp = proto == 6;
+	ok = ok && l4o + (tcp ? 20 : 8) <= p.lim;
+	const uint32_t t3 = lds_u32(p, (ok && tcp) ? l4o + 12 : 0);  // TCP data offset byte at +12
+	const uint32_t doff = (t3 & 0xFF) >> 4;
+	// TcpLayer::isDataValid (TcpLayer.h:596-601) / UDP needs 8 bytes
+	ok = ok && (tcp ? (pl >= 20 && doff >= 5 && pl >= doff * 4) : pl >= 8);
+	const uint32_t l4hdr = tcp ? doff * 4 : 8;
+	const bool payload = pl > l4hdr;
+	const uint32_t pw = lds_u32(p, ok ? l4o : 0);
+	const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
+	bool l7 = tcp ? (tcp_l7(sport) || tcp_l7(dport)) : udp_l7(sport, dport);
+	if (!tcp && payload && pl - 8 >= 4)
+	{
+		ok = ok && l4o + 12 <= p.lim;
+		const uint32_t s4 = lds_u32(p, ok ? l4o + 8 : 0);
+		l7 = l7 || sip_key(__builtin_bswap32(s4));
+	}
+	l7 = l7 && payload;
+	// the IPv4 header checksum reads the whole header from LDS too
+	ok = ok && (!v4 || o + hdr <= p.lim);
+	f.nv = nv;
+	f.ipo = o;
+	f.iphdr = hdr;
+	f.ipdlen = dlen;
+	f.v6 = v6;
+	f.l4o = l4o;
+	f.l4hdr = l4hdr;
+	f.l4dlen = pl;
+	f.tcp = tcp;
+	f.payload = payload && !l7;
+	f.l7 = l7;
+	const uint32_t end = o + dlen;
+	f.trailer = (!l7 && end < cap) ? cap - end : 0;
+	return ok;
+}
+
+// the Walk summary of a fast-path packet
+__device__ __forceinline__ Walk fast_to_walk(const Fast& f, uint32_t ml)
+{
+	const uint32_t cap_layers = ml ? ml : PCPPX_MAX_LAYERS;
+	const uint32_t count = 3 + f.nv + f.payload + (f.trailer ? 1 : 0);
+	Walk w;
+	w.flags = (f.l7 ? PCPPX_F_NEEDS_HOST_L7 : 0) | (f.trailer ? PCPPX_F_TRAILER : 0) |
+	          (count > cap_layers ? PCPPX_F_DEPTH_OVERFLOW : 0);
+	w.n_layers = count > cap_layers ? cap_layers : count;
+	w.mask = (1ull << P_ETH) | (f.nv ? (1ull << P_VLAN) : 0) | (1ull << (f.v6 ? P_IPV6 : P_IPV4)) |
+	         (1ull << (f.tcp ? P_TCP : P_UDP)) | (f.payload ? (1ull << P_PAYLOAD) : 0) |
+	         (f.trailer ? (1ull << P_TRAILER) : 0);
+	w.v4 = f.v6 ? -1 : (int32_t)f.ipo;
+	w.v6 = f.v6 ? (int32_t)f.ipo : -1;
+	w.v4_dlen = f.ipdlen;
+	w.l4i = (int32_t)(2 + f.nv);
+	w.l4o = f.l4o;
+	w.l4dlen = f.l4dlen;
+	w.l4pp = f.v6 ? P_IPV6 : P_IPV4;
+	w.l4ppo = f.ipo;
+	w.is_tcp = f.tcp;
+	return w;
+}
+
+// layer record k of a fast-path packet (k < count)
+__device__ __forceinline__ uint2 fast_layer(const Fast& f, uint32_t cap, uint32_t k)
+{
+	uint32_t proto, osi, o, hdr, dlen;
+	if (k == 0) { proto = P_ETH; osi = 2; o = 0; hdr = 14; dlen = cap; }
+	else if (k <= f.nv) { proto = P_VLAN; osi = 2; o = 14 + 4 * (k - 1); hdr = 4; dlen = cap - o; }
+	else if (k == f.nv + 1) { proto = f.v6 ? P_IPV6 : P_IPV4; osi = 3; o = f.ipo; hdr = f.iphdr; dlen = f.ipdlen; }
+	else if (k == f.nv + 2) { proto = f.tcp ? P_TCP : P_UDP; osi = 4; o = f.l4o; hdr = f.l4hdr; dlen = f.l4dlen; }
+	else if (k == f.nv + 3 && f.payload)
+	{
+		proto = P_PAYLOAD; osi = 7; o = f.l4o + f.l4hdr; hdr = dlen = f.l4dlen - f.l4hdr;
+	}
+	else { proto = P_TRAILER; osi = 2; o = f.ipo + f.ipdlen; hdr = dlen = f.trailer; }
+	return make_uint2(proto | (osi << 8) | (o << 16), (hdr & 0xFFFF) | (dlen << 16));
+}
+
+// hash5Tuple x2 + hash2Tuple from dword reads (same byte sequences as hashes())
+__device__ __forceinline__ uint32_t fnv4(uint32_t h, uint32_t v)
+{
+	h = fnv(h, v & 0xFF);
+	h = fnv(h, (v >> 8) & 0xFF);
+	h = fnv(h, (v >> 16) & 0xFF);
+	return fnv(h, v >> 24);
+}
+
+__device__ void fast_hashes(const Pkt& p, const Fast& f, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
+{
+	uint32_t s[4], d[4];
+	const uint32_t na = f.v6 ? 4 : 1;
+	const uint32_t so = f.ipo + (f.v6 ? 8 : 12), dofs = f.ipo + (f.v6 ? 24 : 16);
+	int cmp = 0;  // sign of memcmp(dst, src) (IPv6) / (dst < src) on LE u32 (IPv4)
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+	{
+		s[k] = (uint32_t)k < na ? lds_u32(p, so + 4 * k) : 0;
+		d[k] = (uint32_t)k < na ? lds_u32(p, dofs + 4 * k) : 0;
+	}
+	if (!f.v6)
+		cmp = d[0] < s[0] ? -1 : (d[0] > s[0] ? 1 : 0);
+	else
+	{
+#pragma unroll
+		for (int k = 3; k >= 0; --k)
+		{
+			const uint32_t a = __builtin_bswap32(d[k]), b = __builtin_bswap32(s[k]);
+			cmp = a < b ? -1 : (a > b ? 1 : cmp);
+		}
+	}
+	const bool sw2 = cmp < 0;
+	uint32_t x = 2166136261u;
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+		if ((uint32_t)k < na) x = fnv4(x, sw2 ? d[k] : s[k]);
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+		if ((uint32_t)k < na) x = fnv4(x, sw2 ? s[k] : d[k]);
+	h2 = x;
+	const uint32_t pw = lds_u32(p, f.l4o);
+	const uint32_t sp = pw & 0xFFFF, dp = pw >> 16;  // raw network-order values, LE-loaded
+	const uint32_t proto = f.tcp ? 6 : 17;
+	for (int dir = 0; dir < 2; ++dir)
+	{
+		const bool swap = !dir && (dp < sp || (dp == sp && cmp < 0));
+		uint32_t y = 2166136261u;
+		const uint32_t fp = swap ? dp : sp, sp2 = swap ? sp : dp;
+		y = fnv(fnv(y, fp & 0xFF), fp >> 8);
+		y = fnv(fnv(y, sp2 & 0xFF), sp2 >> 8);
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			if ((uint32_t)k < na) y = fnv4(y, swap ? d[k] : s[k]);
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			if ((uint32_t)k < na) y = fnv4(y, swap ? s[k] : d[k]);
+		y = fnv(y, proto);
+		if (dir) h5d = y; else h5 = y;
+	}
+}
+
+// IPv4 header checksum from dword reads of the (fully staged) header
+__device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Fast& f, uint32_t* stored)
+{
+	uint32_t acc = 0;
+	for (uint32_t t = 0; t < f.iphdr; t += 4)
+		acc += halves(lds_u32(p, f.ipo + t));
+	const uint32_t w5 = lds_u32(p, f.ipo + 8) >> 16;  // bytes 10-11 as a LE word
+	*stored = swap16(w5);
+	uint32_t r = (mod65535(acc) + 65535u - mod65535(w5)) % 65535u;
+	return finish_checksum(r);
+}
+
+// ================= tile kernel: one wave = one tile of 64 consecutive packets =================
+//
+// (1) descriptors, coalesced; (2) each packet's first 112 B gathered into LDS with 8 lanes per packet
+// (one 16-B piece each: 8 packets per wave-instruction instead of 64 scattered lines); (3) lane-per-
+// packet chain walk, hashes and IPv4 checksum out of LDS; (4) the L4 checksums: the wave streams the
+// tile's byte span once with coalesced 16-B-per-lane loads, turns each 16-B chunk into its sum of
+// 16-bit halves and a wave-wide inclusive prefix (DPP scan) into an LDS window; every packet lane
+// then takes the sum of its whole-chunk L4 range as a difference of two prefixes and adds its two
+// partial edge chunks. The ones'-complement sum only needs the byte-order fix-up for an odd L4
+// start at the very end (a multiply by 256 mod 65535).
+constexpr int kTile = 64;
+constexpr int kTStageChunks = 7;                   // 112 B staged per packet
+constexpr int kTSlotDw = 4 * kTStageChunks + 1;    // + 1 pad dword against bank conflicts
+constexpr int kWin = 512;                          // prefix window: 512 chunks = 8 KiB of span
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+	// Hillis-Steele inside 16-lane rows, then row broadcasts (wave64 on a GFX9-family target)
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+	return x;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+{
+	for (int m = 32; m >= 1; m >>= 1)
+	{
+		uint64_t o = __shfl_xor(v, m, 64);
+		v = o < v ? o : v;
+	}
+	return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
+{
+	for (int m = 32; m >= 1; m >>= 1)
+	{
+		uint64_t o = __shfl_xor(v, m, 64);
+		v = o > v ? o : v;
+	}
+	return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+{
+	for (int m = 32; m >= 1; m >>= 1)
+		v += __shfl_xor(v, m, 64);
+	return v;
+}
+
+// masked halves-sum of the bytes [lo, hi) of one 16-B chunk (LDS copy if staged, else HBM)
+__device__ __forceinline__ uint32_t edge_sum(const Pkt& p, uintptr_t lo, uintptr_t hi)
+{
+	if (hi <= lo)
+		return 0;
+	const uintptr_t c = lo & ~(uintptr_t)15;
+	const uint32_t ci = (uint32_t)((c - p.a0) >> 4);
+	uint4 v;
+	if (ci < p.nch)
+	{
+		lptr32 w = reinterpret_cast<lptr32>(p.s) + ci * 4;
+		v = make_uint4(w[0], w[1], w[2], w[3]);
+	}
+	else
+		v = ld16(c);
+	return chunk_sum(v, c, lo, hi);
+}
+
+// halves-sum of whole chunks [c0, c1) straight from HBM (fallback for tiles whose span is not packed)
+__device__ uint32_t full_chunks_sum(uintptr_t c0, uintptr_t c1)
+{
+	uint32_t acc = 0;
+	uintptr_t c = c0;
+	for (; c + 64 <= c1; c += 64)
+	{
+		uint4 v0 = ld16(c), v1 = ld16(c + 16), v2 = ld16(c + 32), v3 = ld16(c + 48);
+		acc += halves(v0.x) + halves(v0.y) + halves(v0.z) + halves(v0.w) + halves(v1.x) + halves(v1.y) +
+		       halves(v1.z) + halves(v1.w) + halves(v2.x) + halves(v2.y) + halves(v2.z) + halves(v2.w) +
+		       halves(v3.x) + halves(v3.y) + halves(v3.z) + halves(v3.w);
+	}
+	for (; c < c1; c += 16)
+	{
+		uint4 v = ld16(c);
+		acc += halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
+	}
+	return acc;
+}
+
+__global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
+{
+	// stage doubles as the layer-record staging area at the end (64 rows x 16 layers x 8 B = 8 KiB)
+	__shared__ uint32_t stage[2048];
+	__shared__ uint64_t m_a0[kTile];
+	__shared__ uint32_t m_nch[kTile];
+	__shared__ uint32_t pre[kWin];
+	static_assert(kTile * kTSlotDw <= 2048, "stage too small");
+
+	const uint32_t lane = threadIdx.x;
+	const uint32_t i = blockIdx.x * kTile + lane;
+	const bool in = i < prm.n;
+	const uint64_t off = in ? prm.offsets[i] : 0;
+	const uint32_t cap = in ? prm.caplens[i] : 0;
+	bool empty = true;
+	const uint32_t bad = in ? desc_flags(off, cap, prm.data_len, &empty) : 0;
+	const bool live = in && !bad && !empty;
+
+	// ---- (2) header gather into LDS ----
+	Pkt p;
+	p.g = (gptr8)(prm.data + (live ? off : 0));
+	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
+	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+	{
+		const uint32_t need = (p.mis + cap + 15) >> 4;
+		p.nch = live ? (need < kTStageChunks ? need : kTStageChunks) : 0;
+	}
+	m_a0[lane] = p.a0;
+	m_nch[lane] = p.nch;
+	__syncthreads();
+	{
+		const uint32_t sub = lane & 7, grp = lane >> 3;
+		uint4 v[8];
+#pragma unroll
+		for (int j = 0; j < 8; ++j)
+		{
+			const uint32_t q = 8 * j + grp;
+			if (sub < m_nch[q])
+				v[j] = ld16(m_a0[q] + 16 * sub);
+		}
+#pragma unroll
+		for (int j = 0; j < 8; ++j)
+		{
+			const uint32_t q = 8 * j + grp;
+			if (sub < m_nch[q])
+			{
+				lptr32w slot = (lptr32w)(stage) + q * kTSlotDw + 4 * sub;
+				slot[0] = v[j].x;
+				slot[1] = v[j].y;
+				slot[2] = v[j].z;
+				slot[3] = v[j].w;
+			}
+		}
+	}
+	__syncthreads();
+	p.s = reinterpret_cast<lptr8>((lptr32w)(stage) + lane * kTSlotDw);
+	{
+		const uint32_t staged = 16 * p.nch - p.mis;
+		p.lim = live ? (staged < cap ? staged : cap) : 0;
+	}
+
+	// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
+	const uint32_t ml = prm.max_layers;
+	const bool stage_layers = prm.layers != nullptr && ml != 0;
+	Walk w;
+	w.flags = bad;
+	w.n_layers = 0;
+	w.mask = 0;
+	w.v4 = w.v6 = -1;
+	w.l4i = -1;
+	w.l4o = w.l4dlen = 0;
+	w.is_tcp = false;
+	Fast f;
+	bool fast = false;
+	uint32_t h5 = 0, h5d = 0, h2 = 0, ipc = 0, ips = 0, l4c = 0, l4s = 0;
+	if (live)
+	{
+		fast = fast_walk(p, cap, prm, f);
+		if (fast)
+		{
+			w = fast_to_walk(f, ml);
+			fast_hashes(p, f, h5, h5d, h2);
+			if (prm.want_csum && !f.v6)
+			{
+				ipc = fast_ipv4_checksum(p, f, &ips);
+				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+			}
+		}
+		else
+		{
+			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
+			w = walk_chain(p, cap, prm, lay_out);
+			hashes(p, w, h5, h5d, h2);
+			if (prm.want_csum && w.v4 >= 0)
+			{
+				ipc = ipv4_checksum(p, w, &ips);
+				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+			}
+		}
+	}
+
+	// ---- (4) L4 checksums over the tile span ----
+	if (prm.want_csum)  // uniform
+	{
+		const bool need = live && w.l4i >= 0;
+		const uintptr_t as = (uintptr_t)p.g + w.l4o, ae = as + w.l4dlen;
+		const uintptr_t f0 = (as + 15) & ~(uintptr_t)15, f1 = ae & ~(uintptr_t)15;
+		const bool full = need && f0 < f1;
+		const uint64_t smin = wave_min_u64(full ? (uint64_t)f0 : ~0ull);
+		const uint64_t emax = wave_max_u64(full ? (uint64_t)f1 : 0ull);
+		uint32_t fsum = 0;
+		if (emax > smin)
+		{
+			const uint64_t span = emax - smin;
+			const uint64_t wire = wave_sum_u64(live ? cap : 0);
+			if (span <= 2 * wire + 65536)
+			{
+				const uint32_t nchunks = (uint32_t)(span >> 4);
+				const uint32_t c0 = full ? (uint32_t)((f0 - smin) >> 4) : 0;
+				const uint32_t c1 = full ? (uint32_t)((f1 - smin) >> 4) : 0;
+				uint32_t carry = 0;
+				for (uint32_t w0 = 0; w0 < nchunks; w0 += kWin)
+				{
+					const uint32_t carry_w0 = carry;
+					uint4 v[kWin / 64];
+#pragma unroll
+					for (int k = 0; k < kWin / 64; ++k)
+					{
+						const uint32_t c = w0 + 64 * k + lane;
+						v[k] = c < nchunks ? ld16(smin + 16ull * c) : make_uint4(0, 0, 0, 0);
+					}
+#pragma unroll
+					for (int k = 0; k < kWin / 64; ++k)
+					{
+						const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+						const uint32_t x = wave_incl_scan(h);
+						pre[64 * k + lane] = carry + x;
+						carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+					}
+					__syncthreads();
+					if (full)
+					{
+						const uint32_t lo = c0 > w0 ? c0 : w0;
+						const uint32_t hi = c1 < w0 + kWin ? c1 : w0 + kWin;
+						if (lo < hi)
+							fsum += pre[hi - 1 - w0] - (lo > w0 ? pre[lo - 1 - w0] : carry_w0);
+					}
+					__syncthreads();
+				}
+			}
+			else if (full)
+				fsum = full_chunks_sum(f0, f1);
+		}
+		if (need)
+		{
+			uint32_t acc = mod65535(fsum);
+			if (f0 <= f1)
+				acc += edge_sum(p, as, f0) + edge_sum(p, f1, ae);
+			else
+				acc += edge_sum(p, as, ae);
+			uint32_t r = mod65535(acc);
+			if (as & 1)
+				r = (r * 256u) % 65535u;
+			l4c = l4_checksum(p, w, r, &l4s);
+			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
+		}
+	}
+
+	if (in)
+		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
+
+	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores ----
+	if (stage_layers)  // uniform
+	{
+		__syncthreads();  // every lane is done with the header stage
+		m_nch[lane] = fast ? 1u : 0u;
+		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+		typedef __attribute__((address_space(3))) u32x2* lptr64w;
+		lptr64w rows = (lptr64w)(stage);
+		if (fast)
+		{
+			const uint32_t cnt = w.n_layers;
+			for (uint32_t k = 0; k < ml; ++k)
+			{
+				const uint2 r = k < cnt ? fast_layer(f, cap, k) : make_uint2(0, 0);
+				u32x2 e;
+				e.x = r.x;
+				e.y = r.y;
+				rows[lane * ml + k] = e;
+			}
+		}
+		__syncthreads();
+		const uint32_t first = blockIdx.x * kTile;
+		const uint32_t nrows = prm.n - first < (uint32_t)kTile ? prm.n - first : (uint32_t)kTile;
+		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)first * ml;
+		for (uint32_t q = lane; q < nrows * ml; q += kTile)
+			if (m_nch[q / ml])
+				dst[q] = rows[q];
+	}
 }
 
 // ---- per-flow counters keyed by hash5Tuple (FilterTraffic's flow table, AppWorkerThread.h:99-125) ----
@@ -759,9 +1351,18 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	prm.want_csum = o->want_checksums;
 	prm.max_layers = o->max_layers;
 	prm.linktype = b->linktype;
-	dim3 grid((b->n + kBlock - 1) / kBlock);
-	hipLaunchKernelGGL(parse_kernel, grid, dim3(kBlock), 0, stream, prm);
-	return check_launch("parse_kernel", stream);
+	// variant 1 (or PCPPX_KERNEL=lane) selects the lane-per-packet kernel for A/B measurements
+	static const bool lane_env = [] {
+		const char* e = getenv("PCPPX_KERNEL");
+		return e != nullptr && e[0] == 'l';
+	}();
+	if (o->variant == 1 || lane_env)
+	{
+		hipLaunchKernelGGL(parse_lane_kernel, dim3((b->n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, prm);
+		return check_launch("parse_lane_kernel", stream);
+	}
+	hipLaunchKernelGGL(parse_tile_kernel, dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
+	return check_launch("parse_tile_kernel", stream);
 }
 
 int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,

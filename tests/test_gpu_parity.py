@@ -20,22 +20,28 @@ from pcapplusplus_amd.pcap import from_packets
 pytestmark = pytest.mark.gpu
 
 
+def variant(opts: abi.Opts, v: int) -> abi.Opts:
+    return abi.make_opts(opts.parse_until_family, opts.parse_until_osi, bool(opts.want_checksums), opts.max_layers, v)
+
+
+@pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.stem)
-def test_gpu_golden(engine, path):
+def test_gpu_golden(engine, path, kernel):
     batch, variants = load_golden(path)
     for v, (opts, rsum, rlay) in variants.items():
-        gsum, glay = parse_on_device(engine, batch, opts)
+        gsum, glay = parse_on_device(engine, batch, variant(opts, kernel))
         osum, olay = oracle.oracle_parse(batch, opts)
         oracle.compare_exact(gsum, glay, osum, olay)
         oracle.compare_engine_to_reference(gsum, glay, rsum, rlay)
 
 
+@pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
 @pytest.mark.parametrize("gaps", [False, True])
-def test_gpu_crafted_deep_stacks(engine, gaps):
+def test_gpu_crafted_deep_stacks(engine, gaps, kernel):
     b = as_batch(crafted(), gaps=gaps, seed=11)
     for opts in (abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 3, True, 5),
                  abi.make_opts(0, 8, True, 0), abi.make_opts(0, 8, False, 16)):
-        g = parse_on_device(engine, b, opts)
+        g = parse_on_device(engine, b, variant(opts, kernel))
         o = oracle.oracle_parse(b, opts)
         oracle.compare_exact(g[0], g[1], o[0], o[1])
         if oracle.ref_available():
@@ -43,11 +49,13 @@ def test_gpu_crafted_deep_stacks(engine, gaps):
             oracle.compare_engine_to_reference(g[0], g[1], r[0], r[1])
 
 
-def test_gpu_mutations(engine):
+@pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
+@pytest.mark.parametrize("gaps", [False, True])
+def test_gpu_mutations(engine, gaps, kernel):
     seedb, _ = load_golden([p for p in golden_files() if p.stem == "pcap_lt1"][0])
     pk = [seedb.packet(i) for i in range(seedb.n)]
-    b = as_batch(mutate(pk, 40000, 5), gaps=True, seed=5)
-    g = parse_on_device(engine, b)
+    b = as_batch(mutate(pk, 40000, 5), gaps=gaps, seed=5)
+    g = parse_on_device(engine, b, abi.make_opts(variant=kernel))
     o = oracle.oracle_parse(b, threads=8)
     oracle.compare_exact(g[0], g[1], o[0], o[1])
 

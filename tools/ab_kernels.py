@@ -1,0 +1,49 @@
+"""Interleaved A/B timing of kernel variants in one process (cdna guide §5.4 rule 24).
+
+  python tools/ab_kernels.py [packets] [rounds]
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch  # noqa: E402
+
+from pcapplusplus_amd import abi, synth  # noqa: E402
+from pcapplusplus_amd.engine import Engine, to_device  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+b = synth.config(cfg, n)
+eng = Engine(0)
+data, offs, caps = to_device(b)
+summ = torch.empty(n * 32, dtype=torch.uint8, device="cuda:0")
+lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device="cuda:0")
+st = torch.cuda.current_stream()
+read_bytes = int(b.caplens.sum(dtype=np.int64)) + 12 * n
+cases = {
+    "tile/ml8/csum": abi.make_opts(0, 8, True, 8, 0),
+    "lane/ml8/csum": abi.make_opts(0, 8, True, 8, 1),
+    "tile/ml0/csum": abi.make_opts(0, 8, True, 0, 0),
+    "tile/ml8/nocsum": abi.make_opts(0, 8, False, 8, 0),
+}
+import os  # noqa: E402
+only = os.environ.get("AB_CASES")
+if only:
+    cases = {k: v for k, v in cases.items() if k in only.split(",")}
+times = {k: [] for k in cases}
+for r in range(rounds):
+    for name, o in cases.items():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        eng.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream)
+        e1.record(st)
+        torch.cuda.synchronize()
+        if r > 0:
+            times[name].append(e0.elapsed_time(e1))
+for name, t in times.items():
+    t = np.array(t)
+    print(f"{name:18s} median {np.median(t):.4f} ms  min {t.min():.4f} ms  -> {n / np.median(t) / 1e3:8.1f} Mpkt/s"
+          f"  read {read_bytes / np.median(t) / 1e6:8.1f} GB/s ({read_bytes / np.median(t) / 1e6 / 8000 * 100:.1f}% of 8 TB/s)")
