@@ -80,7 +80,7 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    from pcapplusplus_amd import abi, synth
+    from pcapplusplus_amd import abi, shard, synth
     from pcapplusplus_amd.engine import Engine, to_device
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,11 +96,11 @@ def main() -> None:
     # ---- synthetic shard for this rank (per-GPU work fixed: weak scaling) ----
     t0 = time.time()
     if args.config == 3:
-        batch = synth.imix(args.packets, 3 + 1000 * rank)
+        batch = synth.imix(args.packets, shard.shard_seed(3, rank))
     elif args.config == 4:
-        batch = synth.imix(args.packets, 4 + 1000 * rank, flows=1_000_000, corrupt_frac=0.0)
+        batch = synth.imix(args.packets, shard.shard_seed(4, rank), flows=1_000_000, corrupt_frac=0.0)
     else:
-        batch = synth.small64(args.packets, 2 + 1000 * rank)
+        batch = synth.small64(args.packets, shard.shard_seed(2, rank))
     gen_s = time.time() - t0
     want_csum = not args.no_checksums
     opts = abi.make_opts(0, 8, want_csum, args.max_layers)
