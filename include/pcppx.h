@@ -148,6 +148,48 @@ int pcppx_flow_count_device(pcppx_ctx* ctx, const pcppx_summary* summary, const 
                             uint32_t n, uint32_t* keys, uint64_t* packets, uint64_t* bytes,
                             uint32_t capacity, uint64_t* stats, void* hip_stream);
 
+/* ---- DpdkExample-FilterTraffic's worker on the device ----
+ * PacketMatchingEngine::isMatched (Examples/DpdkExample-FilterTraffic/PacketMatchingEngine.h:43-107),
+ * the matched-flow table keyed by hash5Tuple and PacketStats::collectStats (AppWorkerThread.h:85-139,
+ * Common.h:83-104), over a parsed device batch (records from pcppx_parse_batch_device; max_layers >= 1).
+ * Packet order is the worker's receive order: packet i of the batch has sequence number seq_base + i,
+ * and a packet matches if it matches on its own or an earlier packet of the same 5-tuple flow matched.
+ * The flow table (flow_keys / flow_first, `capacity` slots, power of two, zero-initialised) persists
+ * across batches like the worker's m_FlowTable. */
+typedef struct pcppx_match_spec {
+	uint32_t src_ip;   /* IPv4Address::toInt() (network byte order in memory); 0 = any */
+	uint32_t dst_ip;   /* 0 = any */
+	uint16_t src_port; /* host order; 0 = any */
+	uint16_t dst_port; /* 0 = any */
+	uint8_t protocol;  /* pcpp::TCP (4) or pcpp::UDP (5); anything else = any */
+	uint8_t reserved[3];
+} pcppx_match_spec;
+
+typedef struct pcppx_packet_stats { /* PacketStats, Examples/DpdkExample-FilterTraffic/Common.h:57-142 */
+	uint64_t packet_count, eth_count, arp_count, ipv4_count, ipv6_count, tcp_count, udp_count;
+	uint64_t http_count, dns_count, tls_count; /* L7: counted by the host for PCPPX_F_NEEDS_HOST_L7 packets */
+	uint64_t matched_tcp_flows, matched_udp_flows, matched_packets;
+	uint64_t needs_host_count;                  /* packets whose chain the engine did not finish */
+} pcppx_packet_stats;
+
+int pcppx_filter_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
+                        const pcppx_match_spec* spec, uint64_t seq_base, uint64_t* flow_keys, uint64_t* flow_first,
+                        uint32_t capacity, uint8_t* matched, pcppx_packet_stats* stats, void* hip_stream);
+
+/* ---- host ingest: pcap files into packed batch buffers ---- */
+typedef struct pcppx_pcap pcppx_pcap;
+int pcppx_pcap_open(const char* path, pcppx_pcap** out); /* PcapFileReaderDevice::open, PcapFileDevice.cpp:707-768 */
+uint32_t pcppx_pcap_linktype(const pcppx_pcap* reader);
+/* Append up to max_packets records back to back into data[0, data_cap) (pinned memory feeds
+ * pcppx_parse_batch_host without a staging copy); *n_out = packets read (0 at end of file). Record checks
+ * as PcapFileReaderDevice::readNextPacket, PcapFileDevice.cpp:799-880. */
+int pcppx_pcap_read_batch(pcppx_pcap* reader, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
+                          uint32_t* caplens, uint64_t* timestamps_ns, uint32_t max_packets, uint32_t* n_out,
+                          uint64_t* bytes_out);
+void pcppx_pcap_close(pcppx_pcap* reader);
+void* pcppx_host_alloc(size_t bytes); /* page-locked host memory (hipHostMalloc) */
+void pcppx_host_free(void* p);
+
 #ifdef __cplusplus
 }
 #endif

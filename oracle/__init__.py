@@ -59,6 +59,9 @@ def ref_lib() -> C.CDLL:
         lib.pcppx_ref_bench.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Opts), C.c_int,
                                         C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
         lib.pcppx_ref_bench.restype = C.c_int
+        lib.pcppx_ref_filter.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.MatchSpec), C.c_void_p,
+                                         C.POINTER(abi.PacketStats)]
+        lib.pcppx_ref_filter.restype = C.c_int
         _ref = lib
     return _ref
 
@@ -108,6 +111,95 @@ def ref_bench(batch, opts: abi.Opts, threads: int) -> tuple[float, int]:
     if rc != 0:
         raise RuntimeError("reference bench failed")
     return sec.value, dig.value
+
+
+def make_spec(src_ip: str | int = 0, dst_ip: str | int = 0, src_port: int = 0, dst_port: int = 0,
+              protocol: int = 0) -> abi.MatchSpec:
+    sip = abi.ipv4_to_int(src_ip) if isinstance(src_ip, str) else int(src_ip)
+    dip = abi.ipv4_to_int(dst_ip) if isinstance(dst_ip, str) else int(dst_ip)
+    return abi.MatchSpec(sip, dip, src_port, dst_port, protocol)
+
+
+def ref_filter(batch, spec: abi.MatchSpec):
+    """The reference FilterTraffic worker loop (real PacketMatchingEngine + hash5Tuple flow table +
+    collectStats) over a host batch: (matched u8[n], stats dict)."""
+    matched = np.zeros(max(batch.n, 1), dtype=np.uint8)
+    st = abi.PacketStats()
+    b = batch.c_batch()
+    rc = ref_lib().pcppx_ref_filter(C.byref(b), C.byref(spec), matched.ctypes.data, C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"reference filter failed {rc}")
+    return matched[: batch.n], st.as_dict()
+
+
+P_ETH, P_IPV4, P_IPV6, P_TCP, P_UDP, P_ARP = 1, 2, 3, 4, 5, 8
+
+
+def oracle_filter(batch, summary, layers, spec: abi.MatchSpec, flow_table: dict | None = None):
+    """Restatement of the FilterTraffic worker (AppWorkerThread.h:85-139; PacketMatchingEngine.h:43-107;
+    Common.h:83-104) over parse records, in receive order. Pure Python: small batches only.
+    Returns (matched u8[n], stats dict without the L7 counters). `flow_table` persists across calls."""
+    ft = {} if flow_table is None else flow_table
+    m_sip, m_dip = spec.src_ip != 0, spec.dst_ip != 0
+    m_sp, m_dp = spec.src_port != 0, spec.dst_port != 0
+    m_proto = spec.protocol in (P_TCP, P_UDP)
+    st = {k: 0 for k in abi.STATS_FIELDS}
+    matched = np.zeros(batch.n, dtype=np.uint8)
+    data = batch.data
+    for i in range(batch.n):
+        mask = int(summary["proto_mask"][i])
+        has = lambda p: (mask >> p) & 1  # noqa: E731
+        st["packet_count"] += 1
+        for key, p in (("eth_count", P_ETH), ("arp_count", P_ARP), ("ipv4_count", P_IPV4),
+                       ("ipv6_count", P_IPV6), ("tcp_count", P_TCP), ("udp_count", P_UDP)):
+            st[key] += has(p)
+        if int(summary["flags"][i]) & abi.F_NEEDS_HOST:
+            st["needs_host_count"] += 1
+        base = int(batch.offsets[i])
+        nl = min(int(summary["n_layers"][i]), layers.shape[1])
+        first = {}
+        for k in range(nl):
+            first.setdefault(int(layers[i, k]["proto"]), int(layers[i, k]["offset"]))
+
+        def is_matched() -> bool:
+            if m_sip or m_dip:
+                if not has(P_IPV4):
+                    return False
+                o = base + first[P_IPV4]
+                if m_sip and int.from_bytes(data[o + 12:o + 16].tobytes(), "little") != spec.src_ip:
+                    return False
+                if m_dip and int.from_bytes(data[o + 16:o + 20].tobytes(), "little") != spec.dst_ip:
+                    return False
+            if m_sp or m_dp:
+                if has(P_TCP):
+                    o = base + first[P_TCP]
+                elif has(P_UDP):
+                    o = base + first[P_UDP]
+                else:
+                    return False
+                sp, dp = int(data[o]) << 8 | int(data[o + 1]), int(data[o + 2]) << 8 | int(data[o + 3])
+                if m_sp and sp != spec.src_port:
+                    return False
+                if m_dp and dp != spec.dst_port:
+                    return False
+            if m_proto and not has(spec.protocol):
+                return False
+            return True
+
+        h = int(summary["hash5"][i])
+        if ft.get(h, False):
+            ok = True
+        else:
+            ok = is_matched()
+            if ok:
+                ft[h] = True
+                if has(P_TCP):
+                    st["matched_tcp_flows"] += 1
+                elif has(P_UDP):
+                    st["matched_udp_flows"] += 1
+        st["matched_packets"] += int(ok)
+        matched[i] = ok
+    return matched, st
 
 
 def checksum(bufs: list[bytes]) -> int:

@@ -9,7 +9,7 @@
  *   - where the reference would hand an L4 payload to an L7 dissector (port/content triggers of
  *     TcpLayer.cpp:372-491 and UdpLayer.cpp:103-178, incl. the SIP content heuristic
  *     SipLayer.cpp:127-160) the chain stops after the TCP/UDP layer and PCPPX_F_NEEDS_HOST_L7 is set;
- *   - where it would build an out-of-scope L2/L3 layer (ARP, PPPoE, WoL, ICMP, IGMP, AH, ESP, VRRP,
+ *   - where it would build an out-of-scope L2/L3 layer (PPPoE, WoL, ICMP, IGMP, AH, ESP, VRRP,
  *     ICMPv6, STP, SLL/SLL2/NULL/NFLOG/C_HDLC first layers) the chain stops before it and
  *     PCPPX_F_NEEDS_HOST_PROTO is set;
  *   - no trailer is appended to a flagged chain; hashes and checksums are computed over the emitted chain.
@@ -29,12 +29,12 @@
 
 /* ---- ProtocolType ids (Packet++/header/ProtocolType.h:42-258) and OSI (:266-284) ---- */
 enum {
-	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14,
+	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14,
 	P_GREV0 = 15, P_GREV1 = 16, P_PPTP = 17, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44
 };
 
 enum kind { K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP,
-	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7 };
+	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP };
 
 static uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
@@ -186,7 +186,8 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		case 0x86DD: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
 		case 0x8100: case 0x88A8: NEXT(pl >= 4 ? K_VLAN : K_PAYLOAD, po, pl); break;
 		case 0x8847: NEXT(pl >= 4 ? K_MPLS : K_PAYLOAD, po, pl); break;
-		case 0x0806: case 0x8864: case 0x8863: case 0x0842: NEXT(K_OUT, po, pl); break; /* ARP, PPPoE, WoL */
+		case 0x0806: NEXT(pl >= 28 ? K_ARP : K_PAYLOAD, po, pl); break; /* ArpLayer::isDataValid, ArpLayer.h:279-282 */
+		case 0x8864: case 0x8863: case 0x0842: NEXT(K_OUT, po, pl); break; /* PPPoE, WoL */
 		default: NEXT(K_PAYLOAD, po, pl); break;
 		}
 		break;
@@ -212,7 +213,8 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		case 0x86DD: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
 		case 0x8100: case 0x88A8: NEXT(K_VLAN, po, pl); break; /* unchecked */
 		case 0x8847: NEXT(K_MPLS, po, pl); break;              /* unchecked */
-		case 0x0806: case 0x8864: case 0x8863: NEXT(K_OUT, po, pl); break;
+		case 0x0806: NEXT(K_ARP, po, pl); break; /* unchecked */
+		case 0x8864: case 0x8863: NEXT(K_OUT, po, pl); break;
 		default:
 			if (be16(p + 2) < 1500) NEXT(llc_valid(pkt + po, pl) ? K_LLC : K_PAYLOAD, po, pl);
 			else NEXT(K_PAYLOAD, po, pl);
@@ -351,6 +353,9 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		if (len <= 8) break;
 		po = off + 8; pl = len - 8;
 		NEXT((udp_l7_port(be16(p), be16(p + 2)) || sip_heuristic(pkt + po, pl)) ? K_L7 : K_PAYLOAD, po, pl);
+		break;
+	case K_ARP: /* ArpLayer: dataLen := sizeof(arphdr) = 28 whatever remains, no next (ArpLayer.h:151-155,242-273) */
+		L.proto = P_ARP; L.osi = 3; L.hdr = 28; L.dlen = 28;
 		break;
 	case K_PAYLOAD: /* PayloadLayer: header = whole data, no next (PayloadLayer.h:61-81) */
 		L.proto = P_PAYLOAD; L.osi = 7; L.hdr = len;

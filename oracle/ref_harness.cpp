@@ -21,10 +21,12 @@
 #include "UdpLayer.h"
 #include "PacketUtils.h"
 #include "Logger.h"
+#include "PacketMatchingEngine.h"  // Examples/DpdkExample-FilterTraffic/PacketMatchingEngine.h (header-only)
 
 #include <chrono>
 #include <cstring>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace
@@ -150,6 +152,58 @@ namespace
 
 extern "C"
 {
+	// DpdkExample-FilterTraffic's per-packet worker loop (AppWorkerThread.h:85-139) over a host batch, with
+	// the real PacketMatchingEngine and hash5Tuple; PacketStats::collectStats is restated from
+	// Common.h:83-104 (Common.h itself includes DPDK headers). matched[i] = whether packet i was matched.
+	int pcppx_ref_filter(const pcppx_batch* b, const pcppx_match_spec* spec, uint8_t* matched,
+	                     pcppx_packet_stats* st)
+	{
+		if (b == nullptr || spec == nullptr || matched == nullptr || st == nullptr)
+			return PCPPX_E_INVAL;
+		pcpp::Logger::getInstance().suppressLogs();
+		Prepared p;
+		prepare(b, p);
+		PacketMatchingEngine engine(pcpp::IPv4Address(spec->src_ip), pcpp::IPv4Address(spec->dst_ip), spec->src_port,
+		                            spec->dst_port, static_cast<pcpp::ProtocolType>(spec->protocol));
+		std::unordered_map<uint32_t, bool> flowTable;
+		std::memset(st, 0, sizeof(*st));
+		for (uint32_t i = 0; i < b->n; ++i)
+		{
+			pcpp::Packet parsedPacket(&p.raws[i]);
+			st->packet_count++;
+			st->eth_count += parsedPacket.isPacketOfType(pcpp::Ethernet);
+			st->arp_count += parsedPacket.isPacketOfType(pcpp::ARP);
+			st->ipv4_count += parsedPacket.isPacketOfType(pcpp::IPv4);
+			st->ipv6_count += parsedPacket.isPacketOfType(pcpp::IPv6);
+			st->tcp_count += parsedPacket.isPacketOfType(pcpp::TCP);
+			st->udp_count += parsedPacket.isPacketOfType(pcpp::UDP);
+			st->http_count += parsedPacket.isPacketOfType(pcpp::HTTP);
+			st->dns_count += parsedPacket.isPacketOfType(pcpp::DNS);
+			st->tls_count += parsedPacket.isPacketOfType(pcpp::SSL);
+			bool packetMatched;
+			uint32_t hash = pcpp::hash5Tuple(&parsedPacket);
+			auto it = flowTable.find(hash);
+			if (it != flowTable.end() && it->second)
+				packetMatched = true;
+			else
+			{
+				packetMatched = engine.isMatched(parsedPacket);
+				if (packetMatched)
+				{
+					flowTable[hash] = true;
+					if (parsedPacket.isPacketOfType(pcpp::TCP))
+						st->matched_tcp_flows++;
+					else if (parsedPacket.isPacketOfType(pcpp::UDP))
+						st->matched_udp_flows++;
+				}
+			}
+			if (packetMatched)
+				st->matched_packets++;
+			matched[i] = packetMatched ? 1 : 0;
+		}
+		return PCPPX_OK;
+	}
+
 	// Parse a host batch with the reference Packet++ and fill host records.
 	int pcppx_ref_parse_batch(const pcppx_batch* b, const pcppx_opts* opts, pcppx_records* out)
 	{

@@ -92,6 +92,31 @@ class Records(C.Structure):
     _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p)]
 
 
+class MatchSpec(C.Structure):
+    """pcppx_match_spec: PacketMatchingEngine's criteria (PacketMatchingEngine.h:28-41)."""
+    _fields_ = [("src_ip", C.c_uint32), ("dst_ip", C.c_uint32), ("src_port", C.c_uint16), ("dst_port", C.c_uint16),
+                ("protocol", C.c_uint8), ("reserved", C.c_uint8 * 3)]
+
+
+STATS_FIELDS = ("packet_count", "eth_count", "arp_count", "ipv4_count", "ipv6_count", "tcp_count", "udp_count",
+                "http_count", "dns_count", "tls_count", "matched_tcp_flows", "matched_udp_flows", "matched_packets",
+                "needs_host_count")
+
+
+class PacketStats(C.Structure):
+    """pcppx_packet_stats: PacketStats (Examples/DpdkExample-FilterTraffic/Common.h:57-142)."""
+    _fields_ = [(f, C.c_uint64) for f in STATS_FIELDS]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f in STATS_FIELDS}
+
+
+def ipv4_to_int(dotted: str) -> int:
+    """IPv4Address::toInt(): the address bytes in memory order read as a little-endian u32."""
+    b = bytes(int(x) for x in dotted.split("."))
+    return int.from_bytes(b, "little")
+
+
 def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checksums: bool = True,
               max_layers: int = MAX_LAYERS, variant: int = 0) -> Opts:
     """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection."""
@@ -119,6 +144,22 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_parse_batch_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records), P]
     lib.pcppx_parse_batch_host.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records)]
     lib.pcppx_flow_count_device.argtypes = [P, P, P, C.c_uint32, P, P, P, C.c_uint32, P, P]
+    lib.pcppx_filter_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Records), C.c_uint8, C.POINTER(MatchSpec),
+                                        C.c_uint64, P, P, C.c_uint32, P, P, P]
+    lib.pcppx_filter_device.restype = C.c_int
+    lib.pcppx_pcap_open.argtypes = [C.c_char_p, C.POINTER(P)]
+    lib.pcppx_pcap_open.restype = C.c_int
+    lib.pcppx_pcap_linktype.argtypes = [P]
+    lib.pcppx_pcap_linktype.restype = C.c_uint32
+    lib.pcppx_pcap_read_batch.argtypes = [P, P, C.c_uint64, P, P, P, C.c_uint32, C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_uint64)]
+    lib.pcppx_pcap_read_batch.restype = C.c_int
+    lib.pcppx_pcap_close.argtypes = [P]
+    lib.pcppx_pcap_close.restype = None
+    lib.pcppx_host_alloc.argtypes = [C.c_size_t]
+    lib.pcppx_host_alloc.restype = P
+    lib.pcppx_host_free.argtypes = [P]
+    lib.pcppx_host_free.restype = None
     for name in ("pcppx_device_count", "pcppx_open", "pcppx_sync", "pcppx_parse_batch_device",
                  "pcppx_parse_batch_host", "pcppx_flow_count_device"):
         getattr(lib, name).restype = C.c_int
@@ -131,7 +172,8 @@ _ENGINE: C.CDLL | None = None
 EXPORTED_SYMBOLS = (
     "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_runtime_info", "pcppx_open", "pcppx_close",
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
-    "pcppx_flow_count_device",
+    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_pcap_open", "pcppx_pcap_linktype",
+    "pcppx_pcap_read_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
 )
 
 

@@ -327,6 +327,24 @@ extern "C"
 		return PCPPX_OK;
 	}
 
+	int pcppx_filter_device(pcppx_ctx* c, const pcppx_batch* b, const pcppx_records* r, uint8_t max_layers,
+	                        const pcppx_match_spec* spec, uint64_t seq_base, uint64_t* flow_keys, uint64_t* flow_first,
+	                        uint32_t capacity, uint8_t* matched, pcppx_packet_stats* stats, void* hip_stream)
+	{
+		if (c == nullptr || b == nullptr || r == nullptr || spec == nullptr || max_layers == 0 ||
+		    max_layers > PCPPX_MAX_LAYERS || capacity == 0 || (capacity & (capacity - 1)) != 0)
+			return PCPPX_E_INVAL;
+		if (b->n == 0)
+			return PCPPX_OK;
+		if (b->data == nullptr || b->offsets == nullptr || r->summary == nullptr || r->layers == nullptr ||
+		    flow_keys == nullptr || flow_first == nullptr || matched == nullptr || stats == nullptr)
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		return pcppx::launch_filter(b, r, max_layers, spec, seq_base, flow_keys, flow_first, capacity, matched, stats,
+		                            static_cast<hipStream_t>(hip_stream));
+	}
+
 	int pcppx_flow_count_device(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* caplens, uint32_t n,
 	                            uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity,
 	                            uint64_t* stats, void* hip_stream)

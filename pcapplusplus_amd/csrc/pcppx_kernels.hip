@@ -31,7 +31,7 @@ constexpr int kStageChunks = 8;  // 8 x 16 B = 128 B staged per packet
 // ProtocolType ids (Packet++/header/ProtocolType.h:42-258)
 enum : uint32_t
 {
-	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_VLAN = 9, P_MPLS = 14, P_GREV0 = 15,
+	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_MPLS = 14, P_GREV0 = 15,
 	P_GREV1 = 16, P_PPTP = 17, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44
 };
 
@@ -39,7 +39,7 @@ enum : uint32_t
 enum : uint32_t
 {
 	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
-	K_PAYLOAD, K_OUT, K_L7
+	K_PAYLOAD, K_OUT, K_L7, K_ARP
 };
 
 // explicit address spaces: keep packet reads as global_load / ds_read, never flat
@@ -83,6 +83,28 @@ __device__ __forceinline__ uint32_t le16(const Pkt& p, uint32_t j)
 __device__ __forceinline__ uint32_t le32(const Pkt& p, uint32_t j)
 {
 	return rb(p, j) | (rb(p, j + 1) << 8) | (rb(p, j + 2) << 16) | (rb(p, j + 3) << 24);
+}
+// bytes j..j+3 of the packet, little-endian, from the LDS window: one aligned dword pair and a
+// v_alignbyte. The slot's pad dword keeps both reads inside the slot; bytes at or past p.lim are
+// garbage and only used by callers that checked j + 4 <= p.lim (or mask them off).
+__device__ __forceinline__ uint32_t lds_u32(const Pkt& p, uint32_t j)
+{
+	const uint32_t pos = p.mis + j;
+	lptr32 w = reinterpret_cast<lptr32>(p.s) + (pos >> 2);
+	return __builtin_amdgcn_alignbyte(w[1], w[0], pos & 3);
+}
+__device__ __forceinline__ uint32_t swap16(uint32_t v)
+{
+	return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF);
+}
+// little-endian 32/16-bit reads of packet bytes that exist (< caplen): LDS when staged, else bytes
+__device__ __forceinline__ uint32_t rd32(const Pkt& p, uint32_t j)
+{
+	return j + 4 <= p.lim ? lds_u32(p, j) : le32(p, j);
+}
+__device__ __forceinline__ uint32_t rd16(const Pkt& p, uint32_t j)
+{
+	return j + 2 <= p.lim ? (lds_u32(p, j) & 0xFFFF) : le16(p, j);
 }
 
 // ---- validity predicates (isDataValid of each layer; cited in oracle/pcppx_oracle.c) ----
@@ -275,7 +297,8 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
 		else if (et == 0x8100 || et == 0x88A8) nk = pl >= 4 ? K_VLAN : K_PAYLOAD;
 		else if (et == 0x8847) nk = pl >= 4 ? K_MPLS : K_PAYLOAD;
-		else if (et == 0x0806 || et == 0x8864 || et == 0x8863 || et == 0x0842) nk = K_OUT;
+		else if (et == 0x0806) nk = pl >= 28 ? K_ARP : K_PAYLOAD;
+		else if (et == 0x8864 || et == 0x8863 || et == 0x0842) nk = K_OUT;
 		else nk = K_PAYLOAD;
 		break;
 	}
@@ -301,7 +324,8 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
 		else if (et == 0x8100 || et == 0x88A8) nk = K_VLAN;
 		else if (et == 0x8847) nk = K_MPLS;
-		else if (et == 0x0806 || et == 0x8864 || et == 0x8863) nk = K_OUT;
+		else if (et == 0x0806) nk = K_ARP;  // unchecked
+		else if (et == 0x8864 || et == 0x8863) nk = K_OUT;
 		else if (et < 1500) nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
 		else nk = K_PAYLOAD;
 		break;
@@ -435,6 +459,9 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 		nk = l7 ? K_L7 : K_PAYLOAD;
 		break;
 	}
+	case K_ARP:  // ArpLayer: dataLen := 28 whatever remains, no next (ArpLayer.h:151-155,242-273)
+		proto = P_ARP; osi = 3; hdr = 28; dlen = 28;
+		break;
 	default:  // K_PAYLOAD: PayloadLayer.h:61-81
 		proto = P_PAYLOAD; osi = 7; hdr = len;
 		break;
@@ -456,6 +483,7 @@ struct Params
 	uint32_t want_csum;
 	uint32_t max_layers;
 	uint32_t linktype;
+	uint32_t diag;  // 0 normal; 2 = stream-only diagnostic (no gather/parse; L4 range = [14, caplen))
 };
 
 // Everything the summary needs after the chain walk.
@@ -646,15 +674,16 @@ __device__ uint32_t ipv4_checksum(const Pkt& p, const Walk& w, uint32_t* stored)
 __device__ uint32_t l4_checksum(const Pkt& p, const Walk& w, uint32_t l4_residue, uint32_t* stored)
 {
 	const uint32_t field = w.is_tcp ? 16 : 6;
-	*stored = be16(p, w.l4o + field);
+	const uint32_t fw = rd16(p, w.l4o + field);  // the field as a little-endian stream word
+	*stored = swap16(fw);
 	uint32_t res = 0;
 	if (w.l4pp == P_IPV4 || w.l4pp == P_IPV6)
 	{
-		uint32_t r = (l4_residue + 65535u - mod65535(le16(p, w.l4o + field))) % 65535u;
+		uint32_t r = (l4_residue + 65535u - mod65535(fw)) % 65535u;
 		uint32_t ph = 0;
 		const uint32_t as = w.l4pp == P_IPV4 ? w.l4ppo + 12 : w.l4ppo + 8;
-		const uint32_t nw = w.l4pp == P_IPV4 ? 4 : 16;  // 16-bit words of src+dst
-		for (uint32_t j = 0; j < nw; ++j) ph += le16(p, as + 2 * j);
+		const uint32_t nd = w.l4pp == P_IPV4 ? 2 : 8;  // dwords of src+dst
+		for (uint32_t j = 0; j < nd; ++j) ph += halves(rd32(p, as + 4 * j));
 		ph += ((w.l4dlen & 0xFF) << 8) | ((w.l4dlen >> 8) & 0xFF);  // htobe16(dataLen)
 		ph += (w.is_tcp ? 6u : 17u) << 8;                              // htobe16(protocol)
 		r = (r + mod65535(ph)) % 65535u;
@@ -763,17 +792,6 @@ __global__ __launch_bounds__(kBlock) void parse_lane_kernel(Params prm)
 // it report "not applicable" and the generic walk_chain() runs instead. Results are identical to
 // walk_chain() by construction: same rules, same records (checked bit-exactly by tests/).
 
-// bytes j..j+3 of the packet, little-endian, from the LDS window (caller guarantees j + 4 <= p.lim)
-__device__ __forceinline__ uint32_t lds_u32(const Pkt& p, uint32_t j)
-{
-	const uint32_t pos = p.mis + j;
-	lptr32 w = reinterpret_cast<lptr32>(p.s) + (pos >> 2);
-	return __builtin_amdgcn_alignbyte(w[1], w[0], pos & 3);
-}
-__device__ __forceinline__ uint32_t swap16(uint32_t v)
-{
-	return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF);
-}
 
 struct Fast
 {
@@ -1001,7 +1019,7 @@ __device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Fast&
 constexpr int kTile = 64;
 constexpr int kTStageChunks = 7;                   // 112 B staged per packet
 constexpr int kTSlotDw = 4 * kTStageChunks + 1;    // + 1 pad dword against bank conflicts
-constexpr int kWin = 512;                          // prefix window: 512 chunks = 8 KiB of span
+constexpr int kSWin = 256;                         // stream window: 4 x 1 KiB wave-loads, double-buffered
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 {
@@ -1080,12 +1098,11 @@ __device__ uint32_t full_chunks_sum(uintptr_t c0, uintptr_t c1)
 
 __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 {
-	// stage doubles as the layer-record staging area at the end (64 rows x 16 layers x 8 B = 8 KiB)
-	__shared__ uint32_t stage[2048];
+	// stage doubles as the layer-record staging area at the end (64 rows x 17 padded records x 8 B)
+	__shared__ uint32_t stage[kTile * (PCPPX_MAX_LAYERS + 1) * 2];
 	__shared__ uint64_t m_a0[kTile];
 	__shared__ uint32_t m_nch[kTile];
-	__shared__ uint32_t pre[kWin];
-	static_assert(kTile * kTSlotDw <= 2048, "stage too small");
+	static_assert(kTile * kTSlotDw <= kTile * (PCPPX_MAX_LAYERS + 1) * 2, "stage too small");
 
 	const uint32_t lane = threadIdx.x;
 	const uint32_t i = blockIdx.x * kTile + lane;
@@ -1096,6 +1113,26 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 	const uint32_t bad = in ? desc_flags(off, cap, prm.data_len, &empty) : 0;
 	const bool live = in && !bad && !empty;
 
+	// ---- tile span for the L4 checksum stream: whole packets, known before the parse, so the first
+	// stream window is issued now and lands while the headers are gathered and parsed ----
+	const uint64_t pkt_addr = (uint64_t)(uintptr_t)prm.data + off;
+	const uint64_t smin = wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull);
+	const uint64_t emax = wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull);
+	const uint64_t wire = wave_sum_u64(live ? cap : 0);
+	const bool stream = prm.want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
+	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
+	uint4 va[kSWin / 64], vb[kSWin / 64];
+	auto load = [&](uint4 (&v)[kSWin / 64], uint32_t win) {
+#pragma unroll
+		for (int k = 0; k < kSWin / 64; ++k)
+		{
+			const uint32_t c = win * kSWin + 64 * k + lane;
+			v[k] = c < nchunks ? ld16(smin + 16ull * c) : make_uint4(0, 0, 0, 0);
+		}
+	};
+	if (stream)
+		load(va, 0);
+
 	// ---- (2) header gather into LDS ----
 	Pkt p;
 	p.g = (gptr8)(prm.data + (live ? off : 0));
@@ -1103,7 +1140,7 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
 	{
 		const uint32_t need = (p.mis + cap + 15) >> 4;
-		p.nch = live ? (need < kTStageChunks ? need : kTStageChunks) : 0;
+		p.nch = (live && prm.diag != 2) ? (need < kTStageChunks ? need : kTStageChunks) : 0;
 	}
 	m_a0[lane] = p.a0;
 	m_nch[lane] = p.nch;
@@ -1136,7 +1173,7 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 	p.s = reinterpret_cast<lptr8>((lptr32w)(stage) + lane * kTSlotDw);
 	{
 		const uint32_t staged = 16 * p.nch - p.mis;
-		p.lim = live ? (staged < cap ? staged : cap) : 0;
+		p.lim = (live && p.nch) ? (staged < cap ? staged : cap) : 0;
 	}
 
 	// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
@@ -1153,7 +1190,15 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 	Fast f;
 	bool fast = false;
 	uint32_t h5 = 0, h5d = 0, h2 = 0, ipc = 0, ips = 0, l4c = 0, l4s = 0;
-	if (live)
+	if (live && prm.diag == 2)
+	{
+		w.l4i = 0;
+		w.l4o = 14;
+		w.l4dlen = cap > 14 ? cap - 14 : 0;
+		w.is_tcp = true;
+		w.l4pp = 0;
+	}
+	else if (live)
 	{
 		fast = fast_walk(p, cap, prm, f);
 		if (fast)
@@ -1186,56 +1231,74 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 		const uintptr_t as = (uintptr_t)p.g + w.l4o, ae = as + w.l4dlen;
 		const uintptr_t f0 = (as + 15) & ~(uintptr_t)15, f1 = ae & ~(uintptr_t)15;
 		const bool full = need && f0 < f1;
-		const uint64_t smin = wave_min_u64(full ? (uint64_t)f0 : ~0ull);
-		const uint64_t emax = wave_max_u64(full ? (uint64_t)f1 : 0ull);
-		uint32_t fsum = 0;
-		if (emax > smin)
+		const bool tail = need && f0 <= f1 && f1 < ae;  // partial last chunk [f1, ae)
+		uint32_t fsum = 0, tsum = 0;
+		bool tail_done = false;
+		if (stream)
 		{
-			const uint64_t span = emax - smin;
-			const uint64_t wire = wave_sum_u64(live ? cap : 0);
-			if (span <= 2 * wire + 65536)
-			{
-				const uint32_t nchunks = (uint32_t)(span >> 4);
-				const uint32_t c0 = full ? (uint32_t)((f0 - smin) >> 4) : 0;
-				const uint32_t c1 = full ? (uint32_t)((f1 - smin) >> 4) : 0;
-				uint32_t carry = 0;
-				for (uint32_t w0 = 0; w0 < nchunks; w0 += kWin)
+			// Stream the tile span once, 4 x 1 KiB wave-loads per window, two register windows in
+			// flight. Per 64-chunk group: halves-sums -> DPP inclusive scan -> running prefix P; each
+			// lane picks P(c1-1) and P(c0-1) of its own whole-chunk L4 range and its partial tail chunk
+			// straight out of the owning lanes' registers (ds_bpermute), only in groups where some lane
+			// needs them.
+			const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
+			const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
+			const int32_t te = tail ? (int32_t)((f1 - smin) >> 4) : -2;      // tail chunk
+			uint32_t p0 = 0, p1 = 0, carry = 0;
+			const uint32_t nwin = (nchunks + kSWin - 1) / kSWin;
+			auto process = [&](uint4 (&v)[kSWin / 64], uint32_t win) {
+#pragma unroll
+				for (int k = 0; k < kSWin / 64; ++k)
 				{
-					const uint32_t carry_w0 = carry;
-					uint4 v[kWin / 64];
-#pragma unroll
-					for (int k = 0; k < kWin / 64; ++k)
+					const int32_t g = (int32_t)(win * kSWin + 64 * k);
+					const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+					const uint32_t x = wave_incl_scan(h);
+					const uint32_t pre = carry + x;
+					const bool in0 = t0 >= g && t0 < g + 64, in1 = t1 >= g && t1 < g + 64;
+					if (__ballot(in0 || in1))
 					{
-						const uint32_t c = w0 + 64 * k + lane;
-						v[k] = c < nchunks ? ld16(smin + 16ull * c) : make_uint4(0, 0, 0, 0);
+						const uint32_t q0 = __shfl(pre, (t0 - g) & 63, 64);
+						const uint32_t q1 = __shfl(pre, (t1 - g) & 63, 64);
+						p0 = in0 ? q0 : p0;
+						p1 = in1 ? q1 : p1;
 					}
-#pragma unroll
-					for (int k = 0; k < kWin / 64; ++k)
+					const bool ine = te >= g && te < g + 64;
+					if (__ballot(ine))
 					{
-						const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
-						const uint32_t x = wave_incl_scan(h);
-						pre[64 * k + lane] = carry + x;
-						carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+						const int src = (te - g) & 63;
+						const uint4 d = make_uint4(__shfl(v[k].x, src, 64), __shfl(v[k].y, src, 64),
+						                           __shfl(v[k].z, src, 64), __shfl(v[k].w, src, 64));
+						if (ine)
+						{
+							tsum = chunk_sum(d, f1, f1, ae);
+							tail_done = true;
+						}
 					}
-					__syncthreads();
-					if (full)
-					{
-						const uint32_t lo = c0 > w0 ? c0 : w0;
-						const uint32_t hi = c1 < w0 + kWin ? c1 : w0 + kWin;
-						if (lo < hi)
-							fsum += pre[hi - 1 - w0] - (lo > w0 ? pre[lo - 1 - w0] : carry_w0);
-					}
-					__syncthreads();
+					carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+				}
+			};
+			for (uint32_t wi = 0; wi < nwin; wi += 2)
+			{
+				if (wi + 1 < nwin)
+					load(vb, wi + 1);
+				process(va, wi);
+				if (wi + 1 < nwin)
+				{
+					if (wi + 2 < nwin)
+						load(va, wi + 2);
+					process(vb, wi + 1);
 				}
 			}
-			else if (full)
-				fsum = full_chunks_sum(f0, f1);
+			if (full)
+				fsum = p1 - p0;
 		}
+		else if (full)
+			fsum = full_chunks_sum(f0, f1);
 		if (need)
 		{
 			uint32_t acc = mod65535(fsum);
 			if (f0 <= f1)
-				acc += edge_sum(p, as, f0) + edge_sum(p, f1, ae);
+				acc += edge_sum(p, as, f0) + (tail_done ? tsum : edge_sum(p, f1, ae));
 			else
 				acc += edge_sum(p, as, ae);
 			uint32_t r = mod65535(acc);
@@ -1257,6 +1320,7 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 		typedef __attribute__((address_space(3))) u32x2* lptr64w;
 		lptr64w rows = (lptr64w)(stage);
+		const uint32_t rs = ml + 1;  // padded row stride (records): breaks the power-of-two bank pattern
 		if (fast)
 		{
 			const uint32_t cnt = w.n_layers;
@@ -1266,17 +1330,66 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 				u32x2 e;
 				e.x = r.x;
 				e.y = r.y;
-				rows[lane * ml + k] = e;
+				rows[lane * rs + k] = e;
 			}
 		}
 		__syncthreads();
 		const uint32_t first = blockIdx.x * kTile;
 		const uint32_t nrows = prm.n - first < (uint32_t)kTile ? prm.n - first : (uint32_t)kTile;
 		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)first * ml;
-		for (uint32_t q = lane; q < nrows * ml; q += kTile)
-			if (m_nch[q / ml])
-				dst[q] = rows[q];
+		// kTile / ml rows per pass, lane -> (row, record): consecutive lanes write consecutive records
+		const uint32_t per = kTile / ml, rr = lane / ml, kk = lane - rr * ml;
+		for (uint32_t r0 = 0; r0 < nrows; r0 += per)
+		{
+			const uint32_t r = r0 + rr;
+			if (rr < per && r < nrows && m_nch[r])
+				dst[r * ml + kk] = rows[r * rs + kk];
+		}
 	}
+}
+
+// ---- diagnostic streaming kernels (opts.variant 3/4): the read ceiling of the access pattern ----
+// variant 3: 64-lane blocks, each wave sums one contiguous tile-sized span (like the tile kernel);
+// variant 4: 256-lane blocks, grid-stride over the whole buffer, 4 x 16 B per lane in flight.
+__global__ __launch_bounds__(kTile) void diag_tile_read(const uint8_t* data, uint64_t len, uint32_t per_wave,
+                                                         uint32_t* out)
+{
+	const uint64_t base = (uint64_t)blockIdx.x * per_wave;
+	uint32_t acc = 0;
+	for (uint32_t c = threadIdx.x; 16ull * c < per_wave; c += 4 * kTile)
+	{
+		uint4 v[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+		{
+			const uint64_t a = base + 16ull * (c + k * kTile);
+			v[k] = a + 16 <= len ? ld16((uintptr_t)data + a) : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+	}
+	acc = wave_incl_scan(acc);
+	if (threadIdx.x == 63)
+		out[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, uint64_t len, uint32_t* out)
+{
+	const uint64_t nch = len / 16;
+	uint32_t acc = 0;
+	const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+	for (uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x; c < nch; c += 4 * stride)
+	{
+		uint4 v[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			v[k] = c + k * stride < nch ? ld16((uintptr_t)data + 16 * (c + k * stride)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+	}
+	out[blockIdx.x * kBlock + threadIdx.x] = acc;
 }
 
 // ---- per-flow counters keyed by hash5Tuple (FilterTraffic's flow table, AppWorkerThread.h:99-125) ----
@@ -1311,6 +1424,166 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 		slot = (slot + 1) & m;
 	}
 	atomicAdd(&stats[2], 1ull);
+}
+
+// ---- DpdkExample-FilterTraffic's worker on the device (AppWorkerThread.h:85-139) ----
+struct FilterParams
+{
+	const uint8_t* data;
+	const uint64_t* offsets;
+	const pcppx_summary* summary;
+	const pcppx_layer* layers;
+	uint32_t n, ml;
+	uint32_t src_ip, dst_ip, src_port, dst_port, protocol;
+	uint64_t seq_base;
+	unsigned long long* keys;
+	unsigned long long* first;
+	uint32_t capacity;
+	uint8_t* matched;
+	unsigned long long* stats;  // pcppx_packet_stats as 14 u64
+};
+
+// PacketMatchingEngine::isMatched (PacketMatchingEngine.h:43-107) over the engine's records: the first
+// IPv4 layer's addresses, the first TCP (else first UDP) layer's ports, isPacketOfType(TCP/UDP).
+__device__ bool filter_is_matched(const FilterParams& fp, uint32_t i, uint64_t mask, uint32_t nl)
+{
+	const bool m_sip = fp.src_ip != 0, m_dip = fp.dst_ip != 0, m_sp = fp.src_port != 0, m_dp = fp.dst_port != 0;
+	const bool m_proto = fp.protocol == P_TCP || fp.protocol == P_UDP;
+	if (!(m_sip || m_dip || m_sp || m_dp || m_proto))
+		return true;
+	const uint8_t* pkt = fp.data + fp.offsets[i];
+	int v4 = -1, tcp = -1, udp = -1;
+	const pcppx_layer* lay = fp.layers + (size_t)i * fp.ml;
+	for (uint32_t k = 0; k < nl; ++k)
+	{
+		const uint32_t pr = lay[k].proto;
+		const int o = (int)lay[k].offset;
+		if (pr == P_IPV4 && v4 < 0) v4 = o;
+		if (pr == P_TCP && tcp < 0) tcp = o;
+		if (pr == P_UDP && udp < 0) udp = o;
+	}
+	if (m_sip || m_dip)
+	{
+		if (!(mask & (1ull << P_IPV4)) || v4 < 0)
+			return false;
+		const uint32_t sip = pkt[v4 + 12] | (pkt[v4 + 13] << 8) | (pkt[v4 + 14] << 16) | ((uint32_t)pkt[v4 + 15] << 24);
+		const uint32_t dip = pkt[v4 + 16] | (pkt[v4 + 17] << 8) | (pkt[v4 + 18] << 16) | ((uint32_t)pkt[v4 + 19] << 24);
+		if (m_sip && sip != fp.src_ip)
+			return false;
+		if (m_dip && dip != fp.dst_ip)
+			return false;
+	}
+	if (m_sp || m_dp)
+	{
+		int l4 = -1;
+		if ((mask & (1ull << P_TCP)) && tcp >= 0) l4 = tcp;
+		else if ((mask & (1ull << P_UDP)) && udp >= 0) l4 = udp;
+		if (l4 < 0)
+			return false;
+		const uint32_t sp = (pkt[l4] << 8) | pkt[l4 + 1], dp = (pkt[l4 + 2] << 8) | pkt[l4 + 3];
+		if (m_sp && sp != fp.src_port)
+			return false;
+		if (m_dp && dp != fp.dst_port)
+			return false;
+	}
+	if (m_proto)
+	{
+		if (fp.protocol == P_TCP && !(mask & (1ull << P_TCP)))
+			return false;
+		if (fp.protocol == P_UDP && !(mask & (1ull << P_UDP)))
+			return false;
+	}
+	return true;
+}
+
+__device__ __forceinline__ uint32_t flow_mix(uint32_t key)
+{
+	return key * 0x9E3779B1u;
+}
+
+__global__ __launch_bounds__(kBlock) void filter_mark_kernel(FilterParams fp)
+{
+	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+	if (i >= fp.n)
+		return;
+	const pcppx_summary& sm = fp.summary[i];
+	const uint32_t nl = sm.n_layers < fp.ml ? sm.n_layers : fp.ml;
+	if (!filter_is_matched(fp, i, sm.proto_mask, nl))
+		return;
+	const unsigned long long key = (1ull << 32) | sm.hash5;
+	const uint32_t m = fp.capacity - 1;
+	uint32_t slot = flow_mix(sm.hash5) & m;
+	for (uint32_t probe = 0; probe < fp.capacity; ++probe)
+	{
+		const unsigned long long prev = atomicCAS(&fp.keys[slot], 0ull, key);
+		if (prev == 0ull || prev == key)
+		{
+			// stored as ~seq with atomicMax, so a zero-initialised table means "no match yet"
+			atomicMax(&fp.first[slot], ~(unsigned long long)(fp.seq_base + i));
+			return;
+		}
+		slot = (slot + 1) & m;
+	}
+}
+
+__device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred)
+{
+	const unsigned long long b = __ballot(pred);
+	if ((threadIdx.x & 63) == 0 && b)
+		atomicAdd(ctr, (unsigned long long)__popcll(b));
+}
+
+__global__ __launch_bounds__(kBlock) void filter_apply_kernel(FilterParams fp)
+{
+	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+	const bool in = i < fp.n;
+	uint64_t mask = 0;
+	uint32_t flags = 0;
+	bool matched = false, new_tcp = false, new_udp = false;
+	if (in)
+	{
+		const pcppx_summary& sm = fp.summary[i];
+		mask = sm.proto_mask;
+		flags = sm.flags;
+		const uint32_t nl = sm.n_layers < fp.ml ? sm.n_layers : fp.ml;
+		const bool own = filter_is_matched(fp, i, mask, nl);
+		const unsigned long long key = (1ull << 32) | sm.hash5;
+		const uint64_t seq = fp.seq_base + i;
+		const uint32_t m = fp.capacity - 1;
+		uint32_t slot = flow_mix(sm.hash5) & m;
+		uint64_t first = ~0ull;
+		for (uint32_t probe = 0; probe < fp.capacity; ++probe)
+		{
+			const unsigned long long kk = fp.keys[slot];
+			if (kk == key)
+			{
+				first = ~(uint64_t)fp.first[slot];
+				break;
+			}
+			if (kk == 0ull)
+				break;
+			slot = (slot + 1) & m;
+		}
+		matched = own || first < seq;
+		if (own && first == seq)  // the flow's first matching packet: a new matched flow
+		{
+			new_tcp = (mask & (1ull << P_TCP)) != 0;
+			new_udp = !new_tcp && (mask & (1ull << P_UDP)) != 0;
+		}
+		fp.matched[i] = matched ? 1 : 0;
+	}
+	unsigned long long* st = fp.stats;
+	wave_count(st + 0, in);
+	wave_count(st + 1, (mask >> P_ETH) & 1);
+	wave_count(st + 2, (mask >> P_ARP) & 1);
+	wave_count(st + 3, (mask >> P_IPV4) & 1);
+	wave_count(st + 4, (mask >> P_IPV6) & 1);
+	wave_count(st + 5, (mask >> P_TCP) & 1);
+	wave_count(st + 6, (mask >> P_UDP) & 1);
+	wave_count(st + 10, new_tcp);
+	wave_count(st + 11, new_udp);
+	wave_count(st + 12, matched);
+	wave_count(st + 13, in && (flags & PCPPX_F_NEEDS_HOST) != 0);
 }
 
 }  // namespace
@@ -1351,11 +1624,26 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	prm.want_csum = o->want_checksums;
 	prm.max_layers = o->max_layers;
 	prm.linktype = b->linktype;
+	prm.diag = o->variant == 2 ? 2 : 0;
 	// variant 1 (or PCPPX_KERNEL=lane) selects the lane-per-packet kernel for A/B measurements
 	static const bool lane_env = [] {
 		const char* e = getenv("PCPPX_KERNEL");
 		return e != nullptr && e[0] == 'l';
 	}();
+	if (o->variant == 3 || o->variant == 4)
+	{
+		// diagnostics write into the summary array (n * 32 bytes is ample)
+		uint32_t* out = reinterpret_cast<uint32_t*>(r->summary);
+		if (o->variant == 3)
+		{
+			const uint32_t per_wave = 21 * 1024;
+			const uint32_t blocks = (uint32_t)((b->data_len + per_wave - 1) / per_wave);
+			hipLaunchKernelGGL(diag_tile_read, dim3(blocks), dim3(kTile), 0, stream, b->data, b->data_len, per_wave, out);
+		}
+		else
+			hipLaunchKernelGGL(diag_grid_read, dim3(256 * 8), dim3(kBlock), 0, stream, b->data, b->data_len, out);
+		return check_launch("diag_read", stream);
+	}
 	if (o->variant == 1 || lane_env)
 	{
 		hipLaunchKernelGGL(parse_lane_kernel, dim3((b->n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, prm);
@@ -1363,6 +1651,39 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	}
 	hipLaunchKernelGGL(parse_tile_kernel, dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel", stream);
+}
+
+int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, const pcppx_match_spec* spec,
+                  uint64_t seq_base, uint64_t* keys, uint64_t* first, uint32_t capacity, uint8_t* matched,
+                  pcppx_packet_stats* stats, hipStream_t stream)
+{
+	if (b->n == 0)
+		return PCPPX_OK;
+	FilterParams fp;
+	fp.data = b->data;
+	fp.offsets = b->offsets;
+	fp.summary = r->summary;
+	fp.layers = r->layers;
+	fp.n = b->n;
+	fp.ml = ml;
+	fp.src_ip = spec->src_ip;
+	fp.dst_ip = spec->dst_ip;
+	fp.src_port = spec->src_port;
+	fp.dst_port = spec->dst_port;
+	fp.protocol = spec->protocol;
+	fp.seq_base = seq_base;
+	fp.keys = reinterpret_cast<unsigned long long*>(keys);
+	fp.first = reinterpret_cast<unsigned long long*>(first);
+	fp.capacity = capacity;
+	fp.matched = matched;
+	fp.stats = reinterpret_cast<unsigned long long*>(stats);
+	const dim3 grid((b->n + kBlock - 1) / kBlock);
+	hipLaunchKernelGGL(filter_mark_kernel, grid, dim3(kBlock), 0, stream, fp);
+	int rc = check_launch("filter_mark_kernel", stream);
+	if (rc != PCPPX_OK)
+		return rc;
+	hipLaunchKernelGGL(filter_apply_kernel, grid, dim3(kBlock), 0, stream, fp);
+	return check_launch("filter_apply_kernel", stream);
 }
 
 int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,

@@ -66,8 +66,64 @@ class Engine:
                                                    abi.ptr(packets), abi.ptr(bytes_), capacity, abi.ptr(stats),
                                                    C.c_void_p(stream or 0)), "pcppx_flow_count_device")
 
+    def filter_device(self, data, offsets, caplens, n: int, linktype: int, summary, layers, max_layers: int,
+                      spec: abi.MatchSpec, seq_base: int, flow_keys, flow_first, capacity: int, matched, stats,
+                      stream: int | None = None) -> None:
+        """FilterTraffic's worker over a parsed device batch (pcppx_filter_device). flow_keys/flow_first:
+        zero-initialised u64 tensors of `capacity` (power of two) slots kept across batches; matched: u8[n];
+        stats: 14 x u64 (abi.STATS_FIELDS order), accumulated."""
+        b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
+        rec = abi.Records(abi.ptr(summary), abi.ptr(layers))
+        abi.check(self.lib.pcppx_filter_device(self.ctx, C.byref(b), C.byref(rec), max_layers, C.byref(spec),
+                                               seq_base, abi.ptr(flow_keys), abi.ptr(flow_first), capacity,
+                                               abi.ptr(matched), abi.ptr(stats), C.c_void_p(stream or 0)),
+                  "pcppx_filter_device")
+
     def sync(self) -> None:
         abi.check(self.lib.pcppx_sync(self.ctx), "pcppx_sync")
+
+
+class PcapReader:
+    """Native pcap ingest (pcppx_pcap_*): records of a capture copied straight into packed batches.
+    Mirrors PcapFileReaderDevice (Pcap++/header/PcapFileDevice.h) open / getNextPackets / close."""
+
+    def __init__(self, path: str, pinned: bool = False):
+        self.lib = abi.load_engine()
+        self.handle = C.c_void_p()
+        abi.check(self.lib.pcppx_pcap_open(str(path).encode(), C.byref(self.handle)), f"pcppx_pcap_open({path})")
+        self.linktype = int(self.lib.pcppx_pcap_linktype(self.handle))
+        self.pinned = pinned
+
+    def read_batch(self, max_packets: int = 1 << 20, data_cap: int = 256 << 20) -> PacketBatch:
+        """Next batch of at most max_packets packets / data_cap bytes (n == 0 at end of file)."""
+        data = np.empty(data_cap, dtype=np.uint8)
+        offsets = np.empty(max_packets, dtype=np.uint64)
+        caplens = np.empty(max_packets, dtype=np.uint32)
+        ts = np.empty(max_packets, dtype=np.uint64)
+        n, used = C.c_uint32(0), C.c_uint64(0)
+        abi.check(self.lib.pcppx_pcap_read_batch(self.handle, data.ctypes.data, data_cap, offsets.ctypes.data,
+                                                 caplens.ctypes.data, ts.ctypes.data, max_packets, C.byref(n),
+                                                 C.byref(used)), "pcppx_pcap_read_batch")
+        k = n.value
+        return PacketBatch(data[: used.value].copy(), offsets[:k].copy(), caplens[:k].copy(), self.linktype,
+                           timestamps_ns=ts[:k].copy())
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.pcppx_pcap_close(self.handle)
+            self.handle = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def device_count() -> int:

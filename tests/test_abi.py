@@ -17,7 +17,7 @@ HEADER = abi.REPO_DIR / "include" / "pcppx.h"
 
 def declared_functions() -> list[str]:
     txt = HEADER.read_text()
-    return sorted(set(re.findall(r"^(?:int|void|void\*|const char\*)\s+(pcppx_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|void|void\*|uint32_t|const char\*)\s+(pcppx_\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_header_declares_expected_api():

@@ -28,6 +28,9 @@ cases = {
     "lane/ml8/csum": abi.make_opts(0, 8, True, 8, 1),
     "tile/ml0/csum": abi.make_opts(0, 8, True, 0, 0),
     "tile/ml8/nocsum": abi.make_opts(0, 8, False, 8, 0),
+    "tile/stream-only": abi.make_opts(0, 8, True, 0, 2),
+    "diag/tile-read": abi.make_opts(0, 8, True, 0, 3),
+    "diag/grid-read": abi.make_opts(0, 8, True, 0, 4),
 }
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")

@@ -10,7 +10,9 @@ rows = defaultdict(lambda: defaultdict(list))
 order = []
 for f in sorted(root.rglob("*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("::")[-1].split("(")[0]
+        kn = r["Kernel_Name"]
+        name = next((x for x in ("parse_tile_kernel", "parse_lane_kernel", "diag_tile_read", "diag_grid_read",
+                                 "flow_count_kernel") if x in kn), kn[:40])
         key = (name, int(r["Dispatch_Id"]) if False else 0, r["Grid_Size"])
         disp = (f.parent.name, r["Dispatch_Id"])
         rows[(name, r["Grid_Size"])][r["Counter_Name"]].append((disp, float(r["Counter_Value"]),
