@@ -176,6 +176,16 @@ int pcppx_filter_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_re
                         const pcppx_match_spec* spec, uint64_t seq_base, uint64_t* flow_keys, uint64_t* flow_first,
                         uint32_t capacity, uint8_t* matched, pcppx_packet_stats* stats, void* hip_stream);
 
+/* The same worker over host batches, with the flow table, packet sequence and statistics held by the
+ * context (one context = one worker, AppWorkerThread.h:45-162): packets are staged to HBM, parsed and
+ * filtered there; matched[i] = 1 for packets the worker would send on (AppWorkerThread.h:127-131).
+ * *stats (may be NULL) receives the statistics accumulated since the last pcppx_filter_reset.
+ * pcppx_filter_reset sizes (capacity: power of two, 0 = 4M slots) and clears the flow table; the first
+ * pcppx_filter_batch_host call does it implicitly. */
+int pcppx_filter_reset(pcppx_ctx* ctx, uint32_t capacity);
+int pcppx_filter_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_match_spec* spec,
+                            uint8_t* matched, pcppx_packet_stats* stats);
+
 /* ---- host ingest: pcap files into packed batch buffers ---- */
 typedef struct pcppx_pcap pcppx_pcap;
 int pcppx_pcap_open(const char* path, pcppx_pcap** out); /* PcapFileReaderDevice::open, PcapFileDevice.cpp:707-768 */

@@ -147,6 +147,10 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_filter_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Records), C.c_uint8, C.POINTER(MatchSpec),
                                         C.c_uint64, P, P, C.c_uint32, P, P, P]
     lib.pcppx_filter_device.restype = C.c_int
+    lib.pcppx_filter_reset.argtypes = [P, C.c_uint32]
+    lib.pcppx_filter_reset.restype = C.c_int
+    lib.pcppx_filter_batch_host.argtypes = [P, C.POINTER(Batch), C.POINTER(MatchSpec), P, C.POINTER(PacketStats)]
+    lib.pcppx_filter_batch_host.restype = C.c_int
     lib.pcppx_pcap_open.argtypes = [C.c_char_p, C.POINTER(P)]
     lib.pcppx_pcap_open.restype = C.c_int
     lib.pcppx_pcap_linktype.argtypes = [P]
@@ -172,7 +176,7 @@ _ENGINE: C.CDLL | None = None
 EXPORTED_SYMBOLS = (
     "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_runtime_info", "pcppx_open", "pcppx_close",
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
-    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_pcap_open", "pcppx_pcap_linktype",
+    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_pcap_open", "pcppx_pcap_linktype",
     "pcppx_pcap_read_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
 )
 

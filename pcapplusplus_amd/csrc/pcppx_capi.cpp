@@ -32,9 +32,13 @@ struct Slot
 	uint32_t* d_cap = nullptr;
 	pcppx_summary* d_sum = nullptr;
 	pcppx_layer* d_lay = nullptr;
+	uint8_t* h_match = nullptr;  // host filter path: per-packet verdicts
+	uint8_t* d_match = nullptr;
 	bool busy = false;
 	uint32_t first = 0, count = 0, ml = 0;
 };
+
+constexpr uint32_t kDefaultFlowSlots = 1u << 22;  // 64 MiB of flow table in HBM
 }  // namespace
 
 struct pcppx_ctx
@@ -43,6 +47,12 @@ struct pcppx_ctx
 	hipStream_t stream = nullptr;
 	bool host_ready = false;
 	Slot slots[2];
+	// host filter path (pcppx_filter_reset / pcppx_filter_batch_host): the worker's flow table in HBM
+	uint64_t* d_keys = nullptr;
+	uint64_t* d_first = nullptr;
+	pcppx_packet_stats* d_stats = nullptr;
+	uint32_t flow_slots = 0;
+	uint64_t seq = 0;
 };
 
 namespace
@@ -73,6 +83,8 @@ void free_slot(Slot& s)
 	(void)hipFree(s.d_cap);
 	(void)hipFree(s.d_sum);
 	(void)hipFree(s.d_lay);
+	(void)hipHostFree(s.h_match);
+	(void)hipFree(s.d_match);
 	s = Slot();
 }
 
@@ -94,7 +106,9 @@ int init_host_path(pcppx_ctx* c)
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_cap), kChunkPackets * sizeof(uint32_t))) &&
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_sum), kChunkPackets * sizeof(pcppx_summary))) &&
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_lay),
-		                         (size_t)kChunkPackets * PCPPX_MAX_LAYERS * sizeof(pcppx_layer)));
+		                         (size_t)kChunkPackets * PCPPX_MAX_LAYERS * sizeof(pcppx_layer))) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_match), kChunkPackets)) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_match), kChunkPackets));
 		if (!good)
 		{
 			for (Slot& t : c->slots)
@@ -104,6 +118,52 @@ int init_host_path(pcppx_ctx* c)
 	}
 	c->host_ready = true;
 	return PCPPX_OK;
+}
+
+// gather packets [i, j) of a host batch into the slot's pinned staging, rebasing offsets; returns j
+uint32_t stage_chunk(Slot& s, const pcppx_batch* b, uint32_t i, size_t* pos_out)
+{
+	size_t pos = 0;
+	uint32_t j = i;
+	while (j < b->n && j - i < kChunkPackets)
+	{
+		const uint64_t off = b->offsets[j];
+		const uint32_t cap = b->caplens[j];
+		const bool in_bounds = off + cap <= b->data_len && off + cap >= off;
+		const size_t take = in_bounds ? cap : 0;
+		if (pos + take > kChunkBytes && j > i)
+			break;
+		if (in_bounds && cap <= kChunkBytes)
+		{
+			std::memcpy(s.h_data + pos, b->data + off, cap);
+			s.h_off[j - i] = pos;
+			pos += cap;
+		}
+		else
+			s.h_off[j - i] = ~0ull >> 1;  // kernel flags PCPPX_F_BAD_DESC
+		s.h_cap[j - i] = cap;
+		++j;
+	}
+	*pos_out = pos;
+	return j;
+}
+
+bool upload_chunk(Slot& s, size_t pos, uint32_t cnt)
+{
+	return ok(hipMemcpyAsync(s.d_data, s.h_data, pos ? pos : 1, hipMemcpyHostToDevice, s.st)) &&
+	       ok(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint64_t), hipMemcpyHostToDevice, s.st)) &&
+	       ok(hipMemcpyAsync(s.d_cap, s.h_cap, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.st));
+}
+
+void free_filter(pcppx_ctx* c)
+{
+	(void)hipFree(c->d_keys);
+	(void)hipFree(c->d_first);
+	(void)hipFree(c->d_stats);
+	c->d_keys = c->d_first = nullptr;
+	c->d_stats = nullptr;
+	c->flow_slots = 0;
+	c->seq = 0;
 }
 
 // copy a finished chunk's records from pinned memory to the caller's arrays
@@ -213,6 +273,7 @@ extern "C"
 				(void)hipStreamSynchronize(s.st);
 			free_slot(s);
 		}
+		free_filter(c);
 		(void)hipStreamDestroy(c->stream);
 		delete c;
 	}
@@ -271,40 +332,17 @@ extern "C"
 					return PCPPX_E_HIP;
 				drain(s, r);
 			}
-			// gather packets [i, j) into pinned staging, rebasing offsets
 			size_t pos = 0;
-			uint32_t j = i;
-			while (j < b->n && j - i < kChunkPackets)
-			{
-				const uint64_t off = b->offsets[j];
-				const uint32_t cap = b->caplens[j];
-				const bool in_bounds = off + cap <= b->data_len && off + cap >= off;
-				const size_t take = in_bounds ? cap : 0;
-				if (pos + take > kChunkBytes && j > i)
-					break;
-				if (in_bounds && cap <= kChunkBytes)
-				{
-					std::memcpy(s.h_data + pos, b->data + off, cap);
-					s.h_off[j - i] = pos;
-					pos += cap;
-				}
-				else
-					s.h_off[j - i] = ~0ull >> 1;  // kernel flags PCPPX_F_BAD_DESC
-				s.h_cap[j - i] = cap;
-				++j;
-			}
+			const uint32_t j = stage_chunk(s, b, i, &pos);
 			const uint32_t cnt = j - i;
-			bool good = ok(hipMemcpyAsync(s.d_data, s.h_data, pos ? pos : 1, hipMemcpyHostToDevice, s.st)) &&
-			            ok(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint64_t), hipMemcpyHostToDevice, s.st)) &&
-			            ok(hipMemcpyAsync(s.d_cap, s.h_cap, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.st));
-			if (!good)
+			if (!upload_chunk(s, pos, cnt))
 				return PCPPX_E_HIP;
 			pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
 			pcppx_records dr{ s.d_sum, ml ? s.d_lay : nullptr };
 			rc = pcppx::launch_parse(&db, o, &dr, s.st);
 			if (rc != PCPPX_OK)
 				return rc;
-			good = ok(hipMemcpyAsync(s.h_sum, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
+			const bool good = ok(hipMemcpyAsync(s.h_sum, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
 			       (ml == 0 || ok(hipMemcpyAsync(s.h_lay, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer),
 			                                     hipMemcpyDeviceToHost, s.st))) &&
 			       ok(hipEventRecord(s.done, s.st));
@@ -343,6 +381,108 @@ extern "C"
 			return PCPPX_E_HIP;
 		return pcppx::launch_filter(b, r, max_layers, spec, seq_base, flow_keys, flow_first, capacity, matched, stats,
 		                            static_cast<hipStream_t>(hip_stream));
+	}
+
+	int pcppx_filter_reset(pcppx_ctx* c, uint32_t capacity)
+	{
+		if (c == nullptr || (capacity & (capacity - 1)) != 0)
+			return PCPPX_E_INVAL;
+		if (capacity == 0)
+			capacity = kDefaultFlowSlots;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		for (Slot& s : c->slots)
+			if (s.st && !ok(hipStreamSynchronize(s.st)))
+				return PCPPX_E_HIP;
+		if (capacity != c->flow_slots)
+		{
+			free_filter(c);
+			if (!ok(hipMalloc(reinterpret_cast<void**>(&c->d_keys), (size_t)capacity * 8)) ||
+			    !ok(hipMalloc(reinterpret_cast<void**>(&c->d_first), (size_t)capacity * 8)) ||
+			    !ok(hipMalloc(reinterpret_cast<void**>(&c->d_stats), sizeof(pcppx_packet_stats))))
+			{
+				free_filter(c);
+				return PCPPX_E_NOMEM;
+			}
+			c->flow_slots = capacity;
+		}
+		c->seq = 0;
+		const bool good = ok(hipMemsetAsync(c->d_keys, 0, (size_t)capacity * 8, c->stream)) &&
+		                  ok(hipMemsetAsync(c->d_first, 0, (size_t)capacity * 8, c->stream)) &&
+		                  ok(hipMemsetAsync(c->d_stats, 0, sizeof(pcppx_packet_stats), c->stream)) &&
+		                  ok(hipStreamSynchronize(c->stream));
+		return good ? PCPPX_OK : PCPPX_E_HIP;
+	}
+
+	int pcppx_filter_batch_host(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* spec, uint8_t* matched,
+	                            pcppx_packet_stats* stats)
+	{
+		if (c == nullptr || b == nullptr || spec == nullptr)
+			return PCPPX_E_INVAL;
+		if (b->n != 0 && (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || matched == nullptr))
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		int rc = c->flow_slots ? PCPPX_OK : pcppx_filter_reset(c, 0);
+		if (rc == PCPPX_OK)
+			rc = init_host_path(c);
+		if (rc != PCPPX_OK)
+			return rc;
+		pcppx_opts o;
+		pcppx_default_opts(&o);
+		o.want_checksums = 0;  // the worker reads addresses, ports and the protocol mask only
+		const uint32_t ml = o.max_layers;
+		uint32_t i = 0, k = 0;
+		Slot* prev = nullptr;
+		while (i < b->n)
+		{
+			Slot& s = c->slots[k & 1];
+			if (s.busy)
+			{
+				if (!ok(hipEventSynchronize(s.done)))
+					return PCPPX_E_HIP;
+				std::memcpy(matched + s.first, s.h_match, s.count);
+				s.busy = false;
+			}
+			size_t pos = 0;
+			const uint32_t j = stage_chunk(s, b, i, &pos);
+			const uint32_t cnt = j - i;
+			if (!upload_chunk(s, pos, cnt))
+				return PCPPX_E_HIP;
+			// the flow table is shared by consecutive chunks: chunk k's lookups run after chunk k-1's marks
+			if (prev != nullptr && !ok(hipStreamWaitEvent(s.st, prev->done, 0)))
+				return PCPPX_E_HIP;
+			pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
+			pcppx_records dr{ s.d_sum, s.d_lay };
+			rc = pcppx::launch_parse(&db, &o, &dr, s.st);
+			if (rc == PCPPX_OK)
+				rc = pcppx::launch_filter(&db, &dr, ml, spec, c->seq + i, c->d_keys, c->d_first, c->flow_slots,
+				                          s.d_match, c->d_stats, s.st);
+			if (rc != PCPPX_OK)
+				return rc;
+			if (!ok(hipMemcpyAsync(s.h_match, s.d_match, cnt, hipMemcpyDeviceToHost, s.st)) ||
+			    !ok(hipEventRecord(s.done, s.st)))
+				return PCPPX_E_HIP;
+			s.busy = true;
+			s.first = i;
+			s.count = cnt;
+			prev = &s;
+			i = j;
+			++k;
+		}
+		for (Slot& s : c->slots)
+			if (s.busy)
+			{
+				if (!ok(hipEventSynchronize(s.done)))
+					return PCPPX_E_HIP;
+				std::memcpy(matched + s.first, s.h_match, s.count);
+				s.busy = false;
+			}
+		c->seq += b->n;
+		if (stats != nullptr &&
+		    (!ok(hipMemcpy(stats, c->d_stats, sizeof(pcppx_packet_stats), hipMemcpyDeviceToHost))))
+			return PCPPX_E_HIP;
+		return PCPPX_OK;
 	}
 
 	int pcppx_flow_count_device(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* caplens, uint32_t n,

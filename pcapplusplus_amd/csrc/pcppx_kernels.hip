@@ -1019,7 +1019,7 @@ __device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Fast&
 constexpr int kTile = 64;
 constexpr int kTStageChunks = 7;                   // 112 B staged per packet
 constexpr int kTSlotDw = 4 * kTStageChunks + 1;    // + 1 pad dword against bank conflicts
-constexpr int kSWin = 256;                         // stream window: 4 x 1 KiB wave-loads, double-buffered
+constexpr int kSWin = 256;                         // default stream window: 4 x 1 KiB wave-loads, double-buffered
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 {
@@ -1096,13 +1096,19 @@ __device__ uint32_t full_chunks_sum(uintptr_t c0, uintptr_t c1)
 	return acc;
 }
 
-__global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
+constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_layers; beyond, direct stores
+
+// MinWaves: __launch_bounds__ minimum waves per SIMD (1 = compiler's choice). LDS is 8 KiB per block
+// (stage 7424 B + 768 B of per-lane state) so 20 blocks = 5 waves/SIMD fit a CU's 160 KiB.
+// SWin: stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers).
+template <int MinWaves, int SWin>
+__global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
-	// stage doubles as the layer-record staging area at the end (64 rows x 17 padded records x 8 B)
-	__shared__ uint32_t stage[kTile * (PCPPX_MAX_LAYERS + 1) * 2];
+	// stage doubles as the layer-record staging area at the end (64 rows x (ml+1) padded records x 8 B)
+	__shared__ uint32_t stage[kTile * kTSlotDw];
 	__shared__ uint64_t m_a0[kTile];
 	__shared__ uint32_t m_nch[kTile];
-	static_assert(kTile * kTSlotDw <= kTile * (PCPPX_MAX_LAYERS + 1) * 2, "stage too small");
+	static_assert(kTile * (kRowMaxMl + 1) * 2 <= kTile * kTSlotDw, "stage too small for layer rows");
 
 	const uint32_t lane = threadIdx.x;
 	const uint32_t i = blockIdx.x * kTile + lane;
@@ -1121,12 +1127,12 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 	const uint64_t wire = wave_sum_u64(live ? cap : 0);
 	const bool stream = prm.want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
 	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
-	uint4 va[kSWin / 64], vb[kSWin / 64];
-	auto load = [&](uint4 (&v)[kSWin / 64], uint32_t win) {
+	uint4 va[SWin / 64], vb[SWin / 64];
+	auto load = [&](uint4 (&v)[SWin / 64], uint32_t win) {
 #pragma unroll
-		for (int k = 0; k < kSWin / 64; ++k)
+		for (int k = 0; k < SWin / 64; ++k)
 		{
-			const uint32_t c = win * kSWin + 64 * k + lane;
+			const uint32_t c = win * SWin + 64 * k + lane;
 			v[k] = c < nchunks ? ld16(smin + 16ull * c) : make_uint4(0, 0, 0, 0);
 		}
 	};
@@ -1245,12 +1251,12 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 			const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
 			const int32_t te = tail ? (int32_t)((f1 - smin) >> 4) : -2;      // tail chunk
 			uint32_t p0 = 0, p1 = 0, carry = 0;
-			const uint32_t nwin = (nchunks + kSWin - 1) / kSWin;
-			auto process = [&](uint4 (&v)[kSWin / 64], uint32_t win) {
+			const uint32_t nwin = (nchunks + SWin - 1) / SWin;
+			auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
 #pragma unroll
-				for (int k = 0; k < kSWin / 64; ++k)
+				for (int k = 0; k < SWin / 64; ++k)
 				{
-					const int32_t g = (int32_t)(win * kSWin + 64 * k);
+					const int32_t g = (int32_t)(win * SWin + 64 * k);
 					const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
 					const uint32_t x = wave_incl_scan(h);
 					const uint32_t pre = carry + x;
@@ -1313,7 +1319,16 @@ __global__ __launch_bounds__(kTile) void parse_tile_kernel(Params prm)
 		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
 
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores ----
-	if (stage_layers)  // uniform
+	if (stage_layers && ml > kRowMaxMl)  // uniform: deep records, each fast lane stores its own row
+	{
+		if (fast)
+		{
+			uint2* dst = reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml;
+			for (uint32_t k = 0; k < ml; ++k)
+				dst[k] = k < w.n_layers ? fast_layer(f, cap, k) : make_uint2(0, 0);
+		}
+	}
+	else if (stage_layers)  // uniform
 	{
 		__syncthreads();  // every lane is done with the header stage
 		m_nch[lane] = fast ? 1u : 0u;
@@ -1649,7 +1664,16 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 		hipLaunchKernelGGL(parse_lane_kernel, dim3((b->n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, prm);
 		return check_launch("parse_lane_kernel", stream);
 	}
-	hipLaunchKernelGGL(parse_tile_kernel, dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
+	const dim3 grid((b->n + kTile - 1) / kTile);
+	// A/B variants: 5 = 5 waves/SIMD, 6 = 128-chunk window, 7 = both
+	if (o->variant == 5)
+		hipLaunchKernelGGL((parse_tile_kernel<5, kSWin>), grid, dim3(kTile), 0, stream, prm);
+	else if (o->variant == 6)
+		hipLaunchKernelGGL((parse_tile_kernel<1, 128>), grid, dim3(kTile), 0, stream, prm);
+	else if (o->variant == 7)
+		hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm);
+	else
+		hipLaunchKernelGGL((parse_tile_kernel<1, kSWin>), grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel", stream);
 }
 

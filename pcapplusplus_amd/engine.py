@@ -79,6 +79,19 @@ class Engine:
                                                abi.ptr(matched), abi.ptr(stats), C.c_void_p(stream or 0)),
                   "pcppx_filter_device")
 
+    def filter_reset(self, capacity: int = 0) -> None:
+        abi.check(self.lib.pcppx_filter_reset(self.ctx, capacity), "pcppx_filter_reset")
+
+    def filter_host(self, batch: PacketBatch, spec: abi.MatchSpec):
+        """FilterTraffic's worker over a host batch (context-held flow table): (matched u8[n], stats dict
+        accumulated since the last filter_reset)."""
+        matched = np.zeros(max(batch.n, 1), dtype=np.uint8)
+        st = abi.PacketStats()
+        b = batch.c_batch()
+        abi.check(self.lib.pcppx_filter_batch_host(self.ctx, C.byref(b), C.byref(spec), matched.ctypes.data,
+                                                   C.byref(st)), "pcppx_filter_batch_host")
+        return matched[: batch.n], st.as_dict()
+
     def sync(self) -> None:
         abi.check(self.lib.pcppx_sync(self.ctx), "pcppx_sync")
 

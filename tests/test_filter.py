@@ -184,3 +184,35 @@ def test_gpu_filter_rejects_bad_args(engine):
         engine.filter_device(t, t, t, 4, 1, t, t, 8, spec, 0, t, t, 6, t, t)
     with pytest.raises(RuntimeError):  # max_layers 0: no layer records to read addresses from
         engine.filter_device(t, t, t, 4, 1, t, t, 0, spec, 0, t, t, 8, t, t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batch", batches(), ids=lambda x: x if isinstance(x, str) else "")
+def test_gpu_filter_host(engine, name, batch):
+    """pcppx_filter_batch_host: the context-held flow table across two calls, stats cumulative."""
+    b = device_finishable(batch)
+    s, lay = oracle.oracle_parse(b, OPTS)
+    for spec in specs_for(b, 2)[:5]:
+        engine.filter_reset(1 << 12)
+        half = b.n // 2
+        m0, _ = engine.filter_host(b.slice(0, half), spec)
+        m1, gst = engine.filter_host(b.slice(half, b.n), spec)
+        om, ost = oracle.oracle_filter(b, s, lay, spec)
+        assert np.array_equal(np.concatenate([m0, m1]), om)
+        compare_stats(gst, ost)
+
+
+@pytest.mark.gpu
+def test_gpu_filter_host_multichunk(engine):
+    """A batch larger than one host-path chunk (256K packets): chunks share the flow table in order."""
+    b = synth.imix(600_000, 17, flows=20_000, corrupt_frac=0.0)
+    spec = specs_for(b.slice(0, 20000), 9)[5]
+    engine.filter_reset(0)
+    gm, gst = engine.filter_host(b, spec)
+    if oracle.ref_available():
+        rm, rst = oracle.ref_filter(b, spec)
+    else:
+        s, lay = oracle.oracle_parse(b, OPTS, threads=8)
+        rm, rst = oracle.oracle_filter(b, s, lay, spec)
+    assert np.array_equal(gm, rm)
+    compare_stats(gst, rst)

@@ -28,6 +28,9 @@ cases = {
     "lane/ml8/csum": abi.make_opts(0, 8, True, 8, 1),
     "tile/ml0/csum": abi.make_opts(0, 8, True, 0, 0),
     "tile/ml8/nocsum": abi.make_opts(0, 8, False, 8, 0),
+    "tile/w5": abi.make_opts(0, 8, True, 8, 5),
+    "tile/win128": abi.make_opts(0, 8, True, 8, 6),
+    "tile/w5win128": abi.make_opts(0, 8, True, 8, 7),
     "tile/stream-only": abi.make_opts(0, 8, True, 0, 2),
     "diag/tile-read": abi.make_opts(0, 8, True, 0, 3),
     "diag/grid-read": abi.make_opts(0, 8, True, 0, 4),
@@ -36,6 +39,23 @@ import os  # noqa: E402
 only = os.environ.get("AB_CASES")
 if only:
     cases = {k: v for k, v in cases.items() if k in only.split(",")}
+# records of every full variant must equal the default tile kernel's, byte for byte
+ref_s = ref_l = None
+for name, o in cases.items():
+    if o.max_layers != 8 or not o.want_checksums or o.variant in (2, 3, 4):
+        continue
+    summ.zero_()
+    lay.zero_()
+    eng.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream)
+    torch.cuda.synchronize()
+    if ref_s is None:
+        ref_s, ref_l = summ.clone(), lay[: n * 64].clone()
+    else:
+        same = torch.equal(summ, ref_s) and torch.equal(lay[: n * 64], ref_l)
+        print(f"{name:18s} records identical to first variant: {same}", flush=True)
+        if not same:
+            raise SystemExit(f"{name}: records differ")
+del ref_s, ref_l
 times = {k: [] for k in cases}
 for r in range(rounds):
     for name, o in cases.items():
