@@ -501,7 +501,7 @@ struct Walk
 // Packet::parsePacket (Packet.cpp:66-196): first layer by link type (createFirstLayer :827-923), the
 // parseNextLayer chain with the parse-until stop rules (:123-175), and the trailer (:178-195).
 // Layer records go straight to lay_out (uint2 per layer) when it is non-null.
-__device__ Walk walk_chain(const Pkt& p, uint32_t cap, const Params& prm, uint2* lay_out)
+__device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Params& prm, uint2* lay_out)
 {
 	uint32_t flags = 0;
 	uint32_t k;
@@ -609,7 +609,7 @@ __device__ Walk walk_chain(const Pkt& p, uint32_t cap, const Params& prm, uint2*
 }
 
 // hash5Tuple (both directions) and hash2Tuple, PacketUtils.cpp:139-245
-__device__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
+__device__ __forceinline__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
 {
 	h5 = h5d = h2 = 0;
 	if (w.v4 < 0 && w.v6 < 0)
@@ -657,7 +657,7 @@ __device__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5, uint32_t& h5d,
 
 // IPv4 header checksum (IPv4Layer.cpp:410-412): computeChecksum over min(IHL*4, dataLen) header bytes
 // with the checksum field zeroed. Returns calc; *stored gets the field.
-__device__ uint32_t ipv4_checksum(const Pkt& p, const Walk& w, uint32_t* stored)
+__device__ __forceinline__ uint32_t ipv4_checksum(const Pkt& p, const Walk& w, uint32_t* stored)
 {
 	const uint32_t o = (uint32_t)w.v4;
 	uint32_t hl = (rb(p, o) & 0xF) * 4;
@@ -671,7 +671,7 @@ __device__ uint32_t ipv4_checksum(const Pkt& p, const Walk& w, uint32_t* stored)
 // {Tcp,Udp}Layer::calculateChecksum(false) (TcpLayer.cpp:271-311, UdpLayer.cpp:47-90) given the
 // residue of the L4 bytes as a stream: subtract the checksum field, add the pseudo header
 // (computePseudoHdrChecksum, PacketUtils.cpp:66-112), fold; UDP maps 0 to 0xFFFF.
-__device__ uint32_t l4_checksum(const Pkt& p, const Walk& w, uint32_t l4_residue, uint32_t* stored)
+__device__ __forceinline__ uint32_t l4_checksum(const Pkt& p, const Walk& w, uint32_t l4_residue, uint32_t* stored)
 {
 	const uint32_t field = w.is_tcp ? 16 : 6;
 	const uint32_t fw = rd16(p, w.l4o + field);  // the field as a little-endian stream word
@@ -941,7 +941,7 @@ __device__ __forceinline__ uint32_t fnv4(uint32_t h, uint32_t v)
 	return fnv(h, v >> 24);
 }
 
-__device__ void fast_hashes(const Pkt& p, const Fast& f, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
+__device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
 {
 	uint32_t s[4], d[4];
 	const uint32_t na = f.v6 ? 4 : 1;
@@ -1051,6 +1051,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
 	}
 	return v;
 }
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
+{
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+	return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
 {
 	for (int m = 32; m >= 1; m >>= 1)
@@ -1122,9 +1128,10 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	// ---- tile span for the L4 checksum stream: whole packets, known before the parse, so the first
 	// stream window is issued now and lands while the headers are gathered and parsed ----
 	const uint64_t pkt_addr = (uint64_t)(uintptr_t)prm.data + off;
-	const uint64_t smin = wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull);
-	const uint64_t emax = wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull);
-	const uint64_t wire = wave_sum_u64(live ? cap : 0);
+	// wave reductions are uniform: moved to SGPRs so the window loop is a scalar loop
+	const uint64_t smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
+	const uint64_t emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
+	const uint64_t wire = uniform_u64(wave_sum_u64(live ? cap : 0));
 	const bool stream = prm.want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
 	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
 	uint4 va[SWin / 64], vb[SWin / 64];
@@ -1132,8 +1139,10 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 #pragma unroll
 		for (int k = 0; k < SWin / 64; ++k)
 		{
+			// clamped, not masked: lanes past the span re-read its last chunk (same line, no extra
+			// traffic); their values lie after every prefix target, so they are inert
 			const uint32_t c = win * SWin + 64 * k + lane;
-			v[k] = c < nchunks ? ld16(smin + 16ull * c) : make_uint4(0, 0, 0, 0);
+			v[k] = ld16(smin + 16ull * (c < nchunks ? c : nchunks - 1));
 		}
 	};
 	if (stream)
@@ -1283,17 +1292,15 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 					carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 				}
 			};
+			// straight-line body (windows padded to an even count; loads past the span are clamped) so
+			// the compiler's vmcnt accounting sees one fixed issue order: one window always in flight
+			load(vb, 1);
 			for (uint32_t wi = 0; wi < nwin; wi += 2)
 			{
-				if (wi + 1 < nwin)
-					load(vb, wi + 1);
 				process(va, wi);
-				if (wi + 1 < nwin)
-				{
-					if (wi + 2 < nwin)
-						load(va, wi + 2);
-					process(vb, wi + 1);
-				}
+				load(va, wi + 2);
+				process(vb, wi + 1);
+				load(vb, wi + 3);
 			}
 			if (full)
 				fsum = p1 - p0;
@@ -1665,15 +1672,17 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 		return check_launch("parse_lane_kernel", stream);
 	}
 	const dim3 grid((b->n + kTile - 1) / kTile);
-	// A/B variants: 5 = 5 waves/SIMD, 6 = 128-chunk window, 7 = both
+	// default: 5 waves/SIMD (96 VGPRs, 8 KiB LDS) with 2 x 2 KiB stream windows -- measured fastest
+	// (profiles/r01_ab_occupancy.txt). A/B variants: 5 = 5 waves + 4 KiB windows, 6 = compiler's
+	// occupancy + 2 KiB windows, 8 = compiler's occupancy + 4 KiB windows (the round-1 first cut).
 	if (o->variant == 5)
-		hipLaunchKernelGGL((parse_tile_kernel<5, kSWin>), grid, dim3(kTile), 0, stream, prm);
+		hipLaunchKernelGGL((parse_tile_kernel<5, 256>), grid, dim3(kTile), 0, stream, prm);
 	else if (o->variant == 6)
 		hipLaunchKernelGGL((parse_tile_kernel<1, 128>), grid, dim3(kTile), 0, stream, prm);
-	else if (o->variant == 7)
-		hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm);
+	else if (o->variant == 8)
+		hipLaunchKernelGGL((parse_tile_kernel<1, 256>), grid, dim3(kTile), 0, stream, prm);
 	else
-		hipLaunchKernelGGL((parse_tile_kernel<1, kSWin>), grid, dim3(kTile), 0, stream, prm);
+		hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel", stream);
 }
 

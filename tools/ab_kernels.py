@@ -28,9 +28,9 @@ cases = {
     "lane/ml8/csum": abi.make_opts(0, 8, True, 8, 1),
     "tile/ml0/csum": abi.make_opts(0, 8, True, 0, 0),
     "tile/ml8/nocsum": abi.make_opts(0, 8, False, 8, 0),
-    "tile/w5": abi.make_opts(0, 8, True, 8, 5),
-    "tile/win128": abi.make_opts(0, 8, True, 8, 6),
-    "tile/w5win128": abi.make_opts(0, 8, True, 8, 7),
+    "tile/w5win256": abi.make_opts(0, 8, True, 8, 5),
+    "tile/w4win128": abi.make_opts(0, 8, True, 8, 6),
+    "tile/w4win256": abi.make_opts(0, 8, True, 8, 8),
     "tile/stream-only": abi.make_opts(0, 8, True, 0, 2),
     "diag/tile-read": abi.make_opts(0, 8, True, 0, 3),
     "diag/grid-read": abi.make_opts(0, 8, True, 0, 4),
