@@ -1,9 +1,17 @@
 """bench.py — device-resident Packet++ parse throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2]): a 10M-packet IMIX batch (64/512/1500 B at
-7:4:1; 25% VLAN; 70% IPv4 / 30% IPv6; TCP/UDP 50/50; 1% corrupted checksums), synthetic, seed 3 (+rank).
+Default workload (BASELINE.json configs[2]): a 10M-packet IMIX batch (64/512/1500 B
+at 7:4:1; 25% VLAN; 70% IPv4 / 30% IPv6; TCP/UDP 50/50; 1% corrupted checksums), synthetic, seed 3 (+rank).
 One step = one pass of the parse kernel over the whole batch already resident in HBM: layer chain
 (8 layer records/packet), hash5Tuple both directions, hash2Tuple, IPv4 + TCP/UDP checksum verify.
+
+--config selects the other BASELINE configs as extra bench lines (not the driver's default):
+  2: 1M x 64 B Eth/IPv4/{TCP,UDP}: parse + hash5Tuple (5-tuple extract), no checksums;
+  4: 12.5M IMIX packets/GPU with Zipf(1.1) 5-tuples over 1M flows: parse + hash5Tuple + per-flow
+     {packets, bytes} counters in an HBM flow table (DpdkExample-FilterTraffic's flow table);
+  5: 10M deep-encapsulation packets (QinQ / MPLS stacks / GREv0 / IPv6 extension chains): parse + hashes.
+Without checksums the algorithmic read is each packet's header extent (end of its last L2-L4 header,
+SURVEY.md §8d) + the 12-B descriptor, computed from the records the kernel wrote.
 
 Multi-GPU: one process per GPU (torch.distributed, launched by torch.distributed.run); packets are
 independent, so each rank parses its own 10M-packet shard with no data-path collective ("weak").
@@ -32,10 +40,11 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--packets", type=int, default=10_000_000, help="packets per GPU")
-    ap.add_argument("--config", type=int, default=3, choices=(2, 3, 4))
-    ap.add_argument("--max-layers", type=int, default=8)
-    ap.add_argument("--no-checksums", action="store_true")
+    ap.add_argument("--packets", type=int, default=None, help="packets per GPU (default: the config's size)")
+    ap.add_argument("--config", type=int, default=3, choices=(2, 3, 4, 5))
+    ap.add_argument("--max-layers", type=int, default=None, help="layer records per packet (default 8; 12 for config 5)")
+    ap.add_argument("--checksums", choices=("auto", "on", "off"), default="auto",
+                    help="IPv4/L4 checksum verify (auto: on for config 3 only)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="packets in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min CPU-baseline time (repeat passes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -45,12 +54,37 @@ def parse_args():
     return ap.parse_args()
 
 
-def algorithmic_read_bytes(batch, want_checksums: bool, summary) -> int:
-    """checksum runs read every caplen byte; otherwise bytes up to the end of the last
-    parsed L2-L4 header; plus a 12-B descriptor per packet."""
+CONFIG_PACKETS = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000_000}
+WORKLOADS = {
+    2: "config 2: 64 B Eth/IPv4/{TCP,UDP} 50/50; parse + hash5Tuple/hash2Tuple (5-tuple extract)",
+    3: "config 3: IMIX 64/512/1500 B 7:4:1, 25% VLAN, 70/30 IPv4/IPv6, TCP/UDP 50/50, 1% bad checksums; "
+       "parse + hashes + IPv4/L4 checksum verify",
+    4: "config 4: IMIX as config 3 with 5-tuples Zipf(1.1) over 1M flows, both directions; parse + hash5Tuple + "
+       "per-flow {packets, bytes} counters (FilterTraffic flow table)",
+    5: "config 5: deep encapsulation (QinQ, 1-3 MPLS labels, GREv0 C/K/S over IPv4|IPv6, IPv6 1-3 extension "
+       "headers) then TCP/UDP, 64/512/1500 B; parse + hashes",
+}
+
+
+def algorithmic_read_bytes(batch, want_checksums: bool, summary=None, layers=None, caplens=None,
+                           max_layers: int = 0) -> int:
+    """checksum runs read every caplen byte; otherwise the bytes up to the end of the last
+    parsed L2-L4 header (from the layer records: max over non-Payload, non-Trailer layers of offset +
+    hdr_len, capped at caplen); plus a 12-B descriptor per packet."""
     if want_checksums:
         return int(batch.caplens.sum(dtype=np.int64)) + DESC_BYTES * batch.n
-    raise NotImplementedError("no-checksum byte model needs the header extent")
+    import torch
+
+    n, ml = batch.n, max_layers
+    lay = layers[: n * ml * 8].view(n, ml, 8).to(torch.int32)
+    proto = lay[:, :, 0]
+    end = (lay[:, :, 2] | (lay[:, :, 3] << 8)) + (lay[:, :, 4] | (lay[:, :, 5] << 8))
+    nl = summary.view(n, 32)[:, 14].to(torch.int32)
+    k = torch.arange(ml, device=layers.device, dtype=torch.int32)
+    valid = (k[None, :] < nl[:, None]) & (proto != 25) & (proto != 30)
+    ext = torch.where(valid, end, torch.zeros_like(end)).amax(dim=1)
+    ext = torch.minimum(ext, caplens.to(torch.int32))
+    return int(ext.sum(dtype=torch.int64).item()) + DESC_BYTES * n
 
 
 def cpu_baseline(batch, opts, sample: int, min_seconds: float) -> dict:
@@ -72,7 +106,8 @@ def cpu_baseline(batch, opts, sample: int, min_seconds: float) -> dict:
     return {"value": round(total_p / total_t / 1e6, 3), "unit": "Mpackets/s", "cores": threads, "kind": kind,
             "sample": f"first {sub.n} packets of the same batch, {total_p // sub.n} passes, "
                       f"{total_t:.1f} s; {'reference Packet++ built from source' if kind == 'reference' else 'C restatement'}"
-                      f": Packet(&raw) + hash5Tuple x2 + hash2Tuple + IPv4/L4 checksums, {threads} threads"}
+                      f": Packet(&raw) + hash5Tuple x2 + hash2Tuple"
+                      f"{' + IPv4/L4 checksums' if opts.want_checksums else ''}, {threads} threads"}
 
 
 def main() -> None:
@@ -94,26 +129,43 @@ def main() -> None:
     torch.cuda.set_device(dev)
 
     # ---- synthetic shard for this rank (per-GPU work fixed: weak scaling) ----
+    cfg = args.config
+    npk = args.packets or CONFIG_PACKETS[cfg]
+    ml = args.max_layers if args.max_layers is not None else (12 if cfg == 5 else 8)
     t0 = time.time()
-    if args.config == 3:
-        batch = synth.imix(args.packets, shard.shard_seed(3, rank))
-    elif args.config == 4:
-        batch = synth.imix(args.packets, shard.shard_seed(4, rank), flows=1_000_000, corrupt_frac=0.0)
+    seed = shard.shard_seed(cfg, rank)
+    if cfg == 3:
+        batch = synth.imix(npk, seed)
+    elif cfg == 4:
+        batch = synth.imix(npk, seed, flows=1_000_000, corrupt_frac=0.0)
+    elif cfg == 5:
+        batch = synth.deep(npk, seed)
     else:
-        batch = synth.small64(args.packets, shard.shard_seed(2, rank))
+        batch = synth.small64(npk, seed)
     gen_s = time.time() - t0
-    want_csum = not args.no_checksums
-    opts = abi.make_opts(0, 8, want_csum, args.max_layers)
+    want_csum = args.checksums == "on" or (args.checksums == "auto" and cfg == 3)
+    opts = abi.make_opts(0, 8, want_csum, ml)
     n = batch.n
     eng = Engine(local)
     data, offsets, caplens = to_device(batch, dev)
     summary = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-    layers = torch.empty(max(n * args.max_layers, 1) * 8, dtype=torch.uint8, device=dev)
+    layers = torch.empty(max(n * ml, 1) * 8, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    flows = None
+    if cfg == 4:  # per-GPU flow table: 2M slots for 1M flows, counters accumulate over all steps
+        cap = 1 << 21
+        flows = (torch.zeros(cap, dtype=torch.int32, device=dev), torch.zeros(cap, dtype=torch.int64, device=dev),
+                 torch.zeros(cap, dtype=torch.int64, device=dev), torch.zeros(4, dtype=torch.int64, device=dev), cap)
+    mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if flows else None
 
-    def step():
+    def step(k=None):
         eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh)
+        if flows is not None:
+            if k is not None:
+                mids[k].record(stream)
+            keys, pk, by, st, cap = flows
+            eng.flow_count_device(summary, caplens, n, keys, pk, by, cap, st, sh)
 
     for _ in range(args.warmup):
         step()
@@ -126,14 +178,17 @@ def main() -> None:
     w0 = time.perf_counter()
     for k in range(args.steps):
         starts[k].record(stream)
-        step()
+        step(k)
         ends[k].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - w0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    step_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    # the parse kernel is the dominant kernel of every config; config 4 also runs the flow-table kernel
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, mids)])) if mids else step_ms
+    flow_ms = step_ms - kern_ms if mids else None
 
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -142,8 +197,8 @@ def main() -> None:
     total_packets = n * world * args.steps
     mpps = total_packets / wall_max / 1e6
     wire = int(batch.caplens.sum(dtype=np.int64))
-    read_bytes = algorithmic_read_bytes(batch, want_csum, None)
-    write_bytes = n * (32 + 8 * args.max_layers)
+    read_bytes = algorithmic_read_bytes(batch, want_csum, summary, layers, caplens, ml)
+    write_bytes = n * (32 + 8 * ml)
     achieved = read_bytes / (kern_ms * 1e-3) / 1e9
 
     # sanity: the records of the last step parse every packet cleanly (synthetic data has no L7 triggers)
@@ -156,7 +211,8 @@ def main() -> None:
     if tp.exists():
         try:
             tj = json.loads(tp.read_text())
-            if tj.get("packets") == n and tj.get("config") == args.config and tj.get("max_layers") == args.max_layers:
+            if tj.get("packets") == n and tj.get("config") == cfg and tj.get("max_layers") == ml and \
+                    tj.get("checksums", True) == want_csum:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
@@ -170,6 +226,14 @@ def main() -> None:
         e2e_t = time.perf_counter() - t1
         e2e = {"Mpackets_per_s": round(sub.n / e2e_t / 1e6, 2),
                "wire_GBps": round(int(sub.caplens.sum(dtype=np.int64)) / e2e_t / 1e9, 2), "packets": sub.n}
+
+    flow_check = None
+    if flows is not None:  # every packet of every launch is counted once: table + key-0 bucket
+        keys, pk, by, st, cap = flows
+        counted = int(pk.sum().item()) + int(st[0].item())
+        flow_check = {"flows": int((keys != 0).sum().item()), "packets_counted": counted,
+                      "expected": n * (args.warmup + args.steps), "table_full_drops": int(st[2].item()),
+                      "flow_kernel_ms": round(flow_ms, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -190,16 +254,15 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"config {args.config}: {n} packets/GPU " + (
-                    "IMIX 64/512/1500 B 7:4:1, 25% VLAN, 70/30 IPv4/IPv6, TCP/UDP 50/50, 1% bad checksums"
-                    if args.config == 3 else "see synth.py"),
+                "workload": f"{n} packets/GPU, " + WORKLOADS[cfg],
                 "packets_per_gpu": n,
                 "wire_bytes_per_gpu": wire,
                 "checksums": want_csum,
-                "max_layers": args.max_layers,
+                "max_layers": ml,
                 "parallelism": f"shard{world} (no collective)",
                 "wire_GBps": round(wire * world * args.steps / wall_max / 1e9, 2),
                 "kernel_ms": round(kern_max, 4),
+                "step_kernel_ms": round(step_ms, 4),
                 "flagged_packets": flagged,
                 "gen_seconds": round(gen_s, 1),
             },
@@ -217,6 +280,8 @@ def main() -> None:
         }
         if e2e is not None:
             line["e2e_host_to_host"] = e2e
+        if flow_check is not None:
+            line["config"]["flow_table"] = flow_check
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

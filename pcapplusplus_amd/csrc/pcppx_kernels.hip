@@ -1019,7 +1019,6 @@ __device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Fast&
 constexpr int kTile = 64;
 constexpr int kTStageChunks = 7;                   // 112 B staged per packet
 constexpr int kTSlotDw = 4 * kTStageChunks + 1;    // + 1 pad dword against bank conflicts
-constexpr int kSWin = 256;                         // default stream window: 4 x 1 KiB wave-loads, double-buffered
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 {
@@ -1415,37 +1414,102 @@ __global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, ui
 }
 
 // ---- per-flow counters keyed by hash5Tuple (FilterTraffic's flow table, AppWorkerThread.h:99-125) ----
+// A block aggregates 1024 packets at a time in an LDS hash table (LDS atomics), then adds one
+// {packets, bytes} pair per distinct flow to the HBM table: Zipf-skewed traffic puts a hot flow in most
+// packets of a batch, and per-packet global atomics on its slot would serialise.
+constexpr uint32_t kFlowLds = 2048;                 // LDS slots per block (>= 2x the packets of a batch)
+constexpr uint32_t kFlowBatch = 4 * kBlock;         // packets aggregated between two flushes
+constexpr uint32_t kFlowGrid = 1024;                // persistent blocks (4 per CU)
+
 __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
                                                             unsigned long long* bytes, uint32_t capacity,
                                                             unsigned long long* stats)
 {
-	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-	if (i >= n)
-		return;
-	const uint32_t key = sum[i].hash5;
-	const unsigned long long len = caplens[i];
-	if (key == 0)
-	{
-		atomicAdd(&stats[0], 1ull);
-		atomicAdd(&stats[1], len);
-		return;
-	}
+	__shared__ uint32_t s_key[kFlowLds];
+	__shared__ uint32_t s_pk[kFlowLds];
+	__shared__ unsigned long long s_by[kFlowLds];
+	const uint32_t t = threadIdx.x;
 	const uint32_t m = capacity - 1;
-	uint32_t slot = (key * 0x9E3779B1u) & m;
-	for (uint32_t probe = 0; probe < capacity; ++probe)
+	unsigned long long z_pk = 0, z_by = 0, lost = 0;  // flow key 0 (PacketUtils.cpp:141-148); table full
+	for (uint32_t j = t; j < kFlowLds; j += kBlock)
 	{
-		uint32_t prev = atomicCAS(&keys[slot], 0u, key);
-		if (prev == 0u || prev == key)
-		{
-			atomicAdd(&packets[slot], 1ull);
-			atomicAdd(&bytes[slot], len);
-			return;
-		}
-		slot = (slot + 1) & m;
+		s_key[j] = 0;
+		s_pk[j] = 0;
+		s_by[j] = 0;
 	}
-	atomicAdd(&stats[2], 1ull);
+	__syncthreads();
+	for (uint64_t base = (uint64_t)blockIdx.x * kFlowBatch; base < n; base += (uint64_t)gridDim.x * kFlowBatch)
+	{
+#pragma unroll
+		for (uint32_t r = 0; r < kFlowBatch / kBlock; ++r)
+		{
+			const uint64_t i = base + r * kBlock + t;
+			if (i >= n)
+				break;
+			const uint32_t key = sum[i].hash5;
+			const uint32_t len = caplens[i];
+			if (key == 0)
+			{
+				z_pk += 1;
+				z_by += len;
+				continue;
+			}
+			uint32_t slot = (key * 0x9E3779B1u) >> 21;  // top 11 bits
+			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
+			{
+				const uint32_t prev = atomicCAS(&s_key[slot], 0u, key);
+				if (prev == 0u || prev == key)
+				{
+					atomicAdd(&s_pk[slot], 1u);
+					atomicAdd(&s_by[slot], (unsigned long long)len);
+					break;
+				}
+				slot = (slot + 1) & (kFlowLds - 1);
+			}
+		}
+		__syncthreads();
+		for (uint32_t j = t; j < kFlowLds; j += kBlock)
+		{
+			const uint32_t key = s_key[j];
+			if (key == 0)
+				continue;
+			uint32_t slot = (key * 0x9E3779B1u) & m;
+			bool done = false;
+			for (uint32_t probe = 0; probe < capacity; ++probe)
+			{
+				const uint32_t prev = atomicCAS(&keys[slot], 0u, key);
+				if (prev == 0u || prev == key)
+				{
+					atomicAdd(&packets[slot], (unsigned long long)s_pk[j]);
+					atomicAdd(&bytes[slot], s_by[j]);
+					done = true;
+					break;
+				}
+				slot = (slot + 1) & m;
+			}
+			if (!done)
+				lost += s_pk[j];
+			s_key[j] = 0;
+			s_pk[j] = 0;
+			s_by[j] = 0;
+		}
+		__syncthreads();
+	}
+	z_pk = wave_sum_u64(z_pk);
+	z_by = wave_sum_u64(z_by);
+	lost = wave_sum_u64(lost);
+	if ((t & 63) == 0)
+	{
+		if (z_pk)
+		{
+			atomicAdd(&stats[0], z_pk);
+			atomicAdd(&stats[1], z_by);
+		}
+		if (lost)
+			atomicAdd(&stats[2], lost);
+	}
 }
 
 // ---- DpdkExample-FilterTraffic's worker on the device (AppWorkerThread.h:85-139) ----
@@ -1675,6 +1739,7 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	// default: 5 waves/SIMD (96 VGPRs, 8 KiB LDS) with 2 x 2 KiB stream windows -- measured fastest
 	// (profiles/r01_ab_occupancy.txt). A/B variants: 5 = 5 waves + 4 KiB windows, 6 = compiler's
 	// occupancy + 2 KiB windows, 8 = compiler's occupancy + 4 KiB windows (the round-1 first cut).
+	// Window size is measured not to matter (profiles/r01_ab_windows.txt).
 	if (o->variant == 5)
 		hipLaunchKernelGGL((parse_tile_kernel<5, 256>), grid, dim3(kTile), 0, stream, prm);
 	else if (o->variant == 6)
@@ -1724,7 +1789,8 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 {
 	if (n == 0)
 		return PCPPX_OK;
-	dim3 grid((n + kBlock - 1) / kBlock);
+	const uint32_t batches = (n + kFlowBatch - 1) / kFlowBatch;
+	dim3 grid(batches < kFlowGrid ? batches : kFlowGrid);
 	hipLaunchKernelGGL(flow_count_kernel, grid, dim3(kBlock), 0, stream, sum, caplens, n, keys,
 	                   reinterpret_cast<unsigned long long*>(packets), reinterpret_cast<unsigned long long*>(bytes),
 	                   capacity, reinterpret_cast<unsigned long long*>(stats));

@@ -9,6 +9,8 @@ TcpLayer.cpp:372-491 / UdpLayer.cpp:103-178), then laid back to back in a random
   config 3: 10M IMIX 64/512/1500 B at 7:4:1, 25% single VLAN, 70% IPv4 / 30% IPv6 (64 B: IPv6/UDP
             without VLAN only), TCP/UDP 50/50, 1% corrupted checksums, seed 3
   config 4: IMIX as config 3 with 5-tuples drawn Zipf(1.1) over a flow table, both directions, seed 4
+  config 5: deep encapsulation -- QinQ, 1-3 MPLS labels, GREv0 (C/K/S) over IPv4/IPv6, IPv6 with 1-3
+            extension headers -- then TCP/UDP, 64/512/1500 B, seed 5
 """
 from __future__ import annotations
 
@@ -60,6 +62,76 @@ def _fold_checksum(s: np.ndarray) -> np.ndarray:
     return res.astype(np.uint16)
 
 
+def _be32(a: np.ndarray) -> np.ndarray:
+    a = a.astype(np.uint64)
+    return np.stack([(a >> 24) & 0xFF, (a >> 16) & 0xFF, (a >> 8) & 0xFF, a & 0xFF], axis=1).astype(np.uint8)
+
+
+def _ipv4_header(rows: np.ndarray, ip: int, proto: int, total: int) -> None:
+    """IPv4 header without options at column ip (addresses and id keep their random bytes); the checksum
+    is set by _ipv4_checksum once every header byte is final."""
+    n = rows.shape[0]
+    rows[:, ip] = 0x45
+    rows[:, ip + 1] = 0
+    rows[:, ip + 2:ip + 4] = _be16(np.full(n, total))
+    rows[:, ip + 6] = 0x40  # DF, offset 0
+    rows[:, ip + 7] = 0
+    rows[:, ip + 8] = 64
+    rows[:, ip + 9] = proto
+    rows[:, ip + 10:ip + 12] = 0
+
+
+def _ipv4_checksum(rows: np.ndarray, ip: int) -> None:
+    rows[:, ip + 10:ip + 12] = 0
+    c = _fold_checksum(_le_word_sum(rows[:, ip:ip + 20]))
+    rows[:, ip + 10] = (c & 0xFF).astype(np.uint8)
+    rows[:, ip + 11] = (c >> 8).astype(np.uint8)
+
+
+def _ipv6_header(rows: np.ndarray, ip: int, next_header: int, payload_len: int) -> None:
+    n = rows.shape[0]
+    rows[:, ip] = 0x60 | (rows[:, ip] & 0x0F)
+    rows[:, ip + 4:ip + 6] = _be16(np.full(n, payload_len))
+    rows[:, ip + 6] = next_header
+    rows[:, ip + 7] = 64
+
+
+def _put_l4(rows: np.ndarray, ip: int, ipv6: bool, l4o: int, tcp: bool, sport: np.ndarray,
+            dport: np.ndarray) -> None:
+    """TCP (20 B) or UDP header at l4o with a valid checksum over the rest of the row, the pseudo header
+    taken from the IP header at ip (computePseudoHdrChecksum, PacketUtils.cpp:66-112)."""
+    n, size = rows.shape
+    l4len = size - l4o
+    proto = 6 if tcp else 17
+    rows[:, l4o:l4o + 2] = _be16(sport)
+    rows[:, l4o + 2:l4o + 4] = _be16(dport)
+    if tcp:
+        rows[:, l4o + 12] = 0x50
+        rows[:, l4o + 13] = 0x18
+        rows[:, l4o + 16:l4o + 20] = 0
+        cs = l4o + 16
+    else:
+        rows[:, l4o + 4:l4o + 6] = _be16(np.full(n, l4len))
+        rows[:, l4o + 6:l4o + 8] = 0
+        cs = l4o + 6
+        # keep the UDP payload clear of the SIP content heuristic (SipLayer.cpp:127-160)
+        if l4len - 8 >= 4:
+            head = rows[:, l4o + 8:l4o + 12].copy().view(">u4").ravel()
+            keys = np.array([int.from_bytes(k, "big") for k in SIP_KEYS], dtype=np.uint32)
+            hit = np.isin(head, keys)
+            rows[hit, l4o + 8] ^= 0x80
+    s = _le_word_sum(rows[:, l4o:])
+    addr_lo, addr_hi = (ip + 8, ip + 40) if ipv6 else (ip + 12, ip + 20)
+    s += _le_word_sum(rows[:, addr_lo:addr_hi])
+    s += np.uint64(((l4len & 0xFF) << 8) | (l4len >> 8))
+    s += np.uint64(proto << 8)
+    c = _fold_checksum(s)
+    if not tcp:
+        c = np.where(c == 0, np.uint16(0xFFFF), c)
+    rows[:, cs] = (c & 0xFF).astype(np.uint8)
+    rows[:, cs + 1] = (c >> 8).astype(np.uint8)
+
+
 def build_rows(rng: np.random.Generator, n: int, size: int, vlan: bool, ipv6: bool, tcp: bool,
                tuples: dict | None = None) -> np.ndarray:
     """n packets of `size` bytes: Eth [VLAN] IPv4|IPv6 TCP|UDP + random payload, valid checksums."""
@@ -82,7 +154,6 @@ def build_rows(rng: np.random.Generator, n: int, size: int, vlan: bool, ipv6: bo
     rows[:, 0] &= 0xFE  # unicast dst
     ip = l2
     l4o = l2 + l3
-    l4len = size - l4o
     if tuples is not None:
         src_ip, dst_ip, sport, dport = tuples["src"], tuples["dst"], tuples["sport"], tuples["dport"]
     else:
@@ -90,58 +161,150 @@ def build_rows(rng: np.random.Generator, n: int, size: int, vlan: bool, ipv6: bo
         sport, dport = safe_ports(rng, n), safe_ports(rng, n)
     proto = 6 if tcp else 17
     if ipv6:
-        rows[:, ip] = 0x60 | (rows[:, ip] & 0x0F)
-        rows[:, ip + 4:ip + 6] = _be16(np.full(n, l4len))
-        rows[:, ip + 6] = proto
-        rows[:, ip + 7] = 64
+        _ipv6_header(rows, ip, proto, size - l4o)
         if src_ip is not None:
             rows[:, ip + 8:ip + 24] = src_ip
             rows[:, ip + 24:ip + 40] = dst_ip
     else:
-        rows[:, ip] = 0x45
-        rows[:, ip + 1] = 0
-        rows[:, ip + 2:ip + 4] = _be16(np.full(n, size - l2))
-        rows[:, ip + 6] = 0x40  # DF, offset 0
-        rows[:, ip + 7] = 0
-        rows[:, ip + 8] = 64
-        rows[:, ip + 9] = proto
-        rows[:, ip + 10:ip + 12] = 0
+        _ipv4_header(rows, ip, proto, size - l2)
         if src_ip is not None:
             rows[:, ip + 12:ip + 16] = src_ip
             rows[:, ip + 16:ip + 20] = dst_ip
-        c = _fold_checksum(_le_word_sum(rows[:, ip:ip + 20]))
-        rows[:, ip + 10] = (c & 0xFF).astype(np.uint8)
-        rows[:, ip + 11] = (c >> 8).astype(np.uint8)
-    rows[:, l4o:l4o + 2] = _be16(sport)
-    rows[:, l4o + 2:l4o + 4] = _be16(dport)
-    if tcp:
-        rows[:, l4o + 12] = 0x50
-        rows[:, l4o + 13] = 0x18
-        rows[:, l4o + 16:l4o + 18] = 0
-        rows[:, l4o + 18:l4o + 20] = 0
-        cs = l4o + 16
-    else:
-        rows[:, l4o + 4:l4o + 6] = _be16(np.full(n, l4len))
-        rows[:, l4o + 6:l4o + 8] = 0
-        cs = l4o + 6
-        # keep the UDP payload clear of the SIP content heuristic (SipLayer.cpp:127-160)
-        if size - l4o - 8 >= 4:
-            head = rows[:, l4o + 8:l4o + 12].copy().view(">u4").ravel()
-            keys = np.array([int.from_bytes(k, "big") for k in SIP_KEYS], dtype=np.uint32)
-            hit = np.isin(head, keys)
-            rows[hit, l4o + 8] ^= 0x80
-    # pseudo header (computePseudoHdrChecksum, PacketUtils.cpp:66-112)
-    s = _le_word_sum(rows[:, l4o:])
-    addr_lo, addr_hi = (ip + 8, ip + 40) if ipv6 else (ip + 12, ip + 20)
-    s += _le_word_sum(rows[:, addr_lo:addr_hi])
-    s += np.uint64(((l4len & 0xFF) << 8) | (l4len >> 8))
-    s += np.uint64(proto << 8)
-    c = _fold_checksum(s)
-    if not tcp:
-        c = np.where(c == 0, np.uint16(0xFFFF), c)
-    rows[:, cs] = (c & 0xFF).astype(np.uint8)
-    rows[:, cs + 1] = (c >> 8).astype(np.uint8)
+        _ipv4_checksum(rows, ip)
+    _put_l4(rows, ip, ipv6, l4o, tcp, sport, dport)
     return rows
+
+
+# ---- config 5: deep encapsulation ----
+K5_PLAIN, K5_MPLS, K5_GRE, K5_EXT = 0, 1, 2, 3
+# IPv6 extension chains: (extension ids, Hdr Ext Len byte of each); 0 Hop-by-Hop, 60 Destination,
+# 43 Routing use 8*(len+1) bytes, 44 Fragment 8 (IPv6Extensions.h:40-43); a last Fragment header makes the
+# rest a Payload (IPv6Layer.cpp:194-312)
+DEEP_EXT = (((0,), (0,)), ((60,), (1,)), ((43,), (2,)), ((0, 60), (0, 1)), ((0, 43), (1, 0)),
+            ((43, 60), (0, 0)), ((0, 43, 60), (0, 1, 0)), ((0, 44), (0, 0)), ((60, 44), (2, 0)),
+            ((0, 60, 44), (0, 0, 0)))
+# template variants per kind: plain 1; MPLS 1-3 labels; GRE outer IPv4/IPv6 (bit 3) x C/K/S option bits
+# (bits 0-2); IPv6 extension chain index
+DEEP_VARIANTS = (1, 3, 16, len(DEEP_EXT))
+
+
+def _deep_hlen(l2: int, kind: int, var: int, inner_v6: bool, tcp: bool) -> int:
+    h = 14 + 4 * l2
+    if kind == K5_MPLS:
+        h += 4 * (var + 1)
+    elif kind == K5_GRE:
+        h += (40 if var >> 3 else 20) + 4 + 4 * bin(var & 7).count("1")
+    if kind == K5_EXT:
+        chain, hls = DEEP_EXT[var]
+        h += 40 + sum(8 if t == 44 else 8 * (hl + 1) for t, hl in zip(chain, hls))
+    else:
+        h += 40 if inner_v6 else 20
+    return h + (20 if tcp else 8)
+
+
+def build_deep_rows(rng: np.random.Generator, n: int, size: int, l2: int, kind: int, var: int, inner_v6: bool,
+                    tcp: bool) -> np.ndarray:
+    """n packets of `size` bytes with one config-5 stack: Ethernet, then none / one 802.1Q tag / QinQ
+    (0x88A8 + 0x8100), then plain IP, an MPLS label stack (1-3), IPv4|IPv6 + GREv0 with C/K/S options, or
+    IPv6 with extension headers, then TCP|UDP + random payload. Valid IPv4 header and L4 checksums."""
+    rows = np.frombuffer(rng.bytes(n * size), dtype=np.uint8).reshape(n, size).copy()
+    rows[:, 0] &= 0xFE
+    v6 = inner_v6 or kind == K5_EXT
+    inner_et = 0x86DD if v6 else 0x0800
+    if kind == K5_MPLS:
+        et = 0x8847
+    elif kind == K5_GRE:
+        et = 0x86DD if var >> 3 else 0x0800
+    else:
+        et = inner_et
+    tags = (0x88A8, 0x8100)[2 - l2:] if l2 else ()
+    seq = (*tags, et)
+    rows[:, 12:14] = _be16(np.full(n, seq[0]))
+    pos = 14
+    for t in range(len(tags)):
+        rows[:, pos:pos + 2] = _be16(rng.integers(1, 4095, size=n))
+        rows[:, pos + 2:pos + 4] = _be16(np.full(n, seq[t + 1]))
+        pos += 4
+    v4 = []
+    if kind == K5_MPLS:  # label(20) TC(3) S(1) TTL(8); S is bit 0 of byte 2 (MplsLayer.cpp:25-28)
+        for k in range(var + 1):
+            label = rng.integers(16, 1 << 20, size=n, dtype=np.int64)
+            rows[:, pos:pos + 4] = _be32((label << 12) | ((1 if k == var else 0) << 8) | 64)
+            pos += 4
+    elif kind == K5_GRE:  # GREv0: C 0x80, K 0x20, S 0x10 of byte 0 (GreLayer.h:14-57)
+        if var >> 3:
+            _ipv6_header(rows, pos, 47, size - pos - 40)
+            pos += 40
+        else:
+            _ipv4_header(rows, pos, 47, size - pos)
+            v4.append(pos)
+            pos += 20
+        flags = var & 7
+        rows[:, pos] = (0x80 if flags & 1 else 0) | (0x20 if flags & 2 else 0) | (0x10 if flags & 4 else 0)
+        rows[:, pos + 1] = 0
+        rows[:, pos + 2:pos + 4] = _be16(np.full(n, inner_et))
+        pos += 4 + 4 * bin(flags).count("1")
+    ip = pos
+    proto = 6 if tcp else 17
+    if kind == K5_EXT:
+        chain, hls = DEEP_EXT[var]
+        _ipv6_header(rows, ip, chain[0], size - ip - 40)
+        e = ip + 40
+        for t, nh, hl in zip(chain, (*chain[1:], proto), hls):
+            rows[:, e] = nh
+            rows[:, e + 1] = 0 if t == 44 else hl
+            e += 8 if t == 44 else 8 * (hl + 1)
+        l4o = e
+    elif v6:
+        _ipv6_header(rows, ip, proto, size - ip - 40)
+        l4o = ip + 40
+    else:
+        _ipv4_header(rows, ip, proto, size - ip)
+        v4.append(ip)
+        l4o = ip + 20
+    _put_l4(rows, ip, v6, l4o, tcp, safe_ports(rng, n), safe_ports(rng, n))
+    for h in v4:
+        _ipv4_checksum(rows, h)
+    return rows
+
+
+def _deep_decode(c: int) -> tuple[int, int, int, bool, bool]:
+    tcp, c = c & 1, c >> 1
+    v6, c = c & 1, c >> 1
+    var, c = c % 16, c // 16
+    return int(c // 4), int(c % 4), int(var), bool(v6), bool(tcp)
+
+
+def deep(n: int, seed: int = 5, sizes=IMIX_SIZES, weights=IMIX_WEIGHTS) -> PacketBatch:
+    """Config 5: deep-encapsulation stress. Sizes 64/512/1500 B at 7:4:1 where the stack fits (else
+    512 B); stacks (build_deep_rows): plain IP 10%, MPLS 30%, GRE 30%, IPv6 extensions 30%; no tag 30%,
+    one VLAN tag 20%, QinQ 50%; inner IPv4/IPv6 50/50; TCP/UDP 50/50."""
+    rng = np.random.default_rng(seed)
+    w = np.array(weights, dtype=np.float64)
+    size_idx = rng.choice(len(sizes), size=n, p=w / w.sum())
+    l2 = rng.choice(3, size=n, p=[0.3, 0.2, 0.5])
+    kind = rng.choice(4, size=n, p=[0.1, 0.3, 0.3, 0.3])
+    var = rng.integers(0, 1 << 30, size=n) % np.array(DEEP_VARIANTS)[kind]
+    inner_v6 = (rng.random(n) < 0.5) | (kind == K5_EXT)
+    tcp = rng.random(n) < 0.5
+    code = ((((l2 * 4 + kind) * 16 + var) * 2 + inner_v6) * 2 + tcp).astype(np.int64)
+    codes, inv = np.unique(code, return_inverse=True)
+    hlen = np.array([_deep_hlen(*_deep_decode(int(c))) for c in codes])[inv]
+    size_idx = np.where(np.array(sizes)[size_idx] < hlen, 1, size_idx)
+    key = code * len(sizes) + size_idx
+    order = np.argsort(key, kind="stable")
+    ukeys, starts = np.unique(key[order], return_index=True)
+    bounds = np.append(starts, n)
+    groups = []
+    for g, k in enumerate(ukeys):
+        c, si = divmod(int(k), len(sizes))
+        idx = order[bounds[g]:bounds[g + 1]]
+        grng = np.random.default_rng([seed, c, si])
+        groups.append((build_deep_rows(grng, len(idx), sizes[si], *_deep_decode(c)), idx))
+    batch = _interleave(groups, n, rng)
+    del groups
+    batch.meta.update(config="deep", seed=seed)
+    return batch
 
 
 def _interleave(groups: list[tuple[np.ndarray, np.ndarray]], n: int, order_rng: np.random.Generator,
@@ -294,4 +457,6 @@ def config(cfg: int, n: int | None = None) -> PacketBatch:
         return imix(n or 10_000_000, 3)
     if cfg == 4:
         return imix(n or 12_500_000, 4, flows=1_000_000, corrupt_frac=0.0)
+    if cfg == 5:
+        return deep(n or 10_000_000, 5)
     raise ValueError(f"unknown config {cfg}")

@@ -70,7 +70,7 @@ def test_gpu_edge_descriptors(engine):
     assert g[0]["flags"][4] == abi.F_OVERSIZE and g[0]["flags"][5] == abi.F_BAD_DESC
 
 
-@pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 200_000), (3, 200_000), (4, 200_000)])
+@pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 200_000), (3, 200_000), (4, 200_000), (5, 200_000)])
 def test_gpu_synthetic_configs(engine, cfg, n):
     b = synth.config(cfg, n)
     for opts in (abi.make_opts(), abi.make_opts(0, 8, False, 8)):
@@ -109,6 +109,33 @@ def test_gpu_full_size_imix_properties(engine):
     assert (last["offset"].astype(np.int64) + last["data_len"] == b.caplens).all()
     # sampled bit-exact comparison with the restatement
     rng = np.random.default_rng(0)
+    idx = np.sort(rng.choice(n, size=100_000, replace=False))
+    sub = from_packets([b.packet(int(i)) for i in idx])
+    o = oracle.oracle_parse(sub, opts, threads=8)
+    oracle.compare_exact(s[idx], lay[idx], o[0], o[1])
+
+
+def test_gpu_full_size_deep_encap_properties(engine):
+    """Config 5 at its full 10M size: every stack is parsed to its Payload with no host fallback, the
+    layer chain is contiguous (each layer starts at its predecessor's offset + header length) and the last
+    layer ends at caplen; plus a sampled bit-exact comparison against the restatement."""
+    n = 10_000_000
+    b = synth.config(5, n)
+    opts = abi.make_opts(0, 8, False, 12)
+    s, lay = parse_on_device(engine, b, opts)
+    fl = s["flags"]
+    assert not (fl & (abi.F_NEEDS_HOST | abi.F_DEPTH_OVERFLOW | abi.F_TRAILER)).any()
+    nl = s["n_layers"].astype(np.int64)
+    assert ((nl >= 3) & (nl <= 10)).all()
+    rows = np.arange(n)
+    last = lay[rows, nl - 1]
+    assert (last["proto"] == 25).all()  # GenericPayload
+    assert (last["offset"].astype(np.int64) + last["data_len"] == b.caplens).all()
+    for k in range(1, 10):
+        m = nl > k
+        prev, cur = lay[m, k - 1], lay[m, k]
+        assert (prev["offset"].astype(np.int64) + prev["hdr_len"] == cur["offset"]).all(), k
+    rng = np.random.default_rng(1)
     idx = np.sort(rng.choice(n, size=100_000, replace=False))
     sub = from_packets([b.packet(int(i)) for i in idx])
     o = oracle.oracle_parse(sub, opts, threads=8)

@@ -82,7 +82,7 @@ def main() -> None:
         batch, names, idx = merge(named)
         dump(f"pcap_lt{lt}", batch, names, idx)
     # 3. small synthetic batches of every config shape
-    for cfg, n in ((1, 400), (2, 3000), (3, 1500), (4, 1000)):
+    for cfg, n in ((1, 400), (2, 3000), (3, 1500), (4, 1000), (5, 1000)):
         b = synth.config(cfg, n)
         dump(f"synth_cfg{cfg}", b, [f"config{cfg}"], np.zeros(b.n, np.int32), {"full": VARIANTS["full"]})
 
