@@ -608,7 +608,67 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	return w;
 }
 
-// hash5Tuple (both directions) and hash2Tuple, PacketUtils.cpp:139-245
+__device__ __forceinline__ uint32_t fnv4(uint32_t h, uint32_t v)
+{
+	h = fnv(h, v & 0xFF);
+	h = fnv(h, (v >> 8) & 0xFF);
+	h = fnv(h, (v >> 16) & 0xFF);
+	return fnv(h, v >> 24);
+}
+
+// hash5Tuple (both directions) and hash2Tuple (PacketUtils.cpp:139-245) from the addresses of the IP
+// header at ipo (s/d: na little-endian dwords each) and the raw port word pw of the L4 layer (has_l4).
+// Byte sequences: [port_a port_b ip_a ip_b proto] and [ip_a ip_b], the pair ordered as the reference
+// orders it (raw-order port compare, then LE u32 (IPv4) / memcmp (IPv6) address compare).
+__device__ __forceinline__ void tuple_hashes(const uint32_t (&s)[4], const uint32_t (&d)[4], uint32_t na, bool has_l4,
+                                             uint32_t pw, uint32_t proto, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
+{
+	int cmp = 0;  // sign of memcmp(dst, src) (IPv6) / (dst <=> src) as LE u32 (IPv4)
+	if (na == 1)
+		cmp = d[0] < s[0] ? -1 : (d[0] > s[0] ? 1 : 0);
+	else
+	{
+#pragma unroll
+		for (int k = 3; k >= 0; --k)
+		{
+			const uint32_t a = __builtin_bswap32(d[k]), b = __builtin_bswap32(s[k]);
+			cmp = a < b ? -1 : (a > b ? 1 : cmp);
+		}
+	}
+	const bool sw2 = cmp < 0;
+	uint32_t x = 2166136261u;
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+		if ((uint32_t)k < na) x = fnv4(x, sw2 ? d[k] : s[k]);
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+		if ((uint32_t)k < na) x = fnv4(x, sw2 ? s[k] : d[k]);
+	h2 = x;
+	h5 = h5d = 0;
+	if (!has_l4)
+		return;
+	const uint32_t sp = pw & 0xFFFF, dp = pw >> 16;  // raw network-order values, LE-loaded
+	for (int dir = 0; dir < 2; ++dir)
+	{
+		const bool swap = !dir && (dp < sp || (dp == sp && cmp < 0));
+		uint32_t y = 2166136261u;
+		const uint32_t fp = swap ? dp : sp, sp2 = swap ? sp : dp;
+		y = fnv(fnv(y, fp & 0xFF), fp >> 8);
+		y = fnv(fnv(y, sp2 & 0xFF), sp2 >> 8);
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			if ((uint32_t)k < na) y = fnv4(y, swap ? d[k] : s[k]);
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			if ((uint32_t)k < na) y = fnv4(y, swap ? s[k] : d[k]);
+		y = fnv(y, proto);
+		if (dir) h5d = y; else h5 = y;
+	}
+}
+
+// hash5Tuple / hash2Tuple of a generic-walk packet: addresses of the first IPv4 (else first IPv6) layer,
+// ports of the last TCP (else last UDP) layer, the IP layer's protocol / next-header byte. Dword reads
+// from the LDS window where the bytes are staged (rd32), else from HBM.
 __device__ __forceinline__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
 {
 	h5 = h5d = h2 = 0;
@@ -616,43 +676,18 @@ __device__ __forceinline__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5
 		return;
 	const bool v4 = w.v4 >= 0;
 	const uint32_t ipo = v4 ? (uint32_t)w.v4 : (uint32_t)w.v6;
-	const uint32_t alen = v4 ? 4 : 16;
-	const uint32_t src_o = ipo + (v4 ? 12 : 8), dst_o = ipo + (v4 ? 16 : 24);
-	// address order: dst < src compared as host LE u32 (IPv4) or memcmp (IPv6)
-	int cmp = 0;
-	if (v4)
+	const uint32_t na = v4 ? 1 : 4;
+	const uint32_t so = ipo + (v4 ? 12 : 8), dofs = ipo + (v4 ? 16 : 24);
+	uint32_t s[4], d[4];
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
 	{
-		uint32_t s = le32(p, src_o), d = le32(p, dst_o);
-		cmp = d < s ? -1 : (d > s ? 1 : 0);
+		s[k] = (uint32_t)k < na ? rd32(p, so + 4 * k) : 0;
+		d[k] = (uint32_t)k < na ? rd32(p, dofs + 4 * k) : 0;
 	}
-	else
-	{
-		for (uint32_t j = 0; j < 16 && cmp == 0; ++j)
-		{
-			uint32_t a = rb(p, dst_o + j), b = rb(p, src_o + j);
-			cmp = a < b ? -1 : (a > b ? 1 : 0);
-		}
-	}
-	const uint32_t a_o = cmp < 0 ? dst_o : src_o, b_o = cmp < 0 ? src_o : dst_o;
-	uint32_t h = 2166136261u;
-	for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, a_o + j));
-	for (uint32_t j = 0; j < alen; ++j) h = fnv(h, rb(p, b_o + j));
-	h2 = h;
-	if (w.l4i < 0)
-		return;
-	const uint32_t sp = le16(p, w.l4o), dp = le16(p, w.l4o + 2);
-	const uint32_t ipproto = rb(p, ipo + (v4 ? 9 : 6));
-	for (int dir = 0; dir < 2; ++dir)
-	{
-		bool swap = !dir && (dp < sp || (dp == sp && cmp < 0));
-		uint32_t x = fnv(fnv(2166136261u, swap ? (dp & 0xFF) : (sp & 0xFF)), swap ? (dp >> 8) : (sp >> 8));
-		x = fnv(fnv(x, swap ? (sp & 0xFF) : (dp & 0xFF)), swap ? (sp >> 8) : (dp >> 8));
-		const uint32_t f_o = swap ? dst_o : src_o, s_o = swap ? src_o : dst_o;
-		for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, f_o + j));
-		for (uint32_t j = 0; j < alen; ++j) x = fnv(x, rb(p, s_o + j));
-		x = fnv(x, ipproto);
-		if (dir) h5d = x; else h5 = x;
-	}
+	const bool has_l4 = w.l4i >= 0;
+	const uint32_t pw = has_l4 ? rd32(p, w.l4o) : 0;
+	tuple_hashes(s, d, na, has_l4, pw, rb(p, ipo + (v4 ? 9 : 6)), h5, h5d, h2);
 }
 
 // IPv4 header checksum (IPv4Layer.cpp:410-412): computeChecksum over min(IHL*4, dataLen) header bytes
@@ -932,66 +967,19 @@ __device__ __forceinline__ uint2 fast_layer(const Fast& f, uint32_t cap, uint32_
 	return make_uint2(proto | (osi << 8) | (o << 16), (hdr & 0xFFFF) | (dlen << 16));
 }
 
-// hash5Tuple x2 + hash2Tuple from dword reads (same byte sequences as hashes())
-__device__ __forceinline__ uint32_t fnv4(uint32_t h, uint32_t v)
-{
-	h = fnv(h, v & 0xFF);
-	h = fnv(h, (v >> 8) & 0xFF);
-	h = fnv(h, (v >> 16) & 0xFF);
-	return fnv(h, v >> 24);
-}
-
+// hash5Tuple x2 + hash2Tuple of a fast-path packet (every byte in the LDS window)
 __device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
 {
 	uint32_t s[4], d[4];
 	const uint32_t na = f.v6 ? 4 : 1;
 	const uint32_t so = f.ipo + (f.v6 ? 8 : 12), dofs = f.ipo + (f.v6 ? 24 : 16);
-	int cmp = 0;  // sign of memcmp(dst, src) (IPv6) / (dst < src) on LE u32 (IPv4)
 #pragma unroll
 	for (int k = 0; k < 4; ++k)
 	{
 		s[k] = (uint32_t)k < na ? lds_u32(p, so + 4 * k) : 0;
 		d[k] = (uint32_t)k < na ? lds_u32(p, dofs + 4 * k) : 0;
 	}
-	if (!f.v6)
-		cmp = d[0] < s[0] ? -1 : (d[0] > s[0] ? 1 : 0);
-	else
-	{
-#pragma unroll
-		for (int k = 3; k >= 0; --k)
-		{
-			const uint32_t a = __builtin_bswap32(d[k]), b = __builtin_bswap32(s[k]);
-			cmp = a < b ? -1 : (a > b ? 1 : cmp);
-		}
-	}
-	const bool sw2 = cmp < 0;
-	uint32_t x = 2166136261u;
-#pragma unroll
-	for (int k = 0; k < 4; ++k)
-		if ((uint32_t)k < na) x = fnv4(x, sw2 ? d[k] : s[k]);
-#pragma unroll
-	for (int k = 0; k < 4; ++k)
-		if ((uint32_t)k < na) x = fnv4(x, sw2 ? s[k] : d[k]);
-	h2 = x;
-	const uint32_t pw = lds_u32(p, f.l4o);
-	const uint32_t sp = pw & 0xFFFF, dp = pw >> 16;  // raw network-order values, LE-loaded
-	const uint32_t proto = f.tcp ? 6 : 17;
-	for (int dir = 0; dir < 2; ++dir)
-	{
-		const bool swap = !dir && (dp < sp || (dp == sp && cmp < 0));
-		uint32_t y = 2166136261u;
-		const uint32_t fp = swap ? dp : sp, sp2 = swap ? sp : dp;
-		y = fnv(fnv(y, fp & 0xFF), fp >> 8);
-		y = fnv(fnv(y, sp2 & 0xFF), sp2 >> 8);
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-			if ((uint32_t)k < na) y = fnv4(y, swap ? d[k] : s[k]);
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-			if ((uint32_t)k < na) y = fnv4(y, swap ? s[k] : d[k]);
-		y = fnv(y, proto);
-		if (dir) h5d = y; else h5 = y;
-	}
+	tuple_hashes(s, d, na, true, lds_u32(p, f.l4o), f.tcp ? 6 : 17, h5, h5d, h2);
 }
 
 // IPv4 header checksum from dword reads of the (fully staged) header
@@ -1017,8 +1005,8 @@ __device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Fast&
 // partial edge chunks. The ones'-complement sum only needs the byte-order fix-up for an odd L4
 // start at the very end (a multiply by 256 mod 65535).
 constexpr int kTile = 64;
-constexpr int kTStageChunks = 7;                   // 112 B staged per packet
-constexpr int kTSlotDw = 4 * kTStageChunks + 1;    // + 1 pad dword against bank conflicts
+// header window per packet: 7 x 16 B = 112 B (160 B measured slower even for deep stacks: occupancy)
+constexpr int kTStageChunks = 7;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 {
@@ -1104,11 +1092,13 @@ __device__ uint32_t full_chunks_sum(uintptr_t c0, uintptr_t c1)
 constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_layers; beyond, direct stores
 
 // MinWaves: __launch_bounds__ minimum waves per SIMD (1 = compiler's choice). LDS is 8 KiB per block
-// (stage 7424 B + 768 B of per-lane state) so 20 blocks = 5 waves/SIMD fit a CU's 160 KiB.
-// SWin: stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers).
-template <int MinWaves, int SWin>
+// with 7-chunk windows (stage 7424 B + 768 B of per-lane state): 20 blocks = 5 waves/SIMD fit a CU's
+// 160 KiB. SWin: stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers).
+// Chunks: 16-B header chunks staged per packet.
+template <int MinWaves, int SWin, int Chunks = kTStageChunks>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
+	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
 	// stage doubles as the layer-record staging area at the end (64 rows x (ml+1) padded records x 8 B)
 	__shared__ uint32_t stage[kTile * kTSlotDw];
 	__shared__ uint64_t m_a0[kTile];
@@ -1154,13 +1144,15 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
 	{
 		const uint32_t need = (p.mis + cap + 15) >> 4;
-		p.nch = (live && prm.diag != 2) ? (need < kTStageChunks ? need : kTStageChunks) : 0;
+		p.nch = (live && prm.diag != 2) ? (need < (uint32_t)Chunks ? need : (uint32_t)Chunks) : 0;
 	}
 	m_a0[lane] = p.a0;
 	m_nch[lane] = p.nch;
 	__syncthreads();
+#pragma unroll
+	for (int r = 0; r < (Chunks + 7) / 8; ++r)  // 8 lanes per packet, one 16-B chunk each per round
 	{
-		const uint32_t sub = lane & 7, grp = lane >> 3;
+		const uint32_t sub = (lane & 7) + 8 * r, grp = lane >> 3;
 		uint4 v[8];
 #pragma unroll
 		for (int j = 0; j < 8; ++j)
@@ -1470,26 +1462,40 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 			}
 		}
 		__syncthreads();
-		for (uint32_t j = t; j < kFlowLds; j += kBlock)
+		// flush: read the HBM slot of every distinct key first (all loads in flight together); present
+		// keys -- every flow after its first batch -- take two no-return atomics, new ones a CAS insert
+		constexpr uint32_t kPer = kFlowLds / kBlock;
+		uint32_t fk[kPer], fs[kPer], fseen[kPer];
+#pragma unroll
+		for (uint32_t u = 0; u < kPer; ++u)
 		{
-			const uint32_t key = s_key[j];
+			fk[u] = s_key[u * kBlock + t];
+			fs[u] = (fk[u] * 0x9E3779B1u) & m;
+			fseen[u] = fk[u] ? keys[fs[u]] : 0u;
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < kPer; ++u)
+		{
+			const uint32_t j = u * kBlock + t;
+			const uint32_t key = fk[u];
 			if (key == 0)
 				continue;
-			uint32_t slot = (key * 0x9E3779B1u) & m;
-			bool done = false;
-			for (uint32_t probe = 0; probe < capacity; ++probe)
+			uint32_t slot = fs[u];
+			bool done = fseen[u] == key;  // a slot's key never changes once set: a plain read is enough
+			for (uint32_t probe = 0; !done && probe < capacity; ++probe)
 			{
 				const uint32_t prev = atomicCAS(&keys[slot], 0u, key);
 				if (prev == 0u || prev == key)
-				{
-					atomicAdd(&packets[slot], (unsigned long long)s_pk[j]);
-					atomicAdd(&bytes[slot], s_by[j]);
 					done = true;
-					break;
-				}
-				slot = (slot + 1) & m;
+				else
+					slot = (slot + 1) & m;
 			}
-			if (!done)
+			if (done)
+			{
+				atomicAdd(&packets[slot], (unsigned long long)s_pk[j]);
+				atomicAdd(&bytes[slot], s_by[j]);
+			}
+			else
 				lost += s_pk[j];
 			s_key[j] = 0;
 			s_pk[j] = 0;
@@ -1739,7 +1745,8 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	// default: 5 waves/SIMD (96 VGPRs, 8 KiB LDS) with 2 x 2 KiB stream windows -- measured fastest
 	// (profiles/r01_ab_occupancy.txt). A/B variants: 5 = 5 waves + 4 KiB windows, 6 = compiler's
 	// occupancy + 2 KiB windows, 8 = compiler's occupancy + 4 KiB windows (the round-1 first cut).
-	// Window size is measured not to matter (profiles/r01_ab_windows.txt).
+	// Window size is measured not to matter (profiles/r01_ab_windows.txt); 160-B header windows lose
+	// (profiles/r01_ab_window160.txt).
 	if (o->variant == 5)
 		hipLaunchKernelGGL((parse_tile_kernel<5, 256>), grid, dim3(kTile), 0, stream, prm);
 	else if (o->variant == 6)

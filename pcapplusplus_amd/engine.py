@@ -139,6 +139,37 @@ class PcapReader:
             pass
 
 
+class PinnedBuffer:
+    """Page-locked host memory (pcppx_host_alloc) viewed as a numpy uint8 array: a host batch whose bytes
+    sit here is copied to HBM by DMA straight from it (no staging copy), as a NIC ring's buffers would be."""
+
+    def __init__(self, nbytes: int):
+        self.lib = abi.load_engine()
+        self.ptr = self.lib.pcppx_host_alloc(max(1, nbytes))
+        if not self.ptr:
+            raise MemoryError(f"pcppx_host_alloc({nbytes}) failed")
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(1, nbytes)).from_address(self.ptr))
+
+    def free(self) -> None:
+        if self.ptr:
+            self.array = None
+            self.lib.pcppx_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def pinned_copy(batch: PacketBatch) -> tuple[PacketBatch, PinnedBuffer]:
+    """The same batch with its bytes in page-locked memory (keep the buffer alive while the batch is used)."""
+    buf = PinnedBuffer(batch.data.nbytes)
+    buf.array[: batch.data.nbytes] = batch.data
+    return PacketBatch(buf.array[: batch.data.nbytes], batch.offsets, batch.caplens, batch.linktype), buf
+
+
 def device_count() -> int:
     n = C.c_int(0)
     abi.check(abi.load_engine().pcppx_device_count(C.byref(n)), "pcppx_device_count")

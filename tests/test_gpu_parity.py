@@ -81,11 +81,24 @@ def test_gpu_synthetic_configs(engine, cfg, n):
 
 
 def test_gpu_host_path_matches_device_path(engine):
-    b = synth.config(3, 300_000)
+    """pcppx_parse_batch_host (chunked, double-buffered) equals the device path: packed pageable input
+    (multi-threaded staging), pinned input (DMA straight from the caller's bytes) and a gapped batch
+    (per-packet gather)."""
+    from pcapplusplus_amd.engine import pinned_copy
+
+    b = synth.config(3, 600_000)
     opts = abi.make_opts(0, 8, True, 8)
-    h = engine.parse_host(b, opts)
     d = parse_on_device(engine, b, opts)
+    h = engine.parse_host(b, opts)
     oracle.compare_exact(h[0], h[1], d[0], d[1])
+    pb, buf = pinned_copy(b)
+    hp = engine.parse_host(pb, opts)
+    oracle.compare_exact(hp[0], hp[1], d[0], d[1])
+    buf.free()
+    g = as_batch([b.packet(i) for i in range(20_000)], gaps=True, seed=3)
+    hg = engine.parse_host(g, opts)
+    dg = parse_on_device(engine, g, opts)
+    oracle.compare_exact(hg[0], hg[1], dg[0], dg[1])
 
 
 def test_gpu_full_size_imix_properties(engine):
