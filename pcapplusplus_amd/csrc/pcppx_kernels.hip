@@ -39,7 +39,10 @@ enum : uint32_t
 enum : uint32_t
 {
 	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
-	K_PAYLOAD, K_OUT, K_L7, K_ARP
+	K_PAYLOAD, K_OUT, K_L7, K_ARP,
+	// candidates: the layer a tryConstructNextLayerWithFallback would build if its isDataValid holds, else
+	// Payload (Layer.h:474-483); resolved from the candidate's own first bytes when the walk reaches it
+	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC
 };
 
 // explicit address spaces: keep packet reads as global_load / ds_read, never flat
@@ -139,51 +142,74 @@ __device__ __forceinline__ bool llc_ok(const Pkt& p, uint32_t o, uint32_t n)
 	return n >= 3 && !(rb(p, o) == 0xFF && rb(p, o + 1) == 0xFF);
 }
 
-// L7 trigger ports (engine contract = oracle tcp_l7_port / udp_l7_port)
-__device__ __forceinline__ bool tcp_l7(uint32_t x)
+// L7 trigger ports (engine contract = oracle tcp_l7_port / udp_l7_port), as 64K-bit tables in constant
+// memory: one table read per port instead of a compare chain (whose per-lane masks are combined by scalar
+// instructions, the walk's bottleneck)
+constexpr uint16_t kTcpL7Ports[] = { 443, 261, 448, 465, 563, 614, 636, 989, 990, 992, 993, 994, 995, 80, 8080, 5060,
+	                                 5061, 179, 22, 53, 5353, 5355, 23, 21, 20, 13400, 3496, 30490, 102, 25, 587, 389,
+	                                 5432, 3306, 2123, 502 };
+constexpr uint16_t kUdpL7Ports[] = { 53, 5353, 5355, 5060, 5061, 1812, 1813, 3799, 2152, 2123, 546, 547, 123, 13400,
+	                                 3496, 30490, 51820 };
+constexpr uint16_t kUdpL7DstPorts[] = { 4789, 0, 7, 9 };  // VXLAN, WakeOnLan (UdpLayer.cpp:103-165)
+struct L7Tables
 {
-	switch (x)
-	{
-	case 443: case 261: case 448: case 465: case 563: case 614: case 636: case 989: case 990: case 992:
-	case 993: case 994: case 995: case 80: case 8080: case 5060: case 5061: case 179: case 22: case 53:
-	case 5353: case 5355: case 23: case 21: case 20: case 13400: case 3496: case 30490: case 102: case 25:
-	case 587: case 389: case 5432: case 3306: case 2123: case 502:
-		return true;
-	default:
-		return false;
-	}
+	uint32_t tcp[2048], udp[2048], udp_dst[2048];
+};
+constexpr L7Tables make_l7_tables()
+{
+	L7Tables t{};
+	for (uint16_t x : kTcpL7Ports)
+		t.tcp[x >> 5] |= 1u << (x & 31);
+	for (uint16_t x : kUdpL7Ports)
+		t.udp[x >> 5] |= 1u << (x & 31);
+	for (uint16_t x : kUdpL7DstPorts)
+		t.udp_dst[x >> 5] |= 1u << (x & 31);
+	return t;
 }
-__device__ __forceinline__ bool udp_l7_one(uint32_t x)
+__constant__ L7Tables kL7 = make_l7_tables();
+
+__device__ __forceinline__ uint32_t port_bit(const uint32_t* t, uint32_t x)
 {
-	switch (x)
-	{
-	case 53: case 5353: case 5355: case 5060: case 5061: case 1812: case 1813: case 3799: case 2152:
-	case 2123: case 546: case 547: case 123: case 13400: case 3496: case 30490: case 51820:
-		return true;
-	default:
-		return false;
-	}
+	return (t[x >> 5] >> (x & 31)) & 1u;
+}
+__device__ __forceinline__ bool tcp_l7(uint32_t src, uint32_t dst)
+{
+	return (port_bit(kL7.tcp, src) | port_bit(kL7.tcp, dst)) != 0;
 }
 __device__ __forceinline__ bool udp_l7(uint32_t src, uint32_t dst)
 {
-	if ((src == 68 && dst == 67) || (src == 67 && dst == 68) || (src == 67 && dst == 67))
-		return true;
-	if (dst == 4789 || dst == 0 || dst == 7 || dst == 9)
-		return true;
-	return udp_l7_one(src) || udp_l7_one(dst);
+	const uint32_t pr = (src << 16) | dst;  // DHCP 68->67, 67->68, 67->67
+	const uint32_t dhcp = (uint32_t)(pr == ((68u << 16) | 67u)) | (uint32_t)(pr == ((67u << 16) | 68u)) |
+	                      (uint32_t)(pr == ((67u << 16) | 67u));
+	return (dhcp | port_bit(kL7.udp_dst, dst) | port_bit(kL7.udp, src) | port_bit(kL7.udp, dst)) != 0;
 }
-// SipLayer::detectSipMessageType keys, big-endian packed ("INVI" = 0x494E5649 ...)
+// SipLayer::detectSipMessageType keys, big-endian packed ("INVI" = 0x494E5649 ...): a perfect hash
+// (k * 0x8a05a7) >> 27 over 32 slots, each slot's key checked
+constexpr uint32_t kSipMul = 0x8a05a7u;
+constexpr uint32_t kSipKeys[] = { 0x494E5649u, 0x41434B20u, 0x42594520u, 0x43414E43u, 0x52454749u,
+	                              0x50524143u, 0x4F505449u, 0x53554253u, 0x4E4F5449u, 0x5055424Cu,
+	                              0x494E464Fu, 0x52454645u, 0x4D455353u, 0x55504441u, 0x5349502Fu };
+struct SipTable
+{
+	uint32_t key[32];
+	uint32_t valid;
+};
+constexpr SipTable make_sip_table()
+{
+	SipTable t{};
+	for (uint32_t k : kSipKeys)
+	{
+		const uint32_t h = (k * kSipMul) >> 27;
+		t.key[h] = k;
+		t.valid |= 1u << h;
+	}
+	return t;
+}
+__constant__ SipTable kSip = make_sip_table();
 __device__ __forceinline__ bool sip_key(uint32_t k)
 {
-	switch (k)
-	{
-	case 0x494E5649u: case 0x41434B20u: case 0x42594520u: case 0x43414E43u: case 0x52454749u:
-	case 0x50524143u: case 0x4F505449u: case 0x53554253u: case 0x4E4F5449u: case 0x5055424Cu:
-	case 0x494E464Fu: case 0x52454645u: case 0x4D455353u: case 0x55504441u: case 0x5349502Fu:
-		return true;
-	default:
-		return false;
-	}
+	const uint32_t h = (k * kSipMul) >> 27;
+	return ((kSip.valid >> h) & 1u) && kSip.key[h] == k;
 }
 
 __device__ __forceinline__ uint32_t fnv(uint32_t h, uint32_t b)
@@ -274,112 +300,97 @@ __device__ __forceinline__ uint32_t finish_checksum(uint32_t residue)
 	return ((result >> 8) | (result << 8)) & 0xFFFFu;
 }
 
-// The next layer of the chain, as Layer::parseNextLayer of the layer of kind k at [o, o+len) computes
-// it. Outputs: the layer (proto, osi, hdr, dlen) and its successor (nk at [po, po+pl)).
+// The first 16 bytes of a layer at [o, o+len), as four little-endian dwords: from the LDS window where
+// staged, else byte by byte (HBM); bytes at or past caplen read as 0 and are never used (every field a
+// layer reads lies inside its own length once the length checks below have passed).
+struct Peek
+{
+	uint32_t q[4];
+	__device__ __forceinline__ uint32_t b(uint32_t j) const { return (q[j >> 2] >> (8 * (j & 3))) & 0xFF; }
+	__device__ __forceinline__ uint32_t be(uint32_t j) const { return (b(j) << 8) | b(j + 1); }
+};
+
+__device__ __forceinline__ Peek peek16(const Pkt& p, uint32_t o, uint32_t cap)
+{
+	Peek k;
+	if (o + 16 <= p.lim)
+	{
+		const uint32_t pos = p.mis + o;
+		lptr32 w = reinterpret_cast<lptr32>(p.s) + (pos >> 2);
+		const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+		k.q[0] = __builtin_amdgcn_alignbyte(w1, w0, pos & 3);
+		k.q[1] = __builtin_amdgcn_alignbyte(w2, w1, pos & 3);
+		k.q[2] = __builtin_amdgcn_alignbyte(w3, w2, pos & 3);
+		k.q[3] = __builtin_amdgcn_alignbyte(w4, w3, pos & 3);
+		return k;
+	}
+#pragma unroll
+	for (uint32_t t = 0; t < 4; ++t)
+	{
+		const uint32_t j = o + 4 * t;
+		if (j + 4 <= p.lim)
+			k.q[t] = lds_u32(p, j);
+		else
+		{
+			uint32_t v = 0;
+			for (uint32_t u = 0; u < 4; ++u)
+				v |= (j + u < cap ? rb(p, j + u) : 0u) << (8 * u);
+			k.q[t] = v;
+		}
+	}
+	return k;
+}
+
+// Resolve a candidate kind from its own first bytes: the isDataValid of IPv4Layer (IPv4Layer.h:626-630),
+// IPv6Layer (IPv6Layer.h:245-249), TcpLayer (TcpLayer.h:596-601), IPLayer::getIPVersion
+// (IPLayer.cpp:5-25), GreLayer::getGREVersion (GreLayer.cpp:23-36, GreLayer.h:247-250,317-320),
+// EthLayer / EthDot3Layer (EthLayer.cpp:100-117, EthDot3Layer.cpp:38-54) and LLCLayer (LLCLayer.cpp:49-52).
+// Selects only: every lane of the wave evaluates every rule (no divergent branches).
+__device__ __forceinline__ uint32_t resolve(uint32_t k, const Peek& q, uint32_t len)
+{
+	const uint32_t b0 = q.b(0), ver = b0 >> 4;
+	k = k == C_IPVER ? (ver == 4 ? C_IPV4 : (ver == 6 ? C_IPV6 : K_PAYLOAD)) : k;
+	const bool ok4 = len >= 20 && ver == 4 && (b0 & 0xF) >= 5;
+	const bool ok6 = len >= 40 && ver == 6;
+	const uint32_t d = q.b(12) >> 4;
+	const bool okt = len >= 20 && d >= 5 && len >= 4 * d;
+	const uint32_t gv = len < 4 ? 0xFF : (q.b(1) & 7);
+	const uint32_t kg = gv == 0 ? K_GRE0 : ((gv == 1 && len >= 8) ? K_GRE1 : K_PAYLOAD);
+	const uint32_t et = q.be(12);
+	const uint32_t ke = len < 14 ? K_PAYLOAD : (et >= 0x0600 ? K_ETH : (et <= 0x05DC ? K_DOT3 : K_PAYLOAD));
+	const bool okl = len >= 3 && !(b0 == 0xFF && q.b(1) == 0xFF);
+	k = k == C_IPV4 ? (ok4 ? K_IPV4 : K_PAYLOAD) : k;
+	k = k == C_IPV6 ? (ok6 ? K_IPV6 : K_PAYLOAD) : k;
+	k = k == C_TCP ? (okt ? K_TCP : K_PAYLOAD) : k;
+	k = k == C_GRE ? kg : k;
+	k = k == C_ETHG ? ke : k;
+	k = k == C_LLC ? (okl ? K_LLC : K_PAYLOAD) : k;
+	return k;
+}
+
+// The layer of (resolved) kind k at [o, o+len) and its successor, as Layer::parseNextLayer computes it:
+//   EthLayer.cpp:28-69, EthDot3Layer.cpp:22-30, LLCLayer.cpp:24-41, VlanLayer.cpp:59-119,
+//   MplsLayer.cpp:101-128, IPv4Layer.cpp:180-197,245-370, IPv6Layer.cpp:28-40,79-147,194-312,
+//   GreLayer.cpp:195-252,547-566, TcpLayer.cpp:360-492, UdpLayer.cpp:92-184, ArpLayer.h:151-155,
+//   PayloadLayer.h:61-81.
+// Outputs: the layer (proto, osi, hdr, dlen) and the next kind nk at [po, po+pl) (possibly a candidate).
+// Written as selects over the 16-byte peek: the wave's lanes sit on different layer kinds, and a switch
+// would run every kind's branch with its own exec mask plus the scalar mask bookkeeping.
 struct Step
 {
 	uint32_t proto, osi, hdr, dlen, nk, po, pl;
 };
 
-__device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o, uint32_t len)
+__device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o, uint32_t len, const Peek& q)
 {
-	uint32_t proto = 0, osi = 0, hdr = 0, dlen = len;
-	uint32_t nk = K_NONE, po = 0, pl = 0;
-	switch (k)
+	const bool isE = k == K_ETH, isD = k == K_DOT3, isL = k == K_LLC, isV = k == K_VLAN, isM = k == K_MPLS;
+	const bool is4 = k == K_IPV4, is6 = k == K_IPV6, isG = k == K_GRE0 || k == K_GRE1, isP = k == K_PPTP;
+	const bool isT = k == K_TCP, isU = k == K_UDP, isA = k == K_ARP;
+	// IPv6 extension headers (IPv6Layer::parseExtensions, no bound check against dataLen): IPv6 lanes only
+	uint32_t nh = q.b(6), ext = 0, last_ext = 0xFFFF;
+	if (is6)
 	{
-	case K_ETH:  // EthLayer::parseNextLayer, EthLayer.cpp:28-69
-	{
-		proto = P_ETH; osi = 2; hdr = 14;
-		if (len <= 14) break;
-		po = o + 14; pl = len - 14;
-		uint32_t et = be16(p, o + 12);
-		if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
-		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-		else if (et == 0x8100 || et == 0x88A8) nk = pl >= 4 ? K_VLAN : K_PAYLOAD;
-		else if (et == 0x8847) nk = pl >= 4 ? K_MPLS : K_PAYLOAD;
-		else if (et == 0x0806) nk = pl >= 28 ? K_ARP : K_PAYLOAD;
-		else if (et == 0x8864 || et == 0x8863 || et == 0x0842) nk = K_OUT;
-		else nk = K_PAYLOAD;
-		break;
-	}
-	case K_DOT3:  // EthDot3Layer::parseNextLayer, EthDot3Layer.cpp:22-30
-		proto = P_DOT3; osi = 2; hdr = 14;
-		if (len <= 14) break;
-		po = o + 14; pl = len - 14;
-		nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
-		break;
-	case K_LLC:  // LLCLayer::parseNextLayer, LLCLayer.cpp:24-41
-		proto = P_LLC; osi = 2; hdr = 3;
-		if (len <= 3) break;
-		po = o + 3; pl = len - 3;
-		nk = (rb(p, o) == 0x42 && rb(p, o + 1) == 0x42) ? K_OUT : K_PAYLOAD;
-		break;
-	case K_VLAN:  // VlanLayer::parseNextLayer, VlanLayer.cpp:59-119
-	{
-		proto = P_VLAN; osi = 2; hdr = 4;
-		if (len <= 4) break;
-		po = o + 4; pl = len - 4;
-		uint32_t et = be16(p, o + 2);
-		if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
-		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-		else if (et == 0x8100 || et == 0x88A8) nk = K_VLAN;
-		else if (et == 0x8847) nk = K_MPLS;
-		else if (et == 0x0806) nk = K_ARP;  // unchecked
-		else if (et == 0x8864 || et == 0x8863) nk = K_OUT;
-		else if (et < 1500) nk = llc_ok(p, po, pl) ? K_LLC : K_PAYLOAD;
-		else nk = K_PAYLOAD;
-		break;
-	}
-	case K_MPLS:  // MplsLayer::parseNextLayer, MplsLayer.cpp:101-128
-	{
-		proto = P_MPLS; osi = 3; hdr = 4;
-		if (len < 5) break;
-		po = o + 4; pl = len - 4;
-		if (!(rb(p, o + 2) & 1)) { nk = K_MPLS; break; }
-		uint32_t nib = rb(p, o + 4) >> 4;
-		nk = nib == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-		              : (nib == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-		break;
-	}
-	case K_IPV4:  // IPv4Layer.cpp:180-197 (dataLen), :245-370 (next layer)
-	{
-		proto = P_IPV4; osi = 3;
-		uint32_t b0 = rb(p, o);
-		hdr = (b0 & 0xF) * 4;
-		uint32_t tl = be16(p, o + 2);
-		if (tl < len && tl != 0)
-		{
-			uint32_t hmin = hdr < len ? hdr : len;
-			dlen = tl > hmin ? tl : hmin;
-		}
-		if (dlen <= hdr) break;
-		po = o + hdr; pl = dlen - hdr;
-		uint32_t b6 = rb(p, o + 6), b7 = rb(p, o + 7);
-		if ((b6 & 0x20) || (((b6 & 0x1F) << 8) | b7) != 0) { nk = K_PAYLOAD; break; }
-		uint32_t ipp = rb(p, o + 9);
-		if (ipp == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
-		else if (ipp == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
-		else if (ipp == 4)
-		{
-			uint32_t ver = rb(p, po) >> 4;
-			nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-			              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-		}
-		else if (ipp == 47)
-		{
-			uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
-			nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
-		}
-		else if (ipp == 41) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-		else if (ipp == 1 || ipp == 2 || ipp == 51 || ipp == 50 || ipp == 112) nk = K_OUT;
-		else nk = K_PAYLOAD;
-		break;
-	}
-	case K_IPV6:  // IPv6Layer.cpp:28-40 (extensions + dataLen), :194-312 (next layer)
-	{
-		proto = P_IPV6; osi = 3;
-		uint32_t nh = rb(p, o + 6);
-		uint32_t eo = 40, ext = 0, last_ext = 0xFFFF;
+		uint32_t eo = 40;
 		while (eo <= len - 2)
 		{
 			uint32_t el;
@@ -391,82 +402,75 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 			eo += el;
 			ext += el;
 		}
-		hdr = 40 + ext;
-		uint32_t total = be16(p, o + 4) + hdr;
-		if (total < len) dlen = total;
-		if (dlen <= hdr) break;
-		po = o + hdr; pl = dlen - hdr;
-		if (last_ext == 44) { nk = K_PAYLOAD; break; }
-		if (nh == 17) nk = pl >= 8 ? K_UDP : K_PAYLOAD;
-		else if (nh == 6) nk = tcp_ok(p, po, pl) ? K_TCP : K_PAYLOAD;
-		else if (nh == 4)
-		{
-			uint32_t ver = rb(p, po) >> 4;
-			nk = ver == 4 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-			              : (ver == 6 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-		}
-		else if (nh == 47)
-		{
-			uint32_t gv = pl < 4 ? 0xFF : (rb(p, po + 1) & 7);
-			nk = gv == 0 ? K_GRE0 : (gv == 1 ? (pl >= 8 ? K_GRE1 : K_PAYLOAD) : K_PAYLOAD);
-		}
-		else if (nh == 51 || nh == 50 || nh == 58 || nh == 112) nk = K_OUT;
-		else nk = K_PAYLOAD;
-		break;
 	}
-	case K_GRE0:
-	case K_GRE1:  // GreLayer.cpp:195-252
-	{
-		proto = k == K_GRE0 ? P_GREV0 : P_GREV1; osi = 3;
-		uint32_t f0 = rb(p, o), f1 = rb(p, o + 1);
-		hdr = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
-		if (len <= hdr) break;
-		po = o + hdr; pl = len - hdr;
-		uint32_t et = be16(p, o + 2);
-		if (et == 0x0800) nk = ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD;
-		else if (et == 0x86DD) nk = ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD;
-		else if (et == 0x8100) nk = K_VLAN;
-		else if (et == 0x8847) nk = K_MPLS;
-		else if (et == 0x880B) nk = pl >= 4 ? K_PPTP : K_PAYLOAD;
-		else if (et == 0x6558) nk = eth_ok(p, po, pl) ? K_ETH : (dot3_ok(p, po, pl) ? K_DOT3 : K_PAYLOAD);
-		else nk = K_PAYLOAD;
-		break;
-	}
-	case K_PPTP:  // PPP_PPTPLayer::parseNextLayer, GreLayer.cpp:547-566
-	{
-		proto = P_PPTP; osi = 5; hdr = 4;
-		if (len <= 4) break;
-		po = o + 4; pl = len - 4;
-		uint32_t pp = be16(p, o + 2);
-		nk = pp == 0x21 ? (ipv4_ok(p, po, pl) ? K_IPV4 : K_PAYLOAD)
-		                : (pp == 0x57 ? (ipv6_ok(p, po, pl) ? K_IPV6 : K_PAYLOAD) : K_PAYLOAD);
-		break;
-	}
-	case K_TCP:  // TcpLayer.cpp:360-492
-		proto = P_TCP; osi = 4; hdr = (rb(p, o + 12) >> 4) * 4;
-		if (len <= hdr) break;
-		po = o + hdr; pl = len - hdr;
-		nk = (tcp_l7(be16(p, o)) || tcp_l7(be16(p, o + 2))) ? K_L7 : K_PAYLOAD;
-		break;
-	case K_UDP:  // UdpLayer.cpp:92-184
-	{
-		proto = P_UDP; osi = 4; hdr = 8;
-		if (len <= 8) break;
-		po = o + 8; pl = len - 8;
-		bool l7 = udp_l7(be16(p, o), be16(p, o + 2));
-		if (!l7 && pl >= 4)
-			l7 = sip_key((rb(p, po) << 24) | (rb(p, po + 1) << 16) | (rb(p, po + 2) << 8) | rb(p, po + 3));
-		nk = l7 ? K_L7 : K_PAYLOAD;
-		break;
-	}
-	case K_ARP:  // ArpLayer: dataLen := 28 whatever remains, no next (ArpLayer.h:151-155,242-273)
-		proto = P_ARP; osi = 3; hdr = 28; dlen = 28;
-		break;
-	default:  // K_PAYLOAD: PayloadLayer.h:61-81
-		proto = P_PAYLOAD; osi = 7; hdr = len;
-		break;
-	}
-	return Step{ proto, osi, hdr, dlen, nk, po, pl };
+	// protocol / OSI layer (ProtocolType.h)
+	uint32_t proto = P_PAYLOAD, osi = 7;
+	proto = isE ? P_ETH : (isD ? P_DOT3 : (isL ? P_LLC : (isV ? P_VLAN : proto)));
+	osi = (isE || isD || isL || isV) ? 2 : osi;
+	proto = isM ? P_MPLS : (is4 ? P_IPV4 : (is6 ? P_IPV6 : (isA ? P_ARP : proto)));
+	proto = isG ? (k == K_GRE0 ? P_GREV0 : P_GREV1) : proto;
+	osi = (isM || is4 || is6 || isG || isA) ? 3 : osi;
+	proto = isP ? P_PPTP : (isT ? P_TCP : (isU ? P_UDP : proto));
+	osi = isP ? 5 : ((isT || isU) ? 4 : osi);
+	// header length
+	const uint32_t f0 = q.b(0), f1 = q.b(1);
+	const uint32_t greh = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
+	uint32_t hdr = len;  // Payload: the whole remainder
+	hdr = (isE || isD) ? 14 : hdr;
+	hdr = isL ? 3 : hdr;
+	hdr = (isV || isM || isP) ? 4 : hdr;
+	hdr = is4 ? (f0 & 0xF) * 4 : hdr;
+	hdr = is6 ? 40 + ext : hdr;
+	hdr = isG ? greh : hdr;
+	hdr = isT ? (q.b(12) >> 4) * 4 : hdr;
+	hdr = isU ? 8 : hdr;
+	hdr = isA ? 28 : hdr;
+	// data length: IPv4 totalLength truncation (0 = TSO keeps it), IPv6 payloadLength + header, ARP 28
+	uint32_t dlen = len;
+	const uint32_t tl = q.be(2);
+	const uint32_t hmin = hdr < len ? hdr : len;
+	dlen = (is4 && tl < len && tl != 0) ? (tl > hmin ? tl : hmin) : dlen;
+	const uint32_t total = q.be(4) + hdr;
+	dlen = (is6 && total < len) ? total : dlen;
+	dlen = isA ? 28 : dlen;
+	// successor: exists iff the layer's data runs past its header (every kind's "no next layer" rule)
+	const bool has_next = dlen > hdr;
+	const uint32_t po = o + hdr, pl = has_next ? dlen - hdr : 0;
+	// EtherType dispatch of Ethernet (EtherType at 12), VLAN and GRE (at 2); PPP protocol of PPP_PPTP (at 2)
+	const uint32_t et = isE ? q.be(12) : q.be(2);
+	uint32_t ne = K_PAYLOAD;
+	ne = et == 0x0800 ? C_IPV4 : ne;
+	ne = et == 0x86DD ? C_IPV6 : ne;
+	ne = (et == 0x8100 || (et == 0x88A8 && !isG)) ? K_VLAN : ne;
+	ne = et == 0x8847 ? K_MPLS : ne;
+	ne = (et == 0x0806 && !isG) ? ((isE && pl < 28) ? K_PAYLOAD : K_ARP) : ne;
+	ne = ((et == 0x8864 || et == 0x8863) && !isG) || (et == 0x0842 && isE) ? K_OUT : ne;
+	ne = (et == 0x880B && isG) ? (pl >= 4 ? K_PPTP : K_PAYLOAD) : ne;
+	ne = (et == 0x6558 && isG) ? C_ETHG : ne;
+	ne = (et < 1500 && isV) ? C_LLC : ne;
+	ne = (isE && pl < 4 && (ne == K_VLAN || ne == K_MPLS)) ? K_PAYLOAD : ne;
+	ne = isP ? (et == 0x21 ? C_IPV4 : (et == 0x57 ? C_IPV6 : K_PAYLOAD)) : ne;
+	// IP protocol / next-header dispatch (IPv4Layer.cpp:245-370, IPv6Layer.cpp:194-312)
+	const uint32_t ipp = is4 ? q.b(9) : nh;
+	uint32_t ni = K_PAYLOAD;
+	ni = ipp == 17 ? (pl >= 8 ? K_UDP : K_PAYLOAD) : ni;
+	ni = ipp == 6 ? C_TCP : ni;
+	ni = ipp == 4 ? C_IPVER : ni;
+	ni = ipp == 47 ? C_GRE : ni;
+	ni = (ipp == 41 && is4) ? C_IPV6 : ni;
+	ni = (ipp == 51 || ipp == 50 || ipp == 112 || (is4 && (ipp == 1 || ipp == 2)) || (!is4 && ipp == 58)) ? K_OUT : ni;
+	const uint32_t b6 = q.b(6);
+	const bool frag = (b6 & 0x20) || (((b6 & 0x1F) << 8) | q.b(7)) != 0;  // IPv4Layer.cpp:415-438
+	ni = ((is4 && frag) || (is6 && last_ext == 44)) ? K_PAYLOAD : ni;
+	uint32_t nk = K_PAYLOAD;
+	nk = (isE || isV || isG || isP) ? ne : nk;
+	nk = (is4 || is6) ? ni : nk;
+	nk = isM ? ((q.b(2) & 1) ? C_IPVER : K_MPLS) : nk;  // bottom of stack: IPv4/IPv6 by version nibble
+	nk = isD ? C_LLC : nk;
+	nk = isL ? ((f0 == 0x42 && f1 == 0x42) ? K_OUT : K_PAYLOAD) : nk;
+	// TCP/UDP: a tentative Payload; walk_chain decides afterwards whether an L7 dissector takes it
+	nk = has_next ? nk : K_NONE;
+	return Step{ proto, osi, hdr, dlen, nk, has_next ? po : 0, pl };
 }
 
 struct Params
@@ -507,17 +511,10 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	uint32_t k;
 	switch (prm.linktype)
 	{
-	case 1:
-		k = eth_ok(p, 0, cap) ? K_ETH : (dot3_ok(p, 0, cap) ? K_DOT3 : K_PAYLOAD);
-		break;
-	case 101: case 12: case 14:
-	{
-		uint32_t v = rb(p, 0) & 0xF0;
-		k = (v == 0x40 && ipv4_ok(p, 0, cap)) ? K_IPV4 : ((v == 0x60 && ipv6_ok(p, 0, cap)) ? K_IPV6 : K_PAYLOAD);
-		break;
-	}
-	case 228: k = ipv4_ok(p, 0, cap) ? K_IPV4 : K_PAYLOAD; break;
-	case 229: k = ipv6_ok(p, 0, cap) ? K_IPV6 : K_PAYLOAD; break;
+	case 1: k = C_ETHG; break;                    // Ethernet, else 802.3, else Payload
+	case 101: case 12: case 14: k = C_IPVER; break;  // raw IP by version nibble
+	case 228: k = C_IPV4; break;
+	case 229: k = C_IPV6; break;
 	case 0: case 113: case 276: case 239: case 104: k = K_OUT; break;
 	default: k = K_PAYLOAD; break;
 	}
@@ -534,6 +531,8 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	uint32_t prev_proto = 0, prev_off = 0;
 	uint32_t last_end = 0;
 	uint32_t o = 0, len = cap;
+	uint32_t l7_o = 0, l7_pl = 0, l7_next = 0, l7_end = 0;  // last TCP/UDP layer: offset, payload, index after it
+	bool l7_tcp = false;
 
 	while (k != K_NONE)
 	{
@@ -547,7 +546,13 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 			flags |= PCPPX_F_NEEDS_HOST_L7;
 			break;
 		}
-		Step s = step_layer(p, k, o, len);
+		Peek q;
+		if (k == K_PAYLOAD || k == K_ARP)  // reads no byte
+			q.q[0] = q.q[1] = q.q[2] = q.q[3] = 0;
+		else
+			q = peek16(p, o, cap);
+		k = resolve(k, q, len);
+		Step s = step_layer(p, k, o, len, q);
 		uint32_t nk = s.nk;
 		// stop rules (inclusive, then roll back one layer; the first layer is never rolled back)
 		const uint32_t proto = s.proto;
@@ -573,11 +578,41 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		if (proto == P_IPV6 && v6 < 0) v6 = (int32_t)o;
 		if (proto == P_TCP) { tcp_i = (int32_t)count; tcp_off = o; tcp_dlen = s.dlen; tcp_pp = prev_proto; tcp_po = prev_off; }
 		if (proto == P_UDP) { udp_i = (int32_t)count; udp_off = o; udp_dlen = s.dlen; udp_pp = prev_proto; udp_po = prev_off; }
+		if (proto == P_TCP || proto == P_UDP)
+		{
+			l7_tcp = proto == P_TCP;
+			l7_o = o;
+			l7_pl = s.pl;
+			l7_next = count + 1;
+			l7_end = o + s.dlen;
+		}
 		prev_proto = proto;
 		prev_off = o;
 		last_end = o + s.dlen;
 		++count;
 		k = nk; o = s.po; len = s.pl;
+	}
+
+	// L7 dispatch of the last TCP/UDP layer's payload (TcpLayer.cpp:372-491, UdpLayer.cpp:103-178): the port
+	// tables and the SIP heuristic, read once per packet after the walk so their latency is not on the
+	// walk's critical path. A payload the reference would hand to an L7 dissector ends the chain after the
+	// L4 layer (the tentative Payload layer is dropped) and flags the packet for the host.
+	if (l7_pl > 0 && !(flags & PCPPX_F_NEEDS_HOST_PROTO))
+	{
+		const uint32_t pw = rd32(p, l7_o);
+		const uint32_t sp = swap16(pw), dp = swap16(pw >> 16);
+		const bool l7 = l7_tcp ? tcp_l7(sp, dp)
+		                       : (udp_l7(sp, dp) || (l7_pl >= 4 && sip_key(__builtin_bswap32(rd32(p, l7_o + 8)))));
+		if (l7)
+		{
+			flags |= PCPPX_F_NEEDS_HOST_L7;
+			if (count > l7_next)  // the tentative Payload was recorded
+			{
+				count = l7_next;
+				mask &= ~(1ull << P_PAYLOAD);
+				last_end = l7_end;
+			}
+		}
 	}
 
 	if (count > 0 && prm.family == 0 && prm.until_osi == 8 && !stopped &&
@@ -899,16 +934,8 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 	ok = ok && (tcp ? (pl >= 20 && doff >= 5 && pl >= doff * 4) : pl >= 8);
 	const uint32_t l4hdr = tcp ? doff * 4 : 8;
 	const bool payload = pl > l4hdr;
-	const uint32_t pw = lds_u32(p, ok ? l4o : 0);
-	const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
-	bool l7 = tcp ? (tcp_l7(sport) || tcp_l7(dport)) : udp_l7(sport, dport);
-	if (!tcp && payload && pl - 8 >= 4)
-	{
-		ok = ok && l4o + 12 <= p.lim;
-		const uint32_t s4 = lds_u32(p, ok ? l4o + 8 : 0);
-		l7 = l7 || sip_key(__builtin_bswap32(s4));
-	}
-	l7 = l7 && payload;
+	// the SIP heuristic (UDP payloads of >= 4 B) reads 4 payload bytes from LDS too
+	ok = ok && (tcp || !payload || pl - 8 < 4 || l4o + 12 <= p.lim);
 	// the IPv4 header checksum reads the whole header from LDS too
 	ok = ok && (!v4 || o + hdr <= p.lim);
 	f.nv = nv;
@@ -920,11 +947,29 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 	f.l4hdr = l4hdr;
 	f.l4dlen = pl;
 	f.tcp = tcp;
+	f.payload = payload;  // until fast_l7 (the L7 decision is taken after the hashes: table-read latency)
+	f.l7 = 0;
+	f.trailer = o + dlen;  // IP end, until fast_l7
+	return ok;
+}
+
+// L7 dispatch of a fast-path packet (same rules as walk_chain's): an L7 payload ends the chain after the
+// L4 layer, with no Payload and no trailer
+__device__ __forceinline__ void fast_l7(const Pkt& p, Fast& f, uint32_t cap)
+{
+	const bool payload = f.payload != 0;
+	bool l7 = false;
+	if (payload)
+	{
+		const uint32_t pw = lds_u32(p, f.l4o);
+		const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
+		l7 = f.tcp ? tcp_l7(sport, dport)
+		           : (udp_l7(sport, dport) || (f.l4dlen - 8 >= 4 && sip_key(__builtin_bswap32(lds_u32(p, f.l4o + 8)))));
+	}
+	const uint32_t end = f.trailer;
 	f.payload = payload && !l7;
 	f.l7 = l7;
-	const uint32_t end = o + dlen;
 	f.trailer = (!l7 && end < cap) ? cap - end : 0;
-	return ok;
 }
 
 // the Walk summary of a fast-path packet
@@ -1209,8 +1254,9 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		fast = fast_walk(p, cap, prm, f);
 		if (fast)
 		{
-			w = fast_to_walk(f, ml);
 			fast_hashes(p, f, h5, h5d, h2);
+			fast_l7(p, f, cap);
+			w = fast_to_walk(f, ml);
 			if (prm.want_csum && !f.v6)
 			{
 				ipc = fast_ipv4_checksum(p, f, &ips);

@@ -16,7 +16,7 @@ for c in "${CASE_LIST[@]}"; do
     i=$((i + 1))
     # shellcheck disable=SC2086
     AB_CASES="$c" timeout -k 10 300 rocprofv3 --pmc $pass -d "$ROOT/$OUT/$tag/p$i" -o "p$i" --output-format csv -- \
-      python3 "$ROOT/tools/ab_kernels.py" "$N" "$R" > "$ROOT/$OUT/$tag/p$i.log" 2>&1 || exit 1
+      python3 "$ROOT/tools/ab_kernels.py" "$N" "$R" "${CFG:-3}" > "$ROOT/$OUT/$tag/p$i.log" 2>&1 || exit 1
   done
   echo "== case $c"
   python3 "$ROOT/tools/pmc_summary.py" "$ROOT/$OUT/$tag"
