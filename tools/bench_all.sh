@@ -15,7 +15,7 @@ export TMPDIR=/tmp
 cd /tmp || exit 2
 for c in $CFGS; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/${TAG}_prof_cfg$c" -o bench --output-format csv -- \
-    python3 "$ROOT/bench.py" --config "$c" --steps 20 --warmup 5 --no-cpu-baseline \
+    python3 "$ROOT/bench.py" --config "$c" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e \
     > "$ROOT/$OUT/${TAG}_prof_bench_cfg$c.json" 2> "$ROOT/$OUT/${TAG}_prof_cfg$c.err" || exit 3
 done
 echo "bench all ok"
