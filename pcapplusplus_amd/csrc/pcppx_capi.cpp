@@ -55,6 +55,9 @@ struct pcppx_ctx
 	pcppx_packet_stats* d_stats = nullptr;
 	uint32_t flow_slots = 0;
 	uint64_t seq = 0;
+	// pcppx_flow_count_device: packed per-slot {packets, bytes} scratch (zero between calls)
+	uint64_t* d_flow_packed = nullptr;
+	uint32_t flow_packed_slots = 0;
 };
 
 namespace
@@ -360,6 +363,7 @@ extern "C"
 			free_slot(s);
 		}
 		free_filter(c);
+		(void)hipFree(c->d_flow_packed);
 		(void)hipStreamDestroy(c->stream);
 		delete c;
 	}
@@ -588,7 +592,20 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
-		return pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats,
-		                                static_cast<hipStream_t>(hip_stream));
+		hipStream_t st = static_cast<hipStream_t>(hip_stream);
+		if (c->flow_packed_slots < capacity)
+		{
+			// the previous scratch may still be in use by work queued on another stream
+			if (!ok(hipDeviceSynchronize()))
+				return PCPPX_E_HIP;
+			(void)hipFree(c->d_flow_packed);
+			c->d_flow_packed = nullptr;
+			c->flow_packed_slots = 0;
+			if (!ok(hipMalloc(reinterpret_cast<void**>(&c->d_flow_packed), (size_t)capacity * 8)) ||
+			    !ok(hipMemsetAsync(c->d_flow_packed, 0, (size_t)capacity * 8, st)))
+				return PCPPX_E_NOMEM;
+			c->flow_packed_slots = capacity;
+		}
+		return pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats, c->d_flow_packed, st);
 	}
 }

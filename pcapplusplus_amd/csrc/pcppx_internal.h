@@ -13,5 +13,6 @@ int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, con
                   uint64_t seq_base, uint64_t* keys, uint64_t* first, uint32_t capacity, uint8_t* matched,
                   pcppx_packet_stats* stats, hipStream_t stream);
 int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
-                      uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, hipStream_t stream);
+                      uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, uint64_t* packed,
+                      hipStream_t stream);
 }  // namespace pcppx

@@ -1457,17 +1457,22 @@ __global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, ui
 // packets of a batch, and per-packet global atomics on its slot would serialise.
 constexpr uint32_t kFlowLds = 2048;                 // LDS slots per block (>= 2x the packets of a batch)
 constexpr uint32_t kFlowBatch = 4 * kBlock;         // packets aggregated between two flushes
-constexpr uint32_t kFlowGrid = 1024;                // persistent blocks (4 per CU)
+constexpr uint32_t kFlowGrid = 512;                 // persistent blocks (2 per CU; A/B in profiles/r01_ab_flow_grid.txt)
+constexpr uint32_t kFlowHot = 2;                    // flows with more packets stay in LDS between flushes
 
+// With `packed` (a zeroed u64 per slot, launches of < 2^24 packets) a flush adds {packets, bytes} as one
+// 64-bit atomic (packets << 40 | bytes: < 2^24 packets x < 2^16 B fit 40 bits) and flow_unpack_kernel
+// moves the sums into the table's own counters afterwards: one global atomic per distinct flow and flush.
 __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
                                                             unsigned long long* bytes, uint32_t capacity,
-                                                            unsigned long long* stats)
+                                                            unsigned long long* stats, unsigned long long* packed)
 {
 	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ uint32_t s_pk[kFlowLds];
 	__shared__ unsigned long long s_by[kFlowLds];
+	__shared__ uint32_t s_kept;
 	const uint32_t t = threadIdx.x;
 	const uint32_t m = capacity - 1;
 	unsigned long long z_pk = 0, z_by = 0, lost = 0;  // flow key 0 (PacketUtils.cpp:141-148); table full
@@ -1507,15 +1512,30 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 				slot = (slot + 1) & (kFlowLds - 1);
 			}
 		}
+		if (t == 0)
+			s_kept = 0;
 		__syncthreads();
 		// flush: read the HBM slot of every distinct key first (all loads in flight together); present
-		// keys -- every flow after its first batch -- take two no-return atomics, new ones a CAS insert
+		// keys -- every flow after its first batch -- take no-return atomics, new ones a CAS insert.
+		// Hot flows (more than kFlowHot packets so far) stay in LDS until the block's last batch: every
+		// block meets the top Zipf flows in every batch, and same-address atomics serialise. They are
+		// kept only while they fill at most half of the table, so the next batch always fits.
+		const bool last = base + (uint64_t)gridDim.x * kFlowBatch >= n;  // uniform
 		constexpr uint32_t kPer = kFlowLds / kBlock;
+		uint32_t hot = 0;
+#pragma unroll
+		for (uint32_t u = 0; u < kPer; ++u)
+			hot |= (s_pk[u * kBlock + t] > kFlowHot ? 1u : 0u) << u;
+		if (!last && hot)
+			atomicAdd(&s_kept, (uint32_t)__popc(hot));
+		__syncthreads();
+		const bool keep_hot = !last && s_kept <= kFlowLds / 2 - kFlowBatch / 2;  // uniform
 		uint32_t fk[kPer], fs[kPer], fseen[kPer];
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
 		{
-			fk[u] = s_key[u * kBlock + t];
+			const uint32_t j = u * kBlock + t;
+			fk[u] = (keep_hot && ((hot >> u) & 1u)) ? 0u : s_key[j];
 			fs[u] = (fk[u] * 0x9E3779B1u) & m;
 			fseen[u] = fk[u] ? keys[fs[u]] : 0u;
 		}
@@ -1536,7 +1556,9 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 				else
 					slot = (slot + 1) & m;
 			}
-			if (done)
+			if (done && packed)
+				atomicAdd(&packed[slot], ((unsigned long long)s_pk[j] << 40) | s_by[j]);
+			else if (done)
 			{
 				atomicAdd(&packets[slot], (unsigned long long)s_pk[j]);
 				atomicAdd(&bytes[slot], s_by[j]);
@@ -1561,6 +1583,21 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 		}
 		if (lost)
 			atomicAdd(&stats[2], lost);
+	}
+}
+
+__global__ __launch_bounds__(kBlock) void flow_unpack_kernel(unsigned long long* packets, unsigned long long* bytes,
+                                                             unsigned long long* packed, uint32_t capacity)
+{
+	for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < capacity; j += gridDim.x * kBlock)
+	{
+		const unsigned long long v = packed[j];
+		if (v)
+		{
+			packets[j] += v >> 40;
+			bytes[j] += v & ((1ull << 40) - 1);
+			packed[j] = 0;
+		}
 	}
 }
 
@@ -1651,13 +1688,19 @@ __global__ __launch_bounds__(kBlock) void filter_mark_kernel(FilterParams fp)
 	const unsigned long long key = (1ull << 32) | sm.hash5;
 	const uint32_t m = fp.capacity - 1;
 	uint32_t slot = flow_mix(sm.hash5) & m;
+	const unsigned long long mine = ~(unsigned long long)(fp.seq_base + i);
 	for (uint32_t probe = 0; probe < fp.capacity; ++probe)
 	{
-		const unsigned long long prev = atomicCAS(&fp.keys[slot], 0ull, key);
+		// plain reads first: a set key never changes, and first[] only grows, so a hot flow's packets
+		// after its first skip both atomics
+		unsigned long long prev = fp.keys[slot];
+		if (prev != key)
+			prev = atomicCAS(&fp.keys[slot], 0ull, key);
 		if (prev == 0ull || prev == key)
 		{
 			// stored as ~seq with atomicMax, so a zero-initialised table means "no match yet"
-			atomicMax(&fp.first[slot], ~(unsigned long long)(fp.seq_base + i));
+			if (fp.first[slot] < mine)
+				atomicMax(&fp.first[slot], mine);
 			return;
 		}
 		slot = (slot + 1) & m;
@@ -1838,16 +1881,39 @@ int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, con
 }
 
 int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
-                      uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, hipStream_t stream)
+                      uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, uint64_t* packed,
+                      hipStream_t stream)
 {
-	if (n == 0)
-		return PCPPX_OK;
-	const uint32_t batches = (n + kFlowBatch - 1) / kFlowBatch;
-	dim3 grid(batches < kFlowGrid ? batches : kFlowGrid);
-	hipLaunchKernelGGL(flow_count_kernel, grid, dim3(kBlock), 0, stream, sum, caplens, n, keys,
-	                   reinterpret_cast<unsigned long long*>(packets), reinterpret_cast<unsigned long long*>(bytes),
-	                   capacity, reinterpret_cast<unsigned long long*>(stats));
-	return check_launch("flow_count_kernel", stream);
+	auto* pk = reinterpret_cast<unsigned long long*>(packets);
+	auto* by = reinterpret_cast<unsigned long long*>(bytes);
+	auto* pc = reinterpret_cast<unsigned long long*>(packed);
+	constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed counters hold
+	static const uint32_t grid_cap = [] {  // PCPPX_FLOW_GRID: A/B of the persistent grid size
+		const char* e = getenv("PCPPX_FLOW_GRID");
+		const int v = e ? atoi(e) : 0;
+		return v > 0 ? (uint32_t)v : kFlowGrid;
+	}();
+	for (uint32_t done = 0; done < n;)
+	{
+		const uint32_t cnt = pc ? (n - done < kPackedMax ? n - done : kPackedMax) : n - done;
+		const uint32_t batches = (cnt + kFlowBatch - 1) / kFlowBatch;
+		dim3 grid(batches < grid_cap ? batches : grid_cap);
+		hipLaunchKernelGGL(flow_count_kernel, grid, dim3(kBlock), 0, stream, sum + done, caplens + done, cnt, keys, pk,
+		                   by, capacity, reinterpret_cast<unsigned long long*>(stats), pc);
+		int rc = check_launch("flow_count_kernel", stream);
+		if (rc != PCPPX_OK)
+			return rc;
+		if (pc)
+		{
+			const uint32_t ub = (capacity + kBlock - 1) / kBlock;
+			hipLaunchKernelGGL(flow_unpack_kernel, dim3(ub < 2048 ? ub : 2048), dim3(kBlock), 0, stream, pk, by, pc, capacity);
+			rc = check_launch("flow_unpack_kernel", stream);
+			if (rc != PCPPX_OK)
+				return rc;
+		}
+		done += cnt;
+	}
+	return PCPPX_OK;
 }
 
 }  // namespace pcppx
