@@ -324,20 +324,20 @@ __device__ __forceinline__ Peek peek16(const Pkt& p, uint32_t o, uint32_t cap)
 		k.q[3] = __builtin_amdgcn_alignbyte(w4, w3, pos & 3);
 		return k;
 	}
+	// past the LDS window: the (at most two) aligned 16-B chunks holding [o, o+16) straight from HBM; the
+	// second only if it starts inside the packet (bytes past caplen are never used)
+	const uintptr_t a = (uintptr_t)p.g + o, base = a & ~(uintptr_t)15;
+	const uint4 c0 = ld16(base);
+	const uint4 c1 = base + 16 < (uintptr_t)p.g + cap ? ld16(base + 16) : make_uint4(0, 0, 0, 0);
+	const uint32_t d[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
+	const uint32_t sw = (uint32_t)(a >> 2) & 3, sb = (uint32_t)a & 3;
+	uint32_t e[5];
 #pragma unroll
-	for (uint32_t t = 0; t < 4; ++t)
-	{
-		const uint32_t j = o + 4 * t;
-		if (j + 4 <= p.lim)
-			k.q[t] = lds_u32(p, j);
-		else
-		{
-			uint32_t v = 0;
-			for (uint32_t u = 0; u < 4; ++u)
-				v |= (j + u < cap ? rb(p, j + u) : 0u) << (8 * u);
-			k.q[t] = v;
-		}
-	}
+	for (int t = 0; t < 5; ++t)  // e[t] = d[sw + t] with compile-time indices (selects, no scratch)
+		e[t] = sw == 0 ? d[t] : (sw == 1 ? d[t + 1] : (sw == 2 ? d[t + 2] : d[t + 3]));
+#pragma unroll
+	for (int t = 0; t < 4; ++t)
+		k.q[t] = __builtin_amdgcn_alignbyte(e[t + 1], e[t], sb);
 	return k;
 }
 
