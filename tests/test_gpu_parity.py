@@ -60,6 +60,26 @@ def test_gpu_mutations(engine, gaps, kernel):
     oracle.compare_exact(g[0], g[1], o[0], o[1])
 
 
+@pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
+@pytest.mark.parametrize("order", ["tile-local", "global"])
+def test_gpu_permuted_descriptors(engine, order, kernel):
+    """Descriptors out of address order: permuted inside each 64-packet tile (the span stream reads a
+    tile's bytes in a different order than its packets) and across the whole batch (spans too sparse to
+    stream: whole-chunk sums straight from HBM). Records must not change."""
+    b = synth.config(3, 100_000)
+    rng = np.random.default_rng(9)
+    n = b.n
+    if order == "global":
+        perm = rng.permutation(n)
+    else:
+        perm = np.concatenate([t0 + rng.permutation(min(64, n - t0)) for t0 in range(0, n, 64)])
+    pb = type(b)(b.data, b.offsets[perm].copy(), b.caplens[perm].copy(), b.linktype)
+    opts = abi.make_opts(0, 8, True, 8, kernel)
+    g = parse_on_device(engine, pb, opts)
+    o = oracle.oracle_parse(pb, abi.make_opts(0, 8, True, 8), threads=8)
+    oracle.compare_exact(g[0], g[1], o[0], o[1])
+
+
 def test_gpu_edge_descriptors(engine):
     pk = [b"", b"\x01", bytes(13), bytes(14), bytes(70000), bytes(60)]
     b = from_packets(pk)
