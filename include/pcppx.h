@@ -186,6 +186,53 @@ int pcppx_filter_reset(pcppx_ctx* ctx, uint32_t capacity);
 int pcppx_filter_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_match_spec* spec,
                             uint8_t* matched, pcppx_packet_stats* stats);
 
+/* ---- reassembly front ends ----
+ * The stateless per-packet half of the two reassemblers, over a parsed device batch:
+ *   IPReassembly::processPacket up to its fragment-table lookup (Packet++/src/IPReassembly.cpp:281-322):
+ *     non-IP / non-fragment / malformed classification, the fragment key hashPacket() (FNV-1 over src, dst,
+ *     IP id: IPReassembly.cpp:103-115 for IPv4, :190-205 for IPv6), getFragmentId / getFragmentOffset and
+ *     isFirstFragment / isLastFragment (IPv4Layer.cpp:415-438, IPv6Extensions.cpp:71-91);
+ *   TcpReassembly::reassemblePacket up to its connection lookup (Packet++/src/TcpReassembly.cpp:81-141):
+ *     non-IP / non-TCP / no-data classification, the TCP payload size and SYN/FIN/RST; the connection key
+ *     is hash5Tuple = pcppx_summary.hash5 (TcpReassembly.cpp:141).
+ * The stateful tables (fragment lists, connection map, callbacks) stay with the host caller.
+ * A packet whose chain the engine did not finish (PCPPX_F_NEEDS_HOST_PROTO, OVERSIZE, BAD_DESC,
+ * DEPTH_OVERFLOW, or NEEDS_HOST_L7 on a UDP payload) gets *_HOST unless its first IPv4 layer is recorded
+ * (then ip_status is exact). NEEDS_HOST_L7 on a TCP payload is exact: the dissectors reached from TCP ports
+ * (TcpLayer.cpp:372-491) build no further IP or TCP layer. */
+#define PCPPX_IPR_NON_IP 0       /* IPReassembly::NON_IP_PACKET */
+#define PCPPX_IPR_NON_FRAGMENT 1 /* IPReassembly::NON_FRAGMENT */
+#define PCPPX_IPR_MALFORMED 2    /* IPReassembly::MALFORMED_FRAGMENT (payload size > data len, :315-320) */
+#define PCPPX_IPR_FRAGMENT 3     /* a fragment: ip_key / frag_id / frag_offset set; the host table decides */
+#define PCPPX_IPR_HOST 15        /* the packet's chain is not finished on the device: the host decides */
+#define PCPPX_IPR_F_FIRST 0x10   /* isFirstFragment() */
+#define PCPPX_IPR_F_LAST 0x20    /* isLastFragment() */
+#define PCPPX_IPR_F_IPV6 0x40    /* the IPv6 wrapper was used (no IPv4 layer in the packet); a fragment header
+                                    lies inside the IPv6 header, which a non-malformed fragment holds whole */
+
+#define PCPPX_TCPR_NON_IP 0  /* TcpReassembly::NonIpPacket */
+#define PCPPX_TCPR_NON_TCP 1 /* TcpReassembly::NonTcpPacket */
+#define PCPPX_TCPR_NO_DATA 2 /* TcpReassembly::Ignore_PacketWithNoData */
+#define PCPPX_TCPR_DATA 3    /* goes on to the connection table keyed by hash5 */
+#define PCPPX_TCPR_HOST 15   /* the packet's chain is not finished on the device: the host decides */
+#define PCPPX_TCPR_F_FIN 0x10
+#define PCPPX_TCPR_F_SYN 0x20
+#define PCPPX_TCPR_F_RST 0x40
+
+typedef struct pcppx_reasm_info { /* 16 bytes per packet */
+	uint32_t ip_key;      /* hashPacket() when ip_status is PCPPX_IPR_FRAGMENT, else 0 */
+	uint32_t frag_id;     /* getFragmentId(): be16 IPv4 id / be32 IPv6 fragment id (0 unless a fragment) */
+	uint16_t frag_offset; /* getFragmentOffset() in bytes (0 unless a fragment) */
+	uint8_t ip_status;    /* PCPPX_IPR_* (low nibble) | PCPPX_IPR_F_* */
+	uint8_t tcp_status;   /* PCPPX_TCPR_* (low nibble) | PCPPX_TCPR_F_* of the last TCP layer */
+	uint32_t tcp_payload; /* the last TCP layer's getLayerPayloadSize() (0 without a TCP layer) */
+} pcppx_reasm_info;
+
+/* batch (device pointers) + its records from pcppx_parse_batch_device (max_layers >= 1, the same
+ * max_layers here) -> info[n] (device). Queued on hip_stream; returns without waiting. */
+int pcppx_reasm_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
+                       pcppx_reasm_info* info, void* hip_stream);
+
 /* ---- host ingest: pcap files into packed batch buffers ---- */
 typedef struct pcppx_pcap pcppx_pcap;
 int pcppx_pcap_open(const char* path, pcppx_pcap** out); /* PcapFileReaderDevice::open, PcapFileDevice.cpp:707-768 */

@@ -40,6 +40,8 @@ def oracle_lib() -> C.CDLL:
         lib.pcppx_oracle_checksum.restype = C.c_uint16
         lib.pcppx_oracle_fnv1.argtypes = [C.c_void_p, C.c_uint32]
         lib.pcppx_oracle_fnv1.restype = C.c_uint32
+        lib.pcppx_oracle_reasm_batch.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Records), C.c_uint8, C.c_void_p]
+        lib.pcppx_oracle_reasm_batch.restype = C.c_int
         _oracle = lib
     return _oracle
 
@@ -62,6 +64,8 @@ def ref_lib() -> C.CDLL:
         lib.pcppx_ref_filter.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.MatchSpec), C.c_void_p,
                                          C.POINTER(abi.PacketStats)]
         lib.pcppx_ref_filter.restype = C.c_int
+        lib.pcppx_ref_reasm.argtypes = [C.POINTER(abi.Batch), C.c_void_p]
+        lib.pcppx_ref_reasm.restype = C.c_int
         _ref = lib
     return _ref
 
@@ -200,6 +204,32 @@ def oracle_filter(batch, summary, layers, spec: abi.MatchSpec, flow_table: dict 
         st["matched_packets"] += int(ok)
         matched[i] = ok
     return matched, st
+
+
+def oracle_reasm(batch, summary, layers):
+    """Restatement of the reassembly front ends (pcppx_reasm_device) from engine-format records
+    (summary[n], layers[n, max_layers]) of the same batch: pcppx_reasm_info[n]."""
+    n, ml = batch.n, layers.shape[1]
+    info = np.zeros(max(n, 1), dtype=abi.REASM_DTYPE)
+    s = np.ascontiguousarray(summary)
+    lay = np.ascontiguousarray(layers)
+    rec = abi.Records(s.ctypes.data, lay.ctypes.data)
+    b = batch.c_batch()
+    rc = oracle_lib().pcppx_oracle_reasm_batch(C.byref(b), C.byref(rec), ml, info.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"oracle reasm failed {rc}")
+    return info[:n]
+
+
+def ref_reasm(batch):
+    """The real reference's IPReassembly / TcpReassembly first-sighting statuses and fragment fields per
+    packet (oracle/ref_harness.cpp: pcppx_ref_reasm): pcppx_reasm_info[n]."""
+    info = np.zeros(max(batch.n, 1), dtype=abi.REASM_DTYPE)
+    b = batch.c_batch()
+    rc = ref_lib().pcppx_ref_reasm(C.byref(b), info.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"reference reasm failed {rc}")
+    return info[: batch.n]
 
 
 def checksum(bufs: list[bytes]) -> int:

@@ -568,6 +568,111 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 	sum->flags = flags;
 }
 
+/* ---- reassembly front ends, from a packet's engine-format records ---- */
+static void reasm_packet(const uint8_t* pkt, const pcppx_summary* s, const pcppx_layer* lay, int ml,
+                         pcppx_reasm_info* out)
+{
+	memset(out, 0, sizeof(*out));
+	int nl = s->n_layers < ml ? s->n_layers : ml;
+	int v4 = -1, v6 = -1, tcp = -1;
+	for (int k = 0; k < nl; ++k) {
+		if (lay[k].proto == P_IPV4 && v4 < 0) v4 = k;
+		if (lay[k].proto == P_IPV6 && v6 < 0) v6 = k;
+		if (lay[k].proto == P_TCP) tcp = k;
+	}
+	/* chain not finished on the device (include/pcppx.h): an L7 dissector behind a TCP port adds no IP/TCP
+	 * layer (TcpLayer.cpp:372-491), every other unfinished case may */
+	int unfinished = (s->flags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC |
+	                              PCPPX_F_DEPTH_OVERFLOW)) != 0;
+	if ((s->flags & PCPPX_F_NEEDS_HOST_L7) && !(nl > 0 && lay[nl - 1].proto == P_TCP)) unfinished = 1;
+
+	/* IPReassembly::processPacket, Packet++/src/IPReassembly.cpp:284-322: the IPv4 wrapper when the packet
+	 * has an IPv4 layer (getLayerOfType<IPv4Layer>() = the first), else the IPv6 wrapper (first IPv6) */
+	uint8_t ips;
+	if (v4 >= 0) {
+		const pcppx_layer* L = &lay[v4];
+		const uint8_t* ip = pkt + L->offset;
+		uint32_t fo = ((uint32_t)(ip[6] & 0x1F) << 8) | ip[7];
+		int more = (ip[6] & 0x20) != 0;
+		if (!more && fo == 0) ips = PCPPX_IPR_NON_FRAGMENT;   /* IPv4Layer::isFragment, IPv4Layer.cpp:415-418 */
+		else if (L->hdr_len > L->data_len) ips = PCPPX_IPR_MALFORMED; /* size_t getLayerPayloadSize wraps */
+		else {
+			ips = PCPPX_IPR_FRAGMENT;
+			out->frag_id = be16(ip + 4);                      /* IPReassembly.cpp:98-101 */
+			out->frag_offset = (uint16_t)(fo * 8);            /* IPv4Layer::getFragmentOffset :435-438 */
+			if (fo == 0) ips |= PCPPX_IPR_F_FIRST;            /* isFirstFragment :420-423 */
+			if (!more) ips |= PCPPX_IPR_F_LAST;               /* isLastFragment :425-428 */
+			uint32_t h = fnv_update(2166136261u, ip + 12, 4); /* hashPacket :103-115: src, dst, raw ipId */
+			h = fnv_update(h, ip + 16, 4);
+			out->ip_key = fnv_update(h, ip + 4, 2);
+		}
+	} else if (unfinished) {
+		ips = PCPPX_IPR_HOST;
+	} else if (v6 >= 0) {
+		const pcppx_layer* L = &lay[v6];
+		const uint8_t* ip = pkt + L->offset;
+		/* getExtensionOfType<IPv6FragmentationHeader>() (IPv6Layer.h:203-210) over the extension list
+		 * parseExtensions built (IPv6Layer.cpp:79-147): replay that walk up to the recorded header length */
+		uint32_t nh = ip[6], eo = 40, fe = 0;
+		int have_frag = 0;
+		while (eo < L->hdr_len) {
+			if (nh == 44 && !have_frag) { have_frag = 1; fe = eo; }
+			uint32_t el = nh == 51 ? 4u * ((uint32_t)ip[eo + 1] + 2) : 8u * ((uint32_t)ip[eo + 1] + 1);
+			nh = ip[eo];
+			eo += el;
+		}
+		ips = PCPPX_IPR_F_IPV6;
+		if (!have_frag) ips |= PCPPX_IPR_NON_FRAGMENT;         /* IPReassembly.cpp:156-159 */
+		else if (L->hdr_len > L->data_len) ips |= PCPPX_IPR_MALFORMED;
+		else {
+			/* ip6_frag fields (IPv6Extensions.h): nextHeader, reserved, fragOffsetAndFlags, id; inside the
+			 * header [0, hdr_len), which hdr_len <= data_len keeps inside the packet */
+			const uint8_t* f = ip + fe;
+			uint32_t off = ((uint32_t)f[2] << 8) | (f[3] & 0xF8); /* getFragmentOffset IPv6Extensions.cpp:87-91 */
+			ips |= PCPPX_IPR_FRAGMENT;
+			out->frag_id = ((uint32_t)f[4] << 24) | ((uint32_t)f[5] << 16) | ((uint32_t)f[6] << 8) | f[7];
+			out->frag_offset = (uint16_t)off;
+			if (off == 0) ips |= PCPPX_IPR_F_FIRST;              /* isFirstFragment :71-74 */
+			if (!(f[3] & 1)) ips |= PCPPX_IPR_F_LAST;            /* isLastFragment / isMoreFragments :76-85 */
+			uint32_t h = fnv_update(2166136261u, ip + 8, 16);    /* hashPacket IPReassembly.cpp:190-205 */
+			h = fnv_update(h, ip + 24, 16);
+			out->ip_key = fnv_update(h, f + 4, 4);
+		}
+	} else {
+		ips = PCPPX_IPR_NON_IP;
+	}
+	out->ip_status = ips;
+
+	/* TcpReassembly::reassemblePacket, Packet++/src/TcpReassembly.cpp:96-136 */
+	uint8_t ts;
+	if (unfinished) ts = PCPPX_TCPR_HOST;
+	else if (v4 < 0 && v6 < 0) ts = PCPPX_TCPR_NON_IP;   /* isPacketOfType(IP) :96-103 */
+	else if (tcp < 0) ts = PCPPX_TCPR_NON_TCP;           /* getLayerOfType<TcpLayer>(true) :106-110 (ICMP never
+	                                                        sits in a finished chain: it is out of scope) */
+	else {
+		const pcppx_layer* L = &lay[tcp];
+		uint8_t fl = pkt[L->offset + 13];                /* tcphdr bitfields, TcpLayer.h:30-52 */
+		uint32_t pay = (uint32_t)L->data_len - L->hdr_len;
+		int fin = fl & 1, syn = (fl >> 1) & 1, rst = (fl >> 2) & 1;
+		ts = (pay == 0 && !syn && !fin && !rst) ? PCPPX_TCPR_NO_DATA : PCPPX_TCPR_DATA; /* :124-136 */
+		ts |= (fin ? PCPPX_TCPR_F_FIN : 0) | (syn ? PCPPX_TCPR_F_SYN : 0) | (rst ? PCPPX_TCPR_F_RST : 0);
+		out->tcp_payload = pay;
+	}
+	out->tcp_status = ts;
+}
+
+int pcppx_oracle_reasm_batch(const pcppx_batch* b, const pcppx_records* r, uint8_t max_layers, pcppx_reasm_info* info)
+{
+	if (!b || !r || !r->summary || !r->layers || !info || max_layers == 0 || max_layers > PCPPX_MAX_LAYERS)
+		return PCPPX_E_INVAL;
+	for (uint32_t i = 0; i < b->n; ++i) {
+		const pcppx_summary* s = &r->summary[i];
+		const uint8_t* pkt = (s->flags & PCPPX_F_BAD_DESC) ? b->data : b->data + b->offsets[i];
+		reasm_packet(pkt, s, r->layers + (size_t)i * max_layers, max_layers, &info[i]);
+	}
+	return PCPPX_OK;
+}
+
 /* ---- batch drivers ---- */
 typedef struct {
 	const pcppx_batch* b;

@@ -30,6 +30,11 @@ int pcppx_oracle_parse_batch(const pcppx_batch* batch, const pcppx_opts* opts, p
 int pcppx_oracle_bench(const pcppx_batch* batch, const pcppx_opts* opts, int threads, double* seconds,
                        uint64_t* digest);
 
+/* Reassembly front ends (include/pcppx.h pcppx_reasm_device) over a host batch and its engine-format
+ * records (max_layers >= 1 per packet); info has n entries. */
+int pcppx_oracle_reasm_batch(const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
+                             pcppx_reasm_info* info);
+
 /* Primitive restatements, exposed for the known-answer tests. */
 uint16_t pcppx_oracle_checksum(const uint8_t* const* bufs, const uint32_t* lens, int nbufs); /* PacketUtils.cpp:12-64 */
 uint32_t pcppx_oracle_fnv1(const uint8_t* buf, uint32_t len);                               /* PacketUtils.cpp:114-137 */

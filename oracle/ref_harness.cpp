@@ -20,6 +20,10 @@
 #include "TcpLayer.h"
 #include "UdpLayer.h"
 #include "PacketUtils.h"
+#include "IPv6Extensions.h"
+#include "IPReassembly.h"
+#include "TcpReassembly.h"
+#include "EndianPortable.h"
 #include "Logger.h"
 #include "PacketMatchingEngine.h"  // Examples/DpdkExample-FilterTraffic/PacketMatchingEngine.h (header-only)
 
@@ -200,6 +204,86 @@ extern "C"
 			if (packetMatched)
 				st->matched_packets++;
 			matched[i] = packetMatched ? 1 : 0;
+		}
+		return PCPPX_OK;
+	}
+
+	// Reassembly front ends of the real reference per packet, as a first sighting: a fresh IPReassembly
+	// (processPacket status, Packet++/src/IPReassembly.cpp:281-) and a fresh TcpReassembly (reassemblePacket
+	// status, Packet++/src/TcpReassembly.cpp:81-) per packet, the fragment key through the public
+	// PacketKey::getHashValue (IPReassembly.cpp:233-269: the same bytes as hashPacket) and the fragment / TCP
+	// fields through the layers' own accessors.
+	int pcppx_ref_reasm(const pcppx_batch* b, pcppx_reasm_info* out)
+	{
+		if (b == nullptr || out == nullptr)
+			return PCPPX_E_INVAL;
+		pcpp::Logger::getInstance().suppressLogs();
+		Prepared p;
+		prepare(b, p);
+		for (uint32_t i = 0; i < b->n; ++i)
+		{
+			pcppx_reasm_info& o = out[i];
+			std::memset(&o, 0, sizeof(o));
+			pcpp::Packet packet(&p.raws[i]);
+			{
+				pcpp::IPReassembly ipr;
+				pcpp::IPReassembly::ReassemblyStatus st = pcpp::IPReassembly::NON_IP_PACKET;
+				pcpp::Packet* r = ipr.processPacket(&packet, st);
+				if (r != nullptr && r != &packet)
+					delete r;
+				uint8_t s = PCPPX_IPR_FRAGMENT;
+				if (st == pcpp::IPReassembly::NON_IP_PACKET)
+					s = PCPPX_IPR_NON_IP;
+				else if (st == pcpp::IPReassembly::NON_FRAGMENT)
+					s = PCPPX_IPR_NON_FRAGMENT;
+				else if (st == pcpp::IPReassembly::MALFORMED_FRAGMENT)
+					s = PCPPX_IPR_MALFORMED;
+				const bool v4 = packet.isPacketOfType(pcpp::IPv4);
+				if (!v4 && s != PCPPX_IPR_NON_IP)
+					s |= PCPPX_IPR_F_IPV6;
+				if ((s & 0xF) == PCPPX_IPR_FRAGMENT && v4)
+				{
+					auto* ip = packet.getLayerOfType<pcpp::IPv4Layer>();
+					const uint16_t id = be16toh(ip->getIPv4Header()->ipId);
+					o.frag_id = id;
+					o.frag_offset = ip->getFragmentOffset();
+					s |= (ip->isFirstFragment() ? PCPPX_IPR_F_FIRST : 0) | (ip->isLastFragment() ? PCPPX_IPR_F_LAST : 0);
+					o.ip_key =
+					    pcpp::IPReassembly::IPv4PacketKey(id, ip->getSrcIPv4Address(), ip->getDstIPv4Address()).getHashValue();
+				}
+				else if ((s & 0xF) == PCPPX_IPR_FRAGMENT)
+				{
+					auto* ip = packet.getLayerOfType<pcpp::IPv6Layer>();
+					auto* fh = ip->getExtensionOfType<pcpp::IPv6FragmentationHeader>();
+					const uint32_t id = be32toh(fh->getFragHeader()->id);
+					o.frag_id = id;
+					o.frag_offset = fh->getFragmentOffset();
+					s |= (fh->isFirstFragment() ? PCPPX_IPR_F_FIRST : 0) | (fh->isLastFragment() ? PCPPX_IPR_F_LAST : 0);
+					o.ip_key =
+					    pcpp::IPReassembly::IPv6PacketKey(id, ip->getSrcIPv6Address(), ip->getDstIPv6Address()).getHashValue();
+				}
+				o.ip_status = s;
+			}
+			{
+				pcpp::TcpReassembly tcr([](int8_t, const pcpp::TcpStreamData&, void*) {});
+				const auto st = tcr.reassemblePacket(packet);
+				uint8_t s = PCPPX_TCPR_DATA;
+				if (st == pcpp::TcpReassembly::NonIpPacket)
+					s = PCPPX_TCPR_NON_IP;
+				else if (st == pcpp::TcpReassembly::NonTcpPacket)
+					s = PCPPX_TCPR_NON_TCP;
+				else if (st == pcpp::TcpReassembly::Ignore_PacketWithNoData)
+					s = PCPPX_TCPR_NO_DATA;
+				auto* tcp = packet.getLayerOfType<pcpp::TcpLayer>(true);
+				if (tcp != nullptr && s != PCPPX_TCPR_NON_IP && s != PCPPX_TCPR_NON_TCP)
+				{
+					const pcpp::tcphdr* h = tcp->getTcpHeader();
+					s |= (h->finFlag ? PCPPX_TCPR_F_FIN : 0) | (h->synFlag ? PCPPX_TCPR_F_SYN : 0) |
+					     (h->rstFlag ? PCPPX_TCPR_F_RST : 0);
+					o.tcp_payload = static_cast<uint32_t>(tcp->getLayerPayloadSize());
+				}
+				o.tcp_status = s;
+			}
 		}
 		return PCPPX_OK;
 	}

@@ -63,7 +63,17 @@ SUMMARY_DTYPE = np.dtype(
 LAYER_DTYPE = np.dtype(
     [("proto", "u1"), ("osi", "u1"), ("offset", "<u2"), ("hdr_len", "<u2"), ("data_len", "<u2")]
 )
-assert SUMMARY_DTYPE.itemsize == 32 and LAYER_DTYPE.itemsize == 8
+REASM_DTYPE = np.dtype(
+    [("ip_key", "<u4"), ("frag_id", "<u4"), ("frag_offset", "<u2"), ("ip_status", "u1"), ("tcp_status", "u1"),
+     ("tcp_payload", "<u4")]
+)
+assert SUMMARY_DTYPE.itemsize == 32 and LAYER_DTYPE.itemsize == 8 and REASM_DTYPE.itemsize == 16
+
+# pcppx_reasm_info status codes (low nibble) and flags
+IPR_NON_IP, IPR_NON_FRAGMENT, IPR_MALFORMED, IPR_FRAGMENT, IPR_HOST = 0, 1, 2, 3, 15
+IPR_F_FIRST, IPR_F_LAST, IPR_F_IPV6 = 0x10, 0x20, 0x40
+TCPR_NON_IP, TCPR_NON_TCP, TCPR_NO_DATA, TCPR_DATA, TCPR_HOST = 0, 1, 2, 3, 15
+TCPR_F_FIN, TCPR_F_SYN, TCPR_F_RST = 0x10, 0x20, 0x40
 
 
 class Batch(C.Structure):
@@ -147,6 +157,8 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_filter_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Records), C.c_uint8, C.POINTER(MatchSpec),
                                         C.c_uint64, P, P, C.c_uint32, P, P, P]
     lib.pcppx_filter_device.restype = C.c_int
+    lib.pcppx_reasm_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Records), C.c_uint8, P, P]
+    lib.pcppx_reasm_device.restype = C.c_int
     lib.pcppx_filter_reset.argtypes = [P, C.c_uint32]
     lib.pcppx_filter_reset.restype = C.c_int
     lib.pcppx_filter_batch_host.argtypes = [P, C.POINTER(Batch), C.POINTER(MatchSpec), P, C.POINTER(PacketStats)]
@@ -176,7 +188,7 @@ _ENGINE: C.CDLL | None = None
 EXPORTED_SYMBOLS = (
     "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_runtime_info", "pcppx_open", "pcppx_close",
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
-    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_pcap_open", "pcppx_pcap_linktype",
+    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_pcap_open", "pcppx_pcap_linktype",
     "pcppx_pcap_read_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
 )
 

@@ -475,6 +475,21 @@ extern "C"
 		                            static_cast<hipStream_t>(hip_stream));
 	}
 
+	int pcppx_reasm_device(pcppx_ctx* c, const pcppx_batch* b, const pcppx_records* r, uint8_t max_layers,
+	                       pcppx_reasm_info* info, void* hip_stream)
+	{
+		if (c == nullptr || b == nullptr || r == nullptr || max_layers == 0 || max_layers > PCPPX_MAX_LAYERS)
+			return PCPPX_E_INVAL;
+		if (b->n == 0)
+			return PCPPX_OK;
+		if (b->data == nullptr || b->offsets == nullptr || r->summary == nullptr || r->layers == nullptr ||
+		    info == nullptr)
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		return pcppx::launch_reasm(b, r, max_layers, info, static_cast<hipStream_t>(hip_stream));
+	}
+
 	int pcppx_filter_reset(pcppx_ctx* c, uint32_t capacity)
 	{
 		if (c == nullptr || (capacity & (capacity - 1)) != 0)

@@ -79,6 +79,15 @@ class Engine:
                                                abi.ptr(matched), abi.ptr(stats), C.c_void_p(stream or 0)),
                   "pcppx_filter_device")
 
+    def reasm_device(self, data, offsets, caplens, n: int, linktype: int, summary, layers, max_layers: int, info,
+                     stream: int | None = None) -> None:
+        """The reassembly front ends (pcppx_reasm_device) over a parsed device batch: info is a uint8 tensor of
+        n * 16 bytes (abi.REASM_DTYPE records)."""
+        b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
+        rec = abi.Records(abi.ptr(summary), abi.ptr(layers))
+        abi.check(self.lib.pcppx_reasm_device(self.ctx, C.byref(b), C.byref(rec), max_layers, abi.ptr(info),
+                                              C.c_void_p(stream or 0)), "pcppx_reasm_device")
+
     def filter_reset(self, capacity: int = 0) -> None:
         abi.check(self.lib.pcppx_filter_reset(self.ctx, capacity), "pcppx_filter_reset")
 

@@ -147,6 +147,79 @@ def crafted(seed: int = 7) -> list[bytes]:
     return pk
 
 
+def fragments(n: int, seed: int = 13) -> list[bytes]:
+    """IP fragments and TCP segments for the reassembly front ends: IPv4 with every MF/offset shape, IHL
+    larger than totalLength (malformed), IPv6 fragment headers first or behind other extensions (and
+    twice), fragment headers cut by caplen, tunnels (IPv4 in IPv6, 6in4, GRE, VLAN/MPLS), TCP with every
+    SYN/FIN/RST/ACK combination with and without payload, and UDP/ICMP around them."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        pay = rng.bytes(int(rng.integers(0, 60))) if rng.random() < 0.7 else b""
+        flags = int(rng.choice([0x02, 0x12, 0x10, 0x18, 0x01, 0x11, 0x04, 0x14, 0x03, 0x07, 0x00]))
+        l4k = int(rng.integers(4))
+        if l4k == 0:
+            l4, proto = _udp(40000 + int(rng.integers(1000)), 50000, pay), 17
+        else:
+            h = bytearray(_tcp(41000 + int(rng.integers(1000)), 51000, pay))
+            h[13] = flags
+            l4, proto = bytes(h), 6
+        kind = int(rng.integers(8))
+        if kind in (0, 1):  # IPv4, any MF/offset, sometimes an IHL past totalLength
+            frag = int(rng.choice([0x0000, 0x4000, 0x2000, 0x2000 | int(rng.integers(1, 8192)),
+                                   int(rng.integers(1, 8192))]))
+            ihl = int(rng.choice([5, 5, 6, 15]))
+            ip = bytearray(_ipv4(proto, len(l4), ihl, frag))
+            ip[4:6] = rng.bytes(2)
+            if rng.random() < 0.15:
+                ip[2:4] = (ihl * 4 - 4 * int(rng.integers(1, 4))).to_bytes(2, "big")  # totalLength < IHL*4
+            pk = _eth(0x0800) + bytes(ip) + l4
+        elif kind in (2, 3, 4):  # IPv6 with a fragment header somewhere in its extension chain
+            chain = [int(x) for x in rng.choice([0, 60, 43, 44], size=int(rng.integers(1, 4)))]
+            if 44 not in chain and rng.random() < 0.8:
+                chain.insert(int(rng.integers(len(chain) + 1)), 44)
+            exts = b""
+            nxt = [*chain[1:], proto]
+            for t, nh in zip(chain, nxt):
+                if t == 44:
+                    off = int(rng.integers(0, 8192)) if rng.random() < 0.6 else 0
+                    m = int(rng.integers(2))
+                    exts += bytes([nh, 0]) + ((off << 3) | m).to_bytes(2, "big") + rng.bytes(4)
+                else:
+                    hl = int(rng.integers(0, 3))
+                    exts += bytes([nh, hl]) + rng.bytes(8 * (hl + 1) - 2)
+            body = exts + l4
+            pk = _eth(0x86DD) + _ipv6(chain[0], len(body)) + body
+            if rng.random() < 0.1:  # cut inside the extension chain
+                pk = pk[: 54 + int(rng.integers(2, max(3, len(exts))))]
+            elif rng.random() < 0.05:  # a leading fragment header cut by caplen (its fields past the packet)
+                body = bytes([proto, 0]) + rng.bytes(6)
+                pk = (_eth(0x86DD) + _ipv6(44, 8) + body)[: 54 + int(rng.integers(2, 8))]
+        elif kind == 5:  # tunnels: IPv4 fragment inside IPv6, IPv6 fragment inside IPv4 (6in4), GRE, VLAN, MPLS
+            inner4 = _ipv4(proto, len(l4), 5, int(rng.choice([0x2000, 0x0100, 0x4000])))
+            inner6 = _ipv6(44, 8 + len(l4)) + bytes([proto, 0, 0, 9]) + rng.bytes(4) + l4
+            t = int(rng.integers(5))
+            if t == 0:
+                pk = _eth(0x86DD) + _ipv6(4, len(inner4) + len(l4)) + inner4 + l4
+            elif t == 1:
+                pk = _eth(0x0800) + _ipv4(41, len(inner6)) + inner6
+            elif t == 2:
+                gre = bytes([0, 0]) + struct.pack(">H", 0x0800) + inner4 + l4
+                pk = _eth(0x86DD) + _ipv6(47, len(gre)) + gre
+            elif t == 3:
+                pk = _eth(0x8100) + struct.pack(">HH", 7, 0x86DD) + inner6
+            else:
+                pk = _eth(0x8847) + struct.pack(">I", 100 << 12 | 1 << 8 | 64) + inner4 + l4
+        elif kind == 6:  # ICMP / non-IP neighbours
+            pk = [_eth(0x0800) + _ipv4(1, 8) + rng.bytes(8), _eth(0x0806) + rng.bytes(28),
+                  _eth(0x9000) + rng.bytes(30)][int(rng.integers(3))]
+        else:  # plain TCP/UDP over IPv4 or IPv6, sometimes padded
+            ip = _ipv4(proto, len(l4)) if rng.random() < 0.5 else _ipv6(proto, len(l4))
+            pk = _eth(0x0800 if len(ip) == 20 else 0x86DD) + ip + l4 + (b"\x00" * int(rng.integers(0, 20)))
+        out.append(pk)
+    return out
+
+
 def as_batch(packets: list[bytes], gaps: bool = False, seed: int = 0) -> PacketBatch:
     """Pack packets; with gaps=True leave random gaps so packets start at every byte alignment."""
     if not gaps:
