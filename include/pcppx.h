@@ -167,9 +167,14 @@ typedef struct pcppx_match_spec {
 
 typedef struct pcppx_packet_stats { /* PacketStats, Examples/DpdkExample-FilterTraffic/Common.h:57-142 */
 	uint64_t packet_count, eth_count, arp_count, ipv4_count, ipv6_count, tcp_count, udp_count;
-	uint64_t http_count, dns_count, tls_count; /* L7: counted by the host for PCPPX_F_NEEDS_HOST_L7 packets */
+	uint64_t http_count, dns_count, tls_count; /* isPacketOfType(HTTP / DNS / SSL) of the packets the device
+	                                              settles: the first L7 layer of a NEEDS_HOST_L7 packet is
+	                                              classified on the device (TcpLayer.cpp:372-415,
+	                                              UdpLayer.cpp:103-116) */
 	uint64_t matched_tcp_flows, matched_udp_flows, matched_packets;
-	uint64_t needs_host_count;                  /* packets whose chain the engine did not finish */
+	uint64_t needs_host_count;                  /* packets whose counters the host must complete: chains stopped
+	                                              before an out-of-scope L2/L3 layer (NEEDS_HOST_PROTO), bad
+	                                              records, or UDP tunnels (VXLAN, GTPv1) carrying inner packets */
 } pcppx_packet_stats;
 
 int pcppx_filter_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,

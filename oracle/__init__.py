@@ -138,11 +138,89 @@ def ref_filter(batch, spec: abi.MatchSpec):
 
 P_ETH, P_IPV4, P_IPV6, P_TCP, P_UDP, P_ARP = 1, 2, 3, 4, 5, 8
 
+# ---- collectStats' L7 counters (Examples/DpdkExample-FilterTraffic/Common.h:83-104) ----
+HTTP_METHODS = {b"GET", b"HEAD", b"POST", b"PUT", b"DELETE", b"TRACE", b"OPTIONS", b"CONNECT", b"PATCH"}  # HttpLayer.cpp:145-155
+HTTP_CODES = {100, 101, 102, 103, 200, 201, 202, 203, 204, 205, 206, 207, 208, 226, 300, 301, 302, 303, 304, 305, 306,
+              307, 308, 400, 401, 402, 403, 404, 405, 406, 407, 408, 409, 410, 411, 412, 413, 414, 415, 416, 417, 418,
+              419, 420, 421, 422, 423, 424, 425, 426, 428, 429, 431, 440, 444, 449, 450, 451, 494, 495, 496, 497, 498,
+              499, 500, 501, 502, 503, 504, 505, 506, 507, 508, 509, 510, 511, 520, 521, 522, 523, 524, 598,
+              599}  # intStatusCodeMap, HttpLayer.cpp:424-508
+SSL_PORTS = {443, 261, 448, 465, 563, 614, 636, 989, 990, 992, 993, 994, 995}  # SSLLayer.h:488-510
+DNS_PORTS = {53, 5353, 5355}  # DnsLayer.h:468-479
+
+
+def _http_request(d: bytes) -> bool:
+    """HttpRequestFirstLine::parseMethod != Unknown (HttpLayer.cpp:261-285)."""
+    if len(d) < 4:
+        return False
+    sp = d.find(b" ")
+    return sp > 0 and d[:sp] in HTTP_METHODS
+
+
+def _http_response(d: bytes) -> bool:
+    """parseVersion != Unknown && !parseStatusCode(...).isUnsupportedCode() (HttpLayer.cpp:850-898,964-984)."""
+    if len(d) < 12 or d[:5] != b"HTTP/" or d[5:8] not in (b"0.9", b"1.0", b"1.1"):
+        return False
+    code = d[9:12]
+    if not all(0x30 <= c <= 0x39 for c in code) or int(code) not in HTTP_CODES:
+        return False
+    nl = d.find(b"\n", 13)
+    if nl < 0:
+        return False
+    msg = d[13:nl]
+    if msg.endswith(b"\r"):
+        msg = msg[:-1]
+    return len(msg) > 0
+
+
+def l7_class(pkt: bytes, l4) -> tuple[int, bool]:
+    """(bits HTTP 1 / DNS 2 / SSL 4 of the first L7 layer, settled) of a NEEDS_HOST_L7 packet whose chain
+    ends with TCP/UDP layer l4 (TcpLayer.cpp:372-415, UdpLayer.cpp:103-116); VXLAN / GTPv1 tunnels bring
+    inner packets the device does not parse: not settled."""
+    o, hl, dl = int(l4["offset"]), int(l4["hdr_len"]), int(l4["data_len"])
+    sp, dp = pkt[o] << 8 | pkt[o + 1], pkt[o + 2] << 8 | pkt[o + 3]
+    d = pkt[o + hl:o + dl]
+    if int(l4["proto"]) == P_UDP:
+        if dp == 4789 or 2152 in (sp, dp):
+            return 0, False
+        dhcp = (sp, dp) in ((68, 67), (67, 68), (67, 67))
+        return (2 if not dhcp and len(d) >= 12 and (sp in DNS_PORTS or dp in DNS_PORTS) else 0), True
+    if dp in (80, 8080) and _http_request(d):
+        return 1, True
+    if sp in (80, 8080) and _http_response(d):
+        return 1, True
+    if (sp in SSL_PORTS or dp in SSL_PORTS) and len(d) >= 5 and (d[3] or d[4]) and 20 <= d[0] <= 23:
+        v = d[1] << 8 | d[2]  # SSLVersion::asEnum(true), SSLCommon.cpp:12-27
+        if 0x0300 <= v <= 0x0304 or 0x7F0E <= v <= 0x7F1C or v in (0xFB17, 0xFB1A):
+            return 4, True
+    if {sp, dp} & {5060, 5061, 179, 22}:
+        return 0, True
+    return (2 if len(d) >= 14 and (sp in DNS_PORTS or dp in DNS_PORTS) else 0), True
+
+
+def stats_settled(batch, summary, layers):
+    """Per packet: (settled, L7 bits) as the device's filter_apply_kernel decides them."""
+    n = batch.n
+    settled = np.zeros(n, bool)
+    l7 = np.zeros(n, np.int32)
+    ml = layers.shape[1]
+    for i in range(n):
+        fl = int(summary["flags"][i])
+        ok = not (fl & (abi.F_NEEDS_HOST_PROTO | abi.F_OVERSIZE | abi.F_BAD_DESC))
+        if ok and fl & abi.F_NEEDS_HOST_L7:
+            nl = min(int(summary["n_layers"][i]), ml)
+            ok = nl == int(summary["n_layers"][i]) and nl > 0 and int(layers[i, nl - 1]["proto"]) in (P_TCP, P_UDP)
+            if ok:
+                l7[i], ok = l7_class(batch.packet(i), layers[i, nl - 1])
+        settled[i] = ok
+    return settled, l7
+
 
 def oracle_filter(batch, summary, layers, spec: abi.MatchSpec, flow_table: dict | None = None):
     """Restatement of the FilterTraffic worker (AppWorkerThread.h:85-139; PacketMatchingEngine.h:43-107;
     Common.h:83-104) over parse records, in receive order. Pure Python: small batches only.
-    Returns (matched u8[n], stats dict without the L7 counters). `flow_table` persists across calls."""
+    Returns (matched u8[n], stats dict; the HTTP/DNS/SSL counters over the settled packets, see
+    stats_settled). `flow_table` persists across calls."""
     ft = {} if flow_table is None else flow_table
     m_sip, m_dip = spec.src_ip != 0, spec.dst_ip != 0
     m_sp, m_dp = spec.src_port != 0, spec.dst_port != 0
@@ -150,6 +228,7 @@ def oracle_filter(batch, summary, layers, spec: abi.MatchSpec, flow_table: dict 
     st = {k: 0 for k in abi.STATS_FIELDS}
     matched = np.zeros(batch.n, dtype=np.uint8)
     data = batch.data
+    settled, l7 = stats_settled(batch, summary, layers)
     for i in range(batch.n):
         mask = int(summary["proto_mask"][i])
         has = lambda p: (mask >> p) & 1  # noqa: E731
@@ -157,7 +236,11 @@ def oracle_filter(batch, summary, layers, spec: abi.MatchSpec, flow_table: dict 
         for key, p in (("eth_count", P_ETH), ("arp_count", P_ARP), ("ipv4_count", P_IPV4),
                        ("ipv6_count", P_IPV6), ("tcp_count", P_TCP), ("udp_count", P_UDP)):
             st[key] += has(p)
-        if int(summary["flags"][i]) & abi.F_NEEDS_HOST:
+        if settled[i]:
+            st["http_count"] += int(l7[i] & 1 != 0)
+            st["dns_count"] += int(l7[i] & 2 != 0)
+            st["tls_count"] += int(l7[i] & 4 != 0)
+        else:
             st["needs_host_count"] += 1
         base = int(batch.offsets[i])
         nl = min(int(summary["n_layers"][i]), layers.shape[1])

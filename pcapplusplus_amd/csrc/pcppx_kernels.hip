@@ -1707,6 +1707,114 @@ __global__ __launch_bounds__(kBlock) void filter_mark_kernel(FilterParams fp)
 	}
 }
 
+// ---- collectStats' L7 counters (Common.h:83-104): the first L7 layer of a NEEDS_HOST_L7 packet ----
+// TcpLayer::parseNextLayer's dispatch order (TcpLayer.cpp:372-415): HTTP request (dst port 80/8080 and
+// HttpRequestFirstLine::parseMethod, HttpLayer.cpp:261-285), HTTP response (src port 80/8080,
+// HttpResponseFirstLine::parseVersion / parseStatusCode, HttpLayer.cpp:850-898,964-984), SSL
+// (SSLLayer::IsSSLMessage, SSLLayer.cpp:14-40), then SIP / BGP / SSH ports (none counted), then DNS over
+// TCP (DnsLayer::isDataValid, DnsLayer.h:481-485); UdpLayer::parseNextLayer (UdpLayer.cpp:103-116): DHCP,
+// VXLAN, then DNS. Layers after these add no HTTP / DNS / SSL layer, except where a tunnel (VXLAN, GTPv1)
+// brings a whole inner packet: those packets are left to the host (settled = false).
+struct HttpCodes
+{
+	uint32_t bits[16];  // status codes 100..599 HttpLayer.cpp:424-508 maps (bit code - 100)
+};
+constexpr HttpCodes make_http_codes()
+{
+	HttpCodes t{};
+	const uint16_t codes[] = { 100, 101, 102, 103, 200, 201, 202, 203, 204, 205, 206, 207, 208, 226, 300, 301, 302,
+		                       303, 304, 305, 306, 307, 308, 400, 401, 402, 403, 404, 405, 406, 407, 408, 409, 410,
+		                       411, 412, 413, 414, 415, 416, 417, 418, 419, 420, 421, 422, 423, 424, 425, 426, 428,
+		                       429, 431, 440, 444, 449, 450, 451, 494, 495, 496, 497, 498, 499, 500, 501, 502, 503,
+		                       504, 505, 506, 507, 508, 509, 510, 511, 520, 521, 522, 523, 524, 598, 599 };
+	for (uint16_t c : codes)
+		t.bits[(c - 100) >> 5] |= 1u << ((c - 100) & 31);
+	return t;
+}
+__constant__ HttpCodes kHttpCodes = make_http_codes();
+
+__device__ __forceinline__ bool ssl_port16(uint32_t x)
+{
+	return x == 443 || x == 261 || x == 448 || x == 465 || x == 563 || x == 614 || x == 636 || x == 989 || x == 990 ||
+	       (x >= 992 && x <= 995);
+}
+__device__ __forceinline__ bool dns_port16(uint32_t x)
+{
+	return x == 53 || x == 5353 || x == 5355;
+}
+__device__ __forceinline__ bool http_method(const uint8_t* d, uint32_t n)
+{
+	if (n < 4)
+		return false;
+	uint32_t sp = 8;  // first space among the first 8 bytes (longer method names are unknown anyway)
+	for (uint32_t j = 0; j < 8 && j < n; ++j)
+		if (d[j] == ' ' && sp == 8)
+			sp = j;
+	if (sp == 8 || sp == 0 || sp >= n)
+		return false;
+	auto is = [&](const char* m, uint32_t l) {
+		if (sp != l)
+			return false;
+		for (uint32_t j = 0; j < l; ++j)
+			if (d[j] != (uint8_t)m[j])
+				return false;
+		return true;
+	};
+	return is("GET", 3) || is("PUT", 3) || is("HEAD", 4) || is("POST", 4) || is("TRACE", 5) || is("PATCH", 5) ||
+	       is("DELETE", 6) || is("OPTIONS", 7) || is("CONNECT", 7);
+}
+__device__ bool http_status(const uint8_t* d, uint32_t n)
+{
+	if (n < 12 || d[0] != 'H' || d[1] != 'T' || d[2] != 'T' || d[3] != 'P' || d[4] != '/')
+		return false;
+	const bool ver = (d[5] == '0' && d[6] == '.' && d[7] == '9') || (d[5] == '1' && d[6] == '.' && (d[7] == '0' || d[7] == '1'));
+	if (!ver)
+		return false;
+	for (int j = 9; j < 12; ++j)
+		if (d[j] < '0' || d[j] > '9')
+			return false;
+	const uint32_t code = (d[9] - '0') * 100u + (d[10] - '0') * 10u + (d[11] - '0');
+	if (code < 100 || code > 599 || !((kHttpCodes.bits[(code - 100) >> 5] >> ((code - 100) & 31)) & 1u))
+		return false;
+	uint32_t off = 13;
+	while (off < n && d[off] != '\n')
+		++off;
+	if (off >= n)
+		return false;  // no end of the first line: HttpStatusCodeUnknown
+	return off > 14 || (off == 14 && d[13] != '\r');  // a non-empty status message
+}
+
+__device__ uint32_t l7_class(const uint8_t* pkt, const pcppx_layer& l4, bool& settled)
+{
+	const uint8_t* h = pkt + l4.offset;
+	const uint32_t sp = ((uint32_t)h[0] << 8) | h[1], dp = ((uint32_t)h[2] << 8) | h[3];
+	const uint8_t* d = h + l4.hdr_len;
+	const uint32_t n = (uint32_t)l4.data_len - l4.hdr_len;
+	if (l4.proto == P_UDP)
+	{
+		if (dp == 4789 || sp == 2152 || dp == 2152)
+		{
+			settled = false;  // VXLAN / GTPv1 carry an inner packet
+			return 0;
+		}
+		const bool dhcp = (sp == 68 && dp == 67) || (sp == 67 && (dp == 68 || dp == 67));
+		return (!dhcp && n >= 12 && (dns_port16(sp) || dns_port16(dp))) ? 2u : 0u;
+	}
+	if ((dp == 80 || dp == 8080) && http_method(d, n))
+		return 1;
+	if ((sp == 80 || sp == 8080) && http_status(d, n))
+		return 1;
+	if ((ssl_port16(sp) || ssl_port16(dp)) && n >= 5 && (d[3] | d[4]) != 0 && d[0] >= 20 && d[0] <= 23)
+	{
+		const uint32_t v = ((uint32_t)d[1] << 8) | d[2];  // SSLVersion::asEnum(true), SSLCommon.cpp:12-27
+		if ((v >= 0x0300 && v <= 0x0304) || (v >= 0x7f0e && v <= 0x7f1c) || v == 0xfb17 || v == 0xfb1a)
+			return 4;
+	}
+	if (sp == 5060 || sp == 5061 || dp == 5060 || dp == 5061 || sp == 179 || dp == 179 || sp == 22 || dp == 22)
+		return 0;
+	return (n >= 14 && (dns_port16(sp) || dns_port16(dp))) ? 2u : 0u;
+}
+
 __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred)
 {
 	const unsigned long long b = __ballot(pred);
@@ -1720,13 +1828,23 @@ __global__ __launch_bounds__(kBlock) void filter_apply_kernel(FilterParams fp)
 	const bool in = i < fp.n;
 	uint64_t mask = 0;
 	uint32_t flags = 0;
-	bool matched = false, new_tcp = false, new_udp = false;
+	bool matched = false, new_tcp = false, new_udp = false, settled = false;
+	uint32_t l7 = 0;
 	if (in)
 	{
 		const pcppx_summary& sm = fp.summary[i];
 		mask = sm.proto_mask;
 		flags = sm.flags;
 		const uint32_t nl = sm.n_layers < fp.ml ? sm.n_layers : fp.ml;
+		// the packet's counters are the device's unless its chain stopped before a layer it does not see
+		settled = (flags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC)) == 0;
+		if (settled && (flags & PCPPX_F_NEEDS_HOST_L7))
+		{
+			const pcppx_layer l4 = fp.layers[(size_t)i * fp.ml + (nl ? nl - 1 : 0)];
+			settled = nl == sm.n_layers && nl > 0 && (l4.proto == P_TCP || l4.proto == P_UDP);
+			if (settled)
+				l7 = l7_class(fp.data + fp.offsets[i], l4, settled);
+		}
 		const bool own = filter_is_matched(fp, i, mask, nl);
 		const unsigned long long key = (1ull << 32) | sm.hash5;
 		const uint64_t seq = fp.seq_base + i;
@@ -1764,7 +1882,10 @@ __global__ __launch_bounds__(kBlock) void filter_apply_kernel(FilterParams fp)
 	wave_count(st + 10, new_tcp);
 	wave_count(st + 11, new_udp);
 	wave_count(st + 12, matched);
-	wave_count(st + 13, in && (flags & PCPPX_F_NEEDS_HOST) != 0);
+	wave_count(st + 7, settled && (l7 & 1));
+	wave_count(st + 8, settled && (l7 & 2));
+	wave_count(st + 9, settled && (l7 & 4));
+	wave_count(st + 13, in && !settled);
 }
 
 
