@@ -41,7 +41,7 @@ void printStats(const pcppx_packet_stats& s)
 	row("IPv6 count", s.ipv6_count);
 	row("TCP count", s.tcp_count);
 	row("UDP count", s.udp_count);
-	row("L7 for host", s.needs_host_count);
+	row("left to host", s.needs_host_count);
 	row("Matched TCP flows", s.matched_tcp_flows);
 	row("Matched UDP flows", s.matched_udp_flows);
 	row("Total packet count", s.packet_count);
