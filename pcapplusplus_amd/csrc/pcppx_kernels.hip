@@ -313,31 +313,39 @@ struct Peek
 __device__ __forceinline__ Peek peek16(const Pkt& p, uint32_t o, uint32_t cap)
 {
 	Peek k;
-	if (o + 16 <= p.lim)
+	// the LDS window read runs for every lane (a lane past the window reads its slot's first bytes and
+	// replaces them below): one divergent region, entered only when some lane is past the window
+	const bool inwin = o + 16 <= p.lim;
 	{
-		const uint32_t pos = p.mis + o;
+		const uint32_t pos = p.mis + (inwin ? o : 0u);
 		lptr32 w = reinterpret_cast<lptr32>(p.s) + (pos >> 2);
 		const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
 		k.q[0] = __builtin_amdgcn_alignbyte(w1, w0, pos & 3);
 		k.q[1] = __builtin_amdgcn_alignbyte(w2, w1, pos & 3);
 		k.q[2] = __builtin_amdgcn_alignbyte(w3, w2, pos & 3);
 		k.q[3] = __builtin_amdgcn_alignbyte(w4, w3, pos & 3);
-		return k;
 	}
-	// past the LDS window: the (at most two) aligned 16-B chunks holding [o, o+16) straight from HBM; the
-	// second only if it starts inside the packet (bytes past caplen are never used)
-	const uintptr_t a = (uintptr_t)p.g + o, base = a & ~(uintptr_t)15;
-	const uint4 c0 = ld16(base);
-	const uint4 c1 = base + 16 < (uintptr_t)p.g + cap ? ld16(base + 16) : make_uint4(0, 0, 0, 0);
-	const uint32_t d[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
-	const uint32_t sw = (uint32_t)(a >> 2) & 3, sb = (uint32_t)a & 3;
-	uint32_t e[5];
+	if (!inwin)
+	{
+		// past the LDS window: the (at most two) aligned 16-B chunks holding [o, o+16) straight from HBM;
+		// the second only if it starts inside the packet (bytes past caplen are never used)
+		const uintptr_t a = (uintptr_t)p.g + o, base = a & ~(uintptr_t)15;
+		const uint4 c0 = ld16(base);
+		const uint4 c1 = base + 16 < (uintptr_t)p.g + cap ? ld16(base + 16) : make_uint4(0, 0, 0, 0);
+		const uint32_t d[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
+		const uint32_t sw = (uint32_t)(a >> 2) & 3, sb = (uint32_t)a & 3;
+		// e[t] = d[sw + t] as and/or with constant masks: a select whose operand is a load is turned into
+		// a branch by the compiler (to load conditionally), with its own exec-mask region
+		const uint32_t m0 = sw == 0 ? ~0u : 0u, m1 = sw == 1 ? ~0u : 0u, m2 = sw == 2 ? ~0u : 0u,
+		               m3 = sw == 3 ? ~0u : 0u;
+		uint32_t e[5];
 #pragma unroll
-	for (int t = 0; t < 5; ++t)  // e[t] = d[sw + t] with compile-time indices (selects, no scratch)
-		e[t] = sw == 0 ? d[t] : (sw == 1 ? d[t + 1] : (sw == 2 ? d[t + 2] : d[t + 3]));
+		for (int t = 0; t < 5; ++t)
+			e[t] = (d[t] & m0) | (d[t + 1] & m1) | (d[t + 2] & m2) | (t + 3 < 8 ? (d[t + 3] & m3) : 0u);
 #pragma unroll
-	for (int t = 0; t < 4; ++t)
-		k.q[t] = __builtin_amdgcn_alignbyte(e[t + 1], e[t], sb);
+		for (int t = 0; t < 4; ++t)
+			k.q[t] = __builtin_amdgcn_alignbyte(e[t + 1], e[t], sb);
+	}
 	return k;
 }
 
@@ -393,12 +401,19 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 		uint32_t eo = 40;
 		while (eo <= len - 2)
 		{
-			uint32_t el;
-			if (nh == 44 || nh == 0 || nh == 60 || nh == 43) el = 8u * (rb(p, o + eo + 1) + 1);
-			else if (nh == 51) el = 4u * (rb(p, o + eo + 1) + 2);
-			else break;
+			const bool std_ext = nh == 44 || nh == 0 || nh == 60 || nh == 43, ah = nh == 51;
+			if (!(std_ext || ah))
+				break;
+			// the extension's next-header and length bytes: LDS window read for every lane, HBM only past it
+			const uint32_t j = o + eo;
+			const bool win = j + 2 <= p.lim;
+			uint32_t two = lds_u32(p, win ? j : 0u) & 0xFFFFu;
+			if (!win)
+				two = le16(p, j);
+			const uint32_t hl = two >> 8;
+			const uint32_t el = ah ? 4u * (hl + 2) : 8u * (hl + 1);
 			last_ext = nh;
-			nh = rb(p, o + eo);
+			nh = two & 0xFFu;
 			eo += el;
 			ext += el;
 		}
@@ -534,58 +549,60 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	uint32_t l7_o = 0, l7_pl = 0, l7_next = 0, l7_end = 0;  // last TCP/UDP layer: offset, payload, index after it
 	bool l7_tcp = false;
 
+	// The loop body is written as selects around three divergent regions (the loop exits, the peek's HBM
+	// fallback, the record store): the 64 lanes sit on different layer kinds, and every `if` becomes an
+	// exec-mask region of scalar bookkeeping plus copies of each value live across it.
 	while (k != K_NONE)
 	{
-		if (k == K_OUT)
+		if (k == K_OUT || k == K_L7)
 		{
-			flags |= PCPPX_F_NEEDS_HOST_PROTO;
+			flags |= k == K_OUT ? PCPPX_F_NEEDS_HOST_PROTO : PCPPX_F_NEEDS_HOST_L7;
 			break;
 		}
-		if (k == K_L7)
-		{
-			flags |= PCPPX_F_NEEDS_HOST_L7;
-			break;
-		}
-		Peek q;
-		if (k == K_PAYLOAD || k == K_ARP)  // reads no byte
-			q.q[0] = q.q[1] = q.q[2] = q.q[3] = 0;
-		else
-			q = peek16(p, o, cap);
+		const bool nob = k == K_PAYLOAD || k == K_ARP;  // reads no byte: peek at 0 (inside the packet), drop it
+		Peek q = peek16(p, nob ? 0u : o, cap);
+		const uint32_t keep = nob ? 0u : ~0u;  // a mask, not a select of the loaded value (see peek16)
+#pragma unroll
+		for (int t = 0; t < 4; ++t)
+			q.q[t] &= keep;
 		k = resolve(k, q, len);
 		Step s = step_layer(p, k, o, len, q);
 		uint32_t nk = s.nk;
 		// stop rules (inclusive, then roll back one layer; the first layer is never rolled back)
 		const uint32_t proto = s.proto;
-		bool member = prm.family != 0 &&
-		              (proto == (prm.family & 0xFF) || (proto << 8) == (prm.family & 0xFF00) ||
-		               (proto << 16) == (prm.family & 0xFF0000) || (proto << 24) == (prm.family & 0xFF000000u));
-		bool fail = s.osi > prm.until_osi;
-		if (!fail)
-		{
-			if (member) found = 1;
-			if (found && !member) fail = true;
-		}
-		if (fail)
-		{
-			stopped = 1;
-			if (count > 0) break;
-			nk = K_NONE;
-		}
+		const bool member = prm.family != 0 &&
+		                    (proto == (prm.family & 0xFF) || (proto << 8) == (prm.family & 0xFF00) ||
+		                     (proto << 16) == (prm.family & 0xFF0000) || (proto << 24) == (prm.family & 0xFF000000u));
+		const bool osi_fail = s.osi > prm.until_osi;
+		found = (!osi_fail && member) ? 1u : found;
+		const bool fail = osi_fail || (found && !member);
+		stopped = fail ? 1u : stopped;
+		if (fail && count > 0)
+			break;
+		nk = fail ? (uint32_t)K_NONE : nk;
 		if (lay_out && count < ml)
 			lay_out[count] = make_uint2(proto | (s.osi << 8) | (o << 16), (s.hdr & 0xFFFF) | (s.dlen << 16));
 		mask |= 1ull << proto;
-		if (proto == P_IPV4 && v4 < 0) { v4 = (int32_t)o; v4_dlen = s.dlen; }
-		if (proto == P_IPV6 && v6 < 0) v6 = (int32_t)o;
-		if (proto == P_TCP) { tcp_i = (int32_t)count; tcp_off = o; tcp_dlen = s.dlen; tcp_pp = prev_proto; tcp_po = prev_off; }
-		if (proto == P_UDP) { udp_i = (int32_t)count; udp_off = o; udp_dlen = s.dlen; udp_pp = prev_proto; udp_po = prev_off; }
-		if (proto == P_TCP || proto == P_UDP)
-		{
-			l7_tcp = proto == P_TCP;
-			l7_o = o;
-			l7_pl = s.pl;
-			l7_next = count + 1;
-			l7_end = o + s.dlen;
-		}
+		const bool first4 = proto == P_IPV4 && v4 < 0;
+		v4_dlen = first4 ? s.dlen : v4_dlen;
+		v4 = first4 ? (int32_t)o : v4;
+		v6 = (proto == P_IPV6 && v6 < 0) ? (int32_t)o : v6;
+		const bool isT = proto == P_TCP, isU = proto == P_UDP, isL4 = isT || isU;
+		tcp_i = isT ? (int32_t)count : tcp_i;
+		tcp_off = isT ? o : tcp_off;
+		tcp_dlen = isT ? s.dlen : tcp_dlen;
+		tcp_pp = isT ? prev_proto : tcp_pp;
+		tcp_po = isT ? prev_off : tcp_po;
+		udp_i = isU ? (int32_t)count : udp_i;
+		udp_off = isU ? o : udp_off;
+		udp_dlen = isU ? s.dlen : udp_dlen;
+		udp_pp = isU ? prev_proto : udp_pp;
+		udp_po = isU ? prev_off : udp_po;
+		l7_tcp = isL4 ? isT : l7_tcp;
+		l7_o = isL4 ? o : l7_o;
+		l7_pl = isL4 ? s.pl : l7_pl;
+		l7_next = isL4 ? count + 1 : l7_next;
+		l7_end = isL4 ? o + s.dlen : l7_end;
 		prev_proto = proto;
 		prev_off = o;
 		last_end = o + s.dlen;
