@@ -331,7 +331,9 @@ __device__ __forceinline__ Peek peek16(const Pkt& p, uint32_t o, uint32_t cap)
 		// the second only if it starts inside the packet (bytes past caplen are never used)
 		const uintptr_t a = (uintptr_t)p.g + o, base = a & ~(uintptr_t)15;
 		const uint4 c0 = ld16(base);
-		const uint4 c1 = base + 16 < (uintptr_t)p.g + cap ? ld16(base + 16) : make_uint4(0, 0, 0, 0);
+		// the second chunk only matters if it starts inside the packet; otherwise re-read the first (the
+		// address is selected, not the loaded value, so no branch)
+		const uint4 c1 = ld16(base + 16 < (uintptr_t)p.g + cap ? base + 16 : base);
 		const uint32_t d[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
 		const uint32_t sw = (uint32_t)(a >> 2) & 3, sb = (uint32_t)a & 3;
 		// e[t] = d[sw + t] as and/or with constant masks: a select whose operand is a load is turned into
@@ -587,22 +589,25 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		v4_dlen = first4 ? s.dlen : v4_dlen;
 		v4 = first4 ? (int32_t)o : v4;
 		v6 = (proto == P_IPV6 && v6 < 0) ? (int32_t)o : v6;
-		const bool isT = proto == P_TCP, isU = proto == P_UDP, isL4 = isT || isU;
-		tcp_i = isT ? (int32_t)count : tcp_i;
-		tcp_off = isT ? o : tcp_off;
-		tcp_dlen = isT ? s.dlen : tcp_dlen;
-		tcp_pp = isT ? prev_proto : tcp_pp;
-		tcp_po = isT ? prev_off : tcp_po;
-		udp_i = isU ? (int32_t)count : udp_i;
-		udp_off = isU ? o : udp_off;
-		udp_dlen = isU ? s.dlen : udp_dlen;
-		udp_pp = isU ? prev_proto : udp_pp;
-		udp_po = isU ? prev_off : udp_po;
-		l7_tcp = isL4 ? isT : l7_tcp;
-		l7_o = isL4 ? o : l7_o;
-		l7_pl = isL4 ? s.pl : l7_pl;
-		l7_next = isL4 ? count + 1 : l7_next;
-		l7_end = isL4 ? o + s.dlen : l7_end;
+		// bookkeeping of the last TCP / UDP layer as and/or with lane masks (a run of selects on one
+		// condition is otherwise folded into a branch)
+		const uint32_t mT = proto == P_TCP ? ~0u : 0u, mU = proto == P_UDP ? ~0u : 0u, mL = mT | mU;
+		auto upd = [](uint32_t old_v, uint32_t new_v, uint32_t m) { return (old_v & ~m) | (new_v & m); };
+		tcp_i = (int32_t)upd((uint32_t)tcp_i, count, mT);
+		tcp_off = upd(tcp_off, o, mT);
+		tcp_dlen = upd(tcp_dlen, s.dlen, mT);
+		tcp_pp = upd(tcp_pp, prev_proto, mT);
+		tcp_po = upd(tcp_po, prev_off, mT);
+		udp_i = (int32_t)upd((uint32_t)udp_i, count, mU);
+		udp_off = upd(udp_off, o, mU);
+		udp_dlen = upd(udp_dlen, s.dlen, mU);
+		udp_pp = upd(udp_pp, prev_proto, mU);
+		udp_po = upd(udp_po, prev_off, mU);
+		l7_tcp = mL ? (mT != 0) : l7_tcp;
+		l7_o = upd(l7_o, o, mL);
+		l7_pl = upd(l7_pl, s.pl, mL);
+		l7_next = upd(l7_next, count + 1, mL);
+		l7_end = upd(l7_end, o + s.dlen, mL);
 		prev_proto = proto;
 		prev_off = o;
 		last_end = o + s.dlen;
