@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <thread>
@@ -41,6 +42,7 @@ struct Slot
 };
 
 constexpr uint32_t kDefaultFlowSlots = 1u << 22;  // 64 MiB of flow table in HBM
+constexpr uint32_t kMaxSlots = 4;                   // host-path chunk slots in flight (PCPPX_HOST_SLOTS, 2..4)
 }  // namespace
 
 struct pcppx_ctx
@@ -48,7 +50,8 @@ struct pcppx_ctx
 	int device = 0;
 	hipStream_t stream = nullptr;
 	bool host_ready = false;
-	Slot slots[2];
+	Slot slots[kMaxSlots];
+	uint32_t nslots = 0;  // slots allocated and used by the host paths
 	// host filter path (pcppx_filter_reset / pcppx_filter_batch_host): the worker's flow table in HBM
 	uint64_t* d_keys = nullptr;
 	uint64_t* d_first = nullptr;
@@ -97,8 +100,14 @@ int init_host_path(pcppx_ctx* c)
 {
 	if (c->host_ready)
 		return PCPPX_OK;
-	for (Slot& s : c->slots)
+	// default 2 (double buffering): 3 and 4 slots measured no faster, the link is the limit
+	// (profiles/r01_ab_host_slots.txt)
+	const char* env = getenv("PCPPX_HOST_SLOTS");
+	const int want = env ? atoi(env) : 2;
+	c->nslots = want < 2 ? 2u : (want > (int)kMaxSlots ? kMaxSlots : (uint32_t)want);
+	for (uint32_t si = 0; si < c->nslots; ++si)
 	{
+		Slot& s = c->slots[si];
 		bool good = ok(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking)) && ok(hipEventCreate(&s.done)) &&
 		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_data), kChunkBytes + 16)) &&
 		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), kChunkPackets * sizeof(uint64_t))) &&
@@ -416,7 +425,7 @@ extern "C"
 		uint32_t i = 0, k = 0;
 		while (i < b->n)
 		{
-			Slot& s = c->slots[k & 1];
+			Slot& s = c->slots[k % c->nslots];
 			if (s.busy)
 			{
 				if (!ok(hipEventSynchronize(s.done)))
@@ -544,7 +553,7 @@ extern "C"
 		Slot* prev = nullptr;
 		while (i < b->n)
 		{
-			Slot& s = c->slots[k & 1];
+			Slot& s = c->slots[k % c->nslots];
 			if (s.busy)
 			{
 				if (!ok(hipEventSynchronize(s.done)))
