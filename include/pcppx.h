@@ -238,6 +238,12 @@ typedef struct pcppx_reasm_info { /* 16 bytes per packet */
 int pcppx_reasm_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
                        pcppx_reasm_info* info, void* hip_stream);
 
+/* pcppx_parse_batch_device and pcppx_reasm_device in one pass: the parse kernel writes info[n] too, from the
+ * header bytes it already holds (no second read of the packets or records). opts->max_layers >= 1. The
+ * records and info equal those of the two calls made one after the other. */
+int pcppx_parse_batch_device_reasm(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
+                                   pcppx_records* out, pcppx_reasm_info* info, void* hip_stream);
+
 /* ---- host ingest: pcap files into packed batch buffers ---- */
 typedef struct pcppx_pcap pcppx_pcap;
 int pcppx_pcap_open(const char* path, pcppx_pcap** out); /* PcapFileReaderDevice::open, PcapFileDevice.cpp:707-768 */

@@ -159,6 +159,8 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_filter_device.restype = C.c_int
     lib.pcppx_reasm_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Records), C.c_uint8, P, P]
     lib.pcppx_reasm_device.restype = C.c_int
+    lib.pcppx_parse_batch_device_reasm.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records), P, P]
+    lib.pcppx_parse_batch_device_reasm.restype = C.c_int
     lib.pcppx_filter_reset.argtypes = [P, C.c_uint32]
     lib.pcppx_filter_reset.restype = C.c_int
     lib.pcppx_filter_batch_host.argtypes = [P, C.POINTER(Batch), C.POINTER(MatchSpec), P, C.POINTER(PacketStats)]
@@ -188,7 +190,7 @@ _ENGINE: C.CDLL | None = None
 EXPORTED_SYMBOLS = (
     "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_runtime_info", "pcppx_open", "pcppx_close",
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
-    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_pcap_open", "pcppx_pcap_linktype",
+    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_parse_batch_device_reasm", "pcppx_pcap_open", "pcppx_pcap_linktype",
     "pcppx_pcap_read_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
 )
 

@@ -484,6 +484,21 @@ extern "C"
 		                            static_cast<hipStream_t>(hip_stream));
 	}
 
+	int pcppx_parse_batch_device_reasm(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r,
+	                                   pcppx_reasm_info* info, void* hip_stream)
+	{
+		if (c == nullptr || b == nullptr || r == nullptr || valid_opts(o) != PCPPX_OK || o->max_layers == 0)
+			return PCPPX_E_INVAL;
+		if (b->n == 0)
+			return PCPPX_OK;
+		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || r->summary == nullptr ||
+		    r->layers == nullptr || info == nullptr)
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		return pcppx::launch_parse_reasm(b, o, r, info, static_cast<hipStream_t>(hip_stream));
+	}
+
 	int pcppx_reasm_device(pcppx_ctx* c, const pcppx_batch* b, const pcppx_records* r, uint8_t max_layers,
 	                       pcppx_reasm_info* info, void* hip_stream)
 	{

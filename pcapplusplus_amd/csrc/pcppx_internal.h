@@ -15,5 +15,7 @@ int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, con
 int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
                       uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, uint64_t* packed,
                       hipStream_t stream);
+int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
+                       hipStream_t stream);
 int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcppx_reasm_info* info, hipStream_t stream);
 }  // namespace pcppx

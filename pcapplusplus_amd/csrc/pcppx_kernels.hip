@@ -505,6 +505,7 @@ struct Params
 	uint32_t max_layers;
 	uint32_t linktype;
 	uint32_t diag;  // 0 normal; 2 = stream-only diagnostic (no gather/parse; L4 range = [14, caplen))
+	pcppx_reasm_info* reasm;  // fused reassembly front ends (pcppx_parse_batch_device_reasm), or null
 };
 
 // Everything the summary needs after the chain walk.
@@ -1061,6 +1062,132 @@ __device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Fast&
 	return finish_checksum(r);
 }
 
+// ---- reassembly front ends (SURVEY.md §8f-4; include/pcppx.h pcppx_reasm_device) ----
+// Lane per packet over the parse records: the stateless half of IPReassembly::processPacket
+// (IPReassembly.cpp:284-322) and TcpReassembly::reassemblePacket (TcpReassembly.cpp:96-136). Restated
+// identically in oracle/pcppx_oracle.c (reasm_packet), which pins it against the reference.
+struct ReasmParams
+{
+	const uint8_t* data;
+	const uint64_t* offsets;
+	const pcppx_summary* summary;
+	const pcppx_layer* layers;
+	uint32_t n, ml;
+	pcppx_reasm_info* info;
+};
+
+__device__ __forceinline__ uint32_t fnv_bytes(uint32_t h, const uint8_t* p, uint32_t n)
+{
+	for (uint32_t j = 0; j < n; ++j)
+		h = fnv(h, p[j]);
+	return h;
+}
+
+// One packet's reassembly record from its summary flags, n_layers and layer records (lay: max_layers
+// entries) and its bytes (pkt): shared by reasm_kernel and the tile kernel's fused output.
+__device__ uint4 reasm_one(uint32_t sflags, uint32_t n_layers, const pcppx_layer* lay, uint32_t ml, const uint8_t* pkt)
+{
+	const uint32_t nl = n_layers < ml ? n_layers : ml;
+	int v4 = -1, v6 = -1, tcp = -1;
+	uint32_t last = 0;
+	for (uint32_t k = 0; k < nl; ++k)
+	{
+		const uint32_t pr = lay[k].proto;
+		v4 = (pr == P_IPV4 && v4 < 0) ? (int)k : v4;
+		v6 = (pr == P_IPV6 && v6 < 0) ? (int)k : v6;
+		tcp = pr == P_TCP ? (int)k : tcp;
+		last = pr;
+	}
+	// the chain is unfinished unless every layer the reassemblers look at is on the device (pcppx.h)
+	bool unfinished = (sflags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC |
+	                               PCPPX_F_DEPTH_OVERFLOW)) != 0;
+	unfinished = unfinished || ((sflags & PCPPX_F_NEEDS_HOST_L7) && !(nl > 0 && last == P_TCP));
+	uint32_t key = 0, fid = 0, foff = 0, ips, ts, pay = 0;
+	if (v4 >= 0)
+	{
+		// IPv4 wrapper (IPReassembly.cpp:68-140): isFragment / getFragmentOffset (IPv4Layer.cpp:415-438)
+		const pcppx_layer L = lay[v4];
+		const uint8_t* ip = pkt + L.offset;
+		const uint32_t b6 = ip[6], fo = ((b6 & 0x1F) << 8) | ip[7];
+		const bool more = (b6 & 0x20) != 0;
+		if (!more && fo == 0)
+			ips = PCPPX_IPR_NON_FRAGMENT;
+		else if (L.hdr_len > L.data_len)  // getLayerPayloadSize() > getDataLen() (:315-320)
+			ips = PCPPX_IPR_MALFORMED;
+		else
+		{
+			ips = PCPPX_IPR_FRAGMENT | (fo == 0 ? PCPPX_IPR_F_FIRST : 0) | (!more ? PCPPX_IPR_F_LAST : 0);
+			fid = ((uint32_t)ip[4] << 8) | ip[5];
+			foff = (fo * 8) & 0xFFFF;
+			key = fnv_bytes(fnv_bytes(fnv_bytes(2166136261u, ip + 12, 4), ip + 16, 4), ip + 4, 2);  // :103-115
+		}
+	}
+	else if (unfinished)
+		ips = PCPPX_IPR_HOST;
+	else if (v6 >= 0)
+	{
+		// IPv6 wrapper (IPReassembly.cpp:142-231): the first fragmentation extension of the list
+		// parseExtensions built (IPv6Layer.cpp:79-147), replayed up to the recorded header length
+		const pcppx_layer L = lay[v6];
+		const uint8_t* ip = pkt + L.offset;
+		uint32_t nh = ip[6], eo = 40, fe = 0;
+		bool have = false;
+		while (eo < L.hdr_len)
+		{
+			if (nh == 44 && !have)
+			{
+				have = true;
+				fe = eo;
+			}
+			const uint32_t el = nh == 51 ? 4u * ((uint32_t)ip[eo + 1] + 2) : 8u * ((uint32_t)ip[eo + 1] + 1);
+			nh = ip[eo];
+			eo += el;
+		}
+		if (!have)
+			ips = PCPPX_IPR_F_IPV6 | PCPPX_IPR_NON_FRAGMENT;
+		else if (L.hdr_len > L.data_len)
+			ips = PCPPX_IPR_F_IPV6 | PCPPX_IPR_MALFORMED;
+		else
+		{
+			const uint8_t* f = ip + fe;  // ip6_frag: next header, reserved, offset+flags, id (IPv6Extensions.h)
+			const uint32_t off = ((uint32_t)f[2] << 8) | (f[3] & 0xF8u);  // IPv6Extensions.cpp:87-91
+			ips = PCPPX_IPR_F_IPV6 | PCPPX_IPR_FRAGMENT | (off == 0 ? PCPPX_IPR_F_FIRST : 0) |
+			      ((f[3] & 1) ? 0 : PCPPX_IPR_F_LAST);
+			fid = ((uint32_t)f[4] << 24) | ((uint32_t)f[5] << 16) | ((uint32_t)f[6] << 8) | f[7];
+			foff = off;
+			key = fnv_bytes(fnv_bytes(fnv_bytes(2166136261u, ip + 8, 16), ip + 24, 16), f + 4, 4);  // :190-205
+		}
+	}
+	else
+		ips = PCPPX_IPR_NON_IP;
+	if (unfinished)
+		ts = PCPPX_TCPR_HOST;
+	else if (v4 < 0 && v6 < 0)
+		ts = PCPPX_TCPR_NON_IP;
+	else if (tcp < 0)
+		ts = PCPPX_TCPR_NON_TCP;
+	else
+	{
+		const pcppx_layer L = lay[tcp];
+		const uint32_t fl = pkt[L.offset + 13];  // FIN bit 0, SYN bit 1, RST bit 2 (TcpLayer.h:30-52)
+		pay = (uint32_t)L.data_len - L.hdr_len;
+		ts = ((pay == 0 && (fl & 7) == 0) ? PCPPX_TCPR_NO_DATA : PCPPX_TCPR_DATA) | ((fl & 1) ? PCPPX_TCPR_F_FIN : 0) |
+		     ((fl & 2) ? PCPPX_TCPR_F_SYN : 0) | ((fl & 4) ? PCPPX_TCPR_F_RST : 0);
+	}
+	return make_uint4(key, fid, foff | (ips << 16) | (ts << 24), pay);
+}
+
+__global__ __launch_bounds__(kBlock) void reasm_kernel(ReasmParams rp)
+{
+	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+	if (i >= rp.n)
+		return;
+	const pcppx_summary sm = rp.summary[i];
+	// read only below a recorded layer: the descriptor was checked by the parse
+	reinterpret_cast<uint4*>(rp.info)[i] = reasm_one(sm.flags, sm.n_layers, rp.layers + (size_t)i * rp.ml, rp.ml,
+	                                                 rp.data + rp.offsets[i]);
+}
+
 // ================= tile kernel: one wave = one tile of 64 consecutive packets =================
 //
 // (1) descriptors, coalesced; (2) each packet's first 112 B gathered into LDS with 8 lanes per packet
@@ -1298,6 +1425,9 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 	}
 
+	// the TCP flags byte for the fused reassembly output (the LDS stage is reused by the layer rows below)
+	const uint32_t tcp_fl = (prm.reasm != nullptr && fast && f.tcp) ? (uint32_t)p.s[p.mis + f.l4o + 13] : 0u;
+
 	// ---- (4) L4 checksums over the tile span ----
 	if (prm.want_csum)  // uniform
 	{
@@ -1426,6 +1556,44 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			if (rr < per && r < nrows && m_nch[r])
 				dst[r * ml + kk] = rows[r * rs + kk];
 		}
+	}
+
+	// ---- (6) fused reassembly front ends (same records as reasm_kernel): fast-path packets straight from
+	// their parse (IPv4 not a fragment, IPv6 without extensions, the TCP flags byte in LDS), the rest from
+	// the layer records this lane wrote ----
+	if (prm.reasm != nullptr && in)  // uniform pointer
+	{
+		uint4 r;
+		if (fast)
+		{
+			const uint32_t nl = w.n_layers, ipk = 1 + f.nv, l4k = 2 + f.nv;
+			const bool unfinished = (w.flags & PCPPX_F_DEPTH_OVERFLOW) || ((w.flags & PCPPX_F_NEEDS_HOST_L7) && !f.tcp);
+			const bool v4r = !f.v6 && ipk < nl, v6r = f.v6 && ipk < nl, tcpr = f.tcp && l4k < nl;
+			const uint32_t ipst = v4r ? PCPPX_IPR_NON_FRAGMENT
+			                          : (unfinished ? PCPPX_IPR_HOST
+			                                        : (v6r ? (PCPPX_IPR_F_IPV6 | PCPPX_IPR_NON_FRAGMENT) : PCPPX_IPR_NON_IP));
+			uint32_t ts, pay = 0;
+			if (unfinished)
+				ts = PCPPX_TCPR_HOST;
+			else if (!v4r && !v6r)
+				ts = PCPPX_TCPR_NON_IP;
+			else if (!tcpr)
+				ts = PCPPX_TCPR_NON_TCP;
+			else
+			{
+				const uint32_t fl = tcp_fl;
+				pay = f.l4dlen - f.l4hdr;
+				ts = ((pay == 0 && (fl & 7) == 0) ? PCPPX_TCPR_NO_DATA : PCPPX_TCPR_DATA) |
+				     ((fl & 1) ? PCPPX_TCPR_F_FIN : 0) | ((fl & 2) ? PCPPX_TCPR_F_SYN : 0) | ((fl & 4) ? PCPPX_TCPR_F_RST : 0);
+			}
+			r = make_uint4(0, 0, (ipst << 16) | (ts << 24), pay);
+		}
+		else
+		{
+			__threadfence_block();  // this lane's own layer records, written by the walk
+			r = reasm_one(w.flags, w.n_layers, prm.layers + (size_t)i * ml, ml, prm.data + off);
+		}
+		reinterpret_cast<uint4*>(prm.reasm)[i] = r;
 	}
 }
 
@@ -1911,126 +2079,6 @@ __global__ __launch_bounds__(kBlock) void filter_apply_kernel(FilterParams fp)
 }
 
 
-// ---- reassembly front ends (SURVEY.md §8f-4; include/pcppx.h pcppx_reasm_device) ----
-// Lane per packet over the parse records: the stateless half of IPReassembly::processPacket
-// (IPReassembly.cpp:284-322) and TcpReassembly::reassemblePacket (TcpReassembly.cpp:96-136). Restated
-// identically in oracle/pcppx_oracle.c (reasm_packet), which pins it against the reference.
-struct ReasmParams
-{
-	const uint8_t* data;
-	const uint64_t* offsets;
-	const pcppx_summary* summary;
-	const pcppx_layer* layers;
-	uint32_t n, ml;
-	pcppx_reasm_info* info;
-};
-
-__device__ __forceinline__ uint32_t fnv_bytes(uint32_t h, const uint8_t* p, uint32_t n)
-{
-	for (uint32_t j = 0; j < n; ++j)
-		h = fnv(h, p[j]);
-	return h;
-}
-
-__global__ __launch_bounds__(kBlock) void reasm_kernel(ReasmParams rp)
-{
-	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-	if (i >= rp.n)
-		return;
-	const pcppx_summary sm = rp.summary[i];
-	const uint32_t nl = sm.n_layers < rp.ml ? sm.n_layers : rp.ml;
-	const pcppx_layer* lay = rp.layers + (size_t)i * rp.ml;
-	int v4 = -1, v6 = -1, tcp = -1;
-	uint32_t last = 0;
-	for (uint32_t k = 0; k < nl; ++k)
-	{
-		const uint32_t pr = lay[k].proto;
-		v4 = (pr == P_IPV4 && v4 < 0) ? (int)k : v4;
-		v6 = (pr == P_IPV6 && v6 < 0) ? (int)k : v6;
-		tcp = pr == P_TCP ? (int)k : tcp;
-		last = pr;
-	}
-	// the chain is unfinished unless every layer the reassemblers look at is on the device (pcppx.h)
-	bool unfinished = (sm.flags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC |
-	                               PCPPX_F_DEPTH_OVERFLOW)) != 0;
-	unfinished = unfinished || ((sm.flags & PCPPX_F_NEEDS_HOST_L7) && !(nl > 0 && last == P_TCP));
-	const uint8_t* pkt = rp.data + rp.offsets[i];  // read only below a recorded layer: descriptor checked
-	uint32_t key = 0, fid = 0, foff = 0, ips, ts, pay = 0;
-	if (v4 >= 0)
-	{
-		// IPv4 wrapper (IPReassembly.cpp:68-140): isFragment / getFragmentOffset (IPv4Layer.cpp:415-438)
-		const pcppx_layer L = lay[v4];
-		const uint8_t* ip = pkt + L.offset;
-		const uint32_t b6 = ip[6], fo = ((b6 & 0x1F) << 8) | ip[7];
-		const bool more = (b6 & 0x20) != 0;
-		if (!more && fo == 0)
-			ips = PCPPX_IPR_NON_FRAGMENT;
-		else if (L.hdr_len > L.data_len)  // getLayerPayloadSize() > getDataLen() (:315-320)
-			ips = PCPPX_IPR_MALFORMED;
-		else
-		{
-			ips = PCPPX_IPR_FRAGMENT | (fo == 0 ? PCPPX_IPR_F_FIRST : 0) | (!more ? PCPPX_IPR_F_LAST : 0);
-			fid = ((uint32_t)ip[4] << 8) | ip[5];
-			foff = (fo * 8) & 0xFFFF;
-			key = fnv_bytes(fnv_bytes(fnv_bytes(2166136261u, ip + 12, 4), ip + 16, 4), ip + 4, 2);  // :103-115
-		}
-	}
-	else if (unfinished)
-		ips = PCPPX_IPR_HOST;
-	else if (v6 >= 0)
-	{
-		// IPv6 wrapper (IPReassembly.cpp:142-231): the first fragmentation extension of the list
-		// parseExtensions built (IPv6Layer.cpp:79-147), replayed up to the recorded header length
-		const pcppx_layer L = lay[v6];
-		const uint8_t* ip = pkt + L.offset;
-		uint32_t nh = ip[6], eo = 40, fe = 0;
-		bool have = false;
-		while (eo < L.hdr_len)
-		{
-			if (nh == 44 && !have)
-			{
-				have = true;
-				fe = eo;
-			}
-			const uint32_t el = nh == 51 ? 4u * ((uint32_t)ip[eo + 1] + 2) : 8u * ((uint32_t)ip[eo + 1] + 1);
-			nh = ip[eo];
-			eo += el;
-		}
-		if (!have)
-			ips = PCPPX_IPR_F_IPV6 | PCPPX_IPR_NON_FRAGMENT;
-		else if (L.hdr_len > L.data_len)
-			ips = PCPPX_IPR_F_IPV6 | PCPPX_IPR_MALFORMED;
-		else
-		{
-			const uint8_t* f = ip + fe;  // ip6_frag: next header, reserved, offset+flags, id (IPv6Extensions.h)
-			const uint32_t off = ((uint32_t)f[2] << 8) | (f[3] & 0xF8u);  // IPv6Extensions.cpp:87-91
-			ips = PCPPX_IPR_F_IPV6 | PCPPX_IPR_FRAGMENT | (off == 0 ? PCPPX_IPR_F_FIRST : 0) |
-			      ((f[3] & 1) ? 0 : PCPPX_IPR_F_LAST);
-			fid = ((uint32_t)f[4] << 24) | ((uint32_t)f[5] << 16) | ((uint32_t)f[6] << 8) | f[7];
-			foff = off;
-			key = fnv_bytes(fnv_bytes(fnv_bytes(2166136261u, ip + 8, 16), ip + 24, 16), f + 4, 4);  // :190-205
-		}
-	}
-	else
-		ips = PCPPX_IPR_NON_IP;
-	if (unfinished)
-		ts = PCPPX_TCPR_HOST;
-	else if (v4 < 0 && v6 < 0)
-		ts = PCPPX_TCPR_NON_IP;
-	else if (tcp < 0)
-		ts = PCPPX_TCPR_NON_TCP;
-	else
-	{
-		const pcppx_layer L = lay[tcp];
-		const uint32_t fl = pkt[L.offset + 13];  // FIN bit 0, SYN bit 1, RST bit 2 (TcpLayer.h:30-52)
-		pay = (uint32_t)L.data_len - L.hdr_len;
-		ts = ((pay == 0 && (fl & 7) == 0) ? PCPPX_TCPR_NO_DATA : PCPPX_TCPR_DATA) | ((fl & 1) ? PCPPX_TCPR_F_FIN : 0) |
-		     ((fl & 2) ? PCPPX_TCPR_F_SYN : 0) | ((fl & 4) ? PCPPX_TCPR_F_RST : 0);
-	}
-	uint4 o = make_uint4(key, fid, foff | (ips << 16) | (ts << 24), pay);
-	reinterpret_cast<uint4*>(rp.info)[i] = o;
-}
-
 }  // namespace
 
 // Launch-error check; with PCPPX_SYNC_CHECK=1 in the environment every launch is also synchronised
@@ -2070,6 +2118,7 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	prm.max_layers = o->max_layers;
 	prm.linktype = b->linktype;
 	prm.diag = o->variant == 2 ? 2 : 0;
+	prm.reasm = nullptr;
 	// variant 1 (or PCPPX_KERNEL=lane) selects the lane-per-packet kernel for A/B measurements
 	static const bool lane_env = [] {
 		const char* e = getenv("PCPPX_KERNEL");
@@ -2178,6 +2227,30 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 		done += cnt;
 	}
 	return PCPPX_OK;
+}
+
+int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
+                       hipStream_t stream)
+{
+	if (b->n == 0)
+		return PCPPX_OK;
+	Params prm;
+	prm.data = b->data;
+	prm.offsets = b->offsets;
+	prm.caplens = b->caplens;
+	prm.data_len = b->data_len;
+	prm.summary = r->summary;
+	prm.layers = r->layers;
+	prm.n = b->n;
+	prm.family = o->parse_until_family;
+	prm.until_osi = o->parse_until_osi;
+	prm.want_csum = o->want_checksums;
+	prm.max_layers = o->max_layers;
+	prm.linktype = b->linktype;
+	prm.diag = 0;
+	prm.reasm = info;
+	hipLaunchKernelGGL((parse_tile_kernel<5, 128>), dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
+	return check_launch("parse_tile_kernel(reasm)", stream);
 }
 
 int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcppx_reasm_info* info, hipStream_t stream)

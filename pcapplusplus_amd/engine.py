@@ -88,6 +88,15 @@ class Engine:
         abi.check(self.lib.pcppx_reasm_device(self.ctx, C.byref(b), C.byref(rec), max_layers, abi.ptr(info),
                                               C.c_void_p(stream or 0)), "pcppx_reasm_device")
 
+    def parse_reasm_device(self, data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers,
+                           info, stream: int | None = None) -> None:
+        """Parse + reassembly front ends in one kernel pass (pcppx_parse_batch_device_reasm)."""
+        b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
+        rec = abi.Records(abi.ptr(summary), abi.ptr(layers))
+        abi.check(self.lib.pcppx_parse_batch_device_reasm(self.ctx, C.byref(b), C.byref(opts), C.byref(rec),
+                                                          abi.ptr(info), C.c_void_p(stream or 0)),
+                  "pcppx_parse_batch_device_reasm")
+
     def filter_reset(self, capacity: int = 0) -> None:
         abi.check(self.lib.pcppx_filter_reset(self.ctx, capacity), "pcppx_filter_reset")
 

@@ -163,3 +163,50 @@ def test_gpu_reasm_rejects_bad_args(engine):
         engine.reasm_device(t, t, t, 4, 1, t, t, 0, t)
     with pytest.raises(RuntimeError):
         engine.reasm_device(t, t, t, 4, 1, t, t, 17, t)
+
+
+def gpu_parse_reasm_fused(engine, batch, opts):
+    """pcppx_parse_batch_device_reasm: records and reassembly info from one kernel pass."""
+    import torch
+
+    from pcapplusplus_amd.engine import records_from_device, to_device
+
+    dev = "cuda:0"
+    n = batch.n
+    data, offsets, caplens = to_device(batch, dev)
+    summary = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device=dev)
+    layers = torch.zeros(max(n * opts.max_layers, 1) * 8, dtype=torch.uint8, device=dev)
+    info = torch.full((max(n, 1) * 16,), 0xAB, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    engine.parse_reasm_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, info, stream)
+    torch.cuda.synchronize(dev)
+    s, lay = records_from_device(summary, layers, n, opts.max_layers)
+    return s, lay, info.cpu().numpy().view(abi.REASM_DTYPE)[:n]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ml,csum", [(16, False), (8, True), (4, False)])
+def test_gpu_fused_parse_reasm(engine, ml, csum):
+    """The fused pass equals the parse + pcppx_reasm_device pair and the restatement, records included."""
+    from pcapplusplus_amd import synth
+    from pcapplusplus_amd.pcap import concat
+
+    opts = abi.make_opts(0, 8, csum, ml)
+    pk = fragments(8000, 77)
+    sets = [as_batch(pk), as_batch(mutate(pk, 8000, 9), gaps=True, seed=4), synth.config(3, 20000),
+            synth.config(5, 20000)] + [load_golden(p)[0] for p in golden_files() if p.stem in ("pcap_lt1", "dat_ethernet")]
+    for b in sets:
+        s, lay, info = gpu_parse_reasm_fused(engine, b, opts)
+        os_, ol = oracle.oracle_parse(b, opts)
+        oracle.compare_exact(s, lay, os_, ol)
+        assert_equal_info(info, oracle.oracle_reasm(b, os_, ol), "fused")
+        assert_equal_info(info, gpu_reasm(engine, b, ml), "fused vs separate")
+
+
+@pytest.mark.gpu
+def test_gpu_fused_parse_reasm_rejects_bad_args(engine):
+    import torch
+
+    t = torch.zeros(64, dtype=torch.int64, device="cuda:0")
+    with pytest.raises(RuntimeError):  # max_layers 0: the fused pass needs layer records
+        engine.parse_reasm_device(t, t, t, 4, 1, abi.make_opts(0, 8, False, 0), t, t, t)

@@ -6,7 +6,8 @@ Workload: config-3 IMIX (7/8 of the packets) followed by IP fragments / TCP segm
 tests/mutate.py:fragments (1/8) (so fragment keys and IPv6 extension replays are on the path). The parse runs
 once; the timed region is `steps` reasm launches (HIP events on the launch stream). Algorithmic bytes per
 packet: the 32-B summary + the packet's layer records read up to n_layers (8 B each) + 16 B written;
-header bytes of fragments are counted too (<= 40 B). Prints one JSON line.
+header bytes of fragments are counted too (<= 40 B). Also times the parse alone and the fused
+parse + reassembly pass (pcppx_parse_batch_device_reasm). Prints one JSON line.
 """
 import json
 import sys
@@ -48,6 +49,22 @@ for _ in range(steps):
 e1.record(st)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / steps
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(steps):
+        fn()
+    z.record(st)
+    torch.cuda.synchronize()
+    return a.elapsed_time(z) / steps
+
+
+opts = abi.make_opts(0, 8, False, ml)
+parse_ms = timed(lambda: eng.parse_device(data, offsets, caplens, n, b.linktype, opts, summary, layers, st.cuda_stream))
+fused_ms = timed(lambda: eng.parse_reasm_device(data, offsets, caplens, n, b.linktype, opts, summary, layers, info,
+                                                st.cuda_stream))
 s = summary.view(torch.int32).view(n, 8)
 nl = ((s[:, 3] >> 16) & 0xFF).clamp(max=ml).to(torch.int64)
 inf = info.cpu().numpy().view(abi.REASM_DTYPE)
@@ -55,5 +72,6 @@ frag = (inf["ip_status"] & 0xF) == abi.IPR_FRAGMENT
 algo = 32 * n + 8 * int(nl.sum().item()) + 16 * n + 40 * int(frag.sum())
 print(json.dumps({"kernel": "reasm_kernel", "packets": n, "ms": round(ms, 4), "Gpackets_per_s": round(n / ms / 1e6, 2),
                   "algorithmic_bytes": algo, "GBps": round(algo / ms / 1e6, 1), "frac_of_8TBps": round(algo / ms / 8e9, 4),
+                  "parse_only_ms": round(parse_ms, 4), "fused_parse_reasm_ms": round(fused_ms, 4),
                   "fragments": int(frag.sum()), "tcp_data": int(((inf["tcp_status"] & 0xF) == abi.TCPR_DATA).sum())}))
 eng.close()
