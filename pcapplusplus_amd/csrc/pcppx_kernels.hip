@@ -1289,7 +1289,8 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // with 7-chunk windows (stage 7424 B + 768 B of per-lane state): 20 blocks = 5 waves/SIMD fit a CU's
 // 160 KiB. SWin: stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers).
 // Chunks: 16-B header chunks staged per packet.
-template <int MinWaves, int SWin, int Chunks = kTStageChunks>
+// NT: non-temporal span-stream loads and record stores (read-once / write-once data; A/B variant 11)
+template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1325,7 +1326,14 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// clamped, not masked: lanes past the span re-read its last chunk (same line, no extra
 			// traffic); their values lie after every prefix target, so they are inert
 			const uint32_t c = win * SWin + 64 * k + lane;
-			v[k] = ld16(smin + 16ull * (c < nchunks ? c : nchunks - 1));
+			const uintptr_t a = smin + 16ull * (c < nchunks ? c : nchunks - 1);
+			if (NT)
+			{
+				const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<gptr16>(a));
+				v[k] = make_uint4(t.x, t.y, t.z, t.w);
+			}
+			else
+				v[k] = ld16(a);
 		}
 	};
 	if (stream)
@@ -1511,7 +1519,17 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 	}
 
-	if (in)
+	if (in && NT)
+	{
+		const uint32_t l4b = w.l4i >= 0 ? (uint32_t)w.l4i : 0xFFu;
+		u32x4 s0, s1;
+		s0.x = h5; s0.y = h5d; s0.z = h2; s0.w = w.flags | (w.n_layers << 16) | (l4b << 24);
+		s1.x = (uint32_t)w.mask; s1.y = (uint32_t)(w.mask >> 32); s1.z = ipc | (ips << 16); s1.w = l4c | (l4s << 16);
+		u32x4* so = reinterpret_cast<u32x4*>(prm.summary + i);
+		__builtin_nontemporal_store(s0, so);
+		__builtin_nontemporal_store(s1, so + 1);
+	}
+	else if (in)
 		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
 
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores ----
@@ -1554,7 +1572,12 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		{
 			const uint32_t r = r0 + rr;
 			if (rr < per && r < nrows && m_nch[r])
-				dst[r * ml + kk] = rows[r * rs + kk];
+			{
+				if (NT)
+					__builtin_nontemporal_store(rows[r * rs + kk], &dst[r * ml + kk]);
+				else
+					dst[r * ml + kk] = rows[r * rs + kk];
+			}
 		}
 	}
 
@@ -2155,8 +2178,10 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 		hipLaunchKernelGGL((parse_tile_kernel<1, 128>), grid, dim3(kTile), 0, stream, prm);
 	else if (o->variant == 8)
 		hipLaunchKernelGGL((parse_tile_kernel<1, 256>), grid, dim3(kTile), 0, stream, prm);
-	else
+	else if (o->variant == 11)  // cached loads / stores (the default before non-temporal ones, A/B)
 		hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm);
+	else  // default: non-temporal span stream and record stores (profiles/r01_ab_nontemporal.txt)
+		hipLaunchKernelGGL((parse_tile_kernel<5, 128, kTStageChunks, true>), grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel", stream);
 }
 
@@ -2249,7 +2274,8 @@ int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records*
 	prm.linktype = b->linktype;
 	prm.diag = 0;
 	prm.reasm = info;
-	hipLaunchKernelGGL((parse_tile_kernel<5, 128>), dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
+	hipLaunchKernelGGL((parse_tile_kernel<5, 128, kTStageChunks, true>), dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0,
+	                   stream, prm);
 	return check_launch("parse_tile_kernel(reasm)", stream);
 }
 

@@ -31,6 +31,7 @@ cases = {
     "tile/w5win256": abi.make_opts(0, 8, True, 8, 5),
     "tile/w4win128": abi.make_opts(0, 8, True, 8, 6),
     "tile/w4win256": abi.make_opts(0, 8, True, 8, 8),
+    "tile/cached": abi.make_opts(0, 8, True, 8, 11),
     "tile/stream-only": abi.make_opts(0, 8, True, 0, 2),
     "diag/tile-read": abi.make_opts(0, 8, True, 0, 3),
     "diag/grid-read": abi.make_opts(0, 8, True, 0, 4),
