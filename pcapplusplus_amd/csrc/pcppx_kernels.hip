@@ -391,6 +391,36 @@ struct Step
 	uint32_t proto, osi, hdr, dlen, nk, po, pl;
 };
 
+// per-kind ProtocolType (6 bits) and OsiModelLayer (3 bits); kinds without a layer map to Payload / 7
+constexpr uint32_t kind_proto(uint32_t k)
+{
+	return k == K_ETH ? P_ETH : k == K_DOT3 ? P_DOT3 : k == K_LLC ? P_LLC : k == K_VLAN ? P_VLAN : k == K_MPLS ? P_MPLS
+	     : k == K_IPV4 ? P_IPV4 : k == K_IPV6 ? P_IPV6 : k == K_GRE0 ? P_GREV0 : k == K_GRE1 ? P_GREV1
+	     : k == K_PPTP ? P_PPTP : k == K_TCP ? P_TCP : k == K_UDP ? P_UDP : k == K_ARP ? P_ARP : P_PAYLOAD;
+}
+constexpr uint32_t kind_osi(uint32_t k)
+{
+	return (k == K_ETH || k == K_DOT3 || k == K_LLC || k == K_VLAN) ? 2
+	     : (k == K_MPLS || k == K_IPV4 || k == K_IPV6 || k == K_GRE0 || k == K_GRE1 || k == K_ARP) ? 3
+	     : k == K_PPTP ? 5 : (k == K_TCP || k == K_UDP) ? 4 : 7;
+}
+constexpr uint64_t pack_proto(uint32_t first)
+{
+	uint64_t t = 0;
+	for (uint32_t k = first; k < first + 10 && k <= K_ARP; ++k)
+		t |= (uint64_t)kind_proto(k) << (6 * (k - first));
+	return t;
+}
+constexpr uint64_t pack_osi()
+{
+	uint64_t t = 0;
+	for (uint32_t k = 0; k <= K_ARP; ++k)
+		t |= (uint64_t)kind_osi(k) << (3 * k);
+	return t;
+}
+constexpr uint64_t kProtoLo = pack_proto(0), kProtoHi = pack_proto(10), kOsi = pack_osi();
+static_assert(K_ARP < 20 && 3 * K_ARP + 3 <= 64, "kind tables");
+
 __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o, uint32_t len, const Peek& q)
 {
 	const bool isE = k == K_ETH, isD = k == K_DOT3, isL = k == K_LLC, isV = k == K_VLAN, isM = k == K_MPLS;
@@ -420,15 +450,10 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 			ext += el;
 		}
 	}
-	// protocol / OSI layer (ProtocolType.h)
-	uint32_t proto = P_PAYLOAD, osi = 7;
-	proto = isE ? P_ETH : (isD ? P_DOT3 : (isL ? P_LLC : (isV ? P_VLAN : proto)));
-	osi = (isE || isD || isL || isV) ? 2 : osi;
-	proto = isM ? P_MPLS : (is4 ? P_IPV4 : (is6 ? P_IPV6 : (isA ? P_ARP : proto)));
-	proto = isG ? (k == K_GRE0 ? P_GREV0 : P_GREV1) : proto;
-	osi = (isM || is4 || is6 || isG || isA) ? 3 : osi;
-	proto = isP ? P_PPTP : (isT ? P_TCP : (isU ? P_UDP : proto));
-	osi = isP ? 5 : ((isT || isU) ? 4 : osi);
+	// protocol / OSI layer (ProtocolType.h) of kind k, read from per-kind tables packed into 64-bit
+	// constants (two shifts instead of a select chain over every kind)
+	const uint32_t proto = (uint32_t)((k < 10 ? (kProtoLo >> (6 * k)) : (kProtoHi >> (6 * (k - 10)))) & 63u);
+	const uint32_t osi = (uint32_t)((kOsi >> (3 * k)) & 7u);
 	// header length
 	const uint32_t f0 = q.b(0), f1 = q.b(1);
 	const uint32_t greh = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
@@ -541,16 +566,17 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	const uint32_t cap_layers = ml ? ml : PCPPX_MAX_LAYERS;
 	uint32_t count = 0, found = 0, stopped = 0;
 	uint64_t mask = 0;
-	int32_t v4 = -1, v6 = -1;
-	uint32_t v4_dlen = 0;
-	int32_t tcp_i = -1, udp_i = -1;
-	uint32_t tcp_off = 0, tcp_dlen = 0, tcp_pp = 0, tcp_po = 0;
-	uint32_t udp_off = 0, udp_dlen = 0, udp_pp = 0, udp_po = 0;
-	uint32_t prev_proto = 0, prev_off = 0;
+	// loop-carried bookkeeping packed in 16-bit fields (offsets and lengths are < 2^16, counts < 2^8): fewer
+	// live registers means fewer copies at the loop's joins
+	uint32_t v4w = 0xFFFFu;    // first IPv4: offset | dataLen << 16 (offset 0xFFFF: none)
+	uint32_t v6o = 0xFFFFu;    // first IPv6 offset (0xFFFF: none)
+	uint32_t tcpA = 0, tcpB = 0, udpA = 0, udpB = 0;  // last TCP / UDP: index+1 | offset << 16,
+	                                                 // dataLen | previous layer's offset << 16
+	uint32_t pps = 0;          // previous layer's proto of the last TCP (bits 0-7) / UDP (8-15); bits 16-31: the
+	                           // payload length of the last TCP/UDP layer (the L7 decision's input)
+	uint32_t prev = 0;         // previous layer: proto | offset << 16
 	uint32_t last_end = 0;
 	uint32_t o = 0, len = cap;
-	uint32_t l7_o = 0, l7_pl = 0, l7_next = 0, l7_end = 0;  // last TCP/UDP layer: offset, payload, index after it
-	bool l7_tcp = false;
 
 	// The loop body is written as selects around three divergent regions (the loop exits, the peek's HBM
 	// fallback, the record store): the 64 lanes sit on different layer kinds, and every `if` becomes an
@@ -586,31 +612,21 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		if (lay_out && count < ml)
 			lay_out[count] = make_uint2(proto | (s.osi << 8) | (o << 16), (s.hdr & 0xFFFF) | (s.dlen << 16));
 		mask |= 1ull << proto;
-		const bool first4 = proto == P_IPV4 && v4 < 0;
-		v4_dlen = first4 ? s.dlen : v4_dlen;
-		v4 = first4 ? (int32_t)o : v4;
-		v6 = (proto == P_IPV6 && v6 < 0) ? (int32_t)o : v6;
-		// bookkeeping of the last TCP / UDP layer as and/or with lane masks (a run of selects on one
-		// condition is otherwise folded into a branch)
-		const uint32_t mT = proto == P_TCP ? ~0u : 0u, mU = proto == P_UDP ? ~0u : 0u, mL = mT | mU;
-		auto upd = [](uint32_t old_v, uint32_t new_v, uint32_t m) { return (old_v & ~m) | (new_v & m); };
-		tcp_i = (int32_t)upd((uint32_t)tcp_i, count, mT);
-		tcp_off = upd(tcp_off, o, mT);
-		tcp_dlen = upd(tcp_dlen, s.dlen, mT);
-		tcp_pp = upd(tcp_pp, prev_proto, mT);
-		tcp_po = upd(tcp_po, prev_off, mT);
-		udp_i = (int32_t)upd((uint32_t)udp_i, count, mU);
-		udp_off = upd(udp_off, o, mU);
-		udp_dlen = upd(udp_dlen, s.dlen, mU);
-		udp_pp = upd(udp_pp, prev_proto, mU);
-		udp_po = upd(udp_po, prev_off, mU);
-		l7_tcp = mL ? (mT != 0) : l7_tcp;
-		l7_o = upd(l7_o, o, mL);
-		l7_pl = upd(l7_pl, s.pl, mL);
-		l7_next = upd(l7_next, count + 1, mL);
-		l7_end = upd(l7_end, o + s.dlen, mL);
-		prev_proto = proto;
-		prev_off = o;
+		v4w = (proto == P_IPV4 && v4w == 0xFFFFu) ? (o | (s.dlen << 16)) : v4w;
+		v6o = (proto == P_IPV6 && v6o == 0xFFFFu) ? o : v6o;
+		// the last TCP / UDP layer, as and/or with lane masks (a run of selects on one condition is
+		// otherwise folded into a branch)
+		const uint32_t mT = proto == P_TCP ? ~0u : 0u, mU = proto == P_UDP ? ~0u : 0u;
+		const uint32_t a_new = (count + 1) | (o << 16);
+		const uint32_t b_new = (s.dlen & 0xFFFFu) | (prev & 0xFFFF0000u);
+		tcpA = (tcpA & ~mT) | (a_new & mT);
+		tcpB = (tcpB & ~mT) | (b_new & mT);
+		udpA = (udpA & ~mU) | (a_new & mU);
+		udpB = (udpB & ~mU) | (b_new & mU);
+		const uint32_t mP = (mT & 0xFFu) | (mU & 0xFF00u) | ((mT | mU) & 0xFFFF0000u);
+		const uint32_t p_new = (prev & 0xFFu) * 0x101u | (s.pl << 16);
+		pps = (pps & ~mP) | (p_new & mP);
+		prev = proto | (o << 16);
 		last_end = o + s.dlen;
 		++count;
 		k = nk; o = s.po; len = s.pl;
@@ -620,6 +636,10 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	// tables and the SIP heuristic, read once per packet after the walk so their latency is not on the
 	// walk's critical path. A payload the reference would hand to an L7 dissector ends the chain after the
 	// L4 layer (the tentative Payload layer is dropped) and flags the packet for the host.
+	// the last TCP/UDP layer: whichever of the two came later
+	const bool l7_tcp = (tcpA & 0xFFFFu) > (udpA & 0xFFFFu);
+	const uint32_t l7A = l7_tcp ? tcpA : udpA, l7B = l7_tcp ? tcpB : udpB;
+	const uint32_t l7_o = l7A >> 16, l7_next = l7A & 0xFFFFu, l7_end = l7_o + (l7B & 0xFFFFu), l7_pl = pps >> 16;
 	if (l7_pl > 0 && !(flags & PCPPX_F_NEEDS_HOST_PROTO))
 	{
 		const uint32_t pw = rd32(p, l7_o);
@@ -654,15 +674,16 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	w.flags = flags;
 	w.n_layers = count > cap_layers ? cap_layers : count;
 	w.mask = mask;
-	w.v4 = v4;
-	w.v6 = v6;
-	w.v4_dlen = v4_dlen;
-	w.is_tcp = tcp_i >= 0;
-	w.l4i = w.is_tcp ? tcp_i : udp_i;
-	w.l4o = w.is_tcp ? tcp_off : udp_off;
-	w.l4dlen = w.is_tcp ? tcp_dlen : udp_dlen;
-	w.l4pp = w.is_tcp ? tcp_pp : udp_pp;
-	w.l4ppo = w.is_tcp ? tcp_po : udp_po;
+	w.v4 = (v4w & 0xFFFFu) == 0xFFFFu ? -1 : (int32_t)(v4w & 0xFFFFu);
+	w.v6 = v6o == 0xFFFFu ? -1 : (int32_t)v6o;
+	w.v4_dlen = v4w >> 16;
+	w.is_tcp = tcpA != 0;
+	const uint32_t A = w.is_tcp ? tcpA : udpA, B = w.is_tcp ? tcpB : udpB;
+	w.l4i = (int32_t)(A & 0xFFFFu) - 1;  // -1: no TCP/UDP layer (A == 0)
+	w.l4o = A >> 16;
+	w.l4dlen = B & 0xFFFFu;
+	w.l4pp = w.is_tcp ? (pps & 0xFFu) : ((pps >> 8) & 0xFFu);
+	w.l4ppo = B >> 16;
 	return w;
 }
 
