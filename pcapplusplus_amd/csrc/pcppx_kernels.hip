@@ -433,8 +433,11 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 		uint32_t eo = 40;
 		while (eo <= len - 2)
 		{
-			const bool std_ext = nh == 44 || nh == 0 || nh == 60 || nh == 43, ah = nh == 51;
-			if (!(std_ext || ah))
+			// extension next-header values 0, 43, 44, 51 (AH), 60 as one 64-bit set (a compare chain becomes a
+			// branch tree)
+			constexpr uint64_t kExt = (1ull << 0) | (1ull << 43) | (1ull << 44) | (1ull << 51) | (1ull << 60);
+			const bool ah = nh == 51;
+			if (nh >= 64 || !((kExt >> nh) & 1ull))
 				break;
 			// the extension's next-header and length bytes: LDS window read for every lane, HBM only past it
 			const uint32_t j = o + eo;
