@@ -1692,40 +1692,40 @@ __global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, ui
 // A block aggregates 1024 packets at a time in an LDS hash table (LDS atomics), then adds one
 // {packets, bytes} pair per distinct flow to the HBM table: Zipf-skewed traffic puts a hot flow in most
 // packets of a batch, and per-packet global atomics on its slot would serialise.
-constexpr uint32_t kFlowLds = 2048;                 // LDS slots per block (>= 2x the packets of a batch)
-constexpr uint32_t kFlowBatch = 4 * kBlock;         // packets aggregated between two flushes
-constexpr uint32_t kFlowGrid = 512;                 // persistent blocks (2 per CU; A/B in profiles/r01_ab_flow_grid.txt)
+// Shape variants (block threads, LDS slots, packets per batch) are A/B'd in profiles/r01_ab_flow_shape.txt;
+// every shape keeps LDS slots >= 2x the packets of a batch.
+constexpr uint32_t kFlowGrid = 512;                 // persistent blocks of shape 0 (A/B in profiles/r01_ab_flow_grid.txt)
 constexpr uint32_t kFlowHot = 2;                    // flows with more packets stay in LDS between flushes
+constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 
 // With `packed` (a zeroed u64 per slot, launches of < 2^24 packets) a flush adds {packets, bytes} as one
 // 64-bit atomic (packets << 40 | bytes: < 2^24 packets x < 2^16 B fit 40 bits) and flow_unpack_kernel
 // moves the sums into the table's own counters afterwards: one global atomic per distinct flow and flush.
-__global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
+template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch>
+__global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
                                                             unsigned long long* bytes, uint32_t capacity,
                                                             unsigned long long* stats, unsigned long long* packed)
 {
 	__shared__ uint32_t s_key[kFlowLds];
-	__shared__ uint32_t s_pk[kFlowLds];
-	__shared__ unsigned long long s_by[kFlowLds];
+	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
 	__shared__ uint32_t s_kept;
 	const uint32_t t = threadIdx.x;
 	const uint32_t m = capacity - 1;
 	unsigned long long z_pk = 0, z_by = 0, lost = 0;  // flow key 0 (PacketUtils.cpp:141-148); table full
-	for (uint32_t j = t; j < kFlowLds; j += kBlock)
+	for (uint32_t j = t; j < kFlowLds; j += kFB)
 	{
 		s_key[j] = 0;
-		s_pk[j] = 0;
-		s_by[j] = 0;
+		s_cnt[j] = 0;
 	}
 	__syncthreads();
 	for (uint64_t base = (uint64_t)blockIdx.x * kFlowBatch; base < n; base += (uint64_t)gridDim.x * kFlowBatch)
 	{
 #pragma unroll
-		for (uint32_t r = 0; r < kFlowBatch / kBlock; ++r)
+		for (uint32_t r = 0; r < kFlowBatch / kFB; ++r)
 		{
-			const uint64_t i = base + r * kBlock + t;
+			const uint64_t i = base + r * kFB + t;
 			if (i >= n)
 				break;
 			const uint32_t key = sum[i].hash5;
@@ -1736,14 +1736,14 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 				z_by += len;
 				continue;
 			}
-			uint32_t slot = (key * 0x9E3779B1u) >> 21;  // top 11 bits
+			static_assert(2 * kFlowBatch <= kFlowLds && (kFlowLds & (kFlowLds - 1)) == 0, "flow shape");
+			uint32_t slot = (key * 0x9E3779B1u) >> (32 - log2u(kFlowLds));  // top bits
 			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
 			{
 				const uint32_t prev = atomicCAS(&s_key[slot], 0u, key);
 				if (prev == 0u || prev == key)
 				{
-					atomicAdd(&s_pk[slot], 1u);
-					atomicAdd(&s_by[slot], (unsigned long long)len);
+					atomicAdd(&s_cnt[slot], (1ull << 40) | len);
 					break;
 				}
 				slot = (slot + 1) & (kFlowLds - 1);
@@ -1758,11 +1758,11 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 		// block meets the top Zipf flows in every batch, and same-address atomics serialise. They are
 		// kept only while they fill at most half of the table, so the next batch always fits.
 		const bool last = base + (uint64_t)gridDim.x * kFlowBatch >= n;  // uniform
-		constexpr uint32_t kPer = kFlowLds / kBlock;
+		constexpr uint32_t kPer = kFlowLds / kFB;
 		uint32_t hot = 0;
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
-			hot |= (s_pk[u * kBlock + t] > kFlowHot ? 1u : 0u) << u;
+			hot |= ((s_cnt[u * kFB + t] >> 40) > kFlowHot ? 1u : 0u) << u;
 		if (!last && hot)
 			atomicAdd(&s_kept, (uint32_t)__popc(hot));
 		__syncthreads();
@@ -1771,7 +1771,7 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
 		{
-			const uint32_t j = u * kBlock + t;
+			const uint32_t j = u * kFB + t;
 			fk[u] = (keep_hot && ((hot >> u) & 1u)) ? 0u : s_key[j];
 			fs[u] = (fk[u] * 0x9E3779B1u) & m;
 			fseen[u] = fk[u] ? keys[fs[u]] : 0u;
@@ -1779,7 +1779,7 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
 		{
-			const uint32_t j = u * kBlock + t;
+			const uint32_t j = u * kFB + t;
 			const uint32_t key = fk[u];
 			if (key == 0)
 				continue;
@@ -1794,17 +1794,16 @@ __global__ __launch_bounds__(kBlock) void flow_count_kernel(const pcppx_summary*
 					slot = (slot + 1) & m;
 			}
 			if (done && packed)
-				atomicAdd(&packed[slot], ((unsigned long long)s_pk[j] << 40) | s_by[j]);
+				atomicAdd(&packed[slot], s_cnt[j]);
 			else if (done)
 			{
-				atomicAdd(&packets[slot], (unsigned long long)s_pk[j]);
-				atomicAdd(&bytes[slot], s_by[j]);
+				atomicAdd(&packets[slot], s_cnt[j] >> 40);
+				atomicAdd(&bytes[slot], s_cnt[j] & ((1ull << 40) - 1));
 			}
 			else
-				lost += s_pk[j];
+				lost += s_cnt[j] >> 40;
 			s_key[j] = 0;
-			s_pk[j] = 0;
-			s_by[j] = 0;
+			s_cnt[j] = 0;
 		}
 		__syncthreads();
 	}
@@ -2253,15 +2252,31 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 	static const uint32_t grid_cap = [] {  // PCPPX_FLOW_GRID: A/B of the persistent grid size
 		const char* e = getenv("PCPPX_FLOW_GRID");
 		const int v = e ? atoi(e) : 0;
-		return v > 0 ? (uint32_t)v : kFlowGrid;
+		return v > 0 ? (uint32_t)v : 0u;
+	}();
+	static const int shape = [] {  // PCPPX_FLOW_SHAPE: A/B of block threads / LDS slots / batch
+		const char* e = getenv("PCPPX_FLOW_SHAPE");
+		return e ? atoi(e) : 2;
 	}();
 	for (uint32_t done = 0; done < n;)
 	{
-		const uint32_t cnt = pc ? (n - done < kPackedMax ? n - done : kPackedMax) : n - done;
-		const uint32_t batches = (cnt + kFlowBatch - 1) / kFlowBatch;
-		dim3 grid(batches < grid_cap ? batches : grid_cap);
-		hipLaunchKernelGGL(flow_count_kernel, grid, dim3(kBlock), 0, stream, sum + done, caplens + done, cnt, keys, pk,
-		                   by, capacity, reinterpret_cast<unsigned long long*>(stats), pc);
+		const uint32_t cnt = n - done < kPackedMax ? n - done : kPackedMax;  // the LDS counters are packed too
+		auto* st = reinterpret_cast<unsigned long long*>(stats);
+		auto go = [&](auto kern, uint32_t threads, uint32_t batch, uint32_t def_grid) {
+			const uint32_t batches = (cnt + batch - 1) / batch;
+			const uint32_t cap = grid_cap ? grid_cap : def_grid;
+			hipLaunchKernelGGL(kern, dim3(batches < cap ? batches : cap), dim3(threads), 0, stream, sum + done,
+			                   caplens + done, cnt, keys, pk, by, capacity, st, pc);
+		};
+		switch (shape)
+		{
+		case 1: go(flow_count_kernel<512, 4096, 2048>, 512, 2048, 512); break;
+		case 3: go(flow_count_kernel<256, 4096, 2048>, 256, 2048, 512); break;
+		case 4: go(flow_count_kernel<512, 8192, 4096>, 512, 4096, 256); break;
+		case 5: go(flow_count_kernel<1024, 8192, 2048>, 1024, 2048, 256); break;
+		case 0: go(flow_count_kernel<256, 2048, 1024>, 256, 1024, kFlowGrid); break;
+		default: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;  // shape 2
+		}
 		int rc = check_launch("flow_count_kernel", stream);
 		if (rc != PCPPX_OK)
 			return rc;
