@@ -1701,7 +1701,7 @@ constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 // With `packed` (a zeroed u64 per slot, launches of < 2^24 packets) a flush adds {packets, bytes} as one
 // 64-bit atomic (packets << 40 | bytes: < 2^24 packets x < 2^16 B fit 40 bits) and flow_unpack_kernel
 // moves the sums into the table's own counters afterwards: one global atomic per distinct flow and flush.
-template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch>
+template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -1762,7 +1762,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		uint32_t hot = 0;
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
-			hot |= ((s_cnt[u * kFB + t] >> 40) > kFlowHot ? 1u : 0u) << u;
+			hot |= ((s_cnt[u * kFB + t] >> 40) > kHot ? 1u : 0u) << u;
 		if (!last && hot)
 			atomicAdd(&s_kept, (uint32_t)__popc(hot));
 		__syncthreads();
@@ -2275,6 +2275,9 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 		case 4: go(flow_count_kernel<512, 8192, 4096>, 512, 4096, 256); break;
 		case 5: go(flow_count_kernel<1024, 8192, 2048>, 1024, 2048, 256); break;
 		case 0: go(flow_count_kernel<256, 2048, 1024>, 256, 1024, kFlowGrid); break;
+		case 6: go(flow_count_kernel<1024, 8192, 4096, 1>, 1024, 4096, 256); break;
+		case 7: go(flow_count_kernel<1024, 8192, 4096, 4>, 1024, 4096, 256); break;
+		case 8: go(flow_count_kernel<1024, 8192, 4096, 8>, 1024, 4096, 256); break;
 		default: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;  // shape 2
 		}
 		int rc = check_launch("flow_count_kernel", stream);
