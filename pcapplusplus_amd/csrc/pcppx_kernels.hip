@@ -1701,7 +1701,7 @@ constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 // With `packed` (a zeroed u64 per slot, launches of < 2^24 packets) a flush adds {packets, bytes} as one
 // 64-bit atomic (packets << 40 | bytes: < 2^24 packets x < 2^16 B fit 40 bits) and flow_unpack_kernel
 // moves the sums into the table's own counters afterwards: one global atomic per distinct flow and flush.
-template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot>
+template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -1720,16 +1720,33 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		s_cnt[j] = 0;
 	}
 	__syncthreads();
+	// kPrefetch: the next batch's keys and lengths are loaded into registers before this batch's flush,
+	// so their latency overlaps the flush's HBM reads and atomics
+	constexpr uint32_t kR = kFlowBatch / kFB;
+	uint32_t pkey[kR], plen[kR], pvalid = 0;
+	auto fetch = [&](uint64_t b) {
+		pvalid = 0;
+#pragma unroll
+		for (uint32_t r = 0; r < kR; ++r)
+		{
+			const uint64_t i = b + r * kFB + t;
+			pkey[r] = i < n ? sum[i].hash5 : 0u;
+			plen[r] = i < n ? caplens[i] : 0u;
+			pvalid |= (i < n ? 1u : 0u) << r;
+		}
+	};
+	if (kPrefetch)
+		fetch((uint64_t)blockIdx.x * kFlowBatch);
 	for (uint64_t base = (uint64_t)blockIdx.x * kFlowBatch; base < n; base += (uint64_t)gridDim.x * kFlowBatch)
 	{
 #pragma unroll
-		for (uint32_t r = 0; r < kFlowBatch / kFB; ++r)
+		for (uint32_t r = 0; r < kR; ++r)
 		{
 			const uint64_t i = base + r * kFB + t;
-			if (i >= n)
+			if (kPrefetch ? !((pvalid >> r) & 1u) : i >= n)
 				break;
-			const uint32_t key = sum[i].hash5;
-			const uint32_t len = caplens[i];
+			const uint32_t key = kPrefetch ? pkey[r] : sum[i].hash5;
+			const uint32_t len = kPrefetch ? plen[r] : caplens[i];
 			if (key == 0)
 			{
 				z_pk += 1;
@@ -1749,6 +1766,8 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				slot = (slot + 1) & (kFlowLds - 1);
 			}
 		}
+		if (kPrefetch)
+			fetch(base + (uint64_t)gridDim.x * kFlowBatch);
 		if (t == 0)
 			s_kept = 0;
 		__syncthreads();
@@ -2256,7 +2275,7 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 	}();
 	static const int shape = [] {  // PCPPX_FLOW_SHAPE: A/B of block threads / LDS slots / batch
 		const char* e = getenv("PCPPX_FLOW_SHAPE");
-		return e ? atoi(e) : 2;
+		return e ? atoi(e) : 9;
 	}();
 	for (uint32_t done = 0; done < n;)
 	{
@@ -2276,9 +2295,11 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 		case 5: go(flow_count_kernel<1024, 8192, 2048>, 1024, 2048, 256); break;
 		case 0: go(flow_count_kernel<256, 2048, 1024>, 256, 1024, kFlowGrid); break;
 		case 6: go(flow_count_kernel<1024, 8192, 4096, 1>, 1024, 4096, 256); break;
+		case 2: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;
+		case 10: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true>, 512, 2048, 512); break;
 		case 7: go(flow_count_kernel<1024, 8192, 4096, 4>, 1024, 4096, 256); break;
 		case 8: go(flow_count_kernel<1024, 8192, 4096, 8>, 1024, 4096, 256); break;
-		default: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;  // shape 2
+		default: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true>, 1024, 4096, 256); break;  // shape 9
 		}
 		int rc = check_launch("flow_count_kernel", stream);
 		if (rc != PCPPX_OK)
