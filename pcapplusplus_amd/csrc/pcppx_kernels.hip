@@ -2297,6 +2297,7 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 		case 6: go(flow_count_kernel<1024, 8192, 4096, 1>, 1024, 4096, 256); break;
 		case 2: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;
 		case 10: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true>, 512, 2048, 512); break;
+		case 11: go(flow_count_kernel<1024, 4096, 2048, kFlowHot, true>, 1024, 2048, 512); break;
 		case 7: go(flow_count_kernel<1024, 8192, 4096, 4>, 1024, 4096, 256); break;
 		case 8: go(flow_count_kernel<1024, 8192, 4096, 8>, 1024, 4096, 256); break;
 		default: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true>, 1024, 4096, 256); break;  // shape 9
