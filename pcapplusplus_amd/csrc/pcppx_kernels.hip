@@ -1693,7 +1693,7 @@ __global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, ui
 // {packets, bytes} pair per distinct flow to the HBM table: Zipf-skewed traffic puts a hot flow in most
 // packets of a batch, and per-packet global atomics on its slot would serialise.
 // Shape variants (block threads, LDS slots, packets per batch) are A/B'd in profiles/r01_ab_flow_shape.txt;
-// every shape keeps LDS slots >= 2x the packets of a batch.
+// every shape keeps fewer packets per batch than LDS slots (hot flows kept only while kept + batch fit).
 constexpr uint32_t kFlowGrid = 512;                 // persistent blocks of shape 0 (A/B in profiles/r01_ab_flow_grid.txt)
 constexpr uint32_t kFlowHot = 2;                    // flows with more packets stay in LDS between flushes
 constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
@@ -1753,7 +1753,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				z_by += len;
 				continue;
 			}
-			static_assert(2 * kFlowBatch <= kFlowLds && (kFlowLds & (kFlowLds - 1)) == 0, "flow shape");
+			static_assert(kFlowBatch < kFlowLds && kFlowBatch % kFB == 0 && (kFlowLds & (kFlowLds - 1)) == 0, "flow shape");
 			uint32_t slot = (key * 0x9E3779B1u) >> (32 - log2u(kFlowLds));  // top bits
 			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
 			{
@@ -2298,6 +2298,7 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 		case 2: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;
 		case 10: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true>, 512, 2048, 512); break;
 		case 11: go(flow_count_kernel<1024, 4096, 2048, kFlowHot, true>, 1024, 2048, 512); break;
+		case 12: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true>, 1024, 6144, 256); break;
 		case 7: go(flow_count_kernel<1024, 8192, 4096, 4>, 1024, 4096, 256); break;
 		case 8: go(flow_count_kernel<1024, 8192, 4096, 8>, 1024, 4096, 256); break;
 		default: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true>, 1024, 4096, 256); break;  // shape 9
