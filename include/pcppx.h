@@ -32,7 +32,9 @@
 extern "C" {
 #endif
 
-#define PCPPX_ABI_VERSION 1
+#define PCPPX_ABI_VERSION 2
+/* the library is built with hidden visibility: exactly the functions declared here are exported */
+#define PCPPX_API __attribute__((visibility("default")))
 #define PCPPX_MAX_LAYERS 16     /* fixed depth cap; deeper chains set PCPPX_F_DEPTH_OVERFLOW */
 #define PCPPX_MAX_CAPLEN 65535  /* larger packets are flagged PCPPX_F_OVERSIZE and not parsed */
 
@@ -105,8 +107,7 @@ typedef struct pcppx_opts {
 	uint8_t parse_until_osi;     /* pcpp::OsiModelLayer; 8 = OsiModelLayerUnknown */
 	uint8_t want_checksums;      /* compute IPv4 / L4 checksums */
 	uint8_t max_layers;          /* 0 = do not write layers; else layers stride per packet (1..16) */
-	uint8_t variant;             /* kernel variant, for A/B measurement only: 0 = default (tile kernel),
-	                                1 = lane-per-packet kernel. Results are identical. */
+	uint8_t reserved;            /* must be 0 */
 } pcppx_opts;
 
 /* Output arrays (same memory space as the batch for the _device call, host for the _host call). */
@@ -118,25 +119,25 @@ typedef struct pcppx_records {
 typedef struct pcppx_ctx pcppx_ctx;
 
 /* library / device management */
-int pcppx_abi_version(void);
-const char* pcppx_strerror(int err);
-int pcppx_device_count(int* out);
-int pcppx_runtime_info(int device, char* buf, size_t len); /* HIP runtime/driver versions, device name */
-int pcppx_open(int device_ordinal, pcppx_ctx** out); /* one per host thread & GPU */
-void pcppx_close(pcppx_ctx* ctx);
-int pcppx_sync(pcppx_ctx* ctx);                      /* wait for everything queued on ctx's stream */
-void* pcppx_ctx_stream(pcppx_ctx* ctx);              /* the context's own hipStream_t */
-void pcppx_default_opts(pcppx_opts* opts);           /* Packet(RawPacket*) defaults + checksums + 16 layers */
+PCPPX_API int pcppx_abi_version(void);
+PCPPX_API const char* pcppx_strerror(int err);
+PCPPX_API int pcppx_device_count(int* out);
+PCPPX_API int pcppx_runtime_info(int device, char* buf, size_t len); /* HIP runtime/driver versions, device name */
+PCPPX_API int pcppx_open(int device_ordinal, pcppx_ctx** out); /* one per host thread & GPU */
+PCPPX_API void pcppx_close(pcppx_ctx* ctx);
+PCPPX_API int pcppx_sync(pcppx_ctx* ctx);                      /* wait for everything queued on ctx's stream */
+PCPPX_API void* pcppx_ctx_stream(pcppx_ctx* ctx);              /* the context's own hipStream_t */
+PCPPX_API void pcppx_default_opts(pcppx_opts* opts);           /* Packet(RawPacket*) defaults + checksums + 16 layers */
 
 /* Device-resident parse. batch and records hold device pointers; the kernels are queued on
  * hip_stream (a hipStream_t; NULL = the null/default stream, as everywhere in HIP) and the call returns
  * without waiting. pcppx_ctx_stream() gives the context's own non-blocking stream. */
-int pcppx_parse_batch_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
+PCPPX_API int pcppx_parse_batch_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
                              pcppx_records* out, void* hip_stream);
 
 /* Host-to-host parse: batch and records hold host pointers. The context stages the bytes through pinned
  * buffers in chunks, overlapping H2D copies, kernels and D2H copies; returns when out is filled. */
-int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
+PCPPX_API int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
                            pcppx_records* out);
 
 /* Per-flow counters keyed by hash5Tuple (Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:99-125).
@@ -144,7 +145,7 @@ int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx
  * `capacity` slots (power of two); keys[i]==0 marks an empty slot — flow key 0 (non-5-tuple packets,
  * PacketUtils.cpp:141-148) is counted in stats[0] (packets) / stats[1] (bytes) instead, and packets
  * that found no free slot in stats[2]. Counts accumulate across calls. */
-int pcppx_flow_count_device(pcppx_ctx* ctx, const pcppx_summary* summary, const uint32_t* caplens,
+PCPPX_API int pcppx_flow_count_device(pcppx_ctx* ctx, const pcppx_summary* summary, const uint32_t* caplens,
                             uint32_t n, uint32_t* keys, uint64_t* packets, uint64_t* bytes,
                             uint32_t capacity, uint64_t* stats, void* hip_stream);
 
@@ -177,7 +178,7 @@ typedef struct pcppx_packet_stats { /* PacketStats, Examples/DpdkExample-FilterT
 	                                              records, or UDP tunnels (VXLAN, GTPv1) carrying inner packets */
 } pcppx_packet_stats;
 
-int pcppx_filter_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
+PCPPX_API int pcppx_filter_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
                         const pcppx_match_spec* spec, uint64_t seq_base, uint64_t* flow_keys, uint64_t* flow_first,
                         uint32_t capacity, uint8_t* matched, pcppx_packet_stats* stats, void* hip_stream);
 
@@ -187,8 +188,8 @@ int pcppx_filter_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_re
  * *stats (may be NULL) receives the statistics accumulated since the last pcppx_filter_reset.
  * pcppx_filter_reset sizes (capacity: power of two, 0 = 4M slots) and clears the flow table; the first
  * pcppx_filter_batch_host call does it implicitly. */
-int pcppx_filter_reset(pcppx_ctx* ctx, uint32_t capacity);
-int pcppx_filter_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_match_spec* spec,
+PCPPX_API int pcppx_filter_reset(pcppx_ctx* ctx, uint32_t capacity);
+PCPPX_API int pcppx_filter_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_match_spec* spec,
                             uint8_t* matched, pcppx_packet_stats* stats);
 
 /* ---- reassembly front ends ----
@@ -235,28 +236,28 @@ typedef struct pcppx_reasm_info { /* 16 bytes per packet */
 
 /* batch (device pointers) + its records from pcppx_parse_batch_device (max_layers >= 1, the same
  * max_layers here) -> info[n] (device). Queued on hip_stream; returns without waiting. */
-int pcppx_reasm_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
+PCPPX_API int pcppx_reasm_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,
                        pcppx_reasm_info* info, void* hip_stream);
 
 /* pcppx_parse_batch_device and pcppx_reasm_device in one pass: the parse kernel writes info[n] too, from the
  * header bytes it already holds (no second read of the packets or records). opts->max_layers >= 1. The
  * records and info equal those of the two calls made one after the other. */
-int pcppx_parse_batch_device_reasm(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
+PCPPX_API int pcppx_parse_batch_device_reasm(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
                                    pcppx_records* out, pcppx_reasm_info* info, void* hip_stream);
 
 /* ---- host ingest: pcap files into packed batch buffers ---- */
 typedef struct pcppx_pcap pcppx_pcap;
-int pcppx_pcap_open(const char* path, pcppx_pcap** out); /* PcapFileReaderDevice::open, PcapFileDevice.cpp:707-768 */
-uint32_t pcppx_pcap_linktype(const pcppx_pcap* reader);
+PCPPX_API int pcppx_pcap_open(const char* path, pcppx_pcap** out); /* PcapFileReaderDevice::open, PcapFileDevice.cpp:707-768 */
+PCPPX_API uint32_t pcppx_pcap_linktype(const pcppx_pcap* reader);
 /* Append up to max_packets records back to back into data[0, data_cap) (pinned memory feeds
  * pcppx_parse_batch_host without a staging copy); *n_out = packets read (0 at end of file). Record checks
  * as PcapFileReaderDevice::readNextPacket, PcapFileDevice.cpp:799-880. */
-int pcppx_pcap_read_batch(pcppx_pcap* reader, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
+PCPPX_API int pcppx_pcap_read_batch(pcppx_pcap* reader, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
                           uint32_t* caplens, uint64_t* timestamps_ns, uint32_t max_packets, uint32_t* n_out,
                           uint64_t* bytes_out);
-void pcppx_pcap_close(pcppx_pcap* reader);
-void* pcppx_host_alloc(size_t bytes); /* page-locked host memory (hipHostMalloc) */
-void pcppx_host_free(void* p);
+PCPPX_API void pcppx_pcap_close(pcppx_pcap* reader);
+PCPPX_API void* pcppx_host_alloc(size_t bytes); /* page-locked host memory (hipHostMalloc) */
+PCPPX_API void pcppx_host_free(void* p);
 
 #ifdef __cplusplus
 }

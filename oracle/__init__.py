@@ -363,6 +363,40 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
     return stats
 
 
+# protocols the engine builds itself (include/pcppx.h: everything else is a host layer)
+ENGINE_PROTOS = (1, 2, 3, 4, 5, 8, 9, 14, 15, 16, 17, 25, 30, 33, 44)
+
+
+def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:
+    """The NEEDS_HOST flags against the reference chain (records with max_layers >= 1):
+      - every packet whose reference chain holds a layer the engine does not build is flagged
+        (NEEDS_HOST_L7 / NEEDS_HOST_PROTO, or not parsed at all: OVERSIZE / BAD_DESC);
+      - a flagged packet whose reference chain holds no such layer is one where the host's dissector, at the
+        point the engine stopped, built nothing or fell back to a Payload layer (the engine cannot tell without
+        the dissector's own validity rules): the reference layer at index n_layers is GenericPayload or absent.
+    Returns counters {flagged, foreign, payload_fallback}."""
+    host = (eng_sum["flags"] & (abi.F_NEEDS_HOST_L7 | abi.F_NEEDS_HOST_PROTO)) != 0
+    unparsed = (eng_sum["flags"] & (abi.F_OVERSIZE | abi.F_BAD_DESC)) != 0
+    ml = ref_lay.shape[1]
+    rn = np.minimum(ref_sum["n_layers"].astype(np.int64), ml)
+    valid = np.arange(ml)[None, :] < rn[:, None]
+    foreign = (valid & ~np.isin(ref_lay["proto"], ENGINE_PROTOS)).any(axis=1)
+    miss = np.nonzero(foreign & ~host & ~unparsed)[0]
+    if len(miss):
+        i = int(miss[0])
+        raise AssertionError(f"{len(miss)} packets hold a host layer but are not flagged; first #{i}: "
+                             f"engine={eng_sum[i]} ref={ref_lay[i][: rn[i]]}")
+    over = np.nonzero(host & ~foreign)[0]
+    en = eng_sum["n_layers"][over].astype(np.int64)
+    nxt = np.where(en < rn[over], ref_lay["proto"][over, np.minimum(en, ml - 1)], 25)
+    bad = over[nxt != 25]
+    if len(bad):
+        i = int(bad[0])
+        raise AssertionError(f"{len(bad)} flagged packets whose reference chain continues with an engine layer; "
+                             f"first #{i}: engine={eng_sum[i]} ref={ref_lay[i][: rn[i]]}")
+    return {"flagged": int(host.sum()), "foreign": int(foreign.sum()), "payload_fallback": int(len(over))}
+
+
 def compare_exact(a_sum, a_lay, b_sum, b_lay) -> None:
     """Bit-exact equality of two engine-format record sets (GPU vs oracle), all packets."""
     for f in a_sum.dtype.names:

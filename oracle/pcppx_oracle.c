@@ -130,6 +130,62 @@ static int sip_heuristic(const uint8_t* p, uint32_t n)
 	return 0;
 }
 
+/* ---- parse-until roll-back of a layer this path does not build (Packet.cpp:134-155, 168-175) ----
+ * Where the chain reaches a layer the engine leaves to the host (an L7 dissector, or an out-of-scope
+ * L2/L3 layer), Packet::parsePacket still builds it and then applies the stop rules to it: it is rolled
+ * back (and with it everything the host would parse behind it) when its OSI layer is above
+ * parseUntilLayer, or when the parse-until family was already found and the layer is not a member. The
+ * engine does not know WHICH layer the host builds, only the candidates; the roll-back is certain when it
+ * holds for every candidate:
+ *   - every candidate's OSI layer exceeds parse_until_osi (min_osi below: the smallest candidate OSI), or
+ *   - the family was found and holds only protocols the engine itself builds, which no candidate is
+ *     (GenericPayload excluded: a port-triggered dissector may fall back to Payload).
+ * The chain is then exact and ends before that layer: no NEEDS_HOST flag.
+ *
+ * Candidate OSI layers (each Layer::getOsiModelLayer override in Packet++/header):
+ *   TCP payload (TcpLayer.cpp:372-491): TPKT 102 (TpktLayer.h:98-101) and GTPv2 2123 (GtpLayer.h:1112-1115)
+ *     transport 4; SIP 5060/5061 session 5 (SipLayer.h:96-99); SSL presentation 6 (SSLLayer.h:246-249);
+ *     every other dissector and Payload application 7.
+ *   UDP payload (UdpLayer.cpp:103-183): VXLAN dst 4789 (VxlanLayer.h:141-144) and WakeOnLan dst 0/7/9
+ *     (WakeOnLanLayer.h:133-135) data link 2; WireGuard 51820 network 3 (WireGuardLayer.h:114-117); GTPv1
+ *     2152/2123 (GtpLayer.h:386-389,408-411) and GTPv2 2123 transport 4; SIP by port or by the content
+ *     heuristic session 5; the rest 7.
+ *   Out-of-scope L2 layers (PPPoE PPPoELayer.h:92, WakeOnLan, STP StpLayer.h:204-207) 2; out-of-scope
+ *   IP-protocol layers (ICMP, IGMP, AH, VRRP, ICMPv6: network 3; ESP transport 4) 3. */
+static uint8_t tcp_l7_min_osi(uint16_t sp, uint16_t dp)
+{
+	if (sp == 102 || dp == 102 || sp == 2123 || dp == 2123) return 4;
+	if (sp == 5060 || sp == 5061 || dp == 5060 || dp == 5061) return 5;
+	if (ssl_port(sp) || ssl_port(dp)) return 6;
+	return 7;
+}
+static uint8_t udp_l7_min_osi(uint16_t sp, uint16_t dp, int sip_content)
+{
+	if (dp == 4789 || dp == 0 || dp == 7 || dp == 9) return 2;
+	if (sp == 51820 || dp == 51820) return 3;
+	if (sp == 2152 || dp == 2152 || sp == 2123 || dp == 2123) return 4;
+	if (sp == 5060 || sp == 5061 || dp == 5060 || dp == 5061 || sip_content) return 5;
+	return 7;
+}
+/* the protocols the engine builds itself (ProtocolType.h:42-258), GenericPayload excluded */
+static int engine_proto(uint32_t p)
+{
+	switch (p) {
+	case P_ETH: case P_IPV4: case P_IPV6: case P_TCP: case P_UDP: case P_ARP: case P_VLAN: case P_MPLS:
+	case P_GREV0: case P_GREV1: case P_PPTP: case P_TRAILER: case P_DOT3: case P_LLC: return 1;
+	default: return 0;
+	}
+}
+static int family_engine_only(uint32_t fam)
+{
+	if (fam == 0) return 0;
+	for (int k = 0; k < 4; ++k) {
+		uint32_t b = (fam >> (8 * k)) & 0xFF;
+		if (b != 0 && !engine_proto(b)) return 0;
+	}
+	return 1;
+}
+
 /* ---- computeChecksum, Packet++/src/PacketUtils.cpp:12-64 ---- */
 uint16_t pcppx_oracle_checksum(const uint8_t* const* bufs, const uint32_t* lens, int nbufs)
 {
@@ -169,11 +225,13 @@ static int family_member(uint32_t fam, uint8_t p)
 
 /* Build layer `k` at [off, off+len) and report its next layer through nk, noff, nlen.
  * Returns the layer descriptor. */
-static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int* nk, uint32_t* noff, uint32_t* nlen)
+static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int* nk, uint32_t* noff, uint32_t* nlen,
+                      uint8_t* nosi)
 {
 	const uint8_t* p = pkt + off;
 	lay L = { 0, 0, off, 0, len };
 	*nk = K_NONE;
+	*nosi = 7; /* smallest OSI layer of the host-built candidates when *nk is K_OUT / K_L7 */
 	uint32_t po, pl; /* payload of this layer */
 #define NEXT(K, O, N) do { *nk = (K); *noff = (O); *nlen = (N); } while (0)
 	switch (k) {
@@ -187,7 +245,7 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		case 0x8100: case 0x88A8: NEXT(pl >= 4 ? K_VLAN : K_PAYLOAD, po, pl); break;
 		case 0x8847: NEXT(pl >= 4 ? K_MPLS : K_PAYLOAD, po, pl); break;
 		case 0x0806: NEXT(pl >= 28 ? K_ARP : K_PAYLOAD, po, pl); break; /* ArpLayer::isDataValid, ArpLayer.h:279-282 */
-		case 0x8864: case 0x8863: case 0x0842: NEXT(K_OUT, po, pl); break; /* PPPoE, WoL */
+		case 0x8864: case 0x8863: case 0x0842: NEXT(K_OUT, po, pl); *nosi = 2; break; /* PPPoE, WoL */
 		default: NEXT(K_PAYLOAD, po, pl); break;
 		}
 		break;
@@ -201,7 +259,7 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		L.proto = P_LLC; L.osi = 2; L.hdr = 3;
 		if (len <= 3) break;
 		po = off + 3; pl = len - 3;
-		if (p[0] == 0x42 && p[1] == 0x42) NEXT(K_OUT, po, pl); /* STP (or Payload): host */
+		if (p[0] == 0x42 && p[1] == 0x42) { NEXT(K_OUT, po, pl); *nosi = 2; } /* STP (or Payload): host */
 		else NEXT(K_PAYLOAD, po, pl);
 		break;
 	case K_VLAN: /* VlanLayer::parseNextLayer, Packet++/src/VlanLayer.cpp:59-119 */
@@ -214,7 +272,7 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		case 0x8100: case 0x88A8: NEXT(K_VLAN, po, pl); break; /* unchecked */
 		case 0x8847: NEXT(K_MPLS, po, pl); break;              /* unchecked */
 		case 0x0806: NEXT(K_ARP, po, pl); break; /* unchecked */
-		case 0x8864: case 0x8863: NEXT(K_OUT, po, pl); break;
+		case 0x8864: case 0x8863: NEXT(K_OUT, po, pl); *nosi = 2; break;
 		default:
 			if (be16(p + 2) < 1500) NEXT(llc_valid(pkt + po, pl) ? K_LLC : K_PAYLOAD, po, pl);
 			else NEXT(K_PAYLOAD, po, pl);
@@ -260,7 +318,7 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 			else NEXT(K_PAYLOAD, po, pl);
 			break;
 		case 41: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
-		case 1: case 2: case 51: case 50: case 112: NEXT(K_OUT, po, pl); break; /* ICMP IGMP AH ESP VRRP */
+		case 1: case 2: case 51: case 50: case 112: NEXT(K_OUT, po, pl); *nosi = 3; break; /* ICMP IGMP AH ESP VRRP */
 		default: NEXT(K_PAYLOAD, po, pl); break;
 		}
 		break;
@@ -303,7 +361,7 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 			else if ((pkt[po + 1] & 7) == 1) NEXT(pl >= 8 ? K_GRE1 : K_PAYLOAD, po, pl);
 			else NEXT(K_PAYLOAD, po, pl);
 			break;
-		case 51: case 50: case 58: case 112: NEXT(K_OUT, po, pl); break; /* AH ESP ICMPv6 VRRP */
+		case 51: case 50: case 58: case 112: NEXT(K_OUT, po, pl); *nosi = 3; break; /* AH ESP ICMPv6 VRRP */
 		default: NEXT(K_PAYLOAD, po, pl); break;
 		}
 		break;
@@ -347,12 +405,17 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		if (len <= L.hdr) break;
 		po = off + L.hdr; pl = len - L.hdr;
 		NEXT((tcp_l7_port(be16(p)) || tcp_l7_port(be16(p + 2))) ? K_L7 : K_PAYLOAD, po, pl);
+		*nosi = tcp_l7_min_osi(be16(p), be16(p + 2));
 		break;
 	case K_UDP: /* UdpLayer::parseNextLayer, Packet++/src/UdpLayer.cpp:92-184 */
 		L.proto = P_UDP; L.osi = 4; L.hdr = 8;
 		if (len <= 8) break;
 		po = off + 8; pl = len - 8;
-		NEXT((udp_l7_port(be16(p), be16(p + 2)) || sip_heuristic(pkt + po, pl)) ? K_L7 : K_PAYLOAD, po, pl);
+		{
+			int sip = sip_heuristic(pkt + po, pl);
+			NEXT((udp_l7_port(be16(p), be16(p + 2)) || sip) ? K_L7 : K_PAYLOAD, po, pl);
+			*nosi = udp_l7_min_osi(be16(p), be16(p + 2), sip);
+		}
 		break;
 	case K_ARP: /* ArpLayer: dataLen := sizeof(arphdr) = 28 whatever remains, no next (ArpLayer.h:151-155,242-273) */
 		L.proto = P_ARP; L.osi = 3; L.hdr = 28; L.dlen = 28;
@@ -402,11 +465,21 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 	int count = 0, found = 0, stopped_by_rule = 0;
 	uint64_t mask = 0;
 	uint32_t off = 0, len = caplen;
+	uint8_t kosi = 7; /* smallest candidate OSI layer of k when k is K_OUT / K_L7 */
+	const int fam_engine_only = family_engine_only(opts->parse_until_family);
 	while (k != K_NONE) {
-		if (k == K_OUT) { flags |= PCPPX_F_NEEDS_HOST_PROTO; break; }
-		if (k == K_L7) { flags |= PCPPX_F_NEEDS_HOST_L7; break; }
+		if (k == K_OUT || k == K_L7) {
+			/* the host would build this layer, then the stop rules would roll it back (see above) */
+			if (count > 0 && (kosi > opts->parse_until_osi || (found && fam_engine_only))) {
+				stopped_by_rule = 1;
+				break;
+			}
+			flags |= k == K_OUT ? PCPPX_F_NEEDS_HOST_PROTO : PCPPX_F_NEEDS_HOST_L7;
+			break;
+		}
 		int nk; uint32_t noff = 0, nlen = 0;
-		lay L = make_layer(pkt, k, off, len, &nk, &noff, &nlen);
+		uint8_t nosi = 7;
+		lay L = make_layer(pkt, k, off, len, &nk, &noff, &nlen, &nosi);
 		int member = family_member(opts->parse_until_family, L.proto);
 		int fail = L.osi > opts->parse_until_osi;
 		if (!fail) {
@@ -432,7 +505,7 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 		prev = L;
 		last = L;
 		++count;
-		k = nk; off = noff; len = nlen;
+		k = nk; off = noff; len = nlen; kosi = nosi;
 	}
 	/* trailer: Packet.cpp:178-195 (only with no parse-until options, and not for flagged chains) */
 	if (count > 0 && opts->parse_until_family == 0 && opts->parse_until_osi == 8 && !stopped_by_rule &&

@@ -15,7 +15,7 @@ PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 ENGINE_SO = PKG_DIR / "libpcppx.so"
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_LAYERS = 16
 MAX_CAPLEN = 65535
 
@@ -94,7 +94,7 @@ class Opts(C.Structure):
         ("parse_until_osi", C.c_uint8),
         ("want_checksums", C.c_uint8),
         ("max_layers", C.c_uint8),
-        ("variant", C.c_uint8),
+        ("reserved", C.c_uint8),
     ]
 
 
@@ -128,11 +128,11 @@ def ipv4_to_int(dotted: str) -> int:
 
 
 def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checksums: bool = True,
-              max_layers: int = MAX_LAYERS, variant: int = 0) -> Opts:
+              max_layers: int = MAX_LAYERS) -> Opts:
     """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection."""
     if not 0 <= max_layers <= MAX_LAYERS:
         raise ValueError(f"max_layers must be in [0, {MAX_LAYERS}]")
-    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, variant)
+    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, 0)
 
 
 def _declare(lib: C.CDLL) -> C.CDLL:

@@ -42,7 +42,7 @@ struct Slot
 };
 
 constexpr uint32_t kDefaultFlowSlots = 1u << 22;  // 64 MiB of flow table in HBM
-constexpr uint32_t kMaxSlots = 4;                   // host-path chunk slots in flight (PCPPX_HOST_SLOTS, 2..4)
+constexpr uint32_t kMaxSlots = 3;                   // host-path chunk slots in flight
 }  // namespace
 
 struct pcppx_ctx
@@ -58,9 +58,13 @@ struct pcppx_ctx
 	pcppx_packet_stats* d_stats = nullptr;
 	uint32_t flow_slots = 0;
 	uint64_t seq = 0;
-	// pcppx_flow_count_device: packed per-slot {packets, bytes} scratch (zero between calls)
+	// pcppx_flow_count_device: packed per-slot {packets, bytes} scratch (zero between calls), and an event
+	// after each call's last kernel: the next call (on whatever stream) waits for it before touching the
+	// scratch, so calls on one context are ordered even across streams
 	uint64_t* d_flow_packed = nullptr;
 	uint32_t flow_packed_slots = 0;
+	hipEvent_t flow_done = nullptr;
+	bool flow_pending = false;
 };
 
 namespace
@@ -72,7 +76,7 @@ bool ok(hipError_t e)
 
 int valid_opts(const pcppx_opts* o)
 {
-	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS)
+	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->reserved != 0)
 		return PCPPX_E_INVAL;
 	return PCPPX_OK;
 }
@@ -100,11 +104,8 @@ int init_host_path(pcppx_ctx* c)
 {
 	if (c->host_ready)
 		return PCPPX_OK;
-	// default 2 (double buffering): 3 and 4 slots measured no faster, the link is the limit
-	// (profiles/r01_ab_host_slots.txt)
-	const char* env = getenv("PCPPX_HOST_SLOTS");
-	const int want = env ? atoi(env) : 2;
-	c->nslots = want < 2 ? 2u : (want > (int)kMaxSlots ? kMaxSlots : (uint32_t)want);
+	// three slots: the H2D copy of chunk k+1 overlaps the kernel of chunk k and the drain of chunk k-1
+	c->nslots = kMaxSlots;
 	for (uint32_t si = 0; si < c->nslots; ++si)
 	{
 		Slot& s = c->slots[si];
@@ -264,6 +265,19 @@ void free_filter(pcppx_ctx* c)
 	c->seq = 0;
 }
 
+// forget every slot's chunk without copying it out: after an error mid-call, and at the start of each host
+// call, so that a later call never drains a stale chunk into its own (possibly smaller) output arrays
+void abandon_slots(pcppx_ctx* c)
+{
+	for (Slot& s : c->slots)
+	{
+		if (s.st)
+			(void)hipStreamSynchronize(s.st);
+		s.busy = false;
+	}
+	(void)hipGetLastError();
+}
+
 // copy a finished chunk's records from pinned memory to the caller's arrays
 void drain(Slot& s, pcppx_records* out)
 {
@@ -271,6 +285,118 @@ void drain(Slot& s, pcppx_records* out)
 	if (s.ml && out->layers)
 		par_copy(out->layers + (size_t)s.first * s.ml, s.h_lay, (size_t)s.count * s.ml * sizeof(pcppx_layer));
 	s.busy = false;
+}
+// pcppx_parse_batch_host's chunk pipeline (argument checks done; slots idle on entry)
+int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r)
+{
+	int rc = PCPPX_OK;
+	const uint32_t ml = o->max_layers;
+	const bool pinned_in = is_pinned(b->data);
+	uint32_t i = 0, k = 0;
+	while (i < b->n)
+	{
+		Slot& s = c->slots[k % c->nslots];
+		if (s.busy)
+		{
+			if (!ok(hipEventSynchronize(s.done)))
+				return PCPPX_E_HIP;
+			drain(s, r);
+		}
+		size_t pos = 0;
+		const uint8_t* direct = nullptr;
+		const uint32_t j = stage_chunk(s, b, i, &pos, &direct, pinned_in);
+		const uint32_t cnt = j - i;
+		if (!upload_chunk(s, pos, cnt, direct))
+			return PCPPX_E_HIP;
+		pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
+		pcppx_records dr{ s.d_sum, ml ? s.d_lay : nullptr };
+		rc = pcppx::launch_parse(&db, o, &dr, s.st);
+		if (rc != PCPPX_OK)
+			return rc;
+		const bool good = ok(hipMemcpyAsync(s.h_sum, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
+		       (ml == 0 || ok(hipMemcpyAsync(s.h_lay, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer),
+		                                     hipMemcpyDeviceToHost, s.st))) &&
+		       ok(hipEventRecord(s.done, s.st));
+		if (!good)
+			return PCPPX_E_HIP;
+		s.busy = true;
+		s.first = i;
+		s.count = cnt;
+		s.ml = ml;
+		i = j;
+		++k;
+	}
+	for (Slot& s : c->slots)
+		if (s.busy)
+		{
+			if (!ok(hipEventSynchronize(s.done)))
+				return PCPPX_E_HIP;
+			drain(s, r);
+		}
+	return PCPPX_OK;
+}
+// pcppx_filter_batch_host's chunk pipeline (argument checks done; slots idle on entry)
+int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* spec, uint8_t* matched,
+                    pcppx_packet_stats* stats)
+{
+	int rc = PCPPX_OK;
+	pcppx_opts o;
+	pcppx_default_opts(&o);
+	o.want_checksums = 0;  // the worker reads addresses, ports and the protocol mask only
+	const uint32_t ml = o.max_layers;
+	const bool pinned_in = is_pinned(b->data);
+	uint32_t i = 0, k = 0;
+	Slot* prev = nullptr;
+	while (i < b->n)
+	{
+		Slot& s = c->slots[k % c->nslots];
+		if (s.busy)
+		{
+			if (!ok(hipEventSynchronize(s.done)))
+				return PCPPX_E_HIP;
+			std::memcpy(matched + s.first, s.h_match, s.count);
+			s.busy = false;
+		}
+		size_t pos = 0;
+		const uint8_t* direct = nullptr;
+		const uint32_t j = stage_chunk(s, b, i, &pos, &direct, pinned_in);
+		const uint32_t cnt = j - i;
+		if (!upload_chunk(s, pos, cnt, direct))
+			return PCPPX_E_HIP;
+		// the flow table is shared by consecutive chunks: chunk k's lookups run after chunk k-1's marks
+		if (prev != nullptr && !ok(hipStreamWaitEvent(s.st, prev->done, 0)))
+			return PCPPX_E_HIP;
+		pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
+		pcppx_records dr{ s.d_sum, s.d_lay };
+		rc = pcppx::launch_parse(&db, &o, &dr, s.st);
+		if (rc == PCPPX_OK)
+			rc = pcppx::launch_filter(&db, &dr, ml, spec, c->seq + i, c->d_keys, c->d_first, c->flow_slots,
+			                          s.d_match, c->d_stats, s.st);
+		if (rc != PCPPX_OK)
+			return rc;
+		if (!ok(hipMemcpyAsync(s.h_match, s.d_match, cnt, hipMemcpyDeviceToHost, s.st)) ||
+		    !ok(hipEventRecord(s.done, s.st)))
+			return PCPPX_E_HIP;
+		s.busy = true;
+		s.first = i;
+		s.count = cnt;
+		prev = &s;
+		i = j;
+		++k;
+	}
+	for (Slot& s : c->slots)
+		if (s.busy)
+		{
+			if (!ok(hipEventSynchronize(s.done)))
+				return PCPPX_E_HIP;
+			std::memcpy(matched + s.first, s.h_match, s.count);
+			s.busy = false;
+		}
+	c->seq += b->n;
+	if (stats != nullptr &&
+	    (!ok(hipMemcpy(stats, c->d_stats, sizeof(pcppx_packet_stats), hipMemcpyDeviceToHost))))
+		return PCPPX_E_HIP;
+	return PCPPX_OK;
 }
 }  // namespace
 
@@ -333,7 +459,7 @@ extern "C"
 		o->parse_until_osi = 8;     // OsiModelLayerUnknown
 		o->want_checksums = 1;
 		o->max_layers = PCPPX_MAX_LAYERS;
-		o->variant = 0;
+		o->reserved = 0;
 	}
 
 	int pcppx_open(int device, pcppx_ctx** out)
@@ -373,6 +499,8 @@ extern "C"
 		}
 		free_filter(c);
 		(void)hipFree(c->d_flow_packed);
+		if (c->flow_done)
+			(void)hipEventDestroy(c->flow_done);
 		(void)hipStreamDestroy(c->stream);
 		delete c;
 	}
@@ -420,50 +548,11 @@ extern "C"
 		int rc = init_host_path(c);
 		if (rc != PCPPX_OK)
 			return rc;
-		const uint32_t ml = o->max_layers;
-		const bool pinned_in = is_pinned(b->data);
-		uint32_t i = 0, k = 0;
-		while (i < b->n)
-		{
-			Slot& s = c->slots[k % c->nslots];
-			if (s.busy)
-			{
-				if (!ok(hipEventSynchronize(s.done)))
-					return PCPPX_E_HIP;
-				drain(s, r);
-			}
-			size_t pos = 0;
-			const uint8_t* direct = nullptr;
-			const uint32_t j = stage_chunk(s, b, i, &pos, &direct, pinned_in);
-			const uint32_t cnt = j - i;
-			if (!upload_chunk(s, pos, cnt, direct))
-				return PCPPX_E_HIP;
-			pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
-			pcppx_records dr{ s.d_sum, ml ? s.d_lay : nullptr };
-			rc = pcppx::launch_parse(&db, o, &dr, s.st);
-			if (rc != PCPPX_OK)
-				return rc;
-			const bool good = ok(hipMemcpyAsync(s.h_sum, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
-			       (ml == 0 || ok(hipMemcpyAsync(s.h_lay, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer),
-			                                     hipMemcpyDeviceToHost, s.st))) &&
-			       ok(hipEventRecord(s.done, s.st));
-			if (!good)
-				return PCPPX_E_HIP;
-			s.busy = true;
-			s.first = i;
-			s.count = cnt;
-			s.ml = ml;
-			i = j;
-			++k;
-		}
-		for (Slot& s : c->slots)
-			if (s.busy)
-			{
-				if (!ok(hipEventSynchronize(s.done)))
-					return PCPPX_E_HIP;
-				drain(s, r);
-			}
-		return PCPPX_OK;
+		abandon_slots(c);
+		rc = parse_host_run(c, b, o, r);
+		if (rc != PCPPX_OK)
+			abandon_slots(c);
+		return rc;
 	}
 
 	int pcppx_filter_device(pcppx_ctx* c, const pcppx_batch* b, const pcppx_records* r, uint8_t max_layers,
@@ -559,63 +648,11 @@ extern "C"
 			rc = init_host_path(c);
 		if (rc != PCPPX_OK)
 			return rc;
-		pcppx_opts o;
-		pcppx_default_opts(&o);
-		o.want_checksums = 0;  // the worker reads addresses, ports and the protocol mask only
-		const uint32_t ml = o.max_layers;
-		const bool pinned_in = is_pinned(b->data);
-		uint32_t i = 0, k = 0;
-		Slot* prev = nullptr;
-		while (i < b->n)
-		{
-			Slot& s = c->slots[k % c->nslots];
-			if (s.busy)
-			{
-				if (!ok(hipEventSynchronize(s.done)))
-					return PCPPX_E_HIP;
-				std::memcpy(matched + s.first, s.h_match, s.count);
-				s.busy = false;
-			}
-			size_t pos = 0;
-			const uint8_t* direct = nullptr;
-			const uint32_t j = stage_chunk(s, b, i, &pos, &direct, pinned_in);
-			const uint32_t cnt = j - i;
-			if (!upload_chunk(s, pos, cnt, direct))
-				return PCPPX_E_HIP;
-			// the flow table is shared by consecutive chunks: chunk k's lookups run after chunk k-1's marks
-			if (prev != nullptr && !ok(hipStreamWaitEvent(s.st, prev->done, 0)))
-				return PCPPX_E_HIP;
-			pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
-			pcppx_records dr{ s.d_sum, s.d_lay };
-			rc = pcppx::launch_parse(&db, &o, &dr, s.st);
-			if (rc == PCPPX_OK)
-				rc = pcppx::launch_filter(&db, &dr, ml, spec, c->seq + i, c->d_keys, c->d_first, c->flow_slots,
-				                          s.d_match, c->d_stats, s.st);
-			if (rc != PCPPX_OK)
-				return rc;
-			if (!ok(hipMemcpyAsync(s.h_match, s.d_match, cnt, hipMemcpyDeviceToHost, s.st)) ||
-			    !ok(hipEventRecord(s.done, s.st)))
-				return PCPPX_E_HIP;
-			s.busy = true;
-			s.first = i;
-			s.count = cnt;
-			prev = &s;
-			i = j;
-			++k;
-		}
-		for (Slot& s : c->slots)
-			if (s.busy)
-			{
-				if (!ok(hipEventSynchronize(s.done)))
-					return PCPPX_E_HIP;
-				std::memcpy(matched + s.first, s.h_match, s.count);
-				s.busy = false;
-			}
-		c->seq += b->n;
-		if (stats != nullptr &&
-		    (!ok(hipMemcpy(stats, c->d_stats, sizeof(pcppx_packet_stats), hipMemcpyDeviceToHost))))
-			return PCPPX_E_HIP;
-		return PCPPX_OK;
+		abandon_slots(c);
+		rc = filter_host_run(c, b, spec, matched, stats);
+		if (rc != PCPPX_OK)
+			abandon_slots(c);
+		return rc;
 	}
 
 	int pcppx_flow_count_device(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* caplens, uint32_t n,
@@ -645,6 +682,17 @@ extern "C"
 				return PCPPX_E_NOMEM;
 			c->flow_packed_slots = capacity;
 		}
-		return pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats, c->d_flow_packed, st);
+		if (c->flow_done == nullptr && !ok(hipEventCreateWithFlags(&c->flow_done, hipEventDisableTiming)))
+			return PCPPX_E_HIP;
+		if (c->flow_pending && !ok(hipStreamWaitEvent(st, c->flow_done, 0)))
+			return PCPPX_E_HIP;
+		const int rc =
+		    pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats, c->d_flow_packed, st);
+		if (rc != PCPPX_OK)
+			return rc;
+		if (!ok(hipEventRecord(c->flow_done, st)))
+			return PCPPX_E_HIP;
+		c->flow_pending = true;
+		return PCPPX_OK;
 	}
 }

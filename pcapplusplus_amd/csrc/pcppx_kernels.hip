@@ -25,8 +25,6 @@ namespace
 {
 
 constexpr int kBlock = 256;
-constexpr int kSlotDw = 33;  // 32 dwords of staged bytes + 1 pad dword: consecutive lanes land on different banks
-constexpr int kStageChunks = 8;  // 8 x 16 B = 128 B staged per packet
 
 // ProtocolType ids (Packet++/header/ProtocolType.h:42-258)
 enum : uint32_t
@@ -39,7 +37,7 @@ enum : uint32_t
 enum : uint32_t
 {
 	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
-	K_PAYLOAD, K_OUT, K_L7, K_ARP,
+	K_PAYLOAD, K_OUT, K_ARP,
 	// candidates: the layer a tryConstructNextLayerWithFallback would build if its isDataValid holds, else
 	// Payload (Layer.h:474-483); resolved from the candidate's own first bytes when the walk reaches it
 	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC
@@ -210,6 +208,31 @@ __device__ __forceinline__ bool sip_key(uint32_t k)
 {
 	const uint32_t h = (k * kSipMul) >> 27;
 	return ((kSip.valid >> h) & 1u) && kSip.key[h] == k;
+}
+
+// Smallest OSI layer among the layers the host would build on an L4 payload the port / SIP triggers hand to
+// a dissector (each Layer::getOsiModelLayer override; the table is in oracle/pcppx_oracle.c,
+// tcp_l7_min_osi / udp_l7_min_osi): the parse-until stop rules roll that layer back when it lies above
+// parseUntilLayer (Packet.cpp:134-140,168-175).
+__device__ __forceinline__ uint32_t l7_min_osi(bool tcp, uint32_t sp, uint32_t dp, bool sip)
+{
+	const bool e102 = sp == 102 || dp == 102, e2123 = sp == 2123 || dp == 2123;
+	const bool esip = sp == 5060 || sp == 5061 || dp == 5060 || dp == 5061;
+	const uint32_t t = (e102 || e2123) ? 4u : (esip ? 5u : 7u);
+	if (tcp)
+	{
+		// SSL ports (SSLLayer.h:488-510) give the presentation layer 6
+		const bool ssl_s = sp == 443 || sp == 261 || sp == 448 || sp == 465 || sp == 563 || sp == 614 || sp == 636 ||
+		                   sp == 989 || sp == 990 || (sp >= 992 && sp <= 995);
+		const bool ssl_d = dp == 443 || dp == 261 || dp == 448 || dp == 465 || dp == 563 || dp == 614 || dp == 636 ||
+		                   dp == 989 || dp == 990 || (dp >= 992 && dp <= 995);
+		return t == 7u && (ssl_s || ssl_d) ? 6u : t;
+	}
+	uint32_t u = (esip || sip) ? 5u : 7u;
+	u = (sp == 2152 || dp == 2152 || e2123) ? 4u : u;
+	u = (sp == 51820 || dp == 51820) ? 3u : u;
+	u = (dp == 4789 || dp == 0 || dp == 7 || dp == 9) ? 2u : u;
+	return u;
 }
 
 __device__ __forceinline__ uint32_t fnv(uint32_t h, uint32_t b)
@@ -532,7 +555,7 @@ struct Params
 	uint32_t want_csum;
 	uint32_t max_layers;
 	uint32_t linktype;
-	uint32_t diag;  // 0 normal; 2 = stream-only diagnostic (no gather/parse; L4 range = [14, caplen))
+	uint32_t fam_engine_only;  // family != 0 and every protocol of it is one the engine builds (host-computed)
 	pcppx_reasm_info* reasm;  // fused reassembly front ends (pcppx_parse_batch_device_reasm), or null
 };
 
@@ -586,9 +609,15 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	// exec-mask region of scalar bookkeeping plus copies of each value live across it.
 	while (k != K_NONE)
 	{
-		if (k == K_OUT || k == K_L7)
+		if (k == K_OUT)
 		{
-			flags |= k == K_OUT ? PCPPX_F_NEEDS_HOST_PROTO : PCPPX_F_NEEDS_HOST_L7;
+			// an out-of-scope layer: rolled back by the stop rules when every candidate fails one
+			// (oracle/pcppx_oracle.c, family_engine_only): L2 candidates (PPPoE, WoL, STP) have OSI 2, the
+			// IP-protocol ones (ICMP, IGMP, AH, ESP, VRRP, ICMPv6) 3
+			const uint32_t pp = prev & 0xFFu;
+			const uint32_t kosi = (pp == P_IPV4 || pp == P_IPV6) ? 3u : 2u;
+			if (!(count > 0 && (kosi > prm.until_osi || (found && prm.fam_engine_only))))
+				flags |= PCPPX_F_NEEDS_HOST_PROTO;
 			break;
 		}
 		const bool nob = k == K_PAYLOAD || k == K_ARP;  // reads no byte: peek at 0 (inside the packet), drop it
@@ -647,8 +676,12 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	{
 		const uint32_t pw = rd32(p, l7_o);
 		const uint32_t sp = swap16(pw), dp = swap16(pw >> 16);
-		const bool l7 = l7_tcp ? tcp_l7(sp, dp)
-		                       : (udp_l7(sp, dp) || (l7_pl >= 4 && sip_key(__builtin_bswap32(rd32(p, l7_o + 8)))));
+		const bool sip = !l7_tcp && l7_pl >= 4 && sip_key(__builtin_bswap32(rd32(p, l7_o + 8)));
+		bool l7 = l7_tcp ? tcp_l7(sp, dp) : (udp_l7(sp, dp) || sip);
+		// parse-until options: the dissector's layer is rolled back (Packet.cpp:134-155,168-175) when every
+		// candidate lies above parseUntilLayer, or the family was found and holds only engine-built protocols
+		if (l7 && (prm.family != 0 || prm.until_osi < 8))  // uniform
+			l7 = !(l7_min_osi(l7_tcp, sp, dp, sip) > prm.until_osi || (found && prm.fam_engine_only));
 		if (l7)
 		{
 			flags |= PCPPX_F_NEEDS_HOST_L7;
@@ -832,73 +865,6 @@ __device__ __forceinline__ uint32_t desc_flags(uint64_t off, uint32_t cap, uint6
 	if (cap == 0)
 		*empty = true;
 	return 0;
-}
-
-// ================= lane kernel: one lane streams one whole packet (reference / fallback) =================
-__global__ __launch_bounds__(kBlock) void parse_lane_kernel(Params prm)
-{
-	__shared__ uint32_t stage[kBlock * kSlotDw];
-
-	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-	if (i >= prm.n)
-		return;
-	pcppx_summary* sum_out = prm.summary + i;
-	const uint64_t off = prm.offsets[i];
-	const uint32_t cap = prm.caplens[i];
-	bool empty;
-	uint32_t bad = desc_flags(off, cap, prm.data_len, &empty);
-	if (bad || empty)
-	{
-		write_summary(sum_out, 0, 0, 0, bad, 0, -1, 0, 0, 0, 0, 0);
-		return;
-	}
-
-	Pkt p;
-	p.g = (gptr8)(prm.data + off);
-	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
-	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
-	{
-		uint32_t need = (p.mis + cap + 15) >> 4;
-		p.nch = need < kStageChunks ? need : kStageChunks;
-		lptr32w slot = (lptr32w)(stage) + threadIdx.x * kSlotDw;
-		uint4 v[kStageChunks];
-#pragma unroll
-		for (int c = 0; c < kStageChunks; ++c)
-			if ((uint32_t)c < p.nch)
-				v[c] = ld16(p.a0 + 16 * c);
-#pragma unroll
-		for (int c = 0; c < kStageChunks; ++c)
-			if ((uint32_t)c < p.nch)
-			{
-				slot[4 * c + 0] = v[c].x;
-				slot[4 * c + 1] = v[c].y;
-				slot[4 * c + 2] = v[c].z;
-				slot[4 * c + 3] = v[c].w;
-			}
-		p.s = reinterpret_cast<lptr8>(slot);
-		uint32_t staged = 16 * p.nch - p.mis;
-		p.lim = staged < cap ? staged : cap;
-	}
-
-	uint2* lay_out = prm.layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * prm.max_layers : nullptr;
-	Walk w = walk_chain(p, cap, prm, lay_out);
-	uint32_t h5, h5d, h2;
-	hashes(p, w, h5, h5d, h2);
-	uint32_t flags = w.flags, ipc = 0, ips = 0, l4c = 0, l4s = 0;
-	if (prm.want_csum)
-	{
-		if (w.v4 >= 0)
-		{
-			ipc = ipv4_checksum(p, w, &ips);
-			flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
-		}
-		if (w.l4i >= 0)
-		{
-			l4c = l4_checksum(p, w, range_residue(p, w.l4o, w.l4o + w.l4dlen), &l4s);
-			flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
-		}
-	}
-	write_summary(sum_out, h5, h5d, h2, flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
 }
 
 // ---------------- fast path for the common stacks (branch-free, dword LDS reads) ----------------
@@ -1314,7 +1280,7 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // 160 KiB. SWin: stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers).
 // Chunks: 16-B header chunks staged per packet.
 // NT: non-temporal span-stream loads and record stores (read-once / write-once data; A/B variant 11)
-template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false>
+template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1370,7 +1336,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
 	{
 		const uint32_t need = (p.mis + cap + 15) >> 4;
-		p.nch = (live && prm.diag != 2) ? (need < (uint32_t)Chunks ? need : (uint32_t)Chunks) : 0;
+		p.nch = (live && !StreamOnly) ? (need < (uint32_t)Chunks ? need : (uint32_t)Chunks) : 0;
 	}
 	m_a0[lane] = p.a0;
 	m_nch[lane] = p.nch;
@@ -1422,7 +1388,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	Fast f;
 	bool fast = false;
 	uint32_t h5 = 0, h5d = 0, h2 = 0, ipc = 0, ips = 0, l4c = 0, l4s = 0;
-	if (live && prm.diag == 2)
+	if (live && StreamOnly)
 	{
 		w.l4i = 0;
 		w.l4o = 14;
@@ -1644,57 +1610,12 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	}
 }
 
-// ---- diagnostic streaming kernels (opts.variant 3/4): the read ceiling of the access pattern ----
-// variant 3: 64-lane blocks, each wave sums one contiguous tile-sized span (like the tile kernel);
-// variant 4: 256-lane blocks, grid-stride over the whole buffer, 4 x 16 B per lane in flight.
-__global__ __launch_bounds__(kTile) void diag_tile_read(const uint8_t* data, uint64_t len, uint32_t per_wave,
-                                                         uint32_t* out)
-{
-	const uint64_t base = (uint64_t)blockIdx.x * per_wave;
-	uint32_t acc = 0;
-	for (uint32_t c = threadIdx.x; 16ull * c < per_wave; c += 4 * kTile)
-	{
-		uint4 v[4];
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-		{
-			const uint64_t a = base + 16ull * (c + k * kTile);
-			v[k] = a + 16 <= len ? ld16((uintptr_t)data + a) : make_uint4(0, 0, 0, 0);
-		}
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
-	}
-	acc = wave_incl_scan(acc);
-	if (threadIdx.x == 63)
-		out[blockIdx.x] = acc;
-}
-
-__global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, uint64_t len, uint32_t* out)
-{
-	const uint64_t nch = len / 16;
-	uint32_t acc = 0;
-	const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-	for (uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x; c < nch; c += 4 * stride)
-	{
-		uint4 v[4];
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-			v[k] = c + k * stride < nch ? ld16((uintptr_t)data + 16 * (c + k * stride)) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
-	}
-	out[blockIdx.x * kBlock + threadIdx.x] = acc;
-}
-
 // ---- per-flow counters keyed by hash5Tuple (FilterTraffic's flow table, AppWorkerThread.h:99-125) ----
 // A block aggregates 1024 packets at a time in an LDS hash table (LDS atomics), then adds one
 // {packets, bytes} pair per distinct flow to the HBM table: Zipf-skewed traffic puts a hot flow in most
 // packets of a batch, and per-packet global atomics on its slot would serialise.
 // Shape variants (block threads, LDS slots, packets per batch) are A/B'd in profiles/r01_ab_flow_shape.txt;
 // every shape keeps fewer packets per batch than LDS slots (hot flows kept only while kept + batch fit).
-constexpr uint32_t kFlowGrid = 512;                 // persistent blocks of shape 0 (A/B in profiles/r01_ab_flow_grid.txt)
 constexpr uint32_t kFlowHot = 2;                    // flows with more packets stay in LDS between flushes
 constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 
@@ -2143,32 +2064,27 @@ __global__ __launch_bounds__(kBlock) void filter_apply_kernel(FilterParams fp)
 	wave_count(st + 13, in && !settled);
 }
 
-
-}  // namespace
-
-// Launch-error check; with PCPPX_SYNC_CHECK=1 in the environment every launch is also synchronised
-// and its execution status reported (debug aid: turns asynchronous faults into a named failure).
-int check_launch(const char* what, hipStream_t stream)
+// the protocols the engine builds itself (ProtocolType.h:42-258), GenericPayload excluded: a parse-until
+// family made only of these never holds a layer the host would build (oracle/pcppx_oracle.c,
+// family_engine_only)
+bool family_engine_only(uint32_t fam)
 {
-	static const bool sync_check = [] {
-		const char* e = getenv("PCPPX_SYNC_CHECK");
-		return e != nullptr && e[0] == '1';
-	}();
-	hipError_t e = hipGetLastError();
-	if (e == hipSuccess && sync_check)
-		e = hipStreamSynchronize(stream);
-	if (e != hipSuccess)
+	if (fam == 0)
+		return false;
+	for (int k = 0; k < 4; ++k)
 	{
-		fprintf(stderr, "pcppx: %s failed: %s\n", what, hipGetErrorString(e));
-		return PCPPX_E_HIP;
+		const uint32_t b = (fam >> (8 * k)) & 0xFFu;
+		const bool own = b == P_ETH || b == P_IPV4 || b == P_IPV6 || b == P_TCP || b == P_UDP || b == P_ARP ||
+		                 b == P_VLAN || b == P_MPLS || b == P_GREV0 || b == P_GREV1 || b == P_PPTP ||
+		                 b == P_TRAILER || b == P_DOT3 || b == P_LLC;
+		if (b != 0 && !own)
+			return false;
 	}
-	return PCPPX_OK;
+	return true;
 }
 
-int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream)
+Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info)
 {
-	if (b->n == 0)
-		return PCPPX_OK;
 	Params prm;
 	prm.data = b->data;
 	prm.offsets = b->offsets;
@@ -2182,49 +2098,54 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	prm.want_csum = o->want_checksums;
 	prm.max_layers = o->max_layers;
 	prm.linktype = b->linktype;
-	prm.diag = o->variant == 2 ? 2 : 0;
-	prm.reasm = nullptr;
-	// variant 1 (or PCPPX_KERNEL=lane) selects the lane-per-packet kernel for A/B measurements
-	static const bool lane_env = [] {
-		const char* e = getenv("PCPPX_KERNEL");
-		return e != nullptr && e[0] == 'l';
-	}();
-	if (o->variant == 3 || o->variant == 4)
+	prm.fam_engine_only = family_engine_only(o->parse_until_family) ? 1u : 0u;
+	prm.reasm = info;
+	return prm;
+}
+
+// the parse kernel's shape: 5 waves/SIMD (96 VGPRs, 8 KiB LDS), 2 x 2 KiB span-stream windows, 112-B header
+// windows, non-temporal span loads and record stores -- the fastest of the measured shapes
+// (profiles/r01_ab_occupancy.txt, r01_ab_windows.txt, r01_ab_window160.txt, r01_ab_nontemporal.txt; the
+// other shapes are built only into tools/ab/libpcppx_ab.so)
+constexpr int kParseWaves = 5, kParseSWin = 128;
+#define PCPPX_PARSE_KERNEL parse_tile_kernel<kParseWaves, kParseSWin, kTStageChunks, true>
+
+// the flow-table shape: 1024-thread blocks, 8192 LDS slots, 4096-packet batches with the next batch prefetched,
+// 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)
+#define PCPPX_FLOW_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true>
+constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 4096, kFlowBlocks = 256;
+constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed LDS/HBM counters hold
+
+}  // namespace
+
+int check_launch(const char* what, hipStream_t /*stream*/)
+{
+	const hipError_t e = hipGetLastError();
+	if (e != hipSuccess)
 	{
-		// diagnostics write into the summary array (n * 32 bytes is ample)
-		uint32_t* out = reinterpret_cast<uint32_t*>(r->summary);
-		if (o->variant == 3)
-		{
-			const uint32_t per_wave = 21 * 1024;
-			const uint32_t blocks = (uint32_t)((b->data_len + per_wave - 1) / per_wave);
-			hipLaunchKernelGGL(diag_tile_read, dim3(blocks), dim3(kTile), 0, stream, b->data, b->data_len, per_wave, out);
-		}
-		else
-			hipLaunchKernelGGL(diag_grid_read, dim3(256 * 8), dim3(kBlock), 0, stream, b->data, b->data_len, out);
-		return check_launch("diag_read", stream);
+		fprintf(stderr, "pcppx: %s failed: %s\n", what, hipGetErrorString(e));
+		return PCPPX_E_HIP;
 	}
-	if (o->variant == 1 || lane_env)
-	{
-		hipLaunchKernelGGL(parse_lane_kernel, dim3((b->n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, prm);
-		return check_launch("parse_lane_kernel", stream);
-	}
-	const dim3 grid((b->n + kTile - 1) / kTile);
-	// default: 5 waves/SIMD (96 VGPRs, 8 KiB LDS) with 2 x 2 KiB stream windows -- measured fastest
-	// (profiles/r01_ab_occupancy.txt). A/B variants: 5 = 5 waves + 4 KiB windows, 6 = compiler's
-	// occupancy + 2 KiB windows, 8 = compiler's occupancy + 4 KiB windows (the round-1 first cut).
-	// Window size is measured not to matter (profiles/r01_ab_windows.txt); 160-B header windows lose
-	// (profiles/r01_ab_window160.txt).
-	if (o->variant == 5)
-		hipLaunchKernelGGL((parse_tile_kernel<5, 256>), grid, dim3(kTile), 0, stream, prm);
-	else if (o->variant == 6)
-		hipLaunchKernelGGL((parse_tile_kernel<1, 128>), grid, dim3(kTile), 0, stream, prm);
-	else if (o->variant == 8)
-		hipLaunchKernelGGL((parse_tile_kernel<1, 256>), grid, dim3(kTile), 0, stream, prm);
-	else if (o->variant == 11)  // cached loads / stores (the default before non-temporal ones, A/B)
-		hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm);
-	else  // default: non-temporal span stream and record stores (profiles/r01_ab_nontemporal.txt)
-		hipLaunchKernelGGL((parse_tile_kernel<5, 128, kTStageChunks, true>), grid, dim3(kTile), 0, stream, prm);
+	return PCPPX_OK;
+}
+
+int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream)
+{
+	if (b->n == 0)
+		return PCPPX_OK;
+	const Params prm = make_params(b, o, r, nullptr);
+	hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel", stream);
+}
+
+int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
+                       hipStream_t stream)
+{
+	if (b->n == 0)
+		return PCPPX_OK;
+	const Params prm = make_params(b, o, r, info);
+	hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
+	return check_launch("parse_tile_kernel(reasm)", stream);
 }
 
 int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, const pcppx_match_spec* spec,
@@ -2267,81 +2188,24 @@ int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_
 	auto* pk = reinterpret_cast<unsigned long long*>(packets);
 	auto* by = reinterpret_cast<unsigned long long*>(bytes);
 	auto* pc = reinterpret_cast<unsigned long long*>(packed);
-	constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed counters hold
-	static const uint32_t grid_cap = [] {  // PCPPX_FLOW_GRID: A/B of the persistent grid size
-		const char* e = getenv("PCPPX_FLOW_GRID");
-		const int v = e ? atoi(e) : 0;
-		return v > 0 ? (uint32_t)v : 0u;
-	}();
-	static const int shape = [] {  // PCPPX_FLOW_SHAPE: A/B of block threads / LDS slots / batch
-		const char* e = getenv("PCPPX_FLOW_SHAPE");
-		return e ? atoi(e) : 9;
-	}();
+	auto* st = reinterpret_cast<unsigned long long*>(stats);
 	for (uint32_t done = 0; done < n;)
 	{
-		const uint32_t cnt = n - done < kPackedMax ? n - done : kPackedMax;  // the LDS counters are packed too
-		auto* st = reinterpret_cast<unsigned long long*>(stats);
-		auto go = [&](auto kern, uint32_t threads, uint32_t batch, uint32_t def_grid) {
-			const uint32_t batches = (cnt + batch - 1) / batch;
-			const uint32_t cap = grid_cap ? grid_cap : def_grid;
-			hipLaunchKernelGGL(kern, dim3(batches < cap ? batches : cap), dim3(threads), 0, stream, sum + done,
-			                   caplens + done, cnt, keys, pk, by, capacity, st, pc);
-		};
-		switch (shape)
-		{
-		case 1: go(flow_count_kernel<512, 4096, 2048>, 512, 2048, 512); break;
-		case 3: go(flow_count_kernel<256, 4096, 2048>, 256, 2048, 512); break;
-		case 4: go(flow_count_kernel<512, 8192, 4096>, 512, 4096, 256); break;
-		case 5: go(flow_count_kernel<1024, 8192, 2048>, 1024, 2048, 256); break;
-		case 0: go(flow_count_kernel<256, 2048, 1024>, 256, 1024, kFlowGrid); break;
-		case 6: go(flow_count_kernel<1024, 8192, 4096, 1>, 1024, 4096, 256); break;
-		case 2: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;
-		case 10: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true>, 512, 2048, 512); break;
-		case 11: go(flow_count_kernel<1024, 4096, 2048, kFlowHot, true>, 1024, 2048, 512); break;
-		case 12: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true>, 1024, 6144, 256); break;
-		case 7: go(flow_count_kernel<1024, 8192, 4096, 4>, 1024, 4096, 256); break;
-		case 8: go(flow_count_kernel<1024, 8192, 4096, 8>, 1024, 4096, 256); break;
-		default: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true>, 1024, 4096, 256); break;  // shape 9
-		}
+		const uint32_t cnt = n - done < kPackedMax ? n - done : kPackedMax;
+		const uint32_t batches = (cnt + kFlowBatchPk - 1) / kFlowBatchPk;
+		hipLaunchKernelGGL(PCPPX_FLOW_KERNEL, dim3(batches < kFlowBlocks ? batches : kFlowBlocks), dim3(kFlowThreads), 0,
+		                   stream, sum + done, caplens + done, cnt, keys, pk, by, capacity, st, pc);
 		int rc = check_launch("flow_count_kernel", stream);
 		if (rc != PCPPX_OK)
 			return rc;
-		if (pc)
-		{
-			const uint32_t ub = (capacity + kBlock - 1) / kBlock;
-			hipLaunchKernelGGL(flow_unpack_kernel, dim3(ub < 2048 ? ub : 2048), dim3(kBlock), 0, stream, pk, by, pc, capacity);
-			rc = check_launch("flow_unpack_kernel", stream);
-			if (rc != PCPPX_OK)
-				return rc;
-		}
+		const uint32_t ub = (capacity + kBlock - 1) / kBlock;
+		hipLaunchKernelGGL(flow_unpack_kernel, dim3(ub < 2048 ? ub : 2048), dim3(kBlock), 0, stream, pk, by, pc, capacity);
+		rc = check_launch("flow_unpack_kernel", stream);
+		if (rc != PCPPX_OK)
+			return rc;
 		done += cnt;
 	}
 	return PCPPX_OK;
-}
-
-int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
-                       hipStream_t stream)
-{
-	if (b->n == 0)
-		return PCPPX_OK;
-	Params prm;
-	prm.data = b->data;
-	prm.offsets = b->offsets;
-	prm.caplens = b->caplens;
-	prm.data_len = b->data_len;
-	prm.summary = r->summary;
-	prm.layers = r->layers;
-	prm.n = b->n;
-	prm.family = o->parse_until_family;
-	prm.until_osi = o->parse_until_osi;
-	prm.want_csum = o->want_checksums;
-	prm.max_layers = o->max_layers;
-	prm.linktype = b->linktype;
-	prm.diag = 0;
-	prm.reasm = info;
-	hipLaunchKernelGGL((parse_tile_kernel<5, 128, kTStageChunks, true>), dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0,
-	                   stream, prm);
-	return check_launch("parse_tile_kernel(reasm)", stream);
 }
 
 int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcppx_reasm_info* info, hipStream_t stream)

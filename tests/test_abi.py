@@ -17,7 +17,8 @@ HEADER = abi.REPO_DIR / "include" / "pcppx.h"
 
 def declared_functions() -> list[str]:
     txt = HEADER.read_text()
-    return sorted(set(re.findall(r"^(?:int|void|void\*|uint32_t|const char\*)\s+(pcppx_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^PCPPX_API\s+(?:int|void|void\*|uint32_t|const char\*)\s+(pcppx_\w+)\s*\(", txt,
+                                 flags=re.M)))
 
 
 def test_header_declares_expected_api():
@@ -34,6 +35,23 @@ def test_engine_library_exports_every_symbol():
     assert lib.pcppx_abi_version() == abi.ABI_VERSION
 
 
+def test_engine_library_exports_only_the_header_api():
+    """Hidden visibility: the product library exports exactly include/pcppx.h (no A/B or launcher symbols)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", str(abi.ENGINE_SO)], capture_output=True, text=True,
+                         check=True).stdout
+    names = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    ours = sorted(n for n in names if "pcppx" in n)
+    assert ours == declared_functions()
+
+
+def test_product_sources_read_no_environment():
+    """No runtime knobs: the kernel / launch shapes are fixed in the product library (A/B shapes live in
+    tools/ab/)."""
+    csrc = abi.PKG_DIR / "csrc"
+    for f in list(csrc.glob("*.hip")) + list(csrc.glob("*.cpp")):
+        assert "getenv" not in f.read_text(), f
+
+
 def test_engine_rejects_bad_arguments_without_gpu():
     lib = abi.load_engine()
     assert lib.pcppx_parse_batch_device(None, None, None, None, None) == abi.E_INVAL
@@ -42,6 +60,10 @@ def test_engine_rejects_bad_arguments_without_gpu():
     lib.pcppx_default_opts(C.byref(o))
     assert (o.parse_until_family, o.parse_until_osi, o.want_checksums, o.max_layers) == (0, 8, 1, 16)
     assert lib.pcppx_strerror(abi.E_INVAL) == b"invalid argument"
+    o.reserved = 1  # the reserved opts byte must be zero
+    b = abi.Batch(1, 1, 1, 1, 1, 1, 0)
+    r = abi.Records(1, 1)
+    assert lib.pcppx_parse_batch_device(C.c_void_p(1), C.byref(b), C.byref(o), C.byref(r), None) == abi.E_INVAL
 
 
 def test_struct_layout_matches_header():

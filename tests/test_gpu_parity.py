@@ -20,8 +20,14 @@ from pcapplusplus_amd.pcap import from_packets
 pytestmark = pytest.mark.gpu
 
 
-def variant(opts: abi.Opts, v: int) -> abi.Opts:
-    return abi.make_opts(opts.parse_until_family, opts.parse_until_osi, bool(opts.want_checksums), opts.max_layers, v)
+def run(engine, batch, opts, kernel: int):
+    """kernel 0: the product path (libpcppx.so); 1: the lane-per-packet cross-check kernel of the tools-only
+    A/B library (tools/ab/libpcppx_ab.so), an independent implementation of the same records."""
+    if kernel == 0:
+        return parse_on_device(engine, batch, opts)
+    from tools import ab
+
+    return ab.parse_on_device(batch, opts, ab.LANE)
 
 
 @pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
@@ -29,7 +35,7 @@ def variant(opts: abi.Opts, v: int) -> abi.Opts:
 def test_gpu_golden(engine, path, kernel):
     batch, variants = load_golden(path)
     for v, (opts, rsum, rlay) in variants.items():
-        gsum, glay = parse_on_device(engine, batch, variant(opts, kernel))
+        gsum, glay = run(engine, batch, opts, kernel)
         osum, olay = oracle.oracle_parse(batch, opts)
         oracle.compare_exact(gsum, glay, osum, olay)
         oracle.compare_engine_to_reference(gsum, glay, rsum, rlay)
@@ -41,7 +47,7 @@ def test_gpu_crafted_deep_stacks(engine, gaps, kernel):
     b = as_batch(crafted(), gaps=gaps, seed=11)
     for opts in (abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 3, True, 5),
                  abi.make_opts(0, 8, True, 0), abi.make_opts(0, 8, False, 16)):
-        g = parse_on_device(engine, b, variant(opts, kernel))
+        g = run(engine, b, opts, kernel)
         o = oracle.oracle_parse(b, opts)
         oracle.compare_exact(g[0], g[1], o[0], o[1])
         if oracle.ref_available():
@@ -55,7 +61,7 @@ def test_gpu_mutations(engine, gaps, kernel):
     seedb, _ = load_golden([p for p in golden_files() if p.stem == "pcap_lt1"][0])
     pk = [seedb.packet(i) for i in range(seedb.n)]
     b = as_batch(mutate(pk, 40000, 5), gaps=gaps, seed=5)
-    g = parse_on_device(engine, b, abi.make_opts(variant=kernel))
+    g = run(engine, b, abi.make_opts(), kernel)
     o = oracle.oracle_parse(b, threads=8)
     oracle.compare_exact(g[0], g[1], o[0], o[1])
 
@@ -74,8 +80,8 @@ def test_gpu_permuted_descriptors(engine, order, kernel):
     else:
         perm = np.concatenate([t0 + rng.permutation(min(64, n - t0)) for t0 in range(0, n, 64)])
     pb = type(b)(b.data, b.offsets[perm].copy(), b.caplens[perm].copy(), b.linktype)
-    opts = abi.make_opts(0, 8, True, 8, kernel)
-    g = parse_on_device(engine, pb, opts)
+    opts = abi.make_opts(0, 8, True, 8)
+    g = run(engine, pb, opts, kernel)
     o = oracle.oracle_parse(pb, abi.make_opts(0, 8, True, 8), threads=8)
     oracle.compare_exact(g[0], g[1], o[0], o[1])
 
@@ -263,3 +269,20 @@ def test_gpu_flow_table_full_conserves_packets(engine):
         assert want[key] == v, key
     assert sum(v[0] for v in got.values()) + int(st[2]) + int(st[0]) == b.n
     assert int(st[0]) == zero[0] and int(st[2]) > 0
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.stem)
+def test_gpu_flag_contract_parse_until(engine, path):
+    """The device's NEEDS_HOST flags against the reference chain (oracle.check_flag_contract) under the full parse,
+    Packet(&raw, TCP) (benchmark.cpp:91) and Packet(&raw, OsiModelNetworkLayer): a packet is flagged when the
+    reference chain holds a layer the engine does not build, or the host's dissector fell back to Payload where
+    the engine stopped; parse-until roll-backs of the host's layer (Packet.cpp:134-175) leave exact, unflagged
+    chains."""
+    batch, variants = load_golden(path)
+    for v in ("full", "until_tcp", "until_osi3"):
+        if v not in variants:
+            continue
+        opts, rsum, rlay = variants[v]
+        gsum, glay = parse_on_device(engine, batch, opts)
+        oracle.compare_engine_to_reference(gsum, glay, rsum, rlay)
+        oracle.check_flag_contract(gsum, rsum, rlay)

@@ -1,0 +1,227 @@
+// pcppx_ab.hip — TOOLS ONLY: the A/B and diagnostic kernels of the parse path, built into
+// tools/ab/libpcppx_ab.so (never into the product library pcapplusplus_amd/libpcppx.so).
+//
+// This translation unit includes the product kernels (pcapplusplus_amd/csrc/pcppx_kernels.hip) and adds
+//   - the lane-per-packet parse kernel (the round-1 baseline: one lane streams one whole packet), used as an
+//     independent cross-check of the tile kernel in tests/ and as the "before" leg of measurements;
+//   - tile-kernel shape variants (occupancy, stream windows, cached vs non-temporal loads) and the
+//     stream-only diagnostic, whose measurements chose the product shape (profiles/r01_ab_*.txt);
+//   - read-ceiling diagnostics (tile-shaped and grid-stride streaming reads of the batch bytes);
+//   - the flow-table shape variants (block threads / LDS slots / batch / hot-flow threshold / prefetch).
+// Entry points are plain C; everything else is hidden.
+#include "../../pcapplusplus_amd/csrc/pcppx_kernels.hip"
+
+#define PCPPX_AB_API extern "C" __attribute__((visibility("default")))
+
+namespace pcppx
+{
+namespace
+{
+constexpr int kSlotDw = 33;      // 32 dwords of staged bytes + 1 pad dword: consecutive lanes land on different banks
+constexpr int kStageChunks = 8;  // 8 x 16 B = 128 B staged per packet
+
+// ================= lane kernel: one lane streams one whole packet (reference / fallback) =================
+__global__ __launch_bounds__(kBlock) void parse_lane_kernel(Params prm)
+{
+	__shared__ uint32_t stage[kBlock * kSlotDw];
+
+	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+	if (i >= prm.n)
+		return;
+	pcppx_summary* sum_out = prm.summary + i;
+	const uint64_t off = prm.offsets[i];
+	const uint32_t cap = prm.caplens[i];
+	bool empty;
+	uint32_t bad = desc_flags(off, cap, prm.data_len, &empty);
+	if (bad || empty)
+	{
+		write_summary(sum_out, 0, 0, 0, bad, 0, -1, 0, 0, 0, 0, 0);
+		return;
+	}
+
+	Pkt p;
+	p.g = (gptr8)(prm.data + off);
+	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
+	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+	{
+		uint32_t need = (p.mis + cap + 15) >> 4;
+		p.nch = need < kStageChunks ? need : kStageChunks;
+		lptr32w slot = (lptr32w)(stage) + threadIdx.x * kSlotDw;
+		uint4 v[kStageChunks];
+#pragma unroll
+		for (int c = 0; c < kStageChunks; ++c)
+			if ((uint32_t)c < p.nch)
+				v[c] = ld16(p.a0 + 16 * c);
+#pragma unroll
+		for (int c = 0; c < kStageChunks; ++c)
+			if ((uint32_t)c < p.nch)
+			{
+				slot[4 * c + 0] = v[c].x;
+				slot[4 * c + 1] = v[c].y;
+				slot[4 * c + 2] = v[c].z;
+				slot[4 * c + 3] = v[c].w;
+			}
+		p.s = reinterpret_cast<lptr8>(slot);
+		uint32_t staged = 16 * p.nch - p.mis;
+		p.lim = staged < cap ? staged : cap;
+	}
+
+	uint2* lay_out = prm.layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * prm.max_layers : nullptr;
+	Walk w = walk_chain(p, cap, prm, lay_out);
+	uint32_t h5, h5d, h2;
+	hashes(p, w, h5, h5d, h2);
+	uint32_t flags = w.flags, ipc = 0, ips = 0, l4c = 0, l4s = 0;
+	if (prm.want_csum)
+	{
+		if (w.v4 >= 0)
+		{
+			ipc = ipv4_checksum(p, w, &ips);
+			flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+		}
+		if (w.l4i >= 0)
+		{
+			l4c = l4_checksum(p, w, range_residue(p, w.l4o, w.l4o + w.l4dlen), &l4s);
+			flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
+		}
+	}
+	write_summary(sum_out, h5, h5d, h2, flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
+}
+
+// ---- diagnostic streaming kernels (opts.variant 3/4): the read ceiling of the access pattern ----
+// variant 3: 64-lane blocks, each wave sums one contiguous tile-sized span (like the tile kernel);
+// variant 4: 256-lane blocks, grid-stride over the whole buffer, 4 x 16 B per lane in flight.
+__global__ __launch_bounds__(kTile) void diag_tile_read(const uint8_t* data, uint64_t len, uint32_t per_wave,
+                                                         uint32_t* out)
+{
+	const uint64_t base = (uint64_t)blockIdx.x * per_wave;
+	uint32_t acc = 0;
+	for (uint32_t c = threadIdx.x; 16ull * c < per_wave; c += 4 * kTile)
+	{
+		uint4 v[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+		{
+			const uint64_t a = base + 16ull * (c + k * kTile);
+			v[k] = a + 16 <= len ? ld16((uintptr_t)data + a) : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+	}
+	acc = wave_incl_scan(acc);
+	if (threadIdx.x == 63)
+		out[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, uint64_t len, uint32_t* out)
+{
+	const uint64_t nch = len / 16;
+	uint32_t acc = 0;
+	const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+	for (uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x; c < nch; c += 4 * stride)
+	{
+		uint4 v[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			v[k] = c + k * stride < nch ? ld16((uintptr_t)data + 16 * (c + k * stride)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+	}
+	out[blockIdx.x * kBlock + threadIdx.x] = acc;
+}
+
+}  // namespace
+}  // namespace pcppx
+
+using namespace pcppx;
+
+/* variant: 1 lane kernel; 2 stream-only diagnostic (no header gather / parse; L4 range = [14, caplen));
+ * 3 / 4 tile-shaped / grid-stride read of the batch bytes (results written over summary[]);
+ * 5 tile 5 waves + 4 KiB windows; 6 compiler occupancy + 2 KiB; 8 compiler occupancy + 4 KiB;
+ * 11 cached loads and stores; anything else: the product kernel. Records equal the product's for 1, 5, 6, 8, 11. */
+PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, void* hip_stream,
+                                       int variant)
+{
+	if (b == nullptr || o == nullptr || r == nullptr || o->max_layers > PCPPX_MAX_LAYERS)
+		return PCPPX_E_INVAL;
+	if (b->n == 0)
+		return PCPPX_OK;
+	hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+	const Params prm = make_params(b, o, r, nullptr);
+	const dim3 grid((b->n + kTile - 1) / kTile);
+	switch (variant)
+	{
+	case 1:
+		hipLaunchKernelGGL(parse_lane_kernel, dim3((b->n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, prm);
+		break;
+	case 2: hipLaunchKernelGGL((parse_tile_kernel<5, 128, kTStageChunks, true, true>), grid, dim3(kTile), 0, stream, prm); break;
+	case 3:
+	case 4:
+	{
+		uint32_t* out = reinterpret_cast<uint32_t*>(r->summary);  // n * 32 bytes is ample
+		if (variant == 3)
+		{
+			const uint32_t per_wave = 21 * 1024;
+			const uint32_t blocks = (uint32_t)((b->data_len + per_wave - 1) / per_wave);
+			hipLaunchKernelGGL(diag_tile_read, dim3(blocks), dim3(kTile), 0, stream, b->data, b->data_len, per_wave, out);
+		}
+		else
+			hipLaunchKernelGGL(diag_grid_read, dim3(256 * 8), dim3(kBlock), 0, stream, b->data, b->data_len, out);
+		break;
+	}
+	case 5: hipLaunchKernelGGL((parse_tile_kernel<5, 256>), grid, dim3(kTile), 0, stream, prm); break;
+	case 6: hipLaunchKernelGGL((parse_tile_kernel<1, 128>), grid, dim3(kTile), 0, stream, prm); break;
+	case 8: hipLaunchKernelGGL((parse_tile_kernel<1, 256>), grid, dim3(kTile), 0, stream, prm); break;
+	case 11: hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm); break;
+	default: return launch_parse(b, o, r, stream);
+	}
+	return check_launch("pcppx_ab_parse_device", stream);
+}
+
+/* Flow-table shapes 0-12 of profiles/r01_ab_flow_shape.txt (9 = the product's); grid 0 = the shape's default
+ * persistent grid. packed: zeroed u64[capacity] scratch (the product's packed accumulator) or NULL. */
+PCPPX_AB_API int pcppx_ab_flow_count_device(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n,
+                                            uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity,
+                                            uint64_t* stats, uint64_t* packed, void* hip_stream, int shape,
+                                            uint32_t grid)
+{
+	if (sum == nullptr || caplens == nullptr || keys == nullptr || capacity == 0 || (capacity & (capacity - 1)) != 0 ||
+	    n > kPackedMax)
+		return PCPPX_E_INVAL;
+	if (n == 0)
+		return PCPPX_OK;
+	hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+	auto* pk = reinterpret_cast<unsigned long long*>(packets);
+	auto* by = reinterpret_cast<unsigned long long*>(bytes);
+	auto* pc = reinterpret_cast<unsigned long long*>(packed);
+	auto* st = reinterpret_cast<unsigned long long*>(stats);
+	auto go = [&](auto kern, uint32_t threads, uint32_t batch, uint32_t def_grid) {
+		const uint32_t batches = (n + batch - 1) / batch;
+		const uint32_t cap = grid ? grid : def_grid;
+		hipLaunchKernelGGL(kern, dim3(batches < cap ? batches : cap), dim3(threads), 0, stream, sum, caplens, n, keys, pk,
+		                   by, capacity, st, pc);
+	};
+	switch (shape)
+	{
+	case 0: go(flow_count_kernel<256, 2048, 1024>, 256, 1024, 512); break;  // 512 persistent blocks (r01_ab_flow_grid.txt)
+	case 1: go(flow_count_kernel<512, 4096, 2048>, 512, 2048, 512); break;
+	case 2: go(flow_count_kernel<1024, 8192, 4096>, 1024, 4096, 256); break;
+	case 3: go(flow_count_kernel<256, 4096, 2048>, 256, 2048, 512); break;
+	case 4: go(flow_count_kernel<512, 8192, 4096>, 512, 4096, 256); break;
+	case 5: go(flow_count_kernel<1024, 8192, 2048>, 1024, 2048, 256); break;
+	case 6: go(flow_count_kernel<1024, 8192, 4096, 1>, 1024, 4096, 256); break;
+	case 7: go(flow_count_kernel<1024, 8192, 4096, 4>, 1024, 4096, 256); break;
+	case 8: go(flow_count_kernel<1024, 8192, 4096, 8>, 1024, 4096, 256); break;
+	case 10: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true>, 512, 2048, 512); break;
+	case 11: go(flow_count_kernel<1024, 4096, 2048, kFlowHot, true>, 1024, 2048, 512); break;
+	case 12: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true>, 1024, 6144, 256); break;
+	default: go(PCPPX_FLOW_KERNEL, kFlowThreads, kFlowBatchPk, kFlowBlocks); break;
+	}
+	int rc = check_launch("pcppx_ab_flow_count_device", stream);
+	if (rc != PCPPX_OK || pc == nullptr)
+		return rc;
+	const uint32_t ub = (capacity + kBlock - 1) / kBlock;
+	hipLaunchKernelGGL(flow_unpack_kernel, dim3(ub < 2048 ? ub : 2048), dim3(kBlock), 0, stream, pk, by, pc, capacity);
+	return check_launch("flow_unpack_kernel", stream);
+}

@@ -1,4 +1,5 @@
-"""Interleaved A/B timing of kernel variants in one process (cdna guide §5.4 rule 24).
+"""Interleaved A/B timing of kernel variants in one process (cdna guide §5.4 rule 24), through the tools-only
+library tools/ab/libpcppx_ab.so (variant 0 = the product kernel).
 
   python tools/ab_kernels.py [packets] [rounds]
 """
@@ -11,30 +12,30 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch  # noqa: E402
 
 from pcapplusplus_amd import abi, synth  # noqa: E402
-from pcapplusplus_amd.engine import Engine, to_device  # noqa: E402
+from pcapplusplus_amd.engine import to_device  # noqa: E402
+from tools import ab  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 b = synth.config(cfg, n)
-eng = Engine(0)
 data, offs, caps = to_device(b)
 summ = torch.empty(n * 32, dtype=torch.uint8, device="cuda:0")
 lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device="cuda:0")
 st = torch.cuda.current_stream()
 read_bytes = int(b.caplens.sum(dtype=np.int64)) + 12 * n
 cases = {
-    "tile/ml8/csum": abi.make_opts(0, 8, True, 8, 0),
-    "lane/ml8/csum": abi.make_opts(0, 8, True, 8, 1),
-    "tile/ml0/csum": abi.make_opts(0, 8, True, 0, 0),
-    "tile/ml8/nocsum": abi.make_opts(0, 8, False, 8, 0),
-    "tile/w5win256": abi.make_opts(0, 8, True, 8, 5),
-    "tile/w4win128": abi.make_opts(0, 8, True, 8, 6),
-    "tile/w4win256": abi.make_opts(0, 8, True, 8, 8),
-    "tile/cached": abi.make_opts(0, 8, True, 8, 11),
-    "tile/stream-only": abi.make_opts(0, 8, True, 0, 2),
-    "diag/tile-read": abi.make_opts(0, 8, True, 0, 3),
-    "diag/grid-read": abi.make_opts(0, 8, True, 0, 4),
+    "tile/ml8/csum": (abi.make_opts(0, 8, True, 8), 0),
+    "lane/ml8/csum": (abi.make_opts(0, 8, True, 8), 1),
+    "tile/ml0/csum": (abi.make_opts(0, 8, True, 0), 0),
+    "tile/ml8/nocsum": (abi.make_opts(0, 8, False, 8), 0),
+    "tile/w5win256": (abi.make_opts(0, 8, True, 8), 5),
+    "tile/w4win128": (abi.make_opts(0, 8, True, 8), 6),
+    "tile/w4win256": (abi.make_opts(0, 8, True, 8), 8),
+    "tile/cached": (abi.make_opts(0, 8, True, 8), 11),
+    "tile/stream-only": (abi.make_opts(0, 8, True, 0), 2),
+    "diag/tile-read": (abi.make_opts(0, 8, True, 0), 3),
+    "diag/grid-read": (abi.make_opts(0, 8, True, 0), 4),
 }
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")
@@ -42,13 +43,13 @@ if only:
     cases = {k: v for k, v in cases.items() if k in only.split(",")}
 # records of every full variant must equal the first listed variant's (same checksum mode), byte for byte
 ref_s = ref_l = None
-want_csum_ref = next(iter(cases.values())).want_checksums
-for name, o in cases.items():
-    if o.max_layers != 8 or o.want_checksums != want_csum_ref or o.variant in (2, 3, 4):
+want_csum_ref = next(iter(cases.values()))[0].want_checksums
+for name, (o, v) in cases.items():
+    if o.max_layers != 8 or o.want_checksums != want_csum_ref or v in (2, 3, 4):
         continue
     summ.zero_()
     lay.zero_()
-    eng.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream)
+    ab.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream, v)
     torch.cuda.synchronize()
     if ref_s is None:
         ref_s, ref_l = summ.clone(), lay[: n * 64].clone()
@@ -60,10 +61,10 @@ for name, o in cases.items():
 del ref_s, ref_l
 times = {k: [] for k in cases}
 for r in range(rounds):
-    for name, o in cases.items():
+    for name, (o, v) in cases.items():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        eng.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream)
+        ab.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream, v)
         e1.record(st)
         torch.cuda.synchronize()
         if r > 0:
