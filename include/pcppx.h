@@ -59,6 +59,15 @@ extern "C" {
 #define PCPPX_F_L4_CSUM_OK 0x0080       /* l4_csum_calc == l4_csum_stored */
 #define PCPPX_F_TRAILER 0x0100          /* last layer is a PacketTrailer (Packet.cpp:178-195) */
 #define PCPPX_F_BAD_DESC 0x0200         /* offsets[i] + caplens[i] > batch data_len: not parsed */
+/* The first L7 layer of a NEEDS_HOST_L7 packet, where the device can name it (the content checks of
+ * TcpLayer.cpp:372-415 / UdpLayer.cpp:103-116 it restates): with PCPPX_F_L7_KNOWN set, the packet's chain holds
+ * an HTTPRequest/HTTPResponse, SSL or DNS layer exactly when the matching bit is set, i.e.
+ * Packet::isPacketOfType(HTTP / SSL / DNS) is decided. Not set for tunnels (VXLAN, GTPv1) whose inner packet only
+ * the host parses. */
+#define PCPPX_F_L7_KNOWN 0x0400
+#define PCPPX_F_L7_HTTP 0x0800
+#define PCPPX_F_L7_SSL 0x1000
+#define PCPPX_F_L7_DNS 0x2000
 #define PCPPX_F_NEEDS_HOST \
 	(PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC)
 

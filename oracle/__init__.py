@@ -138,81 +138,14 @@ def ref_filter(batch, spec: abi.MatchSpec):
 
 P_ETH, P_IPV4, P_IPV6, P_TCP, P_UDP, P_ARP = 1, 2, 3, 4, 5, 8
 
-# ---- collectStats' L7 counters (Examples/DpdkExample-FilterTraffic/Common.h:83-104) ----
-HTTP_METHODS = {b"GET", b"HEAD", b"POST", b"PUT", b"DELETE", b"TRACE", b"OPTIONS", b"CONNECT", b"PATCH"}  # HttpLayer.cpp:145-155
-HTTP_CODES = {100, 101, 102, 103, 200, 201, 202, 203, 204, 205, 206, 207, 208, 226, 300, 301, 302, 303, 304, 305, 306,
-              307, 308, 400, 401, 402, 403, 404, 405, 406, 407, 408, 409, 410, 411, 412, 413, 414, 415, 416, 417, 418,
-              419, 420, 421, 422, 423, 424, 425, 426, 428, 429, 431, 440, 444, 449, 450, 451, 494, 495, 496, 497, 498,
-              499, 500, 501, 502, 503, 504, 505, 506, 507, 508, 509, 510, 511, 520, 521, 522, 523, 524, 598,
-              599}  # intStatusCodeMap, HttpLayer.cpp:424-508
-SSL_PORTS = {443, 261, 448, 465, 563, 614, 636, 989, 990, 992, 993, 994, 995}  # SSLLayer.h:488-510
-DNS_PORTS = {53, 5353, 5355}  # DnsLayer.h:468-479
-
-
-def _http_request(d: bytes) -> bool:
-    """HttpRequestFirstLine::parseMethod != Unknown (HttpLayer.cpp:261-285)."""
-    if len(d) < 4:
-        return False
-    sp = d.find(b" ")
-    return sp > 0 and d[:sp] in HTTP_METHODS
-
-
-def _http_response(d: bytes) -> bool:
-    """parseVersion != Unknown && !parseStatusCode(...).isUnsupportedCode() (HttpLayer.cpp:850-898,964-984)."""
-    if len(d) < 12 or d[:5] != b"HTTP/" or d[5:8] not in (b"0.9", b"1.0", b"1.1"):
-        return False
-    code = d[9:12]
-    if not all(0x30 <= c <= 0x39 for c in code) or int(code) not in HTTP_CODES:
-        return False
-    nl = d.find(b"\n", 13)
-    if nl < 0:
-        return False
-    msg = d[13:nl]
-    if msg.endswith(b"\r"):
-        msg = msg[:-1]
-    return len(msg) > 0
-
-
-def l7_class(pkt: bytes, l4) -> tuple[int, bool]:
-    """(bits HTTP 1 / DNS 2 / SSL 4 of the first L7 layer, settled) of a NEEDS_HOST_L7 packet whose chain
-    ends with TCP/UDP layer l4 (TcpLayer.cpp:372-415, UdpLayer.cpp:103-116); VXLAN / GTPv1 tunnels bring
-    inner packets the device does not parse: not settled."""
-    o, hl, dl = int(l4["offset"]), int(l4["hdr_len"]), int(l4["data_len"])
-    sp, dp = pkt[o] << 8 | pkt[o + 1], pkt[o + 2] << 8 | pkt[o + 3]
-    d = pkt[o + hl:o + dl]
-    if int(l4["proto"]) == P_UDP:
-        if dp == 4789 or 2152 in (sp, dp):
-            return 0, False
-        dhcp = (sp, dp) in ((68, 67), (67, 68), (67, 67))
-        return (2 if not dhcp and len(d) >= 12 and (sp in DNS_PORTS or dp in DNS_PORTS) else 0), True
-    if dp in (80, 8080) and _http_request(d):
-        return 1, True
-    if sp in (80, 8080) and _http_response(d):
-        return 1, True
-    if (sp in SSL_PORTS or dp in SSL_PORTS) and len(d) >= 5 and (d[3] or d[4]) and 20 <= d[0] <= 23:
-        v = d[1] << 8 | d[2]  # SSLVersion::asEnum(true), SSLCommon.cpp:12-27
-        if 0x0300 <= v <= 0x0304 or 0x7F0E <= v <= 0x7F1C or v in (0xFB17, 0xFB1A):
-            return 4, True
-    if {sp, dp} & {5060, 5061, 179, 22}:
-        return 0, True
-    return (2 if len(d) >= 14 and (sp in DNS_PORTS or dp in DNS_PORTS) else 0), True
-
-
 def stats_settled(batch, summary, layers):
-    """Per packet: (settled, L7 bits) as the device's filter_apply_kernel decides them."""
-    n = batch.n
-    settled = np.zeros(n, bool)
-    l7 = np.zeros(n, np.int32)
-    ml = layers.shape[1]
-    for i in range(n):
-        fl = int(summary["flags"][i])
-        ok = not (fl & (abi.F_NEEDS_HOST_PROTO | abi.F_OVERSIZE | abi.F_BAD_DESC))
-        if ok and fl & abi.F_NEEDS_HOST_L7:
-            nl = min(int(summary["n_layers"][i]), ml)
-            ok = nl == int(summary["n_layers"][i]) and nl > 0 and int(layers[i, nl - 1]["proto"]) in (P_TCP, P_UDP)
-            if ok:
-                l7[i], ok = l7_class(batch.packet(i), layers[i, nl - 1])
-        settled[i] = ok
+    """Per packet: (settled, L7 bits HTTP 1 / DNS 2 / SSL 4) for collectStats' counters (Common.h:83-104), from the
+    parse flags: a packet is settled unless its chain stopped before an out-of-scope L2/L3 layer, its record is bad,
+    or it has an L7 layer the parse did not classify (PCPPX_F_L7_KNOWN; restated in pcppx_oracle.c tcp_l7/udp_l7)."""
+    fl = summary["flags"].astype(np.int64)
+    settled = ((fl & (abi.F_NEEDS_HOST_PROTO | abi.F_OVERSIZE | abi.F_BAD_DESC)) == 0) & \
+        (((fl & abi.F_NEEDS_HOST_L7) == 0) | ((fl & abi.F_L7_KNOWN) != 0))
+    l7 = (((fl & abi.F_L7_HTTP) != 0) * 1 | ((fl & abi.F_L7_DNS) != 0) * 2 | ((fl & abi.F_L7_SSL) != 0) * 4).astype(np.int32)
     return settled, l7
 
 
@@ -394,7 +327,21 @@ def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:
         i = int(bad[0])
         raise AssertionError(f"{len(bad)} flagged packets whose reference chain continues with an engine layer; "
                              f"first #{i}: engine={eng_sum[i]} ref={ref_lay[i][: rn[i]]}")
-    return {"flagged": int(host.sum()), "foreign": int(foreign.sum()), "payload_fallback": int(len(over))}
+    # the first L7 layer's class (PCPPX_F_L7_*) against the reference chain's HTTPRequest/HTTPResponse (6/7),
+    # SSL (18) and DNS (13) layers
+    fl = eng_sum["flags"]
+    known = ((fl & abi.F_NEEDS_HOST_L7) != 0) & ((fl & abi.F_L7_KNOWN) != 0)
+    m = ref_sum["proto_mask"].astype(np.uint64)
+    bit = lambda p: ((m >> np.uint64(p)) & np.uint64(1)).astype(bool)  # noqa: E731
+    for name, f, has in (("HTTP", abi.F_L7_HTTP, bit(6) | bit(7)), ("SSL", abi.F_L7_SSL, bit(18)),
+                         ("DNS", abi.F_L7_DNS, bit(13))):
+        bad = np.nonzero(known & (((fl & f) != 0) != has))[0]
+        if len(bad):
+            i = int(bad[0])
+            raise AssertionError(f"L7 class {name} differs on {len(bad)} packets; first #{i}: engine={eng_sum[i]} "
+                                 f"ref={ref_lay[i][: rn[i]]}")
+    return {"flagged": int(host.sum()), "foreign": int(foreign.sum()), "payload_fallback": int(len(over)),
+            "l7_known": int(known.sum())}
 
 
 def compare_exact(a_sum, a_lay, b_sum, b_lay) -> None:

@@ -130,6 +130,105 @@ static int sip_heuristic(const uint8_t* p, uint32_t n)
 	return 0;
 }
 
+/* ---- the first L7 layer behind TCP/UDP: the dispatch chains' content checks the engine restates ----
+ * TcpLayer::parseNextLayer (TcpLayer.cpp:372-491) tries, in order, HTTP request (dst port 80/8080 and a known
+ * method), HTTP response (src port 80/8080, known version and supported status code), SSL (SSL port and a
+ * record header), then dissectors that are all gated by their own ports, then Payload. So a payload whose
+ * only trigger ports are HTTP / SSL ports and whose content passes neither check is a plain Payload: exact,
+ * no flag. Every other trigger leaves the packet to the host (NEEDS_HOST_L7) with the class of its first L7
+ * layer where the engine can name it (PCPPX_F_L7_*), for PacketStats::collectStats (Common.h:83-104). */
+static const uint16_t kHttpCodes[] = { /* intStatusCodeMap, HttpLayer.cpp:424-508 */
+	100, 101, 102, 103, 200, 201, 202, 203, 204, 205, 206, 207, 208, 226, 300, 301, 302, 303, 304, 305, 306,
+	307, 308, 400, 401, 402, 403, 404, 405, 406, 407, 408, 409, 410, 411, 412, 413, 414, 415, 416, 417, 418,
+	419, 420, 421, 422, 423, 424, 425, 426, 428, 429, 431, 440, 444, 449, 450, 451, 494, 495, 496, 497, 498,
+	499, 500, 501, 502, 503, 504, 505, 506, 507, 508, 509, 510, 511, 520, 521, 522, 523, 524, 598, 599 };
+/* HttpMessage::isHttpPort, HttpLayer.h:74-77 */
+static int http_port(uint16_t x) { return x == 80 || x == 8080; }
+/* HttpRequestFirstLine::parseMethod != HttpMethodUnknown, HttpLayer.cpp:261-285 (HttpMethodStringToEnum :145-155) */
+static int http_request(const uint8_t* d, uint32_t n)
+{
+	static const char* methods[] = { "GET", "HEAD", "POST", "PUT", "DELETE", "TRACE", "OPTIONS", "CONNECT", "PATCH" };
+	if (n < 4) return 0;
+	uint32_t sp = 0;
+	while (sp < n && d[sp] != ' ') ++sp;
+	if (sp == 0 || sp == n) return 0;
+	for (unsigned k = 0; k < sizeof(methods) / sizeof(methods[0]); ++k)
+		if (strlen(methods[k]) == sp && memcmp(d, methods[k], sp) == 0) return 1;
+	return 0;
+}
+/* HttpResponseFirstLine::parseVersion != Unknown (HttpLayer.cpp:964-984, HttpVersionStringToEnum :160-164) and
+ * !parseStatusCode(..).isUnsupportedCode() (:850-898; HttpResponseStatusCode(int, msg) :510-543 maps codes outside
+ * intStatusCodeMap to values > 599, isUnsupportedCode HttpLayer.h:453-456) */
+static int http_response(const uint8_t* d, uint32_t n)
+{
+	if (n < 8 || memcmp(d, "HTTP/", 5) != 0) return 0;
+	if (memcmp(d + 5, "0.9", 3) != 0 && memcmp(d + 5, "1.0", 3) != 0 && memcmp(d + 5, "1.1", 3) != 0) return 0;
+	if (n < 12) return 0;
+	for (int j = 9; j < 12; ++j)
+		if (d[j] < '0' || d[j] > '9') return 0;
+	uint32_t off = 13;
+	while (off < n && d[off] != '\n') ++off;
+	if (off >= n) return 0;                                  /* no end of line: HttpStatusCodeUnknown */
+	uint32_t mlen = off - 13;
+	if (mlen > 0 && d[off - 1] == '\r') --mlen;             /* messageString.pop_back() */
+	if (mlen == 0) return 0;
+	int code = (d[9] - '0') * 100 + (d[10] - '0') * 10 + (d[11] - '0');
+	for (unsigned k = 0; k < sizeof(kHttpCodes) / sizeof(kHttpCodes[0]); ++k)
+		if (kHttpCodes[k] == code) return 1;
+	return 0;
+}
+/* SSLLayer::IsSSLMessage, SSLLayer.cpp:14-40 (ports checked by the caller; SSLVersion::asEnum(true),
+ * SSLCommon.cpp:12-27) */
+static int ssl_record(const uint8_t* d, uint32_t n)
+{
+	if (n < 5) return 0;                        /* sizeof(ssl_tls_record_layer) */
+	if (d[3] == 0 && d[4] == 0) return 0;       /* length 0 */
+	if (d[0] < 20 || d[0] > 23) return 0;       /* record type */
+	uint32_t v = ((uint32_t)d[1] << 8) | d[2];
+	return (v >= 0x0300 && v <= 0x0304) || (v >= 0x7f0e && v <= 0x7f1c) || v == 0xfb17 || v == 0xfb1a;
+}
+static int dns_port(uint16_t x) { return x == 53 || x == 5353 || x == 5355; } /* DnsLayer::isDnsPort, DnsLayer.h:468-479 */
+
+/* TCP payload (sp/dp host order): 0 = plain Payload, else PCPPX_F_NEEDS_HOST_L7 | class bits */
+static uint16_t tcp_l7(const uint8_t* d, uint32_t n, uint16_t sp, uint16_t dp)
+{
+	if (http_port(dp) && http_request(d, n)) return PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN | PCPPX_F_L7_HTTP;
+	if (http_port(sp) && http_response(d, n)) return PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN | PCPPX_F_L7_HTTP;
+	if ((ssl_port(sp) || ssl_port(dp)) && ssl_record(d, n))
+		return PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN | PCPPX_F_L7_SSL;
+	/* the rest of the chain is gated by ports other than HTTP's and SSL's */
+	int other = 0;
+	for (int k = 0; k < 2; ++k) {
+		uint16_t x = k ? dp : sp;
+		if (tcp_l7_port(x) && !http_port(x) && !ssl_port(x)) other = 1;
+	}
+	if (!other) return 0;
+	/* SIP (TcpLayer.cpp:387-402), BGP (:403-406) and SSH (:407-410) come before DNS and always take the payload;
+	 * DnsOverTcpLayer needs 14 bytes (DnsLayer::isDataValid(.., true), DnsLayer.h:481-485); nothing after DNS
+	 * builds an HTTP, DNS or SSL layer */
+	uint16_t cls = PCPPX_F_L7_KNOWN;
+	int sip_bgp_ssh = 0;
+	for (int k = 0; k < 2; ++k) {
+		uint16_t x = k ? dp : sp;
+		if (x == 5060 || x == 5061 || x == 179 || x == 22) sip_bgp_ssh = 1;
+	}
+	if (!sip_bgp_ssh && n >= 14 && (dns_port(sp) || dns_port(dp))) cls |= PCPPX_F_L7_DNS;
+	return PCPPX_F_NEEDS_HOST_L7 | cls;
+}
+/* UDP payload: 0 = plain Payload, else PCPPX_F_NEEDS_HOST_L7 | class bits (UdpLayer.cpp:103-183) */
+static uint16_t udp_l7(uint32_t n, uint16_t sp, uint16_t dp, int sip)
+{
+	if (!udp_l7_port(sp, dp) && !sip) return 0;
+	/* VXLAN (dst 4789, VxlanLayer.h:119-122) and GTPv1 (2152/2123, GtpLayer.h:386-389) carry a whole inner
+	 * packet whose layers only the host sees */
+	if (dp == 4789 || sp == 2152 || dp == 2152 || sp == 2123 || dp == 2123) return PCPPX_F_NEEDS_HOST_L7;
+	uint16_t cls = PCPPX_F_L7_KNOWN;
+	int dhcp = (sp == 68 && dp == 67) || (sp == 67 && dp == 68) || (sp == 67 && dp == 67);
+	/* DnsLayer after DHCP and VXLAN (UdpLayer.cpp:103-115): 12 bytes (DnsLayer.h:481-485) and a DNS port */
+	if (!dhcp && n >= 12 && (dns_port(sp) || dns_port(dp))) cls |= PCPPX_F_L7_DNS;
+	return PCPPX_F_NEEDS_HOST_L7 | cls;
+}
+
 /* ---- parse-until roll-back of a layer this path does not build (Packet.cpp:134-155, 168-175) ----
  * Where the chain reaches a layer the engine leaves to the host (an L7 dissector, or an out-of-scope
  * L2/L3 layer), Packet::parsePacket still builds it and then applies the stop rules to it: it is rolled
@@ -226,12 +325,13 @@ static int family_member(uint32_t fam, uint8_t p)
 /* Build layer `k` at [off, off+len) and report its next layer through nk, noff, nlen.
  * Returns the layer descriptor. */
 static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int* nk, uint32_t* noff, uint32_t* nlen,
-                      uint8_t* nosi)
+                      uint8_t* nosi, uint16_t* ncls)
 {
 	const uint8_t* p = pkt + off;
 	lay L = { 0, 0, off, 0, len };
 	*nk = K_NONE;
 	*nosi = 7; /* smallest OSI layer of the host-built candidates when *nk is K_OUT / K_L7 */
+	*ncls = 0; /* K_L7: PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_* */
 	uint32_t po, pl; /* payload of this layer */
 #define NEXT(K, O, N) do { *nk = (K); *noff = (O); *nlen = (N); } while (0)
 	switch (k) {
@@ -404,7 +504,8 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		L.proto = P_TCP; L.osi = 4; L.hdr = (uint32_t)(p[12] >> 4) * 4;
 		if (len <= L.hdr) break;
 		po = off + L.hdr; pl = len - L.hdr;
-		NEXT((tcp_l7_port(be16(p)) || tcp_l7_port(be16(p + 2))) ? K_L7 : K_PAYLOAD, po, pl);
+		*ncls = tcp_l7(pkt + po, pl, be16(p), be16(p + 2));
+		NEXT(*ncls ? K_L7 : K_PAYLOAD, po, pl);
 		*nosi = tcp_l7_min_osi(be16(p), be16(p + 2));
 		break;
 	case K_UDP: /* UdpLayer::parseNextLayer, Packet++/src/UdpLayer.cpp:92-184 */
@@ -413,7 +514,8 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		po = off + 8; pl = len - 8;
 		{
 			int sip = sip_heuristic(pkt + po, pl);
-			NEXT((udp_l7_port(be16(p), be16(p + 2)) || sip) ? K_L7 : K_PAYLOAD, po, pl);
+			*ncls = udp_l7(pl, be16(p), be16(p + 2), sip);
+			NEXT(*ncls ? K_L7 : K_PAYLOAD, po, pl);
 			*nosi = udp_l7_min_osi(be16(p), be16(p + 2), sip);
 		}
 		break;
@@ -466,6 +568,7 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 	uint64_t mask = 0;
 	uint32_t off = 0, len = caplen;
 	uint8_t kosi = 7; /* smallest candidate OSI layer of k when k is K_OUT / K_L7 */
+	uint16_t kcls = 0; /* k == K_L7: the flags it brings */
 	const int fam_engine_only = family_engine_only(opts->parse_until_family);
 	while (k != K_NONE) {
 		if (k == K_OUT || k == K_L7) {
@@ -474,12 +577,13 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 				stopped_by_rule = 1;
 				break;
 			}
-			flags |= k == K_OUT ? PCPPX_F_NEEDS_HOST_PROTO : PCPPX_F_NEEDS_HOST_L7;
+			flags |= k == K_OUT ? PCPPX_F_NEEDS_HOST_PROTO : kcls;
 			break;
 		}
 		int nk; uint32_t noff = 0, nlen = 0;
 		uint8_t nosi = 7;
-		lay L = make_layer(pkt, k, off, len, &nk, &noff, &nlen, &nosi);
+		uint16_t ncls = 0;
+		lay L = make_layer(pkt, k, off, len, &nk, &noff, &nlen, &nosi, &ncls);
 		int member = family_member(opts->parse_until_family, L.proto);
 		int fail = L.osi > opts->parse_until_osi;
 		if (!fail) {
@@ -505,7 +609,7 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 		prev = L;
 		last = L;
 		++count;
-		k = nk; off = noff; len = nlen; kosi = nosi;
+		k = nk; off = noff; len = nlen; kosi = nosi; kcls = ncls;
 	}
 	/* trailer: Packet.cpp:178-195 (only with no parse-until options, and not for flagged chains) */
 	if (count > 0 && opts->parse_until_family == 0 && opts->parse_until_osi == 8 && !stopped_by_rule &&

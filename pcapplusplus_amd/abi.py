@@ -33,6 +33,10 @@ F_L4_CSUM = 0x0040
 F_L4_CSUM_OK = 0x0080
 F_TRAILER = 0x0100
 F_BAD_DESC = 0x0200
+F_L7_KNOWN = 0x0400
+F_L7_HTTP = 0x0800
+F_L7_SSL = 0x1000
+F_L7_DNS = 0x2000
 F_NEEDS_HOST = F_NEEDS_HOST_L7 | F_NEEDS_HOST_PROTO | F_OVERSIZE | F_BAD_DESC
 
 # pcpp::LinkLayerType values used here (Packet++/header/RawPacket.h:24-178)

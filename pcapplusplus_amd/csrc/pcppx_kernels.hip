@@ -152,12 +152,15 @@ constexpr uint16_t kUdpL7DstPorts[] = { 4789, 0, 7, 9 };  // VXLAN, WakeOnLan (U
 struct L7Tables
 {
 	uint32_t tcp[2048], udp[2048], udp_dst[2048];
+	uint32_t tcp_other[2048];  // tcp minus the HTTP and SSL ports (whose dissectors the engine restates)
 };
 constexpr L7Tables make_l7_tables()
 {
 	L7Tables t{};
 	for (uint16_t x : kTcpL7Ports)
 		t.tcp[x >> 5] |= 1u << (x & 31);
+	for (int k = 15; k < (int)(sizeof(kTcpL7Ports) / sizeof(kTcpL7Ports[0])); ++k)  // after 443..995, 80, 8080
+		t.tcp_other[kTcpL7Ports[k] >> 5] |= 1u << (kTcpL7Ports[k] & 31);
 	for (uint16_t x : kUdpL7Ports)
 		t.udp[x >> 5] |= 1u << (x & 31);
 	for (uint16_t x : kUdpL7DstPorts)
@@ -208,6 +211,137 @@ __device__ __forceinline__ bool sip_key(uint32_t k)
 {
 	const uint32_t h = (k * kSipMul) >> 27;
 	return ((kSip.valid >> h) & 1u) && kSip.key[h] == k;
+}
+
+// ---- the first L7 layer behind TCP/UDP (restated in oracle/pcppx_oracle.c: tcp_l7 / udp_l7) ----
+// TcpLayer::parseNextLayer (TcpLayer.cpp:372-491) tries HTTP request (dst 80/8080 + known method), HTTP response
+// (src 80/8080 + known version + supported status code), SSL (SSL port + record header), then dissectors gated by
+// their own ports, then Payload: a payload whose only trigger ports are HTTP / SSL ports and that fails those
+// content checks is a plain Payload. UdpLayer::parseNextLayer (UdpLayer.cpp:103-183) is port-gated except for the
+// SIP content heuristic. The flags name the first L7 layer (PCPPX_F_L7_*) where the device can.
+struct HttpCodes
+{
+	uint32_t bits[16];  // status codes of intStatusCodeMap (HttpLayer.cpp:424-508), bit (code - 100)
+};
+constexpr HttpCodes make_http_codes()
+{
+	HttpCodes t{};
+	const uint16_t codes[] = { 100, 101, 102, 103, 200, 201, 202, 203, 204, 205, 206, 207, 208, 226, 300, 301, 302,
+		                       303, 304, 305, 306, 307, 308, 400, 401, 402, 403, 404, 405, 406, 407, 408, 409, 410,
+		                       411, 412, 413, 414, 415, 416, 417, 418, 419, 420, 421, 422, 423, 424, 425, 426, 428,
+		                       429, 431, 440, 444, 449, 450, 451, 494, 495, 496, 497, 498, 499, 500, 501, 502, 503,
+		                       504, 505, 506, 507, 508, 509, 510, 511, 520, 521, 522, 523, 524, 598, 599 };
+	for (uint16_t c : codes)
+		t.bits[(c - 100) >> 5] |= 1u << ((c - 100) & 31);
+	return t;
+}
+__constant__ HttpCodes kHttpCodes = make_http_codes();
+
+constexpr uint64_t le_str(const char* m)
+{
+	uint64_t v = 0;
+	for (int j = 0; m[j] != 0; ++j)
+		v |= (uint64_t)(uint8_t)m[j] << (8 * j);
+	return v;
+}
+__device__ __forceinline__ bool http_port(uint32_t x)
+{
+	return x == 80 || x == 8080;  // HttpMessage::isHttpPort, HttpLayer.h:74-77
+}
+__device__ __forceinline__ bool ssl_port(uint32_t x)
+{
+	return x == 443 || x == 261 || x == 448 || x == 465 || x == 563 || x == 614 || x == 636 || x == 989 || x == 990 ||
+	       (x >= 992 && x <= 995);  // SSLLayer::isSSLPort, SSLLayer.h:488-510
+}
+__device__ __forceinline__ bool dns_port(uint32_t x)
+{
+	return x == 53 || x == 5353 || x == 5355;  // DnsLayer::isDnsPort, DnsLayer.h:468-479
+}
+// HttpRequestFirstLine::parseMethod != Unknown (HttpLayer.cpp:261-285; methods :145-155): the text before the first
+// space is a known method; the longest is 7 bytes, so only the first 8 bytes matter
+__device__ bool http_request(const Pkt& p, uint32_t o, uint32_t n)
+{
+	if (n < 4)
+		return false;
+	uint64_t w = 0;
+	uint32_t sp = 8;
+	for (uint32_t j = 0; j < 8; ++j)
+	{
+		const uint32_t c = j < n ? rb(p, o + j) : 0x100u;
+		sp = (c == ' ' && sp == 8) ? j : sp;
+		w |= (uint64_t)(c & 0xFF) << (8 * j);
+	}
+	if (sp == 8 || sp == 0 || sp >= n)
+		return false;
+	w &= (1ull << (8 * sp)) - 1;
+	return (sp == 3 && (w == le_str("GET") || w == le_str("PUT"))) ||
+	       (sp == 4 && (w == le_str("HEAD") || w == le_str("POST"))) ||
+	       (sp == 5 && (w == le_str("TRACE") || w == le_str("PATCH"))) || (sp == 6 && w == le_str("DELETE")) ||
+	       (sp == 7 && (w == le_str("OPTIONS") || w == le_str("CONNECT")));
+}
+// HttpResponseFirstLine::parseVersion != Unknown (HttpLayer.cpp:964-984) and a supported status code with a
+// non-empty message (parseStatusCode :850-898, HttpResponseStatusCode(int, msg) :510-543, isUnsupportedCode
+// HttpLayer.h:453-456)
+__device__ bool http_response(const Pkt& p, uint32_t o, uint32_t n)
+{
+	if (n < 12)
+		return false;
+	uint32_t d[12];
+#pragma unroll
+	for (int j = 0; j < 12; ++j)
+		d[j] = rb(p, o + j);
+	if (d[0] != 'H' || d[1] != 'T' || d[2] != 'T' || d[3] != 'P' || d[4] != '/')
+		return false;
+	const bool ver = (d[5] == '0' && d[6] == '.' && d[7] == '9') || (d[5] == '1' && d[6] == '.' && (d[7] == '0' || d[7] == '1'));
+	if (!ver || d[9] - '0' > 9u || d[10] - '0' > 9u || d[11] - '0' > 9u)
+		return false;
+	const uint32_t code = (d[9] - '0') * 100u + (d[10] - '0') * 10u + (d[11] - '0');
+	if (code < 100 || code > 599 || !((kHttpCodes.bits[(code - 100) >> 5] >> ((code - 100) & 31)) & 1u))
+		return false;
+	uint32_t off = 13;
+	while (off < n && rb(p, o + off) != '\n')
+		++off;
+	if (off >= n)
+		return false;  // no end of the first line: HttpStatusCodeUnknown
+	return off > 14 || (off == 14 && rb(p, o + 13) != '\r');  // a non-empty status message
+}
+// SSLLayer::IsSSLMessage past its port check (SSLLayer.cpp:14-40; SSLVersion::asEnum(true), SSLCommon.cpp:12-27)
+__device__ bool ssl_record(const Pkt& p, uint32_t o, uint32_t n)
+{
+	if (n < 5)
+		return false;
+	const uint32_t t = rb(p, o), v = (rb(p, o + 1) << 8) | rb(p, o + 2), len = (rb(p, o + 3) << 8) | rb(p, o + 4);
+	return len != 0 && t >= 20 && t <= 23 &&
+	       ((v >= 0x0300 && v <= 0x0304) || (v >= 0x7f0e && v <= 0x7f1c) || v == 0xfb17 || v == 0xfb1a);
+}
+// The L7 decision for a TCP/UDP payload at [o, o+n) with ports sp/dp (host order): 0 = plain Payload, else
+// PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_*. `trig` = the ports (or the SIP heuristic) trigger a dissector.
+__device__ uint32_t l7_flags(const Pkt& p, bool tcp, uint32_t o, uint32_t n, uint32_t sp, uint32_t dp, bool sip, bool trig)
+{
+	if (!trig)
+		return 0;
+	const uint32_t known = PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN;
+	if (!tcp)
+	{
+		// VXLAN (VxlanLayer.h:119-122) and GTPv1 (GtpLayer.h:386-389) bring an inner packet only the host parses
+		if (dp == 4789 || sp == 2152 || dp == 2152 || sp == 2123 || dp == 2123)
+			return PCPPX_F_NEEDS_HOST_L7;
+		const bool dhcp = (sp == 68 && dp == 67) || (sp == 67 && (dp == 68 || dp == 67));
+		return known | ((!dhcp && n >= 12 && (dns_port(sp) || dns_port(dp))) ? PCPPX_F_L7_DNS : 0u);
+	}
+	if (http_port(dp) && http_request(p, o, n))
+		return known | PCPPX_F_L7_HTTP;
+	if (http_port(sp) && http_response(p, o, n))
+		return known | PCPPX_F_L7_HTTP;
+	if ((ssl_port(sp) || ssl_port(dp)) && ssl_record(p, o, n))
+		return known | PCPPX_F_L7_SSL;
+	// the rest of the chain is gated by ports other than HTTP's and SSL's
+	if (!(port_bit(kL7.tcp_other, sp) | port_bit(kL7.tcp_other, dp)))
+		return 0;
+	// SIP / BGP / SSH (TcpLayer.cpp:387-410) come before DNS over TCP (14 bytes, DnsLayer.h:481-485) and take the
+	// payload; nothing after DNS builds an HTTP, DNS or SSL layer
+	const bool sbs = sp == 5060 || sp == 5061 || sp == 179 || sp == 22 || dp == 5060 || dp == 5061 || dp == 179 || dp == 22;
+	return known | ((!sbs && n >= 14 && (dns_port(sp) || dns_port(dp))) ? PCPPX_F_L7_DNS : 0u);
 }
 
 // Smallest OSI layer among the layers the host would build on an L4 payload the port / SIP triggers hand to
@@ -677,14 +811,16 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		const uint32_t pw = rd32(p, l7_o);
 		const uint32_t sp = swap16(pw), dp = swap16(pw >> 16);
 		const bool sip = !l7_tcp && l7_pl >= 4 && sip_key(__builtin_bswap32(rd32(p, l7_o + 8)));
-		bool l7 = l7_tcp ? tcp_l7(sp, dp) : (udp_l7(sp, dp) || sip);
+		const bool trig = l7_tcp ? tcp_l7(sp, dp) : (udp_l7(sp, dp) || sip);
+		uint32_t lf = trig ? l7_flags(p, l7_tcp, l7_end - l7_pl, l7_pl, sp, dp, sip, true) : 0u;
 		// parse-until options: the dissector's layer is rolled back (Packet.cpp:134-155,168-175) when every
 		// candidate lies above parseUntilLayer, or the family was found and holds only engine-built protocols
-		if (l7 && (prm.family != 0 || prm.until_osi < 8))  // uniform
-			l7 = !(l7_min_osi(l7_tcp, sp, dp, sip) > prm.until_osi || (found && prm.fam_engine_only));
-		if (l7)
+		if (lf && (prm.family != 0 || prm.until_osi < 8) &&  // uniform
+		    (l7_min_osi(l7_tcp, sp, dp, sip) > prm.until_osi || (found && prm.fam_engine_only)))
+			lf = 0;
+		if (lf)
 		{
-			flags |= PCPPX_F_NEEDS_HOST_L7;
+			flags |= lf;
 			if (count > l7_next)  // the tentative Payload was recorded
 			{
 				count = l7_next;
@@ -883,7 +1019,7 @@ struct Fast
 	uint32_t l4o, l4hdr, l4dlen, tcp;
 	uint32_t payload;   // a Payload layer follows the L4 layer
 	uint32_t trailer;   // trailer length (0: none)
-	uint32_t l7;        // L4 payload would go to an L7 dissector
+	uint32_t l7;        // L4 payload goes to an L7 dissector: PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_* (else 0)
 };
 
 __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Params& prm, Fast& f)
@@ -971,17 +1107,20 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 __device__ __forceinline__ void fast_l7(const Pkt& p, Fast& f, uint32_t cap)
 {
 	const bool payload = f.payload != 0;
-	bool l7 = false;
+	uint32_t lf = 0;
 	if (payload)
 	{
 		const uint32_t pw = lds_u32(p, f.l4o);
 		const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
-		l7 = f.tcp ? tcp_l7(sport, dport)
-		           : (udp_l7(sport, dport) || (f.l4dlen - 8 >= 4 && sip_key(__builtin_bswap32(lds_u32(p, f.l4o + 8)))));
+		const bool sip = !f.tcp && f.l4dlen - 8 >= 4 && sip_key(__builtin_bswap32(lds_u32(p, f.l4o + 8)));
+		const bool trig = f.tcp ? tcp_l7(sport, dport) : (udp_l7(sport, dport) || sip);
+		if (trig)
+			lf = l7_flags(p, f.tcp, f.l4o + f.l4hdr, f.l4dlen - f.l4hdr, sport, dport, sip, true);
 	}
+	const bool l7 = lf != 0;
 	const uint32_t end = f.trailer;
 	f.payload = payload && !l7;
-	f.l7 = l7;
+	f.l7 = lf;
 	f.trailer = (!l7 && end < cap) ? cap - end : 0;
 }
 
@@ -991,7 +1130,7 @@ __device__ __forceinline__ Walk fast_to_walk(const Fast& f, uint32_t ml)
 	const uint32_t cap_layers = ml ? ml : PCPPX_MAX_LAYERS;
 	const uint32_t count = 3 + f.nv + f.payload + (f.trailer ? 1 : 0);
 	Walk w;
-	w.flags = (f.l7 ? PCPPX_F_NEEDS_HOST_L7 : 0) | (f.trailer ? PCPPX_F_TRAILER : 0) |
+	w.flags = f.l7 | (f.trailer ? PCPPX_F_TRAILER : 0) |
 	          (count > cap_layers ? PCPPX_F_DEPTH_OVERFLOW : 0);
 	w.n_layers = count > cap_layers ? cap_layers : count;
 	w.mask = (1ull << P_ETH) | (f.nv ? (1ull << P_VLAN) : 0) | (1ull << (f.v6 ? P_IPV6 : P_IPV4)) |
@@ -1883,114 +2022,6 @@ __global__ __launch_bounds__(kBlock) void filter_mark_kernel(FilterParams fp)
 	}
 }
 
-// ---- collectStats' L7 counters (Common.h:83-104): the first L7 layer of a NEEDS_HOST_L7 packet ----
-// TcpLayer::parseNextLayer's dispatch order (TcpLayer.cpp:372-415): HTTP request (dst port 80/8080 and
-// HttpRequestFirstLine::parseMethod, HttpLayer.cpp:261-285), HTTP response (src port 80/8080,
-// HttpResponseFirstLine::parseVersion / parseStatusCode, HttpLayer.cpp:850-898,964-984), SSL
-// (SSLLayer::IsSSLMessage, SSLLayer.cpp:14-40), then SIP / BGP / SSH ports (none counted), then DNS over
-// TCP (DnsLayer::isDataValid, DnsLayer.h:481-485); UdpLayer::parseNextLayer (UdpLayer.cpp:103-116): DHCP,
-// VXLAN, then DNS. Layers after these add no HTTP / DNS / SSL layer, except where a tunnel (VXLAN, GTPv1)
-// brings a whole inner packet: those packets are left to the host (settled = false).
-struct HttpCodes
-{
-	uint32_t bits[16];  // status codes 100..599 HttpLayer.cpp:424-508 maps (bit code - 100)
-};
-constexpr HttpCodes make_http_codes()
-{
-	HttpCodes t{};
-	const uint16_t codes[] = { 100, 101, 102, 103, 200, 201, 202, 203, 204, 205, 206, 207, 208, 226, 300, 301, 302,
-		                       303, 304, 305, 306, 307, 308, 400, 401, 402, 403, 404, 405, 406, 407, 408, 409, 410,
-		                       411, 412, 413, 414, 415, 416, 417, 418, 419, 420, 421, 422, 423, 424, 425, 426, 428,
-		                       429, 431, 440, 444, 449, 450, 451, 494, 495, 496, 497, 498, 499, 500, 501, 502, 503,
-		                       504, 505, 506, 507, 508, 509, 510, 511, 520, 521, 522, 523, 524, 598, 599 };
-	for (uint16_t c : codes)
-		t.bits[(c - 100) >> 5] |= 1u << ((c - 100) & 31);
-	return t;
-}
-__constant__ HttpCodes kHttpCodes = make_http_codes();
-
-__device__ __forceinline__ bool ssl_port16(uint32_t x)
-{
-	return x == 443 || x == 261 || x == 448 || x == 465 || x == 563 || x == 614 || x == 636 || x == 989 || x == 990 ||
-	       (x >= 992 && x <= 995);
-}
-__device__ __forceinline__ bool dns_port16(uint32_t x)
-{
-	return x == 53 || x == 5353 || x == 5355;
-}
-__device__ __forceinline__ bool http_method(const uint8_t* d, uint32_t n)
-{
-	if (n < 4)
-		return false;
-	uint32_t sp = 8;  // first space among the first 8 bytes (longer method names are unknown anyway)
-	for (uint32_t j = 0; j < 8 && j < n; ++j)
-		if (d[j] == ' ' && sp == 8)
-			sp = j;
-	if (sp == 8 || sp == 0 || sp >= n)
-		return false;
-	auto is = [&](const char* m, uint32_t l) {
-		if (sp != l)
-			return false;
-		for (uint32_t j = 0; j < l; ++j)
-			if (d[j] != (uint8_t)m[j])
-				return false;
-		return true;
-	};
-	return is("GET", 3) || is("PUT", 3) || is("HEAD", 4) || is("POST", 4) || is("TRACE", 5) || is("PATCH", 5) ||
-	       is("DELETE", 6) || is("OPTIONS", 7) || is("CONNECT", 7);
-}
-__device__ bool http_status(const uint8_t* d, uint32_t n)
-{
-	if (n < 12 || d[0] != 'H' || d[1] != 'T' || d[2] != 'T' || d[3] != 'P' || d[4] != '/')
-		return false;
-	const bool ver = (d[5] == '0' && d[6] == '.' && d[7] == '9') || (d[5] == '1' && d[6] == '.' && (d[7] == '0' || d[7] == '1'));
-	if (!ver)
-		return false;
-	for (int j = 9; j < 12; ++j)
-		if (d[j] < '0' || d[j] > '9')
-			return false;
-	const uint32_t code = (d[9] - '0') * 100u + (d[10] - '0') * 10u + (d[11] - '0');
-	if (code < 100 || code > 599 || !((kHttpCodes.bits[(code - 100) >> 5] >> ((code - 100) & 31)) & 1u))
-		return false;
-	uint32_t off = 13;
-	while (off < n && d[off] != '\n')
-		++off;
-	if (off >= n)
-		return false;  // no end of the first line: HttpStatusCodeUnknown
-	return off > 14 || (off == 14 && d[13] != '\r');  // a non-empty status message
-}
-
-__device__ uint32_t l7_class(const uint8_t* pkt, const pcppx_layer& l4, bool& settled)
-{
-	const uint8_t* h = pkt + l4.offset;
-	const uint32_t sp = ((uint32_t)h[0] << 8) | h[1], dp = ((uint32_t)h[2] << 8) | h[3];
-	const uint8_t* d = h + l4.hdr_len;
-	const uint32_t n = (uint32_t)l4.data_len - l4.hdr_len;
-	if (l4.proto == P_UDP)
-	{
-		if (dp == 4789 || sp == 2152 || dp == 2152)
-		{
-			settled = false;  // VXLAN / GTPv1 carry an inner packet
-			return 0;
-		}
-		const bool dhcp = (sp == 68 && dp == 67) || (sp == 67 && (dp == 68 || dp == 67));
-		return (!dhcp && n >= 12 && (dns_port16(sp) || dns_port16(dp))) ? 2u : 0u;
-	}
-	if ((dp == 80 || dp == 8080) && http_method(d, n))
-		return 1;
-	if ((sp == 80 || sp == 8080) && http_status(d, n))
-		return 1;
-	if ((ssl_port16(sp) || ssl_port16(dp)) && n >= 5 && (d[3] | d[4]) != 0 && d[0] >= 20 && d[0] <= 23)
-	{
-		const uint32_t v = ((uint32_t)d[1] << 8) | d[2];  // SSLVersion::asEnum(true), SSLCommon.cpp:12-27
-		if ((v >= 0x0300 && v <= 0x0304) || (v >= 0x7f0e && v <= 0x7f1c) || v == 0xfb17 || v == 0xfb1a)
-			return 4;
-	}
-	if (sp == 5060 || sp == 5061 || dp == 5060 || dp == 5061 || sp == 179 || dp == 179 || sp == 22 || dp == 22)
-		return 0;
-	return (n >= 14 && (dns_port16(sp) || dns_port16(dp))) ? 2u : 0u;
-}
-
 __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred)
 {
 	const unsigned long long b = __ballot(pred);
@@ -2012,15 +2043,11 @@ __global__ __launch_bounds__(kBlock) void filter_apply_kernel(FilterParams fp)
 		mask = sm.proto_mask;
 		flags = sm.flags;
 		const uint32_t nl = sm.n_layers < fp.ml ? sm.n_layers : fp.ml;
-		// the packet's counters are the device's unless its chain stopped before a layer it does not see
-		settled = (flags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC)) == 0;
-		if (settled && (flags & PCPPX_F_NEEDS_HOST_L7))
-		{
-			const pcppx_layer l4 = fp.layers[(size_t)i * fp.ml + (nl ? nl - 1 : 0)];
-			settled = nl == sm.n_layers && nl > 0 && (l4.proto == P_TCP || l4.proto == P_UDP);
-			if (settled)
-				l7 = l7_class(fp.data + fp.offsets[i], l4, settled);
-		}
+		// the packet's counters are the device's unless its chain stopped before a layer it does not see: an
+		// out-of-scope L2/L3 layer, a bad record, or an L7 layer the parse could not classify (PCPPX_F_L7_KNOWN)
+		settled = (flags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC)) == 0 &&
+		          (!(flags & PCPPX_F_NEEDS_HOST_L7) || (flags & PCPPX_F_L7_KNOWN));
+		l7 = ((flags & PCPPX_F_L7_HTTP) ? 1u : 0u) | ((flags & PCPPX_F_L7_DNS) ? 2u : 0u) | ((flags & PCPPX_F_L7_SSL) ? 4u : 0u);
 		const bool own = filter_is_matched(fp, i, mask, nl);
 		const unsigned long long key = (1ull << 32) | sm.hash5;
 		const uint64_t seq = fp.seq_base + i;

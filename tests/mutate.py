@@ -235,3 +235,33 @@ def as_batch(packets: list[bytes], gaps: bool = False, seed: int = 0) -> PacketB
         pos += len(p)
     data = np.frombuffer(b"".join(chunks) + b"\0" * 16, dtype=np.uint8).copy()
     return PacketBatch(data, np.array(offs, np.uint64), np.array([len(p) for p in packets], np.uint32))
+
+
+def crafted_l7(seed: int = 13) -> list[bytes]:
+    """TCP/UDP payloads at the edges of the L7 content checks the engine restates (HTTP request method, HTTP
+    response version / status code / status line end, SSL record header, DNS lengths) on HTTP, SSL, DNS and other
+    trigger ports, over IPv4 and IPv6, some behind a VLAN tag (generic walk) and padded past the LDS window."""
+    rng = np.random.default_rng(seed)
+    bodies = [b"GET / HTTP/1.1\r\n", b"GET", b"GET ", b" GET /", b"GETX / HTTP/1.1", b"OPTIONS * HTTP/1.1\r\n",
+              b"CONNECT a:443 HTTP/1.1", b"PATCH /x", b"DELETE", b"TRACE / HTTP/1.0\r\n", b"get / HTTP/1.1",
+              b"HTTP/1.1 200 OK\r\n", b"HTTP/1.1 200 \r\n", b"HTTP/1.1 200\r\n", b"HTTP/1.1 200 X", b"HTTP/1.0 999 X\n",
+              b"HTTP/0.9 404 Not Found\n", b"HTTP/2.0 200 OK\r\n", b"HTTP/1.1 20A OK\r\n", b"HTTP/1.1 599 \r\r\n",
+              b"HTTP/1.1 226 IM Used" + b"x" * 150 + b"\n", b"HTTP/1.1 103 E\n",
+              bytes([22, 3, 1, 0, 5]) + b"hello", bytes([23, 3, 3, 0, 0]), bytes([24, 3, 3, 1, 0]),
+              bytes([20, 0x7f, 0x1c, 0, 1, 1]), bytes([21, 0xfb, 0x1a, 0, 2]), bytes([22, 3, 5, 0, 9]),
+              bytes([22, 3, 0, 1, 0]), bytes([22, 3]), b"", b"x" * 11, b"x" * 12, b"x" * 13, b"x" * 14,
+              b"INVITE sip:a SIP/2.0\r\n", rng.bytes(40)]
+    tcp_ports = [(40000, 80), (80, 40000), (8080, 8080), (443, 40000), (40000, 993), (80, 443), (53, 40000),
+                 (40000, 5353), (22, 80), (443, 179), (5060, 80), (102, 443), (21, 8080), (40000, 40001), (2123, 53)]
+    udp_ports = [(40000, 53), (53, 40000), (5355, 5355), (68, 67), (67, 53), (40000, 4789), (2152, 53), (53, 2123),
+                 (40000, 5060), (40000, 40001), (123, 53), (40000, 9)]
+    pk = []
+    for body in bodies:
+        for sp, dp in tcp_ports:
+            l4 = _tcp(sp, dp, body)
+            pk.append(_eth(0x0800) + _ipv4(6, len(l4)) + l4)
+            pk.append(_eth(0x8100) + struct.pack(">HH", 7, 0x86DD) + _ipv6(6, len(l4)) + l4)
+        for sp, dp in udp_ports:
+            l4 = _udp(sp, dp, body)
+            pk.append(_eth(0x0800) + _ipv4(17, len(l4)) + l4 + bytes(int(rng.integers(0, 3))))
+    return pk

@@ -12,7 +12,7 @@ import pytest
 
 import oracle
 from conftest import golden_files, load_golden
-from mutate import as_batch, crafted, mutate
+from mutate import as_batch, crafted, crafted_l7, mutate
 from pcapplusplus_amd import abi, synth
 from pcapplusplus_amd.engine import parse_on_device
 from pcapplusplus_amd.pcap import from_packets
@@ -53,6 +53,23 @@ def test_gpu_crafted_deep_stacks(engine, gaps, kernel):
         if oracle.ref_available():
             r = oracle.ref_parse(b, opts)
             oracle.compare_engine_to_reference(g[0], g[1], r[0], r[1])
+
+
+@pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
+@pytest.mark.parametrize("gaps", [False, True])
+def test_gpu_crafted_l7_payloads(engine, gaps, kernel):
+    """The L7 content checks (HTTP request / response first line, SSL record header, DNS lengths) at their edges,
+    on the fast path (Eth/IPv4) and the generic walk (VLAN/IPv6), payload bytes in and past the LDS window."""
+    b = as_batch(crafted_l7(), gaps=gaps, seed=17)
+    for opts in (abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 4, True, 16),
+                 abi.make_opts(0, 8, False, 0)):
+        g = run(engine, b, opts, kernel)
+        o = oracle.oracle_parse(b, opts)
+        oracle.compare_exact(g[0], g[1], o[0], o[1])
+        if oracle.ref_available() and opts.max_layers:
+            r = oracle.ref_parse(b, opts)
+            oracle.compare_engine_to_reference(g[0], g[1], r[0], r[1])
+            oracle.check_flag_contract(g[0], r[0], r[1])
 
 
 @pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])

@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 from conftest import golden_files, load_golden
-from mutate import as_batch, crafted, mutate
+from mutate import as_batch, crafted, crafted_l7, mutate
 from pcapplusplus_amd import abi
 
 pytestmark = pytest.mark.skipif(not oracle.ref_available(), reason="reference library not built")
@@ -30,6 +30,21 @@ def test_crafted_stacks_vs_reference(opt_i):
     rs, rl = oracle.ref_parse(b, OPTS[opt_i])
     os_, ol = oracle.oracle_parse(b, OPTS[opt_i])
     oracle.compare_engine_to_reference(os_, ol, rs, rl)
+    if OPTS[opt_i].max_layers >= 8:
+        oracle.check_flag_contract(os_, rs, rl)
+
+
+@pytest.mark.parametrize("opt_i", range(len(OPTS)))
+def test_crafted_l7_payloads_vs_reference(opt_i):
+    """The L7 content checks (HTTP / SSL / DNS first layers; plain Payload otherwise) at their edges."""
+    b = as_batch(crafted_l7())
+    rs, rl = oracle.ref_parse(b, OPTS[opt_i])
+    os_, ol = oracle.oracle_parse(b, OPTS[opt_i])
+    oracle.compare_engine_to_reference(os_, ol, rs, rl)
+    if OPTS[opt_i].max_layers >= 8:
+        st = oracle.check_flag_contract(os_, rs, rl)
+        if opt_i == 0:
+            assert st["l7_known"] > 0 and st["flagged"] < b.n
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -39,3 +54,4 @@ def test_mutations_vs_reference(seed):
         rs, rl = oracle.ref_parse(b, opts)
         os_, ol = oracle.oracle_parse(b, opts)
         oracle.compare_engine_to_reference(os_, ol, rs, rl)
+        oracle.check_flag_contract(os_, rs, rl)
