@@ -266,6 +266,14 @@ static uint8_t udp_l7_min_osi(uint16_t sp, uint16_t dp, int sip_content)
 	if (sp == 5060 || sp == 5061 || dp == 5060 || dp == 5061 || sip_content) return 5;
 	return 7;
 }
+/* a classified first L7 layer has its own OSI layer (HttpLayer.h:87-90 application, SSLLayer.h:246-249
+ * presentation, DnsLayer.h:369-372 application); otherwise the smallest over the port candidates */
+static uint8_t l7_osi(uint16_t cls, uint8_t min_osi)
+{
+	if (cls & PCPPX_F_L7_SSL) return 6;
+	if (cls & (PCPPX_F_L7_HTTP | PCPPX_F_L7_DNS)) return 7;
+	return min_osi;
+}
 /* the protocols the engine builds itself (ProtocolType.h:42-258), GenericPayload excluded */
 static int engine_proto(uint32_t p)
 {
@@ -506,7 +514,7 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		po = off + L.hdr; pl = len - L.hdr;
 		*ncls = tcp_l7(pkt + po, pl, be16(p), be16(p + 2));
 		NEXT(*ncls ? K_L7 : K_PAYLOAD, po, pl);
-		*nosi = tcp_l7_min_osi(be16(p), be16(p + 2));
+		*nosi = l7_osi(*ncls, tcp_l7_min_osi(be16(p), be16(p + 2)));
 		break;
 	case K_UDP: /* UdpLayer::parseNextLayer, Packet++/src/UdpLayer.cpp:92-184 */
 		L.proto = P_UDP; L.osi = 4; L.hdr = 8;
@@ -516,7 +524,7 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 			int sip = sip_heuristic(pkt + po, pl);
 			*ncls = udp_l7(pl, be16(p), be16(p + 2), sip);
 			NEXT(*ncls ? K_L7 : K_PAYLOAD, po, pl);
-			*nosi = udp_l7_min_osi(be16(p), be16(p + 2), sip);
+			*nosi = l7_osi(*ncls, udp_l7_min_osi(be16(p), be16(p + 2), sip));
 		}
 		break;
 	case K_ARP: /* ArpLayer: dataLen := sizeof(arphdr) = 28 whatever remains, no next (ArpLayer.h:151-155,242-273) */

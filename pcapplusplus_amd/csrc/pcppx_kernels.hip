@@ -815,9 +815,14 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		uint32_t lf = trig ? l7_flags(p, l7_tcp, l7_end - l7_pl, l7_pl, sp, dp, sip, true) : 0u;
 		// parse-until options: the dissector's layer is rolled back (Packet.cpp:134-155,168-175) when every
 		// candidate lies above parseUntilLayer, or the family was found and holds only engine-built protocols
-		if (lf && (prm.family != 0 || prm.until_osi < 8) &&  // uniform
-		    (l7_min_osi(l7_tcp, sp, dp, sip) > prm.until_osi || (found && prm.fam_engine_only)))
-			lf = 0;
+		if (lf && (prm.family != 0 || prm.until_osi < 8))  // uniform
+		{
+			// a classified first L7 layer has its own OSI layer (HTTP / DNS application, SSL presentation)
+			const uint32_t osi = (lf & PCPPX_F_L7_SSL) ? 6u
+			                   : (lf & (PCPPX_F_L7_HTTP | PCPPX_F_L7_DNS)) ? 7u : l7_min_osi(l7_tcp, sp, dp, sip);
+			if (osi > prm.until_osi || (found && prm.fam_engine_only))
+				lf = 0;
+		}
 		if (lf)
 		{
 			flags |= lf;

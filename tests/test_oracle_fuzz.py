@@ -15,7 +15,9 @@ from pcapplusplus_amd import abi
 pytestmark = pytest.mark.skipif(not oracle.ref_available(), reason="reference library not built")
 
 OPTS = [abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 3, True, 16),
-        abi.make_opts(0x203, 8, True, 4), abi.make_opts(0, 8, True, 0)]
+        abi.make_opts(0x203, 8, True, 4), abi.make_opts(0, 8, True, 0), abi.make_opts(0, 4, True, 16),
+        abi.make_opts(0, 5, True, 16), abi.make_opts(0, 6, True, 16), abi.make_opts(5, 8, True, 16),
+        abi.make_opts(0x607, 8, True, 16)]
 
 
 def _seed_packets():
@@ -50,7 +52,7 @@ def test_crafted_l7_payloads_vs_reference(opt_i):
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_mutations_vs_reference(seed):
     b = as_batch(mutate(_seed_packets(), 6000, seed), gaps=True, seed=seed)
-    for opts in OPTS[:3]:
+    for opts in OPTS[:3] + OPTS[5:]:
         rs, rl = oracle.ref_parse(b, opts)
         os_, ol = oracle.oracle_parse(b, opts)
         oracle.compare_engine_to_reference(os_, ol, rs, rl)
