@@ -1,14 +1,24 @@
-// benchmark.cpp — the PcapPlusPlus benchmark application's packet mode
-// (Examples/PcapPlusPlus-benchmark/benchmark.cpp:60-115) on the engine.
-//
-//   benchmark <input-file> packet <repetitions>
-//
-// Each repetition reads the whole capture and parses every packet until TCP (Packet(&raw, pcpp::TCP),
-// benchmark.cpp:91) and counts it (handle_packet, :54-58); the output line is the reference's:
-// "<packets per run> <average ms per run>". The parse runs on the GPU in batches of up to 1M packets.
-// The reference's dns mode needs DnsLayer (L7, out of this path's scope) and is not offered.
+/**
+ * PcapPlusPlus benchmark application on the GPU parse engine
+ * ==========================================================
+ * The reference application (Examples/PcapPlusPlus-benchmark/benchmark.cpp:60-109), with one change: instead of
+ * reading one RawPacket and building one Packet at a time, the reader fills a batch (getNextPackets, the reference's
+ * IFileReaderDevice batch read) and the engine parses the whole batch on the GPU (the batch prepass). The
+ * per-packet handler then runs over Packet views with pcpp::Packet's names, as before.
+ *
+ *   benchmark <input-file> packet <repetitions> [--host-parser <lib.so>] [--dump]
+ *
+ * Output: "<packets per run> <average ms per run>", as the reference. The reference's dns mode iterates DnsLayer's
+ * queries and answers, an L7 dissector outside the engine: it is refused. Packets the engine leaves to the host
+ * (an L7 layer it does not dissect) are completed by the caller's own Packet++ parse when --host-parser names a
+ * library exporting `pcppx_host_parse` (include/pcppx.h, pcppx_host_parse_fn). --dump also prints every
+ * packet's layer list and hash5Tuple (used by the tests to compare with the reference).
+ */
+#include <dlfcn.h>
+
 #include <chrono>
-#include <cstdlib>
+#include <cinttypes>
+#include <cstdio>
 #include <iostream>
 #include <numeric>
 #include <string>
@@ -16,60 +26,122 @@
 
 #include "pcppx.hpp"
 
+using namespace pcppx;
+
+size_t count = 0;
+
+bool handle_packet(Packet& packet)
+{
+	(void)packet;
+	count++;
+	return true;
+}
+
+namespace
+{
+// --dump: "<index> <n_layers> <proto>:<offset>:<hdr_len>:<data_len> ... h5=<hash5Tuple> h5d=<dir> h2=<hash2Tuple>"
+void dump(size_t index, const Packet& packet)
+{
+	std::printf("%zu %zu", index, packet.getLayerCount());
+	for (size_t k = 0; k < packet.getRecordedLayerCount(); ++k)
+	{
+		const Layer l = packet.getLayer(k);
+		std::printf(" %u:%u:%zu:%zu", l.getProtocol(), l.getOffset(), l.getHeaderLen(), l.getDataLen());
+	}
+	std::printf(" h5=%" PRIu32 " h5d=%" PRIu32 " h2=%" PRIu32 " host=%d\n", hash5Tuple(&packet),
+	            hash5Tuple(&packet, true), hash2Tuple(&packet), packet.wasHostParsed() ? 1 : 0);
+}
+
+pcppx_host_parse_fn loadHostParser(const std::string& path)
+{
+	void* lib = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+	if (lib == nullptr)
+		throw Error(PCPPX_E_INVAL, std::string("dlopen: ") + dlerror());
+	auto fn = reinterpret_cast<pcppx_host_parse_fn>(dlsym(lib, "pcppx_host_parse"));
+	if (fn == nullptr)
+		throw Error(PCPPX_E_INVAL, path + " does not export pcppx_host_parse");
+	return fn;
+}
+}  // namespace
+
 int main(int argc, char* argv[])
 {
-	if (argc != 4)
+	if (argc < 4)
 	{
-		std::cout << "Usage: " << *argv << " <input-file> <packet> <repetitions>\n";
+		std::cout << "Usage: " << *argv << " <input-file> packet <repetitions> [--host-parser <lib.so>] [--dump]\n";
 		return 1;
 	}
-	const std::string input_type(argv[2]);
+	std::string input_type(argv[2]);
 	if (input_type != "packet")
 	{
-		std::cerr << "only packet mode is supported (dns mode parses L7)\n";
+		// dns mode walks DnsLayer's queries and answers (benchmark.cpp:30-52): an L7 dissector, left to Packet++
+		std::cerr << "only packet mode runs on the engine: dns mode iterates DnsLayer resources (L7)\n";
 		return 1;
 	}
-	const int total_runs = std::stoi(argv[3]);
+	int total_runs = std::stoi(argv[3]);
+	std::string hostParser;
+	bool dumpPackets = false;
+	for (int k = 4; k < argc; ++k)
+	{
+		const std::string a = argv[k];
+		if (a == "--host-parser" && k + 1 < argc)
+			hostParser = argv[++k];
+		else if (a == "--dump")
+			dumpPackets = true;
+		else
+		{
+			std::cout << "Usage: " << *argv << " <input-file> packet <repetitions> [--host-parser <lib.so>] [--dump]\n";
+			return 1;
+		}
+	}
 	size_t total_packets = 0;
 	std::vector<std::chrono::high_resolution_clock::duration> durations;
 	try
 	{
-		pcppx::Engine engine(0);
-		pcppx::PacketParseOptions options(pcppx::TCP);
-		options.computeChecksums = false;  // Packet(&raw, TCP) parses layers only
-		options.maxLayers = 8;
-		pcppx::RawBatch batch;
+		Engine engine(0);
+		if (!hostParser.empty())
+			engine.setHostParser(loadHostParser(hostParser));
+		RawPacketVector batch;
 		for (int i = 0; i < total_runs; ++i)
 		{
-			size_t count = 0;
-			pcppx::PcapFileReaderDevice reader(argv[1]);
-			if (!reader.open())
+			count = 0;
+			size_t index = 0;
+			PcapFileReaderDevice reader(argv[1]);
+			reader.open();
+			std::chrono::high_resolution_clock::time_point start;
 			{
-				std::cerr << "cannot open " << argv[1] << "\n";
-				return 1;
+				start = std::chrono::high_resolution_clock::now();
+				PacketParseOptions options(TCP);  // Packet(&rawPacket, pcpp::TCP)
+				options.computeChecksums = false;
+				while (reader.getNextPackets(batch, 1 << 20) > 0)
+				{
+					ParsedBatch parsed = engine.parse(batch, options);  // the batch prepass
+					for (Packet packet : parsed)
+					{
+						handle_packet(packet);
+						if (dumpPackets && i == 0)
+							dump(index, packet);
+						++index;
+					}
+				}
 			}
-			const auto start = std::chrono::high_resolution_clock::now();
-			while (reader.getNextPackets(batch, 1u << 20) > 0)
-			{
-				pcppx::ParsedBatch parsed = engine.parse(batch, options);
-				count += parsed.size();  // handle_packet: count++
-			}
-			const auto end = std::chrono::high_resolution_clock::now();
+			auto end = std::chrono::high_resolution_clock::now();
 			durations.push_back(end - start);
 			total_packets += count;
 			reader.close();
 		}
 	}
-	catch (const pcppx::Error& e)
+	catch (const Error& e)
 	{
 		std::cerr << e.what() << "\n";
 		return 2;
 	}
-	const auto total_time =
+	auto total_time =
 	    std::accumulate(durations.begin(), durations.end(), std::chrono::high_resolution_clock::duration(0));
+
 	using std::chrono::duration_cast;
 	using std::chrono::milliseconds;
-	const auto total_time_in_ms = duration_cast<milliseconds>(total_time).count();
+	auto total_time_in_ms = duration_cast<milliseconds>(total_time).count();
 	std::cout << (total_packets / total_runs) << " " << (total_time_in_ms / durations.size()) << std::endl;
 	return 0;
 }

@@ -1,99 +1,347 @@
-// filter_traffic.cpp — DpdkExample-FilterTraffic's worker (AppWorkerThread.h:85-139) over a pcap file, on
-// the GPU. Packets are matched with PacketMatchingEngine's criteria (PacketMatchingEngine.h:43-107); once
-// a packet of a 5-tuple flow matches, every later packet of that flow matches too (the worker's flow table
-// keyed by hash5Tuple). Matched packets are written to an output pcap (the worker's
-// writeMatchedPacketsToFile, AppWorkerThread.h:68-75,127-131); the statistics are printed as
-// main.cpp:244-264 prints them. The input file replaces the DPDK RX queues.
-//
-//   filter_traffic -f in.pcap [-o out.pcap] [-s SRC_IP] [-d DST_IP] [-S SRC_PORT] [-D DST_PORT] [-P TCP|UDP]
+/**
+ * DpdkExample-FilterTraffic's worker on the GPU parse engine
+ * ==========================================================
+ * The reference worker (Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:45-162, PacketStats Common.h:57-142,
+ * PacketMatchingEngine.h:43-107, the stats table main.cpp:244-264) with a pcap file in place of the DPDK RX queues
+ * and one change: each received burst is parsed by the engine in one batch (the batch prepass), and the per-packet
+ * loop - collectStats, hash5Tuple, the flow table, isMatched, the pcap writer - runs as before over Packet views
+ * with pcpp::Packet's names. Packets the engine leaves to the host are completed by the caller's own Packet++
+ * parse (--host-parser <lib.so> exporting pcppx_host_parse), so every counter, HTTP/DNS/TLS included, is the
+ * reference's.
+ *
+ * --device-worker runs the whole worker on the GPU instead (pcppx_filter_batch_host: flow table, matching and
+ * statistics in HBM); its HTTP/DNS/TLS counters cover the packets the device settles ("left to host" counts the
+ * rest).
+ *
+ *   filter_traffic -f in.pcap [-o out.pcap] [-s SRC_IP] [-d DST_IP] [-S SRC_PORT] [-D DST_PORT] [-P TCP|UDP]
+ *                  [-b BURST] [--host-parser <lib.so>] [--device-worker]
+ */
+#include <dlfcn.h>
+
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
 #include <iomanip>
 #include <iostream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "pcppx.hpp"
 
 namespace
 {
-void usage(const char* argv0)
+/* PacketStats (Common.h:57-142) */
+struct PacketStats
 {
-	std::cout << "Usage: " << argv0
-	          << " -f <in.pcap> [-o <out.pcap>] [-s <src ip>] [-d <dst ip>] [-S <src port>] [-D <dst port>]"
-	             " [-P <TCP|UDP>]\n";
-}
+	uint64_t packetCount = 0, ethCount = 0, arpCount = 0, ipv4Count = 0, ipv6Count = 0, tcpCount = 0, udpCount = 0,
+	         httpCount = 0, dnsCount = 0, tlsCount = 0;
+	uint64_t matchedTcpFlows = 0, matchedUdpFlows = 0, matchedPackets = 0;
+	uint64_t leftToHost = 0; /* packets a counter of which the device could not settle (device worker only) */
 
-void row(const std::string& name, uint64_t v)
-{
-	std::cout << "| " << std::left << std::setw(22) << name << "| " << std::right << std::setw(12) << v << " |\n";
-}
-
-// PacketStats table (main.cpp:244-264). HTTP/DNS/TLS are L7 and counted by the host for packets flagged
-// PCPPX_F_NEEDS_HOST_L7; this tool reports the flagged count instead.
-void printStats(const pcppx_packet_stats& s)
-{
-	std::cout << "+------------------------------------------+\n";
-	row("Eth count", s.eth_count);
-	row("ARP count", s.arp_count);
-	row("IPv4 count", s.ipv4_count);
-	row("IPv6 count", s.ipv6_count);
-	row("TCP count", s.tcp_count);
-	row("UDP count", s.udp_count);
-	row("left to host", s.needs_host_count);
-	row("Matched TCP flows", s.matched_tcp_flows);
-	row("Matched UDP flows", s.matched_udp_flows);
-	row("Total packet count", s.packet_count);
-	row("Matched packet count", s.matched_packets);
-	std::cout << "+------------------------------------------+\n";
-}
-
-struct PcapWriter
-{
-	FILE* f = nullptr;
-	bool open(const std::string& path, uint32_t linktype)
+	void collectStats(const pcppx::Packet& packet)
 	{
-		f = std::fopen(path.c_str(), "wb");
-		if (f == nullptr)
-			return false;
-		const uint32_t magic = 0xa1b2c3d4, snap = 262144;
-		const uint16_t vmaj = 2, vmin = 4;
-		const int32_t zone = 0;
-		const uint32_t sig = 0;
-		std::fwrite(&magic, 4, 1, f);
-		std::fwrite(&vmaj, 2, 1, f);
-		std::fwrite(&vmin, 2, 1, f);
-		std::fwrite(&zone, 4, 1, f);
-		std::fwrite(&sig, 4, 1, f);
-		std::fwrite(&snap, 4, 1, f);
-		std::fwrite(&linktype, 4, 1, f);
+		packetCount++;
+		if (packet.isPacketOfType(pcppx::Ethernet))
+			ethCount++;
+		if (packet.isPacketOfType(pcppx::ARP))
+			arpCount++;
+		if (packet.isPacketOfType(pcppx::IPv4))
+			ipv4Count++;
+		if (packet.isPacketOfType(pcppx::IPv6))
+			ipv6Count++;
+		if (packet.isPacketOfType(pcppx::TCP))
+			tcpCount++;
+		if (packet.isPacketOfType(pcppx::UDP))
+			udpCount++;
+		if (packet.isPacketOfType(pcppx::HTTP))
+			httpCount++;
+		if (packet.isPacketOfType(pcppx::DNS))
+			dnsCount++;
+		if (packet.isPacketOfType(pcppx::SSL))
+			tlsCount++;
+		if (packet.needsHost())
+			leftToHost++;
+	}
+};
+
+/* PacketMatchingEngine (PacketMatchingEngine.h:15-107): source / destination IPv4, ports, TCP|UDP */
+class PacketMatchingEngine
+{
+public:
+	PacketMatchingEngine(const pcppx::IPv4Address& srcIp, const pcppx::IPv4Address& dstIp, uint16_t srcPort,
+	                     uint16_t dstPort, pcppx::ProtocolType protocol)
+	    : m_SrcIp(srcIp), m_DstIp(dstIp), m_SrcPort(srcPort), m_DstPort(dstPort), m_Protocol(protocol),
+	      m_MatchSrcIp(srcIp != pcppx::IPv4Address::Zero), m_MatchDstIp(dstIp != pcppx::IPv4Address::Zero),
+	      m_MatchSrcPort(srcPort != 0), m_MatchDstPort(dstPort != 0),
+	      m_MatchProtocol(protocol == pcppx::TCP || protocol == pcppx::UDP)
+	{}
+
+	bool isMatched(const pcppx::Packet& packet) const
+	{
+		if (m_MatchSrcIp || m_MatchDstIp)
+		{
+			if (!packet.isPacketOfType(pcppx::IPv4))
+				return false;
+			auto ip4Layer = packet.getLayerOfType<pcppx::IPv4Layer>();
+			if (m_MatchSrcIp && ip4Layer->getSrcIPv4Address() != m_SrcIp)
+				return false;
+			if (m_MatchDstIp && ip4Layer->getDstIPv4Address() != m_DstIp)
+				return false;
+		}
+		if (m_MatchSrcPort || m_MatchDstPort)
+		{
+			uint16_t srcPort, dstPort;
+			if (packet.isPacketOfType(pcppx::TCP))
+			{
+				srcPort = packet.getLayerOfType<pcppx::TcpLayer>()->getSrcPort();
+				dstPort = packet.getLayerOfType<pcppx::TcpLayer>()->getDstPort();
+			}
+			else if (packet.isPacketOfType(pcppx::UDP))
+			{
+				srcPort = packet.getLayerOfType<pcppx::UdpLayer>()->getSrcPort();
+				dstPort = packet.getLayerOfType<pcppx::UdpLayer>()->getDstPort();
+			}
+			else
+				return false;
+			if (m_MatchSrcPort && srcPort != m_SrcPort)
+				return false;
+			if (m_MatchDstPort && dstPort != m_DstPort)
+				return false;
+		}
+		if (m_MatchProtocol)
+		{
+			if (m_Protocol == pcppx::TCP && !packet.isPacketOfType(pcppx::TCP))
+				return false;
+			if (m_Protocol == pcppx::UDP && !packet.isPacketOfType(pcppx::UDP))
+				return false;
+		}
 		return true;
 	}
-	void write(const pcppx::RawBatch& b, size_t i)
+
+	pcppx::MatchSpec spec() const
+	{
+		pcppx::MatchSpec s;
+		s.spec.src_ip = m_SrcIp.toInt();
+		s.spec.dst_ip = m_DstIp.toInt();
+		s.spec.src_port = m_SrcPort;
+		s.spec.dst_port = m_DstPort;
+		s.spec.protocol = m_Protocol;
+		return s;
+	}
+
+private:
+	pcppx::IPv4Address m_SrcIp, m_DstIp;
+	uint16_t m_SrcPort, m_DstPort;
+	pcppx::ProtocolType m_Protocol;
+	bool m_MatchSrcIp, m_MatchDstIp, m_MatchSrcPort, m_MatchDstPort, m_MatchProtocol;
+};
+
+/* PcapFileWriterDevice (Pcap++/header/PcapFileDevice.h): classic pcap, microsecond timestamps */
+class PcapFileWriterDevice
+{
+public:
+	PcapFileWriterDevice(const std::string& path, uint32_t linkType) : m_Path(path), m_LinkType(linkType) {}
+	~PcapFileWriterDevice()
+	{
+		if (m_F)
+			std::fclose(m_F);
+	}
+	bool open()
+	{
+		m_F = std::fopen(m_Path.c_str(), "wb");
+		if (m_F == nullptr)
+			return false;
+		const uint32_t hdr[6] = { 0xa1b2c3d4u, 2u | (4u << 16), 0, 0, 262144, m_LinkType };
+		return std::fwrite(hdr, 4, 6, m_F) == 6;
+	}
+	void writePacket(const pcppx::RawPacketVector& b, size_t i)
 	{
 		const uint64_t ts = b.timestampsNs[i];
 		const uint32_t h[4] = { (uint32_t)(ts / 1000000000ull), (uint32_t)(ts % 1000000000ull / 1000ull), b.caplens[i],
 			                    b.caplens[i] };
-		std::fwrite(h, 4, 4, f);
-		std::fwrite(b.packetData(i), 1, b.caplens[i], f);
+		std::fwrite(h, 4, 4, m_F);
+		std::fwrite(b.packetData(i), 1, b.caplens[i], m_F);
 	}
-	~PcapWriter()
-	{
-		if (f)
-			std::fclose(f);
-	}
+
+private:
+	std::string m_Path;
+	uint32_t m_LinkType;
+	FILE* m_F = nullptr;
 };
+
+/* the worker (AppWorkerThread.h:45-162): the input file replaces the DPDK RX queues */
+class AppWorkerThread
+{
+public:
+	AppWorkerThread(pcppx::Engine& engine, const PacketMatchingEngine& matchingEngine, size_t burst)
+	    : m_Engine(engine), m_PacketMatchingEngine(matchingEngine), m_Burst(burst)
+	{}
+	PacketStats& getStats() { return m_Stats; }
+
+	bool run(pcppx::PcapFileReaderDevice& reader, PcapFileWriterDevice* pcapWriter)
+	{
+		pcppx::RawPacketVector packetArr;
+		pcppx::PacketParseOptions options;  // pcpp::Packet parsedPacket(rawPacket): full parse
+		options.computeChecksums = false;
+		// receive a burst (was dev->receivePackets(packetArr, MAX_RECEIVE_BURST, rxQueue), AppWorkerThread.h:85)
+		while (reader.getNextPackets(packetArr, (int)m_Burst) > 0)
+		{
+			pcppx::ParsedBatch parsed = m_Engine.parse(packetArr, options);  // the batch prepass
+			for (size_t i = 0; i < parsed.size(); i++)
+			{
+				// parse packet
+				pcppx::Packet parsedPacket = parsed[i];
+
+				// collect packet statistics
+				m_Stats.collectStats(parsedPacket);
+
+				bool packetMatched;
+
+				// hash the packet by 5-tuple and look in the flow table to see whether this packet belongs to an
+				// existing or new flow
+				uint32_t hash = pcppx::hash5Tuple(&parsedPacket);
+				auto iter3 = m_FlowTable.find(hash);
+
+				// if packet belongs to an already existing flow
+				if (iter3 != m_FlowTable.end() && iter3->second)
+					packetMatched = true;
+				else  // packet belongs to a new flow
+				{
+					packetMatched = m_PacketMatchingEngine.isMatched(parsedPacket);
+					if (packetMatched)
+					{
+						// put new flow in flow table
+						m_FlowTable[hash] = true;
+
+						// collect stats
+						if (parsedPacket.isPacketOfType(pcppx::TCP))
+							m_Stats.matchedTcpFlows++;
+						else if (parsedPacket.isPacketOfType(pcppx::UDP))
+							m_Stats.matchedUdpFlows++;
+					}
+				}
+
+				if (packetMatched)
+				{
+					// save packet to file if needed
+					if (pcapWriter != nullptr)
+						pcapWriter->writePacket(packetArr, i);
+					m_Stats.matchedPackets++;
+				}
+			}
+		}
+		return true;
+	}
+
+	/* the whole worker on the GPU: flow table, matching and statistics in HBM (pcppx_filter_batch_host) */
+	bool runOnDevice(pcppx::PcapFileReaderDevice& reader, PcapFileWriterDevice* pcapWriter)
+	{
+		pcppx::RawPacketVector packetArr;
+		std::vector<uint8_t> matched;
+		pcppx_packet_stats s{};
+		m_Engine.resetFilter();
+		const pcppx::MatchSpec spec = m_PacketMatchingEngine.spec();
+		while (reader.getNextPackets(packetArr, (int)m_Burst) > 0)
+		{
+			s = m_Engine.filter(packetArr, spec, matched);
+			if (pcapWriter != nullptr)
+				for (size_t i = 0; i < packetArr.size(); ++i)
+					if (matched[i])
+						pcapWriter->writePacket(packetArr, i);
+		}
+		m_Stats.packetCount = s.packet_count;
+		m_Stats.ethCount = s.eth_count;
+		m_Stats.arpCount = s.arp_count;
+		m_Stats.ipv4Count = s.ipv4_count;
+		m_Stats.ipv6Count = s.ipv6_count;
+		m_Stats.tcpCount = s.tcp_count;
+		m_Stats.udpCount = s.udp_count;
+		m_Stats.httpCount = s.http_count;
+		m_Stats.dnsCount = s.dns_count;
+		m_Stats.tlsCount = s.tls_count;
+		m_Stats.matchedTcpFlows = s.matched_tcp_flows;
+		m_Stats.matchedUdpFlows = s.matched_udp_flows;
+		m_Stats.matchedPackets = s.matched_packets;
+		m_Stats.leftToHost = s.needs_host_count;
+		return true;
+	}
+
+private:
+	pcppx::Engine& m_Engine;
+	const PacketMatchingEngine& m_PacketMatchingEngine;
+	size_t m_Burst;
+	PacketStats m_Stats;
+	std::unordered_map<uint32_t, bool> m_FlowTable;
+};
+
+void printRow(const std::string& name, uint64_t v)
+{
+	std::cout << "| " << std::left << std::setw(21) << name << "| " << std::right << std::setw(10) << v << " |\n";
+}
+void printSeparator()
+{
+	std::cout << "+----------------------+-----------+\n";
+}
+/* printStats (main.cpp:244-264) */
+void printStats(const PacketStats& threadStats, const std::string& columnName)
+{
+	printSeparator();
+	std::cout << "| " << std::left << std::setw(21) << columnName << "| " << std::right << std::setw(10) << "Count"
+	          << " |\n";
+	printSeparator();
+	printRow("Eth count", threadStats.ethCount);
+	printRow("ARP count", threadStats.arpCount);
+	printRow("IPv4 count", threadStats.ipv4Count);
+	printRow("IPv6 count", threadStats.ipv6Count);
+	printRow("TCP count", threadStats.tcpCount);
+	printRow("UDP count", threadStats.udpCount);
+	printRow("HTTP count", threadStats.httpCount);
+	printRow("DNS count", threadStats.dnsCount);
+	printRow("TLS count", threadStats.tlsCount);
+	printSeparator();
+	printRow("Matched TCP flows", threadStats.matchedTcpFlows);
+	printRow("Matched UDP flows", threadStats.matchedUdpFlows);
+	printSeparator();
+	printRow("Matched packet count", threadStats.matchedPackets);
+	printRow("Total packet count", threadStats.packetCount);
+	printRow("Left to host", threadStats.leftToHost);
+	printSeparator();
+}
+
+void usage(const char* argv0)
+{
+	std::cout << "Usage: " << argv0
+	          << " -f <in.pcap> [-o <out.pcap>] [-s <src ip>] [-d <dst ip>] [-S <src port>] [-D <dst port>]"
+	             " [-P <TCP|UDP>] [-b <burst>] [--host-parser <lib.so>] [--device-worker]\n";
+}
+
+pcppx_host_parse_fn loadHostParser(const std::string& path)
+{
+	void* lib = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+	if (lib == nullptr)
+		throw pcppx::Error(PCPPX_E_INVAL, std::string("dlopen: ") + dlerror());
+	auto fn = reinterpret_cast<pcppx_host_parse_fn>(dlsym(lib, "pcppx_host_parse"));
+	if (fn == nullptr)
+		throw pcppx::Error(PCPPX_E_INVAL, path + " does not export pcppx_host_parse");
+	return fn;
+}
 }  // namespace
 
 int main(int argc, char* argv[])
 {
-	std::string in, out, sip, dip;
+	std::string in, out, sip, dip, hostParser;
 	uint16_t sport = 0, dport = 0;
+	size_t burst = 1u << 20;
+	bool deviceWorker = false;
 	pcppx::ProtocolType proto = pcppx::UnknownProtocol;
 	for (int k = 1; k < argc; ++k)
 	{
 		const std::string a = argv[k];
+		if (a == "--device-worker")
+		{
+			deviceWorker = true;
+			continue;
+		}
 		if (k + 1 >= argc)
 		{
 			usage(argv[0]);
@@ -106,6 +354,8 @@ int main(int argc, char* argv[])
 		else if (a == "-d") dip = v;
 		else if (a == "-S") sport = (uint16_t)std::atoi(v.c_str());
 		else if (a == "-D") dport = (uint16_t)std::atoi(v.c_str());
+		else if (a == "-b") burst = (size_t)std::atol(v.c_str());
+		else if (a == "--host-parser") hostParser = v;
 		else if (a == "-P")
 		{
 			if (v == "TCP") proto = pcppx::TCP;
@@ -122,40 +372,42 @@ int main(int argc, char* argv[])
 			return 1;
 		}
 	}
-	if (in.empty())
+	if (in.empty() || burst == 0)
 	{
 		usage(argv[0]);
 		return 1;
 	}
 	try
 	{
-		const pcppx::MatchSpec spec(sip, dip, sport, dport, proto);
+		const PacketMatchingEngine matchingEngine(sip.empty() ? pcppx::IPv4Address::Zero : pcppx::IPv4Address(sip),
+		                                          dip.empty() ? pcppx::IPv4Address::Zero : pcppx::IPv4Address(dip),
+		                                          sport, dport, proto);
 		pcppx::Engine engine(0);
-		engine.resetFilter();
+		if (!hostParser.empty())
+			engine.setHostParser(loadHostParser(hostParser));
 		pcppx::PcapFileReaderDevice reader(in);
 		if (!reader.open())
 		{
 			std::cerr << "cannot open " << in << "\n";
 			return 1;
 		}
-		PcapWriter writer;
-		if (!out.empty() && !writer.open(out, reader.getLinkLayerType()))
+		PcapFileWriterDevice* pcapWriter = nullptr;
+		if (!out.empty())
 		{
-			std::cerr << "cannot create " << out << "\n";
-			return 1;
+			pcapWriter = new PcapFileWriterDevice(out, reader.getLinkLayerType());
+			if (!pcapWriter->open())
+			{
+				std::cerr << "Couldn't open pcap writer device\n";
+				return 1;
+			}
 		}
-		pcppx::RawBatch batch;
-		std::vector<uint8_t> matched;
-		pcppx_packet_stats stats{};
-		while (reader.getNextPackets(batch, 1u << 20) > 0)
-		{
-			stats = engine.filter(batch, spec, matched);
-			if (writer.f)
-				for (size_t i = 0; i < batch.size(); ++i)
-					if (matched[i])
-						writer.write(batch, i);
-		}
-		printStats(stats);
+		AppWorkerThread worker(engine, matchingEngine, burst);
+		if (deviceWorker)
+			worker.runOnDevice(reader, pcapWriter);
+		else
+			worker.run(reader, pcapWriter);
+		delete pcapWriter;
+		printStats(worker.getStats(), deviceWorker ? "GPU worker" : "Worker");
 	}
 	catch (const pcppx::Error& e)
 	{

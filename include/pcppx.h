@@ -125,6 +125,15 @@ typedef struct pcppx_records {
 	pcppx_layer* layers;    /* n * max_layers entries, or NULL when max_layers == 0 */
 } pcppx_records;
 
+/* The caller's own host parse of ONE packet — its Packet++ (`pcpp::Packet packet(&raw, parseUntil...)`) turned
+ * into this engine's records: summary + up to opts->max_layers layers, as the engine would write them had it
+ * finished the chain. The engine never calls it and libpcppx.so never links Packet++: the C++ facade
+ * (pcppx.hpp, Engine::setHostParser) calls it for packets flagged PCPPX_F_NEEDS_HOST, so that a caller's
+ * per-packet loop sees every packet completely. INTEGRATION.md §2 has an implementation over pcpp::Packet.
+ * Returns 0 or a negative PCPPX_E_* code. */
+typedef int (*pcppx_host_parse_fn)(const uint8_t* packet, uint32_t caplen, uint16_t linktype, const pcppx_opts* opts,
+                                   pcppx_summary* summary, pcppx_layer* layers);
+
 typedef struct pcppx_ctx pcppx_ctx;
 
 /* library / device management */

@@ -1,20 +1,32 @@
-/* pcppx.hpp — a Packet++-shaped C++ view over the engine's C ABI (pcppx.h). Header-only, no HIP types.
+/* pcppx.hpp — the Packet++-shaped C++ facade over the engine's C ABI (pcppx.h). Header-only, no HIP types, no
+ * Packet++ dependency.
  *
- * Callers of the reference write `pcpp::Packet packet(&rawPacket, parseUntil); packet.isPacketOfType(TCP);
- * pcpp::hash5Tuple(&packet)` per packet (Packet++/header/Packet.h:17-37, :107-116, :271-282;
- * Packet++/header/PacketUtils.h:80-91). Here a whole batch is parsed by one call and each packet is a
- * ParsedPacket view with the same names over the batch's records:
+ * A reference caller writes, per packet (Examples/PcapPlusPlus-benchmark/benchmark.cpp:89-95,
+ * Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:85-139):
  *
- *   pcppx::PcapFileReaderDevice reader("in.pcap");           // Pcap++/header/PcapFileDevice.h
- *   pcppx::RawBatch batch;
- *   pcppx::Engine engine(0);                                 // one GPU = one worker
- *   while (reader.getNextPackets(batch, 1 << 20) > 0) {
- *       pcppx::ParsedBatch parsed = engine.parse(batch, pcppx::PacketParseOptions{pcppx::TCP});
- *       for (size_t i = 0; i < parsed.size(); ++i) {
- *           pcppx::ParsedPacket p = parsed[i];
- *           if (p.isPacketOfType(pcppx::TCP)) flows[p.hash5Tuple()]++;
- *       }
+ *   pcpp::RawPacket rawPacket;
+ *   while (reader.getNextPacket(rawPacket)) {
+ *       pcpp::Packet packet(&rawPacket, pcpp::TCP);              // Packet++/src/Packet.cpp:202-209
+ *       if (packet.isPacketOfType(pcpp::TCP)) flows[pcpp::hash5Tuple(&packet)]++;
  *   }
+ *
+ * With the engine the only change is a batch prepass: the reader fills a RawPacketVector, one call parses the
+ * whole batch on the GPU, and the per-packet loop runs unchanged over pcppx::Packet views with the same names
+ * (isPacketOfType, getLayerOfType<IPv4Layer/TcpLayer/UdpLayer>, getFirstLayer, hash5Tuple(&packet), ...):
+ *
+ *   pcppx::Engine engine(0);
+ *   engine.setHostParser(myPacketPlusPlusParse);                  // optional, see below
+ *   pcppx::RawPacketVector batch;
+ *   while (reader.getNextPackets(batch, 1 << 20) > 0) {
+ *       pcppx::ParsedBatch parsed = engine.parse(batch, pcppx::PacketParseOptions(pcppx::TCP));
+ *       for (pcppx::Packet packet : parsed)
+ *           if (packet.isPacketOfType(pcppx::TCP)) flows[pcppx::hash5Tuple(&packet)]++;
+ *   }
+ *
+ * Packets the engine leaves to the host (PCPPX_F_NEEDS_HOST: an L7 dissector, an out-of-scope L2/L3 layer) carry
+ * an exact layer prefix. A caller that registers a host parser (pcppx_host_parse_fn: its own Packet++ parse of one
+ * packet) gets them completed inside Engine::parse, so every Packet view answers as
+ * pcpp::Packet would; without one, needsHost() reports them. libpcppx.so never links Packet++.
  *
  * Errors are reported as pcppx::Error (a std::runtime_error carrying the PCPPX_E_* code).
  */
@@ -32,13 +44,13 @@
 
 namespace pcppx
 {
-/* ProtocolType / ProtocolTypeFamily / OsiModelLayer values of Packet++/header/ProtocolType.h */
+/* ProtocolType / ProtocolTypeFamily / OsiModelLayer values of Packet++/header/ProtocolType.h:42-284 */
 using ProtocolType = uint8_t;
 using ProtocolTypeFamily = uint32_t;
-constexpr ProtocolType UnknownProtocol = 0, Ethernet = 1, IPv4 = 2, IPv6 = 3, TCP = 4, UDP = 5, ARP = 8, VLAN = 9,
-                       MPLS = 14, GREv0 = 15, GREv1 = 16, PPP_PPTP = 17, GenericPayload = 25, PacketTrailer = 30,
-                       EthernetDot3 = 33, LLC = 44;
-constexpr ProtocolTypeFamily IP = 0x203, GRE = 0xf10;
+constexpr ProtocolType UnknownProtocol = 0, Ethernet = 1, IPv4 = 2, IPv6 = 3, TCP = 4, UDP = 5, HTTPRequest = 6,
+                       HTTPResponse = 7, ARP = 8, VLAN = 9, ICMP = 10, DNS = 13, MPLS = 14, GREv0 = 15, GREv1 = 16,
+                       PPP_PPTP = 17, SSL = 18, GenericPayload = 25, PacketTrailer = 30, EthernetDot3 = 33, LLC = 44;
+constexpr ProtocolTypeFamily IP = 0x203, GRE = 0xf10, HTTP = 0x607;
 enum OsiModelLayer : uint8_t
 {
 	OsiModelPhysicalLayer = 1,
@@ -50,6 +62,9 @@ enum OsiModelLayer : uint8_t
 	OsiModelApplicationLayer = 7,
 	OsiModelLayerUnknown = 8
 };
+
+/* facade-level summary flag: the records were filled by the caller's host parser (Engine::setHostParser) */
+constexpr uint16_t F_HOST_PARSED = 0x4000;
 
 class Error : public std::runtime_error
 {
@@ -66,6 +81,40 @@ inline void check(int rc, const char* what)
 	if (rc != PCPPX_OK)
 		throw Error(rc, what);
 }
+
+/* pcpp::IPv4Address (Common++/header/IpAddress.h:37-40): the four bytes in memory order */
+class IPv4Address
+{
+public:
+	IPv4Address() = default;
+	explicit IPv4Address(uint32_t addrAsInt) : m_Int(addrAsInt) {}
+	explicit IPv4Address(const std::string& dotted)
+	{
+		unsigned v[4];
+		char tail;
+		if (std::sscanf(dotted.c_str(), "%u.%u.%u.%u%c", &v[0], &v[1], &v[2], &v[3], &tail) != 4 || v[0] > 255 ||
+		    v[1] > 255 || v[2] > 255 || v[3] > 255)
+			throw Error(PCPPX_E_INVAL, "bad IPv4 address '" + dotted + "'");
+		const uint8_t b[4] = { (uint8_t)v[0], (uint8_t)v[1], (uint8_t)v[2], (uint8_t)v[3] };
+		std::memcpy(&m_Int, b, 4);
+	}
+	uint32_t toInt() const { return m_Int; }
+	std::string toString() const
+	{
+		uint8_t b[4];
+		std::memcpy(b, &m_Int, 4);
+		char s[16];
+		std::snprintf(s, sizeof(s), "%u.%u.%u.%u", b[0], b[1], b[2], b[3]);
+		return s;
+	}
+	bool operator==(const IPv4Address& o) const { return m_Int == o.m_Int; }
+	bool operator!=(const IPv4Address& o) const { return m_Int != o.m_Int; }
+	static const IPv4Address Zero;
+
+private:
+	uint32_t m_Int = 0;
+};
+inline const IPv4Address IPv4Address::Zero{};
 
 /* PacketParseOptions (Packet++/header/Packet.h:17-37) plus the engine's record options */
 struct PacketParseOptions
@@ -92,8 +141,9 @@ struct PacketParseOptions
 	}
 };
 
-/* Packets back to back in one buffer: packet i = data[offsets[i], offsets[i] + caplens[i]). */
-struct RawBatch
+/* A batch of raw packets back to back in one buffer: packet i = data[offsets[i], offsets[i] + caplens[i]).
+ * Plays the role of pcpp::RawPacketVector (Packet++/header/RawPacket.h) for the batch prepass. */
+struct RawPacketVector
 {
 	std::vector<uint8_t> data;
 	std::vector<uint64_t> offsets;
@@ -109,7 +159,7 @@ struct RawBatch
 		caplens.clear();
 		timestampsNs.clear();
 	}
-	/* RawPacket-style append (RawPacket::setRawData, Packet++/header/RawPacket.h) */
+	/* RawPacket::setRawData-style append (Packet++/header/RawPacket.h) */
 	void add(const uint8_t* bytes, uint32_t len, uint64_t tsNs = 0)
 	{
 		offsets.push_back(data.size());
@@ -124,6 +174,7 @@ struct RawBatch
 			                linkType, 0 };
 	}
 };
+using RawBatch = RawPacketVector;
 
 /* PcapFileReaderDevice (Pcap++/header/PcapFileDevice.h): open / getNextPackets / close */
 class PcapFileReaderDevice
@@ -143,11 +194,14 @@ public:
 	}
 	uint32_t getLinkLayerType() const { return pcppx_pcap_linktype(m_Reader); }
 
-	/* Replace `batch` with the next packets (at most maxPackets / maxBytes); returns the count, 0 at EOF. */
-	size_t getNextPackets(RawBatch& batch, uint32_t maxPackets = 1u << 20, uint64_t maxBytes = 256ull << 20)
+	/* IFileReaderDevice::getNextPackets(RawPacketVector&, int numOfPacketsToRead) (PcapFileDevice.cpp:604-624):
+	 * replaces `batch` with the next packets (at most numOfPacketsToRead, -1 = as many as maxBytes holds); returns
+	 * the count, 0 at end of file. */
+	int getNextPackets(RawPacketVector& batch, int numOfPacketsToRead = -1, uint64_t maxBytes = 256ull << 20)
 	{
 		if (!open())
 			throw Error(PCPPX_E_INVAL, "PcapFileReaderDevice::open(" + m_FileName + ")");
+		const uint32_t maxPackets = numOfPacketsToRead > 0 ? (uint32_t)numOfPacketsToRead : (uint32_t)(maxBytes / 16);
 		batch.data.resize(maxBytes);
 		batch.offsets.resize(maxPackets);
 		batch.caplens.resize(maxPackets);
@@ -162,7 +216,7 @@ public:
 		batch.caplens.resize(n);
 		batch.timestampsNs.resize(n);
 		batch.linkType = (uint16_t)getLinkLayerType();
-		return n;
+		return (int)n;
 	}
 
 private:
@@ -170,40 +224,119 @@ private:
 	pcppx_pcap* m_Reader = nullptr;
 };
 
-/* One layer of a parsed packet: Layer's getProtocol / getOsiModelLayer / getData / getHeaderLen / getDataLen
- * (Packet++/header/Layer.h) */
-class ParsedLayer
+/* One layer of a parsed packet: Layer::getProtocol / getOsiModelLayer / getData / getHeaderLen / getDataLen /
+ * getLayerPayloadSize / isMemberOfProtocolFamily (Packet++/header/Layer.h) */
+class Layer
 {
 public:
-	ParsedLayer(const pcppx_layer* rec, const uint8_t* raw) : m_Rec(rec), m_Raw(raw) {}
+	Layer() = default;
+	Layer(const pcppx_layer* rec, const uint8_t* raw) : m_Rec(rec), m_Raw(raw) {}
 	ProtocolType getProtocol() const { return m_Rec->proto; }
 	OsiModelLayer getOsiModelLayer() const { return (OsiModelLayer)m_Rec->osi; }
 	const uint8_t* getData() const { return m_Raw + m_Rec->offset; }
 	size_t getHeaderLen() const { return m_Rec->hdr_len; }
 	size_t getDataLen() const { return m_Rec->data_len; }
 	size_t getLayerPayloadSize() const { return m_Rec->data_len - m_Rec->hdr_len; }
+	const uint8_t* getLayerPayload() const { return getData() + getHeaderLen(); }
+	bool isMemberOfProtocolFamily(ProtocolTypeFamily family) const
+	{
+		const uint32_t p = m_Rec->proto;
+		return p != 0 && (p == (family & 0xFF) || (p << 8) == (family & 0xFF00) || (p << 16) == (family & 0xFF0000) ||
+		                  (p << 24) == (family & 0xFF000000u));
+	}
 	uint16_t getOffset() const { return m_Rec->offset; }
+	bool valid() const { return m_Rec != nullptr; }
 
-private:
-	const pcppx_layer* m_Rec;
-	const uint8_t* m_Raw;
+protected:
+	uint16_t be16(size_t j) const { return (uint16_t)((getData()[j] << 8) | getData()[j + 1]); }
+	const pcppx_layer* m_Rec = nullptr;
+	const uint8_t* m_Raw = nullptr;
 };
 
-/* A parsed packet: the Packet (Packet++/header/Packet.h) queries this path answers */
-class ParsedPacket
+/* typed views: the accessors the two reference callers use */
+class IPv4Layer : public Layer /* Packet++/header/IPv4Layer.h */
 {
 public:
-	ParsedPacket(const pcppx_summary* s, const pcppx_layer* layers, uint8_t maxLayers, const uint8_t* raw)
-	    : m_Sum(s), m_Layers(layers), m_MaxLayers(maxLayers), m_Raw(raw)
+	static constexpr ProtocolType kProtocol = IPv4;
+	using Layer::Layer;
+	IPv4Address getSrcIPv4Address() const { return IPv4Address(rd32(12)); }
+	IPv4Address getDstIPv4Address() const { return IPv4Address(rd32(16)); }
+	uint8_t getProtocolField() const { return getData()[9]; }
+	bool isFragment() const { return (getData()[6] & 0x20) || (((getData()[6] & 0x1F) << 8) | getData()[7]) != 0; }
+
+private:
+	uint32_t rd32(size_t j) const
+	{
+		uint32_t v;
+		std::memcpy(&v, getData() + j, 4);
+		return v;
+	}
+};
+class IPv6Layer : public Layer /* Packet++/header/IPv6Layer.h */
+{
+public:
+	static constexpr ProtocolType kProtocol = IPv6;
+	using Layer::Layer;
+	const uint8_t* getSrcIPv6AddressBytes() const { return getData() + 8; }
+	const uint8_t* getDstIPv6AddressBytes() const { return getData() + 24; }
+};
+class TcpLayer : public Layer /* Packet++/header/TcpLayer.h: ports in host order */
+{
+public:
+	static constexpr ProtocolType kProtocol = TCP;
+	using Layer::Layer;
+	uint16_t getSrcPort() const { return be16(0); }
+	uint16_t getDstPort() const { return be16(2); }
+	uint8_t getFlags() const { return getData()[13]; }
+};
+class UdpLayer : public Layer /* Packet++/header/UdpLayer.h */
+{
+public:
+	static constexpr ProtocolType kProtocol = UDP;
+	using Layer::Layer;
+	uint16_t getSrcPort() const { return be16(0); }
+	uint16_t getDstPort() const { return be16(2); }
+};
+
+/* what getLayerOfType<T>() returns: a layer view that tests like the reference's T* (null when absent) */
+template <class T>
+class LayerPtr
+{
+public:
+	LayerPtr() = default;
+	explicit LayerPtr(const T& v) : m_V(v), m_Ok(true) {}
+	const T* operator->() const { return &m_V; }
+	const T& operator*() const { return m_V; }
+	explicit operator bool() const { return m_Ok; }
+	bool operator==(std::nullptr_t) const { return !m_Ok; }
+	bool operator!=(std::nullptr_t) const { return m_Ok; }
+
+private:
+	T m_V{};
+	bool m_Ok = false;
+};
+
+/* A parsed packet: the pcpp::Packet (Packet++/header/Packet.h) queries of the two callers */
+class Packet
+{
+public:
+	Packet(const pcppx_summary* s, const pcppx_layer* layers, uint8_t maxLayers, const uint8_t* raw, uint32_t caplen)
+	    : m_Sum(s), m_Layers(layers), m_MaxLayers(maxLayers), m_Raw(raw), m_Caplen(caplen)
 	{}
 
-	/* Packet::isPacketOfType (Packet.cpp:614-640), for a protocol or a family */
+	/* Packet::isPacketOfType (Packet.cpp:614-640), for a protocol or a family. On a packet the engine left to the
+	 * host and no host parser completed, the answer covers its exact layer prefix plus the HTTP / SSL / DNS class
+	 * of its first L7 layer when the device named it (PCPPX_F_L7_KNOWN) */
 	bool isPacketOfType(ProtocolTypeFamily family) const
 	{
+		uint64_t mask = m_Sum->proto_mask;
+		if (m_Sum->flags & PCPPX_F_L7_KNOWN)
+			mask |= ((m_Sum->flags & PCPPX_F_L7_HTTP) ? (1ull << HTTPRequest) | (1ull << HTTPResponse) : 0) |
+			        ((m_Sum->flags & PCPPX_F_L7_SSL) ? 1ull << SSL : 0) | ((m_Sum->flags & PCPPX_F_L7_DNS) ? 1ull << DNS : 0);
 		for (int k = 0; k < 4; ++k)
 		{
 			const uint32_t p = (family >> (8 * k)) & 0xFF;
-			if (p != 0 && p < 64 && (m_Sum->proto_mask >> p) & 1)
+			if (p != 0 && p < 64 && (mask >> p) & 1)
 				return true;
 		}
 		return false;
@@ -211,29 +344,31 @@ public:
 	size_t getLayerCount() const { return m_Sum->n_layers; }
 	/* records held for the first min(getLayerCount(), maxLayers) layers */
 	size_t getRecordedLayerCount() const { return m_Sum->n_layers < m_MaxLayers ? m_Sum->n_layers : m_MaxLayers; }
-	ParsedLayer getLayer(size_t k) const { return ParsedLayer(m_Layers + k, m_Raw); }
-	ParsedLayer getFirstLayer() const { return getLayer(0); }
-	ParsedLayer getLastLayer() const { return getLayer(getRecordedLayerCount() - 1); }
-	/* getLayerOfType<T>(): first recorded layer of `proto`, or false */
-	bool getLayerOfType(ProtocolType proto, ParsedLayer* out) const
+	Layer getLayer(size_t k) const { return Layer(m_Layers + k, m_Raw); }
+	Layer getFirstLayer() const { return getRecordedLayerCount() ? getLayer(0) : Layer(); }
+	Layer getLastLayer() const { return getRecordedLayerCount() ? getLayer(getRecordedLayerCount() - 1) : Layer(); }
+	/* getLayerOfType<T>(reverse) (Packet.h:388-431): the first (or, reverse, the last) recorded layer of T */
+	template <class T>
+	LayerPtr<T> getLayerOfType(bool reverseOrder = false) const
 	{
-		for (size_t k = 0; k < getRecordedLayerCount(); ++k)
-			if (m_Layers[k].proto == proto)
-			{
-				*out = getLayer(k);
-				return true;
-			}
-		return false;
+		const size_t n = getRecordedLayerCount();
+		for (size_t j = 0; j < n; ++j)
+		{
+			const size_t k = reverseOrder ? n - 1 - j : j;
+			if (m_Layers[k].proto == T::kProtocol)
+				return LayerPtr<T>(T(m_Layers + k, m_Raw));
+		}
+		return LayerPtr<T>();
 	}
-	/* PacketUtils.h:80-91 */
-	uint32_t hash5Tuple(bool const& directionUnique = false) const
-	{
-		return directionUnique ? m_Sum->hash5_dir : m_Sum->hash5;
-	}
-	uint32_t hash2Tuple() const { return m_Sum->hash2; }
 
-	/* engine flags: the host must finish the packet (L7, or an L2-L4 protocol outside the device path) */
+	/* the raw packet (RawPacket::getRawData / getRawDataLen) */
+	const uint8_t* getRawData() const { return m_Raw; }
+	uint32_t getRawDataLen() const { return m_Caplen; }
+
+	/* engine flags: the host must finish the packet (an L7 or an out-of-scope L2/L3 layer) and no host parser did */
 	bool needsHost() const { return (m_Sum->flags & PCPPX_F_NEEDS_HOST) != 0; }
+	/* the records come from the caller's host parser (Engine::setHostParser) */
+	bool wasHostParsed() const { return (m_Sum->flags & F_HOST_PARSED) != 0; }
 	bool hasTrailer() const { return (m_Sum->flags & PCPPX_F_TRAILER) != 0; }
 	/* IPv4Layer::computeCalculateFields checksum vs the stored one (IPv4Layer.cpp:410-412) */
 	bool hasIPv4Checksum() const { return (m_Sum->flags & PCPPX_F_IP_CSUM) != 0; }
@@ -250,23 +385,58 @@ private:
 	const pcppx_layer* m_Layers;
 	uint8_t m_MaxLayers;
 	const uint8_t* m_Raw;
+	uint32_t m_Caplen;
 };
+using ParsedPacket = Packet;
+using ParsedLayer = Layer;
 
-/* Records of one parsed batch (owns them); indexes into the RawBatch it was parsed from. */
+/* pcpp::hash5Tuple / hash2Tuple (Packet++/header/PacketUtils.h:58-91) */
+inline uint32_t hash5Tuple(const Packet* packet, bool const& directionUnique = false)
+{
+	return directionUnique ? packet->summary().hash5_dir : packet->summary().hash5;
+}
+inline uint32_t hash2Tuple(const Packet* packet)
+{
+	return packet->summary().hash2;
+}
+
+/* Records of one parsed batch (owns them); indexes into the RawPacketVector it was parsed from. */
 class ParsedBatch
 {
 public:
-	ParsedBatch(const RawBatch& raw, uint8_t maxLayers)
+	ParsedBatch(const RawPacketVector& raw, uint8_t maxLayers)
 	    : m_Raw(&raw), m_MaxLayers(maxLayers), summaries(raw.size()), layers(raw.size() * (size_t)maxLayers)
 	{}
 	size_t size() const { return summaries.size(); }
-	ParsedPacket operator[](size_t i) const
+	Packet operator[](size_t i) const
 	{
-		return ParsedPacket(&summaries[i], layers.data() + i * m_MaxLayers, m_MaxLayers, m_Raw->packetData(i));
+		return Packet(&summaries[i], layers.data() + i * m_MaxLayers, m_MaxLayers, m_Raw->packetData(i),
+		              m_Raw->caplens[i]);
 	}
+	class iterator
+	{
+	public:
+		iterator(const ParsedBatch* b, size_t i) : m_B(b), m_I(i) {}
+		Packet operator*() const { return (*m_B)[m_I]; }
+		iterator& operator++()
+		{
+			++m_I;
+			return *this;
+		}
+		bool operator!=(const iterator& o) const { return m_I != o.m_I; }
+
+	private:
+		const ParsedBatch* m_B;
+		size_t m_I;
+	};
+	iterator begin() const { return iterator(this, 0); }
+	iterator end() const { return iterator(this, size()); }
+	uint8_t maxLayers() const { return m_MaxLayers; }
+	/* packets whose records the host parser filled */
+	size_t hostParsed = 0;
 
 private:
-	const RawBatch* m_Raw;
+	const RawPacketVector* m_Raw;
 	uint8_t m_MaxLayers;
 
 public:
@@ -283,28 +453,11 @@ struct MatchSpec
 	MatchSpec(const std::string& srcIp, const std::string& dstIp, uint16_t srcPort, uint16_t dstPort,
 	          ProtocolType protocol)
 	{
-		spec.src_ip = parseIPv4(srcIp);
-		spec.dst_ip = parseIPv4(dstIp);
+		spec.src_ip = srcIp.empty() ? 0 : IPv4Address(srcIp).toInt();
+		spec.dst_ip = dstIp.empty() ? 0 : IPv4Address(dstIp).toInt();
 		spec.src_port = srcPort;
 		spec.dst_port = dstPort;
 		spec.protocol = protocol;
-	}
-	/* IPv4Address::toInt(): the four address bytes in memory order */
-	static uint32_t parseIPv4(const std::string& dotted)
-	{
-		if (dotted.empty())
-			return 0;
-		uint8_t b[4] = { 0, 0, 0, 0 };
-		unsigned v[4];
-		char tail;
-		if (std::sscanf(dotted.c_str(), "%u.%u.%u.%u%c", &v[0], &v[1], &v[2], &v[3], &tail) != 4 || v[0] > 255 ||
-		    v[1] > 255 || v[2] > 255 || v[3] > 255)
-			throw Error(PCPPX_E_INVAL, "bad IPv4 address '" + dotted + "'");
-		for (int k = 0; k < 4; ++k)
-			b[k] = (uint8_t)v[k];
-		uint32_t out;
-		std::memcpy(&out, b, 4);
-		return out;
 	}
 };
 
@@ -317,24 +470,41 @@ public:
 	Engine(const Engine&) = delete;
 	Engine& operator=(const Engine&) = delete;
 
-	/* Packet(&rawPacket, options) for every packet of the batch, host to host through HBM */
-	ParsedBatch parse(const RawBatch& batch, const PacketParseOptions& options = PacketParseOptions()) const
+	/* the caller's own Packet++ parse of one packet, used to complete packets the engine flags NEEDS_HOST */
+	void setHostParser(pcppx_host_parse_fn fn) { m_HostParser = fn; }
+
+	/* Packet(&rawPacket, options) for every packet of the batch, host to host through HBM; flagged packets are
+	 * completed by the host parser when one is set */
+	ParsedBatch parse(const RawPacketVector& batch, const PacketParseOptions& options = PacketParseOptions()) const
 	{
 		ParsedBatch out(batch, options.maxLayers);
 		parseInto(batch, options, out);
 		return out;
 	}
-	void parseInto(const RawBatch& batch, const PacketParseOptions& options, ParsedBatch& out) const
+	void parseInto(const RawPacketVector& batch, const PacketParseOptions& options, ParsedBatch& out) const
 	{
 		const pcppx_batch b = batch.toC();
 		const pcppx_opts o = options.toC();
 		pcppx_records r{ out.summaries.data(), options.maxLayers ? out.layers.data() : nullptr };
 		check(pcppx_parse_batch_host(m_Ctx, &b, &o, &r), "pcppx_parse_batch_host");
+		out.hostParsed = 0;
+		if (m_HostParser == nullptr || options.maxLayers == 0)
+			return;
+		for (size_t i = 0; i < batch.size(); ++i)
+		{
+			pcppx_summary& s = out.summaries[i];
+			if (!(s.flags & PCPPX_F_NEEDS_HOST) || (s.flags & PCPPX_F_BAD_DESC))
+				continue;
+			pcppx_layer* lay = out.layers.data() + i * (size_t)options.maxLayers;
+			check(m_HostParser(batch.packetData(i), batch.caplens[i], batch.linkType, &o, &s, lay), "host parser");
+			s.flags = (uint16_t)(s.flags | F_HOST_PARSED);
+			++out.hostParsed;
+		}
 	}
 
-	/* FilterTraffic's worker (AppWorkerThread.h:85-139): matched[i] = 1 for packets to send on; the flow
-	 * table persists across calls until resetFilter() */
-	pcppx_packet_stats filter(const RawBatch& batch, const MatchSpec& spec, std::vector<uint8_t>& matched)
+	/* FilterTraffic's whole worker on the device (AppWorkerThread.h:85-139): matched[i] = 1 for packets to send on;
+	 * the flow table persists across calls until resetFilter() */
+	pcppx_packet_stats filter(const RawPacketVector& batch, const MatchSpec& spec, std::vector<uint8_t>& matched)
 	{
 		matched.assign(batch.size(), 0);
 		const pcppx_batch b = batch.toC();
@@ -348,6 +518,7 @@ public:
 
 private:
 	pcppx_ctx* m_Ctx = nullptr;
+	pcppx_host_parse_fn m_HostParser = nullptr;
 };
 
 }  // namespace pcppx

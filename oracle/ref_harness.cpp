@@ -288,6 +288,24 @@ extern "C"
 		return PCPPX_OK;
 	}
 
+	// pcppx_host_parse_fn (include/pcppx.h) over the real reference: the completion step for packets the engine
+	// flags NEEDS_HOST, as a caller's own Packet++ performs it. Test infrastructure: the
+	// example programs load it only when a test passes this library to them.
+	int pcppx_host_parse(const uint8_t* pkt, uint32_t caplen, uint16_t linktype, const pcppx_opts* opts,
+	                     pcppx_summary* summary, pcppx_layer* layers)
+	{
+		if (pkt == nullptr || opts == nullptr || summary == nullptr)
+			return PCPPX_E_INVAL;
+		pcpp::Logger::getInstance().suppressLogs();
+		std::vector<uint8_t> bytes(pkt, pkt + caplen);  // calculateChecksum zeroes and restores a field
+		bytes.push_back(0);
+		timeval ts{ 0, 0 };
+		pcpp::RawPacket raw(bytes.data(), static_cast<int>(caplen), ts, false, static_cast<pcpp::LinkLayerType>(linktype));
+		pcpp::Packet packet(&raw, false, opts->parse_until_family, static_cast<pcpp::OsiModelLayer>(opts->parse_until_osi));
+		fillRecord(packet, raw.getRawData(), opts, summary, opts->max_layers > 0 ? layers : nullptr);
+		return PCPPX_OK;
+	}
+
 	// Parse a host batch with the reference Packet++ and fill host records.
 	int pcppx_ref_parse_batch(const pcppx_batch* b, const pcppx_opts* opts, pcppx_records* out)
 	{

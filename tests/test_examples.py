@@ -1,18 +1,21 @@
-"""The C++ example programs over pcppx.hpp (examples/): the reference's benchmark packet mode and the
-FilterTraffic worker over a pcap file. GPU runs compare with the reference worker / the restatement."""
+"""The reference's two callers in their own shape over the engine (examples/): PcapPlusPlus-benchmark's packet mode
+and DpdkExample-FilterTraffic's worker, reading the reference's own captures (example.pcap whole, example2.pcap
+whole; frozen under tests/golden/). Packets the engine leaves to the host are completed by the caller's Packet++
+parse (pcppx_host_parse_fn); here that is the real reference, oracle/_ref/libpcpp_ref.so, passed by the test as
+--host-parser. Each packet's layer list and hash5Tuple, and the whole PacketStats table (HTTP/DNS/TLS included),
+are compared with the reference."""
 from __future__ import annotations
 
 import re
 import subprocess
-from pathlib import Path
 
 import numpy as np
 import pytest
 
 import oracle
-from conftest import ROOT
+from conftest import GOLDEN, ROOT, load_golden
 from pcapplusplus_amd import abi, synth
-from pcapplusplus_amd.pcap import read_pcap, write_pcap
+from pcapplusplus_amd.pcap import from_packets, read_pcap, write_pcap
 
 BIN = ROOT / "examples" / "bin"
 
@@ -28,20 +31,46 @@ def built():
     return BIN
 
 
+def capture(name: str):
+    """(batch, {variant: (opts, ref summary, ref layers)}) of one whole reference capture."""
+    if name == "example.pcap":
+        return load_golden(GOLDEN / "capture_example.npz")
+    b, variants = load_golden(GOLDEN / "pcap_lt1.npz")
+    k = [i for i, s in enumerate(b.meta["set_names"]) if str(s).endswith("/" + name)][0]
+    idx = np.nonzero(b.meta["set_index"] == k)[0]
+    sub = from_packets([b.packet(int(i)) for i in idx], b.linktype)
+    return sub, {v: (o, s[idx], lay[idx]) for v, (o, s, lay) in variants.items()}
+
+
 def test_usage_without_device(built):
     r = run([built / "benchmark"])
     assert r.returncode == 1 and "Usage" in r.stdout
+    r = run([built / "benchmark", "x.pcap", "dns", "1"])
+    assert r.returncode == 1 and "packet mode" in r.stderr
     r = run([built / "filter_traffic", "-f"])
     assert r.returncode == 1 and "Usage" in r.stdout
     r = run([built / "filter_traffic", "-f", "x.pcap", "-P", "ICMP"])
     assert r.returncode == 1
 
 
+def parse_dump(text: str) -> dict[int, tuple]:
+    out = {}
+    for ln in text.splitlines():
+        f = ln.split()
+        if len(f) < 6 or not f[-1].startswith("host="):
+            continue
+        layers = [tuple(int(x) for x in t.split(":")) for t in f[2:-4]]
+        out[int(f[0])] = (int(f[1]), layers, int(f[-4][3:]), int(f[-3][4:]), int(f[-2][3:]), int(f[-1][5:]))
+    return out
+
+
 def stats_from(text: str) -> dict:
     names = {"Eth count": "eth_count", "ARP count": "arp_count", "IPv4 count": "ipv4_count",
              "IPv6 count": "ipv6_count", "TCP count": "tcp_count", "UDP count": "udp_count",
+             "HTTP count": "http_count", "DNS count": "dns_count", "TLS count": "tls_count",
              "Matched TCP flows": "matched_tcp_flows", "Matched UDP flows": "matched_udp_flows",
-             "Total packet count": "packet_count", "Matched packet count": "matched_packets"}
+             "Total packet count": "packet_count", "Matched packet count": "matched_packets",
+             "Left to host": "needs_host_count"}
     out = {}
     for m in re.finditer(r"\|\s*([A-Za-z0-9 ]+?)\s*\|\s*(\d+)\s*\|", text):
         if m.group(1) in names:
@@ -50,37 +79,121 @@ def stats_from(text: str) -> dict:
 
 
 @pytest.mark.gpu
-def test_benchmark_packet_mode(built, tmp_path):
+@pytest.mark.parametrize("name", ["example.pcap", "example2.pcap"])
+@pytest.mark.parametrize("host", [True, False], ids=["host-parser", "engine-only"])
+def test_benchmark_packet_mode_per_packet(built, tmp_path, name, host):
+    """benchmark <capture> packet: the count line, and every packet's layers + hashes under Packet(&raw, TCP) equal
+    the reference's. With the host parser every packet is exact; without it, unflagged packets are exact and
+    flagged ones an exact prefix."""
+    b, variants = capture(name)
+    f = tmp_path / name
+    write_pcap(f, b)
+    args = [built / "benchmark", f, "packet", 2, "--dump"]
+    if host:
+        if not oracle.ref_available():
+            pytest.skip("reference library not built")
+        args += ["--host-parser", oracle.REF_SO]
+    r = run(args)
+    assert r.returncode == 0, r.stderr
+    count, _ms = (int(x) for x in r.stdout.strip().splitlines()[-1].split())
+    assert count == b.n
+    got = parse_dump(r.stdout)
+    assert len(got) == b.n
+    _opts, rs, rl = variants["until_tcp"]
+    s, _ = oracle.oracle_parse(b, abi.make_opts(4, 8, False, 16))
+    flagged = (s["flags"] & abi.F_NEEDS_HOST) != 0
+    n_host = 0
+    for i in range(b.n):
+        nl, layers, h5, h5d, h2, hp = got[i]
+        want = [(int(x["proto"]), int(x["offset"]), int(x["hdr_len"]), int(x["data_len"]))
+                for x in rl[i][: min(int(rs["n_layers"][i]), 16)]]
+        n_host += hp
+        if host or not flagged[i]:
+            assert (nl, layers, h5, h5d, h2) == (int(rs["n_layers"][i]), want, int(rs["hash5"][i]),
+                                                 int(rs["hash5_dir"][i]), int(rs["hash2"][i])), (i, got[i], want)
+        else:
+            assert layers == want[: len(layers)], (i, got[i], want)
+    assert n_host == (int(flagged.sum()) if host else 0)
+
+
+SPECS = {"all": {}, "tcp_dport80": {"dst_port": 80, "protocol": 4}, "udp": {"protocol": 5}}
+
+
+def _spec_args(b, key):
+    if key == "src_ip":  # the first IPv4 source of the capture
+        s, lay = oracle.oracle_parse(b.slice(0, 200), abi.make_opts(0, 8, False, 16))
+        for i in range(200):
+            for x in lay[i][: s["n_layers"][i]]:
+                if x["proto"] == 2:
+                    p = b.packet(i)
+                    ip = ".".join(str(c) for c in p[x["offset"] + 12:x["offset"] + 16])
+                    return ["-s", ip], oracle.make_spec(src_ip=ip)
+    d = SPECS[key]
+    args = []
+    if "dst_port" in d:
+        args += ["-D", d["dst_port"]]
+    if "protocol" in d:
+        args += ["-P", "TCP" if d["protocol"] == 4 else "UDP"]
+    return args, oracle.make_spec(**d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["example.pcap", "example2.pcap"])
+@pytest.mark.parametrize("key", ["all", "tcp_dport80", "udp", "src_ip"])
+def test_filter_traffic_matches_reference_worker(built, tmp_path, name, key):
+    """The worker loop in the reference's shape, host parser completing flagged packets: the full PacketStats table
+    (HTTP / DNS / TLS included) and the matched packets written to the output pcap equal the reference worker's
+    (oracle/_ref: the real PacketMatchingEngine, hash5Tuple flow table and collectStats)."""
+    if not oracle.ref_available():
+        pytest.skip("reference library not built")
+    b, _ = capture(name)
+    f, o = tmp_path / name, tmp_path / "out.pcap"
+    write_pcap(f, b)
+    args, spec = _spec_args(b, key)
+    r = run([built / "filter_traffic", "-f", f, "-o", o, "-b", 1000, "--host-parser", oracle.REF_SO] + args)
+    assert r.returncode == 0, r.stderr
+    want_m, want = oracle.ref_filter(b, spec)
+    got = stats_from(r.stdout)
+    assert got.pop("needs_host_count") == 0
+    want.pop("needs_host_count")
+    assert got == want
+    w = read_pcap(o)
+    assert [w.packet(i) for i in range(w.n)] == [b.packet(int(i)) for i in np.nonzero(want_m)[0]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["example.pcap", "example2.pcap"])
+def test_filter_traffic_device_worker(built, tmp_path, name):
+    """--device-worker: the whole worker in HBM. Every counter except HTTP/DNS/TLS equals the reference's; those
+    three equal the reference's over the packets the device settles (the restatement's filter), and the matched
+    packets are the reference's."""
+    b, _ = capture(name)
+    f, o = tmp_path / name, tmp_path / "out.pcap"
+    write_pcap(f, b)
+    r = run([built / "filter_traffic", "-f", f, "-o", o, "-D", 80, "--device-worker"])
+    assert r.returncode == 0, r.stderr
+    got = stats_from(r.stdout)
+    spec = oracle.make_spec(dst_port=80)
+    s, lay = oracle.oracle_parse(b, abi.make_opts(0, 8, False, 16))
+    want_m, want = oracle.oracle_filter(b, s, lay, spec)
+    assert got == want
+    if oracle.ref_available():
+        ref_m, ref = oracle.ref_filter(b, spec)
+        for k in ("packet_count", "eth_count", "arp_count", "ipv4_count", "ipv6_count", "tcp_count", "udp_count",
+                  "matched_tcp_flows", "matched_udp_flows", "matched_packets"):
+            assert got[k] == ref[k], k
+        assert (want_m == ref_m).all()
+    w = read_pcap(o)
+    assert [w.packet(i) for i in range(w.n)] == [b.packet(int(i)) for i in np.nonzero(want_m)[0]]
+
+
+@pytest.mark.gpu
+def test_benchmark_synthetic_imix(built, tmp_path):
+    """A 300k-packet synthetic IMIX capture (no L7 triggers): nothing to complete, counts exact."""
     b = synth.config(3, 300_000)
     f = tmp_path / "in.pcap"
     write_pcap(f, b)
     r = run([built / "benchmark", f, "packet", 3])
     assert r.returncode == 0, r.stderr
-    count, ms = (int(x) for x in r.stdout.split())
+    count, _ms = (int(x) for x in r.stdout.split())
     assert count == b.n
-
-
-@pytest.mark.gpu
-def test_filter_traffic_tool(built, tmp_path):
-    b = synth.imix(50_000, 23, flows=2000, corrupt_frac=0.0)
-    f, o = tmp_path / "in.pcap", tmp_path / "out.pcap"
-    write_pcap(f, b)
-    # a destination port seen in the data, TCP only
-    s, lay = oracle.oracle_parse(b.slice(0, 1000), abi.make_opts(0, 8, False, 16))
-    k = int(np.nonzero(s["proto_mask"] & (1 << 4))[0][0])
-    l4 = [int(x["offset"]) for x in lay[k] if x["proto"] == 4][0]
-    pkt = b.packet(k)
-    dport = pkt[l4 + 2] << 8 | pkt[l4 + 3]
-    r = run([built / "filter_traffic", "-f", f, "-o", o, "-D", dport, "-P", "TCP"])
-    assert r.returncode == 0, r.stderr
-    spec = oracle.make_spec(dst_port=dport, protocol=4)
-    if oracle.ref_available():
-        want_m, want = oracle.ref_filter(b, spec)
-    else:
-        s, lay = oracle.oracle_parse(b, abi.make_opts(0, 8, False, 16), threads=8)
-        want_m, want = oracle.oracle_filter(b, s, lay, spec)
-    got = stats_from(r.stdout)
-    for key, v in got.items():
-        assert v == want[key], (key, v, want[key])
-    w = read_pcap(o)
-    assert [w.packet(i) for i in range(w.n)] == [b.packet(i) for i in np.nonzero(want_m)[0]]

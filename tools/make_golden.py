@@ -5,7 +5,8 @@ Tests/Pcap++Test/PcapExamples/*.pcap, Tests/Fuzzers/RegressionTests/regression_s
 seed-generated synthetic batches. Expected outputs come from the REAL reference Packet++ (built from
 /root/reference sources by oracle/Makefile into oracle/_ref/libpcpp_ref.so) through oracle/ref_harness.cpp.
 
-  python tools/make_golden.py
+  python tools/make_golden.py            # everything
+  python tools/make_golden.py captures   # only the whole-capture fixtures (CAPTURES)
 
 Writes tests/golden/<name>.npz with: data, offsets, caplens, linktype, set_names, set_index,
 and per option variant v: sum_<v>, lay_<v> (reference records), opts_<v> (family, osi, csum, max_layers).
@@ -64,9 +65,25 @@ def dump(name: str, batch: PacketBatch, set_names: list[str], set_index: np.ndar
     print(f"{name}: {batch.n} packets, {batch.data.nbytes} bytes -> {(OUT / f'{name}.npz').stat().st_size} B")
 
 
+# whole captures of the reference's Pcap++ tests, each in its own fixture (the example programs' parity tests)
+CAPTURES = {"capture_example": "Tests/Pcap++Test/PcapExamples/example.pcap"}
+
+
+def dump_captures() -> None:
+    from pcapplusplus_amd.pcap import read_pcap
+
+    for name, rel in CAPTURES.items():
+        b = read_pcap(corpus.REF / rel)
+        dump(name, b, [rel], np.zeros(b.n, np.int32))
+
+
 def main() -> None:
     if not oracle.ref_available():
         raise SystemExit("oracle/_ref/libpcpp_ref.so missing: `make -C oracle ref` first")
+    if sys.argv[1:] == ["captures"]:
+        dump_captures()
+        return
+    dump_captures()
     # 1. single-packet .dat fixtures (Ethernet)
     d = corpus.dat_batch()
     dump("dat_ethernet", d, d.meta["names"], np.arange(d.n, dtype=np.int32))
