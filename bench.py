@@ -42,19 +42,65 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU (default: the config's size)")
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 4, 5))
-    ap.add_argument("--max-layers", type=int, default=None, help="layer records per packet (default 8; 12 for config 5)")
+    ap.add_argument("--max-layers", type=int, default=None,
+                    help="layer records per packet (default: 8 for config 3, 12 for config 5, 0 (summary only) for the "
+                         "configs whose consumer reads only the summary: 2's 5-tuple extract, 4's flow table)")
     ap.add_argument("--checksums", choices=("auto", "on", "off"), default="auto",
                     help="IPv4/L4 checksum verify (auto: on for config 3 only)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="packets in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min CPU-baseline time (repeat passes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-to-host (PCIe-inclusive) timing")
-    ap.add_argument("--traffic", default=str(ROOT / "profiles" / "r01_traffic.json"),
-                    help="PMC-derived HBM bytes per launch (from tools/pmc_traffic.py)")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py; default profiles/traffic_cfg<N>.json); "
+                         "used only if it was measured on this kernel source, config, size and record options")
+    ap.add_argument("--no-traffic", action="store_true", help="do not report PMC traffic (the PMC passes themselves)")
     return ap.parse_args()
 
 
 CONFIG_PACKETS = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000_000}
+CONFIG_MAX_LAYERS = {2: 0, 3: 8, 4: 0, 5: 12}
+KERNEL_SRC = ROOT / "pcapplusplus_amd" / "csrc" / "pcppx_kernels.hip"
+
+
+def kernel_sha() -> str:
+    """Identity of the kernel source a traffic measurement belongs to."""
+    import hashlib
+
+    return hashlib.sha256(KERNEL_SRC.read_bytes()).hexdigest()[:16]
+
+
+def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool) -> tuple[int | None, str]:
+    """(HBM bytes per parse launch, note) from a PMC traffic file, only if it matches this run exactly."""
+    if not path.exists():
+        return None, f"no PMC measurement ({path.name})"
+    try:
+        tj = json.loads(path.read_text())
+    except (ValueError, OSError) as e:
+        return None, f"unreadable {path.name}: {e}"
+    want = {"config": cfg, "packets": n, "max_layers": ml, "checksums": csum, "kernel_sha": kernel_sha()}
+    got = {k: tj.get(k) for k in want}
+    if got != want:
+        return None, f"stale {path.name}: measured {got}, this run {want}"
+    return int(tj["hbm_bytes_per_launch"]), f"{path.name} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
+
+
+def cpu_cores() -> tuple[int, str]:
+    """Host cores this process may use: the affinity mask, capped by a cgroup CPU quota (a GPU box's share)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    if quota is not None and quota < aff:
+        return quota, f"{quota} of {aff} affinity cores (cgroup cpu.max quota)"
+    return aff, f"all {aff} cores of the affinity mask"
 WORKLOADS = {
     2: "config 2: 64 B Eth/IPv4/{TCP,UDP} 50/50; parse + hash5Tuple/hash2Tuple (5-tuple extract)",
     3: "config 3: IMIX 64/512/1500 B 7:4:1, 25% VLAN, 70/30 IPv4/IPv6, TCP/UDP 50/50, 1% bad checksums; "
@@ -91,11 +137,7 @@ def cpu_baseline(batch, opts, sample: int, min_seconds: float) -> dict:
     import oracle  # test infrastructure: the checker, timed here only as the reported CPU baseline
 
     sub = batch.slice(0, min(sample, batch.n))
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
+    threads, core_note = cpu_cores()
     kind = "reference" if oracle.ref_available() else "port"
     fn = oracle.ref_bench if kind == "reference" else oracle.oracle_bench
     total_t, total_p = 0.0, 0
@@ -107,7 +149,7 @@ def cpu_baseline(batch, opts, sample: int, min_seconds: float) -> dict:
             "sample": f"first {sub.n} packets of the same batch, {total_p // sub.n} passes, "
                       f"{total_t:.1f} s; {'reference Packet++ built from source' if kind == 'reference' else 'C restatement'}"
                       f": Packet(&raw) + hash5Tuple x2 + hash2Tuple"
-                      f"{' + IPv4/L4 checksums' if opts.want_checksums else ''}, {threads} threads"}
+                      f"{' + IPv4/L4 checksums' if opts.want_checksums else ''}, {threads} threads = {core_note}"}
 
 
 def main() -> None:
@@ -131,7 +173,7 @@ def main() -> None:
     # ---- synthetic shard for this rank (per-GPU work fixed: weak scaling) ----
     cfg = args.config
     npk = args.packets or CONFIG_PACKETS[cfg]
-    ml = args.max_layers if args.max_layers is not None else (12 if cfg == 5 else 8)
+    ml = args.max_layers if args.max_layers is not None else CONFIG_MAX_LAYERS[cfg]
     t0 = time.time()
     seed = shard.shard_seed(cfg, rank)
     if cfg == 3:
@@ -197,7 +239,16 @@ def main() -> None:
     total_packets = n * world * args.steps
     mpps = total_packets / wall_max / 1e6
     wire = int(batch.caplens.sum(dtype=np.int64))
-    read_bytes = algorithmic_read_bytes(batch, want_csum, summary, layers, caplens, ml)
+    if want_csum or ml >= 8:
+        read_bytes = algorithmic_read_bytes(batch, want_csum, summary, layers, caplens, ml)
+    else:
+        # the header extents come from the layer records: one untimed parse with full records
+        ext_sum = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        ext_lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device=dev)
+        eng.parse_device(data, offsets, caplens, n, batch.linktype, abi.make_opts(0, 8, False, 16), ext_sum, ext_lay, sh)
+        torch.cuda.synchronize(dev)
+        read_bytes = algorithmic_read_bytes(batch, False, ext_sum, ext_lay, caplens, 16)
+        del ext_sum, ext_lay
     write_bytes = n * (32 + 8 * ml)
     achieved = read_bytes / (kern_ms * 1e-3) / 1e9
 
@@ -206,16 +257,10 @@ def main() -> None:
     flags = (s[:, 3] & 0xFFFF)
     flagged = int(((flags & abi.F_NEEDS_HOST) != 0).sum().item())
 
-    traffic = None
-    tp = Path(args.traffic)
-    if tp.exists():
-        try:
-            tj = json.loads(tp.read_text())
-            if tj.get("packets") == n and tj.get("config") == cfg and tj.get("max_layers") == ml and \
-                    tj.get("checksums", True) == want_csum:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
+    traffic, traffic_note = None, "not requested"
+    if not args.no_traffic:
+        tp = Path(args.traffic) if args.traffic else ROOT / "profiles" / f"traffic_cfg{cfg}.json"
+        traffic, traffic_note = load_traffic(tp, cfg, n, ml, want_csum)
 
     e2e = None
     if not args.no_e2e and rank == 0 and world == 1:
@@ -240,12 +285,24 @@ def main() -> None:
                 buf.free()
 
     flow_check = None
-    if flows is not None:  # every packet of every launch is counted once: table + key-0 bucket
+    if flows is not None:
+        # FilterTraffic's exit step (Examples/DpdkExample-FilterTraffic/main.cpp:279-287): every GPU's flow table is
+        # merged by key on the host (after the timed region; nothing crosses GPUs on the data path). Conservation:
+        # every packet of every launch on every rank is in a flow, the key-0 bucket or the no-free-slot count.
         keys, pk, by, st, cap = flows
-        counted = int(pk.sum().item()) + int(st[0].item())
-        flow_check = {"flows": int((keys != 0).sum().item()), "packets_counted": counted,
-                      "expected": n * (args.warmup + args.steps), "table_full_drops": int(st[2].item()),
-                      "flow_kernel_ms": round(flow_ms, 4)}
+        mine = shard.compact_device_table(keys.cpu().numpy(), pk.cpu().numpy(), by.cpu().numpy(), st.cpu().numpy())
+        tables = [mine]
+        if world > 1:
+            tables = [None] * world
+            dist.all_gather_object(tables, mine)
+        if rank == 0:
+            merged = shard.merge_device_tables(tables)
+            counted = int(merged["packets"].sum()) + merged["key0_packets"] + merged["dropped"]
+            expected = n * world * (args.warmup + args.steps)
+            flow_check = {"merged_flows": int(len(merged["keys"])), "ranks_merged": len(tables),
+                          "per_rank_flows": [int(len(t["keys"])) for t in tables],
+                          "packets_counted": counted, "expected": expected, "conserved": counted == expected,
+                          "table_full_drops": merged["dropped"], "flow_kernel_ms": round(flow_ms, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -285,6 +342,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_note,
                 "algorithmic_read_bytes": read_bytes,
                 "record_write_bytes": write_bytes,
             },

@@ -1008,33 +1008,82 @@ __device__ __forceinline__ uint32_t desc_flags(uint64_t off, uint32_t cap, uint6
 	return 0;
 }
 
-// ---------------- fast path for the common stacks (branch-free, dword LDS reads) ----------------
+// ---------------- fast path: straight-line stages over the LDS window ----------------
 //
-// Ethernet, up to two 802.1Q/802.1ad tags, IPv4 (any IHL, not a fragment) or IPv6 without extension
-// headers, then TCP or UDP, then Payload (or an L7 flag) and a trailer; no parse-until options. Every
-// byte it reads must sit in the LDS window; anything else (or any rule this path does not cover) makes
-// it report "not applicable" and the generic walk_chain() runs instead. Results are identical to
-// walk_chain() by construction: same rules, same records (checked bit-exactly by tests/).
+// Ethernet, up to two 802.1Q/802.1ad tags, up to three MPLS labels, an IPv4 or IPv6 layer (IPv6 with up to three
+// extension headers; an IPv4 fragment or a last Fragment extension makes the rest a Payload), optionally a GREv0
+// layer and an inner IPv4 / IPv6 layer, then TCP or UDP, Payload (or an L7 flag) and a trailer; no parse-until
+// options. Each optional stage (MPLS, IPv6 extensions, GRE) runs only when some lane of the wave needs it (a scalar
+// branch on a ballot), so plain Eth/[VLAN]/IP/L4 waves pay for the plain stages only. Every byte read must sit in
+// the LDS window; anything else (or any rule this path does not cover) makes the packet "not applicable" and the
+// generic walk_chain() runs for it. Same rules and records as walk_chain() (bit-exact in tests/).
 
-
+// A fast-path packet, packed into five registers (it stays live across the checksum stream): offsets and header
+// lengths inside the LDS window fit 8 bits, data lengths 16 bits.
 struct Fast
 {
-	uint32_t nv;        // VLAN tags
-	uint32_t ipo, iphdr, ipdlen, v6;
-	uint32_t l4o, l4hdr, l4dlen, tcp;
-	uint32_t payload;   // a Payload layer follows the L4 layer
-	uint32_t trailer;   // trailer length (0: none)
-	uint32_t l7;        // L4 payload goes to an L7 dissector: PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_* (else 0)
+	uint32_t a;  // o1 | h1 << 8 | o2 << 16 | h2 << 24: the first / inner IP layer's offset and header length
+	uint32_t b;  // d1 | d2 << 16: their data lengths
+	uint32_t c;  // l4o | l4hdr << 8 | gh << 16 | nv << 24 | nm << 26 | gre << 28 | v6a << 29 | v6b << 30 | l4 << 31
+	uint32_t d;  // l4dlen | trailer << 16 (until fast_l7: the last IP layer's end)
+	uint32_t e;  // tcp | payload << 1 | simple << 2 | l7 flags << 16 (PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_*)
+	__device__ __forceinline__ uint32_t o1() const { return a & 0xFF; }
+	__device__ __forceinline__ uint32_t h1() const { return (a >> 8) & 0xFF; }
+	__device__ __forceinline__ uint32_t o2() const { return (a >> 16) & 0xFF; }
+	__device__ __forceinline__ uint32_t h2() const { return a >> 24; }
+	__device__ __forceinline__ uint32_t d1() const { return b & 0xFFFF; }
+	__device__ __forceinline__ uint32_t d2() const { return b >> 16; }
+	__device__ __forceinline__ uint32_t l4o() const { return c & 0xFF; }
+	__device__ __forceinline__ uint32_t l4hdr() const { return (c >> 8) & 0xFF; }
+	__device__ __forceinline__ uint32_t gh() const { return (c >> 16) & 0xFF; }
+	__device__ __forceinline__ uint32_t nv() const { return (c >> 24) & 3; }
+	__device__ __forceinline__ uint32_t nm() const { return (c >> 26) & 3; }
+	__device__ __forceinline__ uint32_t gre() const { return (c >> 28) & 1; }
+	__device__ __forceinline__ uint32_t v6a() const { return (c >> 29) & 1; }
+	__device__ __forceinline__ uint32_t v6b() const { return (c >> 30) & 1; }
+	__device__ __forceinline__ uint32_t l4() const { return c >> 31; }
+	__device__ __forceinline__ uint32_t l4dlen() const { return d & 0xFFFF; }
+	__device__ __forceinline__ uint32_t trailer() const { return d >> 16; }
+	__device__ __forceinline__ uint32_t tcp() const { return e & 1; }
+	__device__ __forceinline__ uint32_t payload() const { return (e >> 1) & 1; }
+	__device__ __forceinline__ uint32_t simple() const { return (e >> 2) & 1; }
+	__device__ __forceinline__ uint32_t l7() const { return e >> 16; }
 };
+
+// an IP layer at [o, o+len): IPv4Layer::isDataValid (IPv4Layer.h:626-630), initLayerInPacket (IPv4Layer.cpp:180-197),
+// isFragment (:415-418); IPv6Layer::isDataValid (IPv6Layer.h:245-249) and its fixed header (the extension headers
+// are walked by the caller). Selects over the same three dwords for both versions.
+struct IpDec
+{
+	uint32_t ok, hdr, dlen, nh, frag, plen;  // plen: IPv6 payload length
+};
+__device__ __forceinline__ IpDec ip_decode(const Pkt& p, uint32_t o, uint32_t len, bool v6)
+{
+	const uint32_t w0 = lds_u32(p, o);      // ver/ihl, tos, total length (v4) | ver/tc/flow (v6)
+	const uint32_t w1 = lds_u32(p, o + 4);  // id, frag (v4) | payload length, next header, hop limit (v6)
+	const uint32_t w2 = lds_u32(p, o + 8);  // ttl, protocol, checksum (v4)
+	const uint32_t b0 = w0 & 0xFF;
+	IpDec d;
+	const uint32_t h4 = (b0 & 0xF) * 4, tl = swap16(w0 >> 16), hmin = h4 < len ? h4 : len;
+	const uint32_t dl4 = (tl < len && tl != 0) ? (tl > hmin ? tl : hmin) : len;
+	const uint32_t b6 = (w1 >> 16) & 0xFF, b7 = w1 >> 24;
+	d.plen = swap16(w1);
+	const uint32_t tot6 = d.plen + 40;
+	d.ok = v6 ? (len >= 40 && (b0 >> 4) == 6) : (len >= 20 && (b0 >> 4) == 4 && (b0 & 0xF) >= 5);
+	d.hdr = v6 ? 40u : h4;
+	d.dlen = v6 ? (tot6 < len ? tot6 : len) : dl4;
+	d.nh = v6 ? b6 : ((w2 >> 8) & 0xFF);
+	d.frag = !v6 && ((b6 & 0x20) || (((b6 & 0x1F) << 8) | b7) != 0);
+	return d;
+}
 
 __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Params& prm, Fast& f)
 {
 	bool ok = prm.linktype == 1 && prm.family == 0 && prm.until_osi == 8 && p.lim >= 20 && cap > 14;
 	// Ethernet (EthLayer.cpp:28-69, isDataValid :100-117)
-	uint32_t d = lds_u32(p, 12);
-	uint32_t et = swap16(d);
+	uint32_t et = swap16(lds_u32(p, 12));
 	ok = ok && et >= 0x0600;
-	uint32_t o = 14, len = cap - 14, nv = 0;
+	uint32_t o = 14, len = cap - 14, nv = 0, nm = 0;
 	// up to two VLAN tags (VlanLayer.cpp:59-119): each needs len > 4 so that a next layer follows
 #pragma unroll
 	for (int t = 0; t < 2; ++t)
@@ -1046,64 +1095,106 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 		len = vl ? len - 4 : len;
 		nv += vl ? 1 : 0;
 	}
-	const bool v4 = et == 0x0800, v6 = et == 0x86DD;
-	ok = ok && (v4 || v6) && o + 40 <= p.lim;  // both IP headers' fixed parts are read below
-	const uint32_t w0 = lds_u32(p, o);      // ver/ihl, tos, total length (v4) | ver/tc/flow (v6)
-	const uint32_t w1 = lds_u32(p, o + 4);  // id, frag (v4) | payload length, next header, hop limit (v6)
-	const uint32_t w2 = lds_u32(p, o + 8);  // ttl, protocol, checksum (v4)
-	const uint32_t b0 = w0 & 0xFF;
-	uint32_t hdr, dlen, proto;
-	if (v4)
+	// up to three MPLS labels (MplsLayer.cpp:101-128): a label has a next layer only with >= 5 bytes (which also
+	// covers Ethernet's >= 4 bytes, EthLayer.cpp:28-69); not bottom of stack: another label (unchecked); bottom of
+	// stack: IPv4 / IPv6 by the next nibble
+	if (__ballot(ok && et == 0x8847))  // wave-uniform
 	{
-		// IPv4Layer::isDataValid (IPv4Layer.h:626-630), initLayerInPacket (IPv4Layer.cpp:180-197)
-		ok = ok && len >= 20 && (b0 >> 4) == 4 && (b0 & 0xF) >= 5;
-		hdr = (b0 & 0xF) * 4;
-		const uint32_t tl = swap16(w0 >> 16);
-		dlen = len;
-		if (tl < len && tl != 0)
+#pragma unroll
+		for (int t = 0; t < 3; ++t)
 		{
-			const uint32_t hmin = hdr < len ? hdr : len;
-			dlen = tl > hmin ? tl : hmin;
+			const bool ml = et == 0x8847 && len >= 5 && o + 5 <= p.lim;
+			const uint32_t w = lds_u32(p, ml ? o : 0), nb = (lds_u32(p, ml ? o + 4 : 0) & 0xFF) >> 4;
+			const uint32_t nxt = ((w >> 16) & 1) ? (nb == 4 ? 0x0800u : (nb == 6 ? 0x86DDu : 0xFFFFu)) : 0x8847u;
+			et = ml ? nxt : et;
+			o = ml ? o + 4 : o;
+			len = ml ? len - 4 : len;
+			nm += ml ? 1 : 0;
 		}
-		const uint32_t b6 = (w1 >> 16) & 0xFF, b7 = w1 >> 24;
-		ok = ok && !((b6 & 0x20) || (((b6 & 0x1F) << 8) | b7) != 0);  // not a fragment (:415-438)
-		proto = (w2 >> 8) & 0xFF;
 	}
-	else
+	// the first IP layer: its fixed header, then IPv6's extension headers (IPv6Layer::parseExtensions,
+	// IPv6Layer.cpp:79-147: next headers 0/43/44/60 take 8*(len+1) bytes, AH 51 4*(len+2); no bound check)
+	const bool v6a = et == 0x86DD;
+	ok = ok && (et == 0x0800 || v6a) && o + 40 <= p.lim;
+	IpDec d1 = ip_decode(p, o, len, v6a);
+	ok = ok && d1.ok;
+	constexpr uint64_t kExt = (1ull << 0) | (1ull << 43) | (1ull << 44) | (1ull << 51) | (1ull << 60);
+	uint32_t ext = 0, last_ext = 0xFFu;
+	if (__ballot(ok && v6a && d1.nh < 64 && ((kExt >> d1.nh) & 1ull)))  // wave-uniform
 	{
-		// IPv6Layer ctor (IPv6Layer.cpp:28-40): next header 6/17 means no extension walk
-		ok = ok && len >= 40 && (b0 >> 4) == 6;
-		hdr = 40;
-		const uint32_t total = swap16(w1) + 40;
-		dlen = total < len ? total : len;
-		proto = (w1 >> 16) & 0xFF;
+		uint32_t eo = 40;
+#pragma unroll
+		for (int t = 0; t < 3; ++t)
+		{
+			const bool e = v6a && d1.nh < 64 && ((kExt >> d1.nh) & 1ull) && eo + 2 <= len && o + eo + 2 <= p.lim;
+			const uint32_t two = lds_u32(p, e ? o + eo : 0) & 0xFFFFu;
+			const uint32_t el = d1.nh == 51 ? 4u * ((two >> 8) + 2) : 8u * ((two >> 8) + 1);
+			last_ext = e ? d1.nh : last_ext;
+			d1.nh = e ? (two & 0xFFu) : d1.nh;
+			ext += e ? el : 0u;
+			eo += e ? el : 0u;
+		}
+		// a chain longer than the stage walks (or one leaving the window) goes to the generic walk
+		ok = ok && !(v6a && d1.nh < 64 && ((kExt >> d1.nh) & 1ull) && eo + 2 <= len);
+		// IPv6Layer: header = 40 + extensions; dataLen = payloadLength + header when shorter (IPv6Layer.cpp:28-40)
+		if (v6a)
+		{
+			d1.hdr = 40 + ext;
+			const uint32_t tot = d1.plen + d1.hdr;
+			d1.dlen = tot < len ? tot : len;
+		}
 	}
-	ok = ok && (proto == 6 || proto == 17) && dlen > hdr;
-	const uint32_t l4o = o + hdr, pl = ok ? dlen - hdr : 0;
-	const bool tcp = proto == 6;
-	ok = ok && l4o + (tcp ? 20 : 8) <= p.lim;
-	const uint32_t t3 = lds_u32(p, (ok && tcp) ? l4o + 12 : 0);  // TCP data offset byte at +12
-	const uint32_t doff = (t3 & 0xFF) >> 4;
-	// TcpLayer::isDataValid (TcpLayer.h:596-601) / UDP needs 8 bytes
-	ok = ok && (tcp ? (pl >= 20 && doff >= 5 && pl >= doff * 4) : pl >= 8);
-	const uint32_t l4hdr = tcp ? doff * 4 : 8;
-	const bool payload = pl > l4hdr;
+	// IP dispatch (IPv4Layer.cpp:245-370, IPv6Layer.cpp:194-312): a fragment (IPv4) or a last Fragment extension
+	// (IPv6) -> Payload; 47 -> GRE; 6 / 17 -> TCP / UDP; anything else -> the generic walk
+	const bool frag1 = d1.frag || (v6a && last_ext == 44);
+	ok = ok && d1.dlen > d1.hdr && (frag1 || d1.nh == 6 || d1.nh == 17 || d1.nh == 47);
+	uint32_t lo = o + d1.hdr, lp = ok ? d1.dlen - d1.hdr : 0, lnh = d1.nh;  // the last IP layer's payload
+	// GREv0 (GreLayer.cpp:23-36,195-252): flags C/R, K, S, A add 4 bytes each; EtherType IPv4 / IPv6 (tryConstruct)
+	uint32_t gre = 0, gh = 0, o2 = 0;
+	IpDec d2{};
+	bool v6b = false;
+	if (__ballot(ok && !frag1 && d1.nh == 47))  // wave-uniform
+	{
+		const bool g = ok && !frag1 && d1.nh == 47;
+		ok = ok && (!g || lo + 4 <= p.lim);
+		const uint32_t gw = lds_u32(p, g ? lo : 0);
+		const uint32_t f0 = gw & 0xFF, f1 = (gw >> 8) & 0xFF, get = swap16(gw >> 16);
+		gh = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
+		ok = ok && (!g || (lp >= 4 && (f1 & 7) == 0 && lp > gh && (get == 0x0800 || get == 0x86DD)));
+		v6b = get == 0x86DD;
+		o2 = lo + gh;
+		const uint32_t len2 = g ? lp - gh : 0;
+		ok = ok && (!g || o2 + 40 <= p.lim);
+		d2 = ip_decode(p, g && ok ? o2 : 0, len2, v6b);
+		// the inner layer: valid, not a fragment, no extension headers, TCP / UDP behind it
+		ok = ok && (!g || (d2.ok && !d2.frag && d2.dlen > d2.hdr && (d2.nh == 6 || d2.nh == 17)));
+		gre = g ? 1u : 0u;
+		lo = g ? o2 + d2.hdr : lo;
+		lp = g ? (ok ? d2.dlen - d2.hdr : 0) : lp;
+		lnh = g ? d2.nh : lnh;
+	}
+	// TCP / UDP (TcpLayer::isDataValid TcpLayer.h:596-601; UDP needs 8 bytes), unless a fragment made a Payload
+	const bool l4 = !frag1;
+	const bool tcp = l4 && lnh == 6;
+	ok = ok && (!l4 || lo + (tcp ? 20 : 8) <= p.lim);
+	const uint32_t doff = (lds_u32(p, (ok && tcp) ? lo + 12 : 0) & 0xFF) >> 4;
+	ok = ok && (!l4 || (tcp ? (lp >= 20 && doff >= 5 && lp >= doff * 4) : lp >= 8));
+	const uint32_t l4hdr = !l4 ? 0u : (tcp ? doff * 4 : 8u);
+	const bool payload = lp > l4hdr;
 	// the SIP heuristic (UDP payloads of >= 4 B) reads 4 payload bytes from LDS too
-	ok = ok && (tcp || !payload || pl - 8 < 4 || l4o + 12 <= p.lim);
-	// the IPv4 header checksum reads the whole header from LDS too
-	ok = ok && (!v4 || o + hdr <= p.lim);
-	f.nv = nv;
-	f.ipo = o;
-	f.iphdr = hdr;
-	f.ipdlen = dlen;
-	f.v6 = v6;
-	f.l4o = l4o;
-	f.l4hdr = l4hdr;
-	f.l4dlen = pl;
-	f.tcp = tcp;
-	f.payload = payload;  // until fast_l7 (the L7 decision is taken after the hashes: table-read latency)
-	f.l7 = 0;
-	f.trailer = o + dlen;  // IP end, until fast_l7
+	ok = ok && (!l4 || tcp || !payload || lp - 8 < 4 || lo + 12 <= p.lim);
+	// the IPv4 header checksum reads the whole first IPv4 header from LDS too
+	ok = ok && (v6a || o + d1.hdr <= p.lim) && (!gre || !v6a || v6b || o2 + d2.hdr <= p.lim);
+	// until fast_l7: trailer = the last IP layer's end, no L7 flags (the L7 decision is taken after the hashes)
+	const uint32_t end = gre ? o2 + d2.dlen : o + d1.dlen;
+	f.a = (o & 0xFF) | ((d1.hdr & 0xFF) << 8) | ((o2 & 0xFF) << 16) | ((d2.hdr & 0xFF) << 24);
+	f.b = (d1.dlen & 0xFFFF) | (d2.dlen << 16);
+	f.c = (lo & 0xFF) | ((l4hdr & 0xFF) << 8) | ((gh & 0xFF) << 16) | (nv << 24) | (nm << 26) | (gre << 28) |
+	      ((v6a ? 1u : 0u) << 29) | ((v6b ? 1u : 0u) << 30) | ((l4 ? 1u : 0u) << 31);
+	f.d = (lp & 0xFFFF) | (end << 16);
+	f.e = (tcp ? 1u : 0u) | ((payload ? 1u : 0u) << 1) | ((nm == 0 && ext == 0 && !frag1 && !gre) ? 4u : 0u);
+	// everything above sits inside the window (< 256 B), lengths below 64 KiB (caplen cap)
+	ok = ok && o + d1.hdr < 256 && o2 + d2.hdr < 256 && lo < 256;
 	return ok;
 }
 
@@ -1111,86 +1202,115 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 // L4 layer, with no Payload and no trailer
 __device__ __forceinline__ void fast_l7(const Pkt& p, Fast& f, uint32_t cap)
 {
-	const bool payload = f.payload != 0;
+	const bool payload = f.payload() != 0, tcp = f.tcp() != 0;
+	const uint32_t l4o = f.l4o(), l4dlen = f.l4dlen();
 	uint32_t lf = 0;
-	if (payload)
+	if (payload && f.l4())
 	{
-		const uint32_t pw = lds_u32(p, f.l4o);
+		const uint32_t pw = lds_u32(p, l4o);
 		const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
-		const bool sip = !f.tcp && f.l4dlen - 8 >= 4 && sip_key(__builtin_bswap32(lds_u32(p, f.l4o + 8)));
-		const bool trig = f.tcp ? tcp_l7(sport, dport) : (udp_l7(sport, dport) || sip);
+		const bool sip = !tcp && l4dlen - 8 >= 4 && sip_key(__builtin_bswap32(lds_u32(p, l4o + 8)));
+		const bool trig = tcp ? tcp_l7(sport, dport) : (udp_l7(sport, dport) || sip);
 		if (trig)
-			lf = l7_flags(p, f.tcp, f.l4o + f.l4hdr, f.l4dlen - f.l4hdr, sport, dport, sip, true);
+			lf = l7_flags(p, tcp, l4o + f.l4hdr(), l4dlen - f.l4hdr(), sport, dport, sip, true);
 	}
 	const bool l7 = lf != 0;
-	const uint32_t end = f.trailer;
-	f.payload = payload && !l7;
-	f.l7 = lf;
-	f.trailer = (!l7 && end < cap) ? cap - end : 0;
+	const uint32_t end = f.trailer();
+	const uint32_t tl = (!l7 && end < cap) ? cap - end : 0;
+	f.d = (f.d & 0xFFFF) | (tl << 16);
+	f.e = (f.e & ~2u) | ((payload && !l7) ? 2u : 0u) | (lf << 16);
+}
+
+// layer indexes of a fast-path packet: IP1 at k1; GRE and IP2 after it; the L4 layer at kl
+__device__ __forceinline__ uint32_t fast_k1(const Fast& f)
+{
+	return 1 + f.nv() + f.nm();
 }
 
 // the Walk summary of a fast-path packet
 __device__ __forceinline__ Walk fast_to_walk(const Fast& f, uint32_t ml)
 {
 	const uint32_t cap_layers = ml ? ml : PCPPX_MAX_LAYERS;
-	const uint32_t count = 3 + f.nv + f.payload + (f.trailer ? 1 : 0);
+	const uint32_t gre = f.gre(), v6a = f.v6a(), v6b = f.v6b(), l4 = f.l4(), tcp = f.tcp(), payload = f.payload();
+	const uint32_t trailer = f.trailer();
+	const uint32_t k1 = fast_k1(f), kl = k1 + 1 + 2 * gre;
+	const uint32_t count = kl + l4 + payload + (trailer ? 1 : 0);
 	Walk w;
-	w.flags = f.l7 | (f.trailer ? PCPPX_F_TRAILER : 0) |
-	          (count > cap_layers ? PCPPX_F_DEPTH_OVERFLOW : 0);
+	w.flags = f.l7() | (trailer ? PCPPX_F_TRAILER : 0) | (count > cap_layers ? PCPPX_F_DEPTH_OVERFLOW : 0);
 	w.n_layers = count > cap_layers ? cap_layers : count;
-	w.mask = (1ull << P_ETH) | (f.nv ? (1ull << P_VLAN) : 0) | (1ull << (f.v6 ? P_IPV6 : P_IPV4)) |
-	         (1ull << (f.tcp ? P_TCP : P_UDP)) | (f.payload ? (1ull << P_PAYLOAD) : 0) |
-	         (f.trailer ? (1ull << P_TRAILER) : 0);
-	w.v4 = f.v6 ? -1 : (int32_t)f.ipo;
-	w.v6 = f.v6 ? (int32_t)f.ipo : -1;
-	w.v4_dlen = f.ipdlen;
-	w.l4i = (int32_t)(2 + f.nv);
-	w.l4o = f.l4o;
-	w.l4dlen = f.l4dlen;
-	w.l4pp = f.v6 ? P_IPV6 : P_IPV4;
-	w.l4ppo = f.ipo;
-	w.is_tcp = f.tcp;
+	w.mask = (1ull << P_ETH) | (f.nv() ? (1ull << P_VLAN) : 0) | (f.nm() ? (1ull << P_MPLS) : 0) |
+	         (1ull << (v6a ? P_IPV6 : P_IPV4)) | (gre ? (1ull << P_GREV0) | (1ull << (v6b ? P_IPV6 : P_IPV4)) : 0) |
+	         (l4 ? (1ull << (tcp ? P_TCP : P_UDP)) : 0) | (payload ? (1ull << P_PAYLOAD) : 0) |
+	         (trailer ? (1ull << P_TRAILER) : 0);
+	// the first IPv4 / IPv6 layers (hash5Tuple's addresses, the IPv4 checksum)
+	const bool v4b = gre && !v6b;
+	w.v4 = !v6a ? (int32_t)f.o1() : (v4b ? (int32_t)f.o2() : -1);
+	w.v6 = v6a ? (int32_t)f.o1() : ((gre && v6b) ? (int32_t)f.o2() : -1);
+	w.v4_dlen = !v6a ? f.d1() : f.d2();
+	w.l4i = l4 ? (int32_t)kl : -1;
+	w.l4o = f.l4o();
+	w.l4dlen = f.l4dlen();
+	const bool lv6 = gre ? v6b : v6a;
+	w.l4pp = lv6 ? P_IPV6 : P_IPV4;
+	w.l4ppo = gre ? f.o2() : f.o1();
+	w.is_tcp = tcp;
 	return w;
 }
 
 // layer record k of a fast-path packet (k < count)
 __device__ __forceinline__ uint2 fast_layer(const Fast& f, uint32_t cap, uint32_t k)
 {
+	const uint32_t nv = f.nv(), gre = f.gre(), l4 = f.l4();
+	const uint32_t k1 = fast_k1(f), kl = k1 + 1 + 2 * gre;
+	const uint32_t o1 = f.o1(), h1 = f.h1(), d1 = f.d1();
+	const uint32_t lasto = gre ? f.o2() : o1, lasth = gre ? f.h2() : h1, lastd = gre ? f.d2() : d1;
 	uint32_t proto, osi, o, hdr, dlen;
 	if (k == 0) { proto = P_ETH; osi = 2; o = 0; hdr = 14; dlen = cap; }
-	else if (k <= f.nv) { proto = P_VLAN; osi = 2; o = 14 + 4 * (k - 1); hdr = 4; dlen = cap - o; }
-	else if (k == f.nv + 1) { proto = f.v6 ? P_IPV6 : P_IPV4; osi = 3; o = f.ipo; hdr = f.iphdr; dlen = f.ipdlen; }
-	else if (k == f.nv + 2) { proto = f.tcp ? P_TCP : P_UDP; osi = 4; o = f.l4o; hdr = f.l4hdr; dlen = f.l4dlen; }
-	else if (k == f.nv + 3 && f.payload)
+	else if (k <= nv) { proto = P_VLAN; osi = 2; o = 14 + 4 * (k - 1); hdr = 4; dlen = cap - o; }
+	else if (k < k1) { proto = P_MPLS; osi = 3; o = 14 + 4 * (k - 1); hdr = 4; dlen = cap - o; }
+	else if (k == k1) { proto = f.v6a() ? P_IPV6 : P_IPV4; osi = 3; o = o1; hdr = h1; dlen = d1; }
+	else if (gre && k == k1 + 1) { proto = P_GREV0; osi = 3; o = o1 + h1; hdr = f.gh(); dlen = d1 - h1; }
+	else if (gre && k == k1 + 2) { proto = f.v6b() ? P_IPV6 : P_IPV4; osi = 3; o = f.o2(); hdr = f.h2(); dlen = f.d2(); }
+	else if (l4 && k == kl) { proto = f.tcp() ? P_TCP : P_UDP; osi = 4; o = f.l4o(); hdr = f.l4hdr(); dlen = f.l4dlen(); }
+	else if (f.payload() && k == kl + l4)
 	{
-		proto = P_PAYLOAD; osi = 7; o = f.l4o + f.l4hdr; hdr = dlen = f.l4dlen - f.l4hdr;
+		proto = P_PAYLOAD; osi = 7;
+		o = l4 ? f.l4o() + f.l4hdr() : lasto + lasth;
+		hdr = dlen = l4 ? f.l4dlen() - f.l4hdr() : lastd - lasth;
 	}
-	else { proto = P_TRAILER; osi = 2; o = f.ipo + f.ipdlen; hdr = dlen = f.trailer; }
+	else { proto = P_TRAILER; osi = 2; o = lasto + lastd; hdr = dlen = f.trailer(); }
 	return make_uint2(proto | (osi << 8) | (o << 16), (hdr & 0xFFFF) | (dlen << 16));
 }
 
-// hash5Tuple x2 + hash2Tuple of a fast-path packet (every byte in the LDS window)
-__device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
+// hash5Tuple x2 + hash2Tuple of a fast-path packet (every byte in the LDS window): the first IPv4 (else the first
+// IPv6) layer's addresses and protocol / next-header byte, the L4 layer's ports
+__device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, const Walk& w, uint32_t& h5, uint32_t& h5d,
+                                            uint32_t& h2)
 {
 	uint32_t s[4], d[4];
-	const uint32_t na = f.v6 ? 4 : 1;
-	const uint32_t so = f.ipo + (f.v6 ? 8 : 12), dofs = f.ipo + (f.v6 ? 24 : 16);
+	const bool v4 = w.v4 >= 0;
+	const uint32_t ipo = v4 ? (uint32_t)w.v4 : (uint32_t)w.v6;
+	const uint32_t na = v4 ? 1 : 4;
+	const uint32_t so = ipo + (v4 ? 12 : 8), dofs = ipo + (v4 ? 16 : 24);
 #pragma unroll
 	for (int k = 0; k < 4; ++k)
 	{
 		s[k] = (uint32_t)k < na ? lds_u32(p, so + 4 * k) : 0;
 		d[k] = (uint32_t)k < na ? lds_u32(p, dofs + 4 * k) : 0;
 	}
-	tuple_hashes(s, d, na, true, lds_u32(p, f.l4o), f.tcp ? 6 : 17, h5, h5d, h2);
+	const uint32_t proto = (lds_u32(p, ipo + (v4 ? 8 : 4)) >> (v4 ? 8 : 16)) & 0xFF;
+	tuple_hashes(s, d, na, f.l4() != 0, lds_u32(p, f.l4o()), proto, h5, h5d, h2);
 }
 
-// IPv4 header checksum from dword reads of the (fully staged) header
-__device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Fast& f, uint32_t* stored)
+// IPv4 header checksum of the first IPv4 layer, from dword reads of the (fully staged) header
+__device__ __forceinline__ uint32_t fast_ipv4_checksum(const Pkt& p, const Walk& w, uint32_t* stored)
 {
+	const uint32_t o = (uint32_t)w.v4;
+	const uint32_t hl = (lds_u32(p, o) & 0xF) * 4;  // <= dataLen: the fast path only takes IP layers with a successor
 	uint32_t acc = 0;
-	for (uint32_t t = 0; t < f.iphdr; t += 4)
-		acc += halves(lds_u32(p, f.ipo + t));
-	const uint32_t w5 = lds_u32(p, f.ipo + 8) >> 16;  // bytes 10-11 as a LE word
+	for (uint32_t t = 0; t < hl; t += 4)
+		acc += halves(lds_u32(p, o + t));
+	const uint32_t w5 = lds_u32(p, o + 8) >> 16;  // bytes 10-11 as a LE word
 	*stored = swap16(w5);
 	uint32_t r = (mod65535(acc) + 65535u - mod65535(w5)) % 65535u;
 	return finish_checksum(r);
@@ -1545,12 +1665,12 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		fast = fast_walk(p, cap, prm, f);
 		if (fast)
 		{
-			fast_hashes(p, f, h5, h5d, h2);
+			fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
 			fast_l7(p, f, cap);
 			w = fast_to_walk(f, ml);
-			if (prm.want_csum && !f.v6)
+			if (prm.want_csum && w.v4 >= 0)
 			{
-				ipc = fast_ipv4_checksum(p, f, &ips);
+				ipc = fast_ipv4_checksum(p, w, &ips);
 				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
 			}
 		}
@@ -1568,7 +1688,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	}
 
 	// the TCP flags byte for the fused reassembly output (the LDS stage is reused by the layer rows below)
-	const uint32_t tcp_fl = (prm.reasm != nullptr && fast && f.tcp) ? (uint32_t)p.s[p.mis + f.l4o + 13] : 0u;
+	const uint32_t tcp_fl = (prm.reasm != nullptr && fast && f.simple() && f.tcp()) ? (uint32_t)p.s[p.mis + f.l4o() + 13] : 0u;
 
 	// ---- (4) L4 checksums over the tile span ----
 	if (prm.want_csum)  // uniform
@@ -1715,17 +1835,22 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 	}
 
-	// ---- (6) fused reassembly front ends (same records as reasm_kernel): fast-path packets straight from
-	// their parse (IPv4 not a fragment, IPv6 without extensions, the TCP flags byte in LDS), the rest from
-	// the layer records this lane wrote ----
-	if (prm.reasm != nullptr && in)  // uniform pointer
+	// ---- (6) fused reassembly front ends (same records as reasm_kernel): plain fast-path packets straight from
+	// their parse (IPv4 not a fragment, IPv6 without extensions, the TCP flags byte read before the LDS reuse), every
+	// other packet from its layer records ----
+	if (prm.reasm != nullptr)  // uniform pointer
+	{
+		__syncthreads();  // the fast-path rows of (5) were stored by other lanes
+		__threadfence_block();
+	}
+	if (prm.reasm != nullptr && in)
 	{
 		uint4 r;
-		if (fast)
+		if (fast && f.simple())
 		{
-			const uint32_t nl = w.n_layers, ipk = 1 + f.nv, l4k = 2 + f.nv;
-			const bool unfinished = (w.flags & PCPPX_F_DEPTH_OVERFLOW) || ((w.flags & PCPPX_F_NEEDS_HOST_L7) && !f.tcp);
-			const bool v4r = !f.v6 && ipk < nl, v6r = f.v6 && ipk < nl, tcpr = f.tcp && l4k < nl;
+			const uint32_t nl = w.n_layers, ipk = 1 + f.nv(), l4k = 2 + f.nv();
+			const bool unfinished = (w.flags & PCPPX_F_DEPTH_OVERFLOW) || ((w.flags & PCPPX_F_NEEDS_HOST_L7) && !f.tcp());
+			const bool v4r = !f.v6a() && ipk < nl, v6r = f.v6a() && ipk < nl, tcpr = f.tcp() && l4k < nl;
 			const uint32_t ipst = v4r ? PCPPX_IPR_NON_FRAGMENT
 			                          : (unfinished ? PCPPX_IPR_HOST
 			                                        : (v6r ? (PCPPX_IPR_F_IPV6 | PCPPX_IPR_NON_FRAGMENT) : PCPPX_IPR_NON_IP));
@@ -1739,17 +1864,14 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			else
 			{
 				const uint32_t fl = tcp_fl;
-				pay = f.l4dlen - f.l4hdr;
+				pay = f.l4dlen() - f.l4hdr();
 				ts = ((pay == 0 && (fl & 7) == 0) ? PCPPX_TCPR_NO_DATA : PCPPX_TCPR_DATA) |
 				     ((fl & 1) ? PCPPX_TCPR_F_FIN : 0) | ((fl & 2) ? PCPPX_TCPR_F_SYN : 0) | ((fl & 4) ? PCPPX_TCPR_F_RST : 0);
 			}
 			r = make_uint4(0, 0, (ipst << 16) | (ts << 24), pay);
 		}
 		else
-		{
-			__threadfence_block();  // this lane's own layer records, written by the walk
 			r = reasm_one(w.flags, w.n_layers, prm.layers + (size_t)i * ml, ml, prm.data + off);
-		}
 		reinterpret_cast<uint4*>(prm.reasm)[i] = r;
 	}
 }

@@ -62,6 +62,67 @@ def test_two_rank_shards_merge_to_single_pass():
     assert tmax == 2.0
 
 
+def _device_format(hash5: np.ndarray, caplens: np.ndarray, capacity: int):
+    """The table pcppx_flow_count_device would hold for these packets (any slot order): keys u32[capacity] with
+    zeros for empty slots, packets / bytes u64[capacity], stats u64[4] (key-0 packets / bytes, drops)."""
+    t = shard.flow_table(hash5, caplens)
+    keys = np.zeros(capacity, np.uint32)
+    pk = np.zeros(capacity, np.uint64)
+    by = np.zeros(capacity, np.uint64)
+    stats = np.zeros(4, np.uint64)
+    rng = np.random.default_rng(len(t))
+    slots = rng.permutation(capacity)
+    j = 0
+    for k, (p, b) in t.items():
+        if k == -1:
+            stats[0], stats[1] = p, b
+            continue
+        keys[slots[j]], pk[slots[j]], by[slots[j]] = k, p, b
+        j += 1
+    return keys, pk, by, stats
+
+
+def _device_worker(rank: int, world: int, port: int, q):
+    """Each rank holds a device-format flow table of its shard; rank 0 merges the compact tables (the bench's
+    config-4 host merge) and compares with one table over the whole batch."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+    import oracle
+    from pcapplusplus_amd import abi, synth
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = synth.imix(30_000, 4, flows=3000, corrupt_frac=0.0)
+    lo, hi = shard.shard_range(b.n, world, rank)
+    part = b.slice(lo, hi)
+    s, _ = oracle.oracle_parse(part, abi.make_opts(0, 8, False, 0))
+    mine = shard.compact_device_table(*_device_format(s["hash5"], part.caplens, 1 << 13))
+    tables = [None] * world
+    dist.all_gather_object(tables, mine)
+    if rank == 0:
+        merged = shard.merge_device_tables(tables)
+        full, _ = oracle.oracle_parse(b, abi.make_opts(0, 8, False, 0))
+        counted = int(merged["packets"].sum()) + merged["key0_packets"] + merged["dropped"]
+        q.put((shard.merged_to_dict(merged) == shard.flow_table(full["hash5"], b.caplens), counted == b.n))
+    dist.destroy_process_group()
+
+
+def test_two_rank_device_tables_merge_to_single_pass():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_device_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    equal, conserved = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+    assert equal and conserved
+
+
 def test_shard_ranges_cover_exactly():
     for n in (0, 1, 7, 100, 12_500_001):
         for world in (1, 2, 3, 8):
