@@ -122,7 +122,9 @@ typedef struct pcppx_opts {
 /* Output arrays (same memory space as the batch for the _device call, host for the _host call). */
 typedef struct pcppx_records {
 	pcppx_summary* summary; /* n entries */
-	pcppx_layer* layers;    /* n * max_layers entries, or NULL when max_layers == 0 */
+	pcppx_layer* layers;    /* n * max_layers entries, or NULL when max_layers == 0; packet i's layer k is
+	                           layers[i * max_layers + k] for k < min(n_layers, max_layers); the entries past
+	                           n_layers are not written */
 } pcppx_records;
 
 /* The caller's own host parse of ONE packet — its Packet++ (`pcpp::Packet packet(&raw, parseUntil...)`) turned

@@ -1115,7 +1115,7 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 	// the first IP layer: its fixed header, then IPv6's extension headers (IPv6Layer::parseExtensions,
 	// IPv6Layer.cpp:79-147: next headers 0/43/44/60 take 8*(len+1) bytes, AH 51 4*(len+2); no bound check)
 	const bool v6a = et == 0x86DD;
-	ok = ok && (et == 0x0800 || v6a) && o + 40 <= p.lim;
+	ok = ok && (et == 0x0800 || v6a) && o + (v6a ? 40 : 20) <= p.lim;  // the fixed header (addresses included)
 	IpDec d1 = ip_decode(p, o, len, v6a);
 	ok = ok && d1.ok;
 	constexpr uint64_t kExt = (1ull << 0) | (1ull << 43) | (1ull << 44) | (1ull << 51) | (1ull << 60);
@@ -1164,7 +1164,7 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 		v6b = get == 0x86DD;
 		o2 = lo + gh;
 		const uint32_t len2 = g ? lp - gh : 0;
-		ok = ok && (!g || o2 + 40 <= p.lim);
+		ok = ok && (!g || o2 + (v6b ? 40 : 20) <= p.lim);
 		d2 = ip_decode(p, g && ok ? o2 : 0, len2, v6b);
 		// the inner layer: valid, not a fragment, no extension headers, TCP / UDP behind it
 		ok = ok && (!g || (d2.ok && !d2.frag && d2.dlen > d2.hdr && (d2.nh == 6 || d2.nh == 17)));
@@ -1257,29 +1257,34 @@ __device__ __forceinline__ Walk fast_to_walk(const Fast& f, uint32_t ml)
 	return w;
 }
 
-// layer record k of a fast-path packet (k < count)
-__device__ __forceinline__ uint2 fast_layer(const Fast& f, uint32_t cap, uint32_t k)
+// the layer records of a fast-path packet in chain order, at most ml of them: sink(k, record) for k = 0, 1, ... (one
+// predicated store per possible layer instead of a select chain per record slot)
+template <class Sink>
+__device__ __forceinline__ void fast_emit(const Fast& f, uint32_t cap, uint32_t ml, Sink sink)
 {
-	const uint32_t nv = f.nv(), gre = f.gre(), l4 = f.l4();
-	const uint32_t k1 = fast_k1(f), kl = k1 + 1 + 2 * gre;
-	const uint32_t o1 = f.o1(), h1 = f.h1(), d1 = f.d1();
-	const uint32_t lasto = gre ? f.o2() : o1, lasth = gre ? f.h2() : h1, lastd = gre ? f.d2() : d1;
-	uint32_t proto, osi, o, hdr, dlen;
-	if (k == 0) { proto = P_ETH; osi = 2; o = 0; hdr = 14; dlen = cap; }
-	else if (k <= nv) { proto = P_VLAN; osi = 2; o = 14 + 4 * (k - 1); hdr = 4; dlen = cap - o; }
-	else if (k < k1) { proto = P_MPLS; osi = 3; o = 14 + 4 * (k - 1); hdr = 4; dlen = cap - o; }
-	else if (k == k1) { proto = f.v6a() ? P_IPV6 : P_IPV4; osi = 3; o = o1; hdr = h1; dlen = d1; }
-	else if (gre && k == k1 + 1) { proto = P_GREV0; osi = 3; o = o1 + h1; hdr = f.gh(); dlen = d1 - h1; }
-	else if (gre && k == k1 + 2) { proto = f.v6b() ? P_IPV6 : P_IPV4; osi = 3; o = f.o2(); hdr = f.h2(); dlen = f.d2(); }
-	else if (l4 && k == kl) { proto = f.tcp() ? P_TCP : P_UDP; osi = 4; o = f.l4o(); hdr = f.l4hdr(); dlen = f.l4dlen(); }
-	else if (f.payload() && k == kl + l4)
-	{
-		proto = P_PAYLOAD; osi = 7;
-		o = l4 ? f.l4o() + f.l4hdr() : lasto + lasth;
-		hdr = dlen = l4 ? f.l4dlen() - f.l4hdr() : lastd - lasth;
-	}
-	else { proto = P_TRAILER; osi = 2; o = lasto + lastd; hdr = dlen = f.trailer(); }
-	return make_uint2(proto | (osi << 8) | (o << 16), (hdr & 0xFFFF) | (dlen << 16));
+	const uint32_t nv = f.nv(), nm = f.nm(), gre = f.gre(), l4 = f.l4(), payload = f.payload(), tl = f.trailer();
+	const uint32_t o1 = f.o1(), h1 = f.h1(), d1 = f.d1(), o2 = f.o2(), h2 = f.h2(), d2 = f.d2();
+	const uint32_t lasto = gre ? o2 : o1, lasth = gre ? h2 : h1, lastd = gre ? d2 : d1;
+	uint32_t k = 0;
+	auto emit = [&](bool on, uint32_t proto, uint32_t osi, uint32_t o, uint32_t hdr, uint32_t dlen) {
+		if (on && k < ml)
+			sink(k, make_uint2(proto | (osi << 8) | (o << 16), (hdr & 0xFFFF) | (dlen << 16)));
+		k += on ? 1u : 0u;
+	};
+	emit(true, P_ETH, 2, 0, 14, cap);
+	emit(nv > 0, P_VLAN, 2, 14, 4, cap - 14);
+	emit(nv > 1, P_VLAN, 2, 18, 4, cap - 18);
+	const uint32_t mo = 14 + 4 * nv;  // MPLS labels follow the tags
+	emit(nm > 0, P_MPLS, 3, mo, 4, cap - mo);
+	emit(nm > 1, P_MPLS, 3, mo + 4, 4, cap - mo - 4);
+	emit(nm > 2, P_MPLS, 3, mo + 8, 4, cap - mo - 8);
+	emit(true, f.v6a() ? P_IPV6 : P_IPV4, 3, o1, h1, d1);
+	emit(gre != 0, P_GREV0, 3, o1 + h1, f.gh(), d1 - h1);
+	emit(gre != 0, f.v6b() ? P_IPV6 : P_IPV4, 3, o2, h2, d2);
+	emit(l4 != 0, f.tcp() ? P_TCP : P_UDP, 4, f.l4o(), f.l4hdr(), f.l4dlen());
+	const uint32_t po = l4 ? f.l4o() + f.l4hdr() : lasto + lasth, pl = l4 ? f.l4dlen() - f.l4hdr() : lastd - lasth;
+	emit(payload != 0, P_PAYLOAD, 7, po, pl, pl);
+	emit(tl != 0, P_TRAILER, 2, lasto + lastd, tl, tl);
 }
 
 // hash5Tuple x2 + hash2Tuple of a fast-path packet (every byte in the LDS window): the first IPv4 (else the first
@@ -1542,17 +1547,26 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // MinWaves: __launch_bounds__ minimum waves per SIMD (1 = compiler's choice). LDS is 8 KiB per block
 // with 7-chunk windows (stage 7424 B + 768 B of per-lane state): 20 blocks = 5 waves/SIMD fit a CU's
 // 160 KiB. SWin: stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers).
-// Chunks: 16-B header chunks staged per packet.
+// Chunks: 16-B header chunks a packet's LDS window holds.
 // NT: non-temporal span-stream loads and record stores (read-once / write-once data; A/B variant 11)
-template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false>
+// Csum: the instance computes checksums when the launch asks (false: a parse-only instance, no span stream).
+// Chunks1 < Chunks: a two-round gather: first min(packet, Chunks1) chunks for every packet, then up to Chunks for
+// the packets the fast path could not take from the first window (deep stacks), which then retry it.
+// MarkFast (tools only): flags bit 0x8000 set on the packets the fast path took. FillTails: the staged layer rows
+// are zero-filled past n_layers and stored whole: full-line stores, 3.5% faster on config 3 than storing only the
+// chain's records (profiles/r02_ab_tails.txt).
+template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
+          bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
 	// stage doubles as the layer-record staging area at the end (64 rows x (ml+1) padded records x 8 B)
 	__shared__ uint32_t stage[kTile * kTSlotDw];
 	__shared__ uint64_t m_a0[kTile];
-	__shared__ uint32_t m_nch[kTile];
+	__shared__ uint32_t m_nch[kTile];  // gather range of each packet: chunks [bits 8-15, bits 0-7)
 	static_assert(kTile * (kRowMaxMl + 1) * 2 <= kTile * kTSlotDw, "stage too small for layer rows");
+	static_assert(Chunks1 <= Chunks && Chunks < 256, "gather rounds");
+	const bool want_csum = Csum && prm.want_csum;  // uniform
 
 	const uint32_t lane = threadIdx.x;
 	const uint32_t i = blockIdx.x * kTile + lane;
@@ -1570,7 +1584,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	const uint64_t smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
 	const uint64_t emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
 	const uint64_t wire = uniform_u64(wave_sum_u64(live ? cap : 0));
-	const bool stream = prm.want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
+	const bool stream = want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
 	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
 	uint4 va[SWin / 64], vb[SWin / 64];
 	auto load = [&](uint4 (&v)[SWin / 64], uint32_t win) {
@@ -1593,50 +1607,83 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	if (stream)
 		load(va, 0);
 
-	// ---- (2) header gather into LDS ----
+	// ---- (2) header gather into LDS: 8 lanes per packet, one 16-B chunk each (8 packets per wave-instruction) ----
 	Pkt p;
 	p.g = (gptr8)(prm.data + (live ? off : 0));
 	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
 	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
-	{
-		const uint32_t need = (p.mis + cap + 15) >> 4;
-		p.nch = (live && !StreamOnly) ? (need < (uint32_t)Chunks ? need : (uint32_t)Chunks) : 0;
-	}
+	const uint32_t need = (p.mis + cap + 15) >> 4;  // chunks holding the whole packet
+	p.nch = (live && !StreamOnly) ? (need < (uint32_t)Chunks1 ? need : (uint32_t)Chunks1) : 0;
 	m_a0[lane] = p.a0;
 	m_nch[lane] = p.nch;
-	__syncthreads();
+	auto gather = [&]() {  // chunks [lo, hi) of every packet of the tile (m_nch)
 #pragma unroll
-	for (int r = 0; r < (Chunks + 7) / 8; ++r)  // 8 lanes per packet, one 16-B chunk each per round
-	{
-		const uint32_t sub = (lane & 7) + 8 * r, grp = lane >> 3;
-		uint4 v[8];
-#pragma unroll
-		for (int j = 0; j < 8; ++j)
+		for (int r = 0; r < (Chunks + 7) / 8; ++r)
 		{
-			const uint32_t q = 8 * j + grp;
-			if (sub < m_nch[q])
-				v[j] = ld16(m_a0[q] + 16 * sub);
-		}
+			const uint32_t sub = (lane & 7) + 8 * r, grp = lane >> 3;
+			uint4 v[8];
 #pragma unroll
-		for (int j = 0; j < 8; ++j)
-		{
-			const uint32_t q = 8 * j + grp;
-			if (sub < m_nch[q])
+			for (int j = 0; j < 8; ++j)
 			{
-				lptr32w slot = (lptr32w)(stage) + q * kTSlotDw + 4 * sub;
-				slot[0] = v[j].x;
-				slot[1] = v[j].y;
-				slot[2] = v[j].z;
-				slot[3] = v[j].w;
+				const uint32_t q = 8 * j + grp, rg = m_nch[q];
+				if (sub >= (rg >> 8) && sub < (rg & 0xFF))
+					v[j] = ld16(m_a0[q] + 16 * sub);
+			}
+#pragma unroll
+			for (int j = 0; j < 8; ++j)
+			{
+				const uint32_t q = 8 * j + grp, rg = m_nch[q];
+				if (sub >= (rg >> 8) && sub < (rg & 0xFF))
+				{
+					lptr32w slot = (lptr32w)(stage) + q * kTSlotDw + 4 * sub;
+					slot[0] = v[j].x;
+					slot[1] = v[j].y;
+					slot[2] = v[j].z;
+					slot[3] = v[j].w;
+				}
 			}
 		}
-	}
+	};
+	__syncthreads();
+	gather();
 	__syncthreads();
 	p.s = reinterpret_cast<lptr8>((lptr32w)(stage) + lane * kTSlotDw);
-	{
+	auto set_lim = [&]() {
 		const uint32_t staged = 16 * p.nch - p.mis;
 		p.lim = (live && p.nch) ? (staged < cap ? staged : cap) : 0;
+	};
+	set_lim();
+	if (Chunks1 < Chunks)
+	{
+		// second round before any walk: the rest of the window for the stacks the first round cannot hold (an MPLS
+		// label, or an IP layer not followed directly by TCP / UDP: GRE, IPv6 extension headers, ...), from a
+		// pre-scan of the Ethernet / VLAN / IP fields of the first window
+		uint32_t et = swap16(lds_u32(p, 12)), o = 14;
+#pragma unroll
+		for (int t = 0; t < 2; ++t)
+		{
+			const bool vl = (et == 0x8100 || et == 0x88A8) && o + 8 <= p.lim;
+			const uint32_t e2 = swap16(lds_u32(p, vl ? o : 0) >> 16);
+			et = vl ? e2 : et;
+			o = vl ? o + 4 : o;
+		}
+		const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 8 <= p.lim ? o + 8 : 0);
+		const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
+		const bool deep = et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
+		const uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
+		const bool more = live && !StreamOnly && deep && full > p.nch;
+		if (__ballot(more))  // wave-uniform
+		{
+			m_nch[lane] = more ? (full | (p.nch << 8)) : 0u;
+			__syncthreads();
+			gather();
+			__syncthreads();
+			p.nch = more ? full : p.nch;
+			set_lim();
+		}
 	}
+	Fast f;
+	const bool fast = live && !StreamOnly && fast_walk(p, cap, prm, f);
 
 	// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
 	const uint32_t ml = prm.max_layers;
@@ -1649,8 +1696,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	w.l4i = -1;
 	w.l4o = w.l4dlen = 0;
 	w.is_tcp = false;
-	Fast f;
-	bool fast = false;
 	uint32_t h5 = 0, h5d = 0, h2 = 0, ipc = 0, ips = 0, l4c = 0, l4s = 0;
 	if (live && StreamOnly)
 	{
@@ -1662,13 +1707,12 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	}
 	else if (live)
 	{
-		fast = fast_walk(p, cap, prm, f);
 		if (fast)
 		{
 			fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
 			fast_l7(p, f, cap);
 			w = fast_to_walk(f, ml);
-			if (prm.want_csum && w.v4 >= 0)
+			if (want_csum && w.v4 >= 0)
 			{
 				ipc = fast_ipv4_checksum(p, w, &ips);
 				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
@@ -1679,7 +1723,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 			w = walk_chain(p, cap, prm, lay_out);
 			hashes(p, w, h5, h5d, h2);
-			if (prm.want_csum && w.v4 >= 0)
+			if (want_csum && w.v4 >= 0)
 			{
 				ipc = ipv4_checksum(p, w, &ips);
 				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
@@ -1691,7 +1735,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	const uint32_t tcp_fl = (prm.reasm != nullptr && fast && f.simple() && f.tcp()) ? (uint32_t)p.s[p.mis + f.l4o() + 13] : 0u;
 
 	// ---- (4) L4 checksums over the tile span ----
-	if (prm.want_csum)  // uniform
+	if (want_csum)  // uniform
 	{
 		const bool need = live && w.l4i >= 0;
 		const uintptr_t as = (uintptr_t)p.g + w.l4o, ae = as + w.l4dlen;
@@ -1777,7 +1821,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	{
 		const uint32_t l4b = w.l4i >= 0 ? (uint32_t)w.l4i : 0xFFu;
 		u32x4 s0, s1;
-		s0.x = h5; s0.y = h5d; s0.z = h2; s0.w = w.flags | (w.n_layers << 16) | (l4b << 24);
+		s0.x = h5; s0.y = h5d; s0.z = h2; s0.w = w.flags | (MarkFast && fast ? 0x8000u : 0u) | (w.n_layers << 16) | (l4b << 24);
 		s1.x = (uint32_t)w.mask; s1.y = (uint32_t)(w.mask >> 32); s1.z = ipc | (ips << 16); s1.w = l4c | (l4s << 16);
 		u32x4* so = reinterpret_cast<u32x4*>(prm.summary + i);
 		__builtin_nontemporal_store(s0, so);
@@ -1786,36 +1830,34 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	else if (in)
 		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
 
-	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores ----
+	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
+	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
 	if (stage_layers && ml > kRowMaxMl)  // uniform: deep records, each fast lane stores its own row
 	{
 		if (fast)
 		{
 			uint2* dst = reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml;
-			for (uint32_t k = 0; k < ml; ++k)
-				dst[k] = k < w.n_layers ? fast_layer(f, cap, k) : make_uint2(0, 0);
+			fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) { dst[k] = r; });
 		}
 	}
 	else if (stage_layers)  // uniform
 	{
 		__syncthreads();  // every lane is done with the header stage
-		m_nch[lane] = fast ? 1u : 0u;
+		m_nch[lane] = fast ? (FillTails ? ml : w.n_layers) : 0u;  // records of the row to store
 		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 		typedef __attribute__((address_space(3))) u32x2* lptr64w;
 		lptr64w rows = (lptr64w)(stage);
 		const uint32_t rs = ml + 1;  // padded row stride (records): breaks the power-of-two bank pattern
-		if (fast)
-		{
-			const uint32_t cnt = w.n_layers;
+		if (FillTails && fast)
 			for (uint32_t k = 0; k < ml; ++k)
-			{
-				const uint2 r = k < cnt ? fast_layer(f, cap, k) : make_uint2(0, 0);
+				rows[lane * rs + k] = u32x2{ 0u, 0u };
+		if (fast)
+			fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) {
 				u32x2 e;
 				e.x = r.x;
 				e.y = r.y;
 				rows[lane * rs + k] = e;
-			}
-		}
+			});
 		__syncthreads();
 		const uint32_t first = blockIdx.x * kTile;
 		const uint32_t nrows = prm.n - first < (uint32_t)kTile ? prm.n - first : (uint32_t)kTile;
@@ -1825,7 +1867,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		for (uint32_t r0 = 0; r0 < nrows; r0 += per)
 		{
 			const uint32_t r = r0 + rr;
-			if (rr < per && r < nrows && m_nch[r])
+			if (rr < per && r < nrows && kk < m_nch[r])
 			{
 				if (NT)
 					__builtin_nontemporal_store(rows[r * rs + kk], &dst[r * ml + kk]);
@@ -2263,6 +2305,12 @@ Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, 
 // other shapes are built only into tools/ab/libpcppx_ab.so)
 constexpr int kParseWaves = 5, kParseSWin = 128;
 #define PCPPX_PARSE_KERNEL parse_tile_kernel<kParseWaves, kParseSWin, kTStageChunks, true>
+// parse-only launches (no checksums): no span stream; a 144-B window reached in two gather rounds (96 B for every
+// packet, the rest only for the deep stacks the first window cannot hold): 99.7% of config 5's deep stacks take the
+// fast path; 16 waves/CU of LDS (144 B: 0.88 ms on config 5, 160 B: 1.00 ms at 14 waves/CU, 112 B: 1.17 ms with
+// 22% of the packets on the generic walk; gpurun_out r02l_ab_cfg5 -> profiles/r02_ab_parse_only.txt)
+constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
+#define PCPPX_PARSE_ONLY_KERNEL parse_tile_kernel<1, 64, kParseOnlyChunks, true, false, false, kParseOnlyChunks1>
 
 // the flow-table shape: 1024-thread blocks, 8192 LDS slots, 4096-packet batches with the next batch prefetched,
 // 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)
@@ -2288,7 +2336,11 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 	if (b->n == 0)
 		return PCPPX_OK;
 	const Params prm = make_params(b, o, r, nullptr);
-	hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
+	const dim3 grid((b->n + kTile - 1) / kTile);
+	if (o->want_checksums)
+		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else
+		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel", stream);
 }
 
@@ -2298,7 +2350,11 @@ int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records*
 	if (b->n == 0)
 		return PCPPX_OK;
 	const Params prm = make_params(b, o, r, info);
-	hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, dim3((b->n + kTile - 1) / kTile), dim3(kTile), 0, stream, prm);
+	const dim3 grid((b->n + kTile - 1) / kTile);
+	if (o->want_checksums)
+		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else
+		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel(reasm)", stream);
 }
 

@@ -9,7 +9,10 @@ from pathlib import Path
 from pcapplusplus_amd import abi
 
 AB_SO = Path(__file__).resolve().parent / "libpcppx_ab.so"
+R01_SO = Path(__file__).resolve().parent / "r01" / "libpcppx_r01.so"
 _lib = None
+_r01 = None
+R01 = -1  # parse_device variant: the round-1 product kernel (tools/ab/r01, rebuilt from git history)
 
 # pcppx_ab_parse_device variants (tools/ab/pcppx_ab.hip)
 LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ, TILE_W5_WIN256, TILE_W1_WIN128, TILE_W1_WIN256, TILE_CACHED = \
@@ -32,10 +35,27 @@ def lib() -> C.CDLL:
     return _lib
 
 
+def r01_lib() -> C.CDLL:
+    global _r01
+    if _r01 is None:
+        if not R01_SO.exists():
+            raise RuntimeError(f"{R01_SO} missing: run `make -C tools/ab/r01`")
+        abi.load_engine()
+        l = C.CDLL(str(R01_SO))
+        l.pcppx_r01_parse_device.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Opts), C.POINTER(abi.Records), C.c_void_p]
+        l.pcppx_r01_parse_device.restype = C.c_int
+        _r01 = l
+    return _r01
+
+
 def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers, stream: int,
                  variant: int) -> None:
     b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
     rec = abi.Records(abi.ptr(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None)
+    if variant == R01:  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
+        abi.check(r01_lib().pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
+                  "pcppx_r01_parse_device")
+        return
     abi.check(lib().pcppx_ab_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0), variant),
               "pcppx_ab_parse_device")
 

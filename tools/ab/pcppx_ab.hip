@@ -174,6 +174,17 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 6: hipLaunchKernelGGL((parse_tile_kernel<1, 128>), grid, dim3(kTile), 0, stream, prm); break;
 	case 8: hipLaunchKernelGGL((parse_tile_kernel<1, 256>), grid, dim3(kTile), 0, stream, prm); break;
 	case 11: hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm); break;
+	case 12: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 7, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // chain records only
+	// parse-only instances (checksums off in opts): window chunks / first-round chunks
+	case 20: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, false, 7>), grid, dim3(kTile), 0, stream, prm); break;
+	case 21: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 10>), grid, dim3(kTile), 0, stream, prm); break;
+	case 22: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	case 23: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
+	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
+	// the product shapes with flags bit 0x8000 marking the packets the fast path took (records otherwise equal)
+	case 30: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 7, true>), grid, dim3(kTile), 0, stream, prm); break;
+	case 31: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 6, true>), grid, dim3(kTile), 0, stream, prm); break;
 	default: return launch_parse(b, o, r, stream);
 	}
 	return check_launch("pcppx_ab_parse_device", stream);

@@ -23,9 +23,11 @@ data, offs, caps = to_device(b)
 summ = torch.empty(n * 32, dtype=torch.uint8, device="cuda:0")
 lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device="cuda:0")
 st = torch.cuda.current_stream()
-read_bytes = int(b.caplens.sum(dtype=np.int64)) + 12 * n
+read_bytes = int(b.caplens.sum(dtype=np.int64)) + 12 * n  # the checksum runs' algorithmic read
 cases = {
     "tile/ml8/csum": (abi.make_opts(0, 8, True, 8), 0),
+    "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
+    "tile/chaintails": (abi.make_opts(0, 8, True, 8), 12),
     "lane/ml8/csum": (abi.make_opts(0, 8, True, 8), 1),
     "tile/ml0/csum": (abi.make_opts(0, 8, True, 0), 0),
     "tile/ml8/nocsum": (abi.make_opts(0, 8, False, 8), 0),
@@ -37,6 +39,18 @@ cases = {
     "diag/tile-read": (abi.make_opts(0, 8, True, 0), 3),
     "diag/grid-read": (abi.make_opts(0, 8, True, 0), 4),
 }
+# parse-only instances (checksums off): LDS window chunks / first-round chunks; records per packet AB_ML
+_ml = int(__import__("os").environ.get("AB_ML", "8"))
+cases.update({
+    "po/product": (abi.make_opts(0, 8, False, _ml), 0),
+    "po/w7": (abi.make_opts(0, 8, False, _ml), 20),
+    "po/w10": (abi.make_opts(0, 8, False, _ml), 21),
+    "po/w10r6": (abi.make_opts(0, 8, False, _ml), 22),
+    "po/w9r6": (abi.make_opts(0, 8, False, _ml), 23),
+    "po/w10r5": (abi.make_opts(0, 8, False, _ml), 24),
+    "po/w7r5": (abi.make_opts(0, 8, False, _ml), 25),
+    "po/r01": (abi.make_opts(0, 8, False, _ml), -1),
+})
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")
 if only:
@@ -45,16 +59,16 @@ if only:
 ref_s = ref_l = None
 want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
-    if o.max_layers != 8 or o.want_checksums != want_csum_ref or v in (2, 3, 4):
+    if o.max_layers != next(iter(cases.values()))[0].max_layers or o.want_checksums != want_csum_ref or v in (2, 3, 4):
         continue
     summ.zero_()
     lay.zero_()
     ab.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream, v)
     torch.cuda.synchronize()
     if ref_s is None:
-        ref_s, ref_l = summ.clone(), lay[: n * 64].clone()
+        ref_s, ref_l = summ.clone(), lay[: n * 8 * o.max_layers].clone()
     else:
-        same = torch.equal(summ, ref_s) and torch.equal(lay[: n * 64], ref_l)
+        same = torch.equal(summ, ref_s) and torch.equal(lay[: n * 8 * o.max_layers], ref_l)
         print(f"{name:18s} records identical to first variant: {same}", flush=True)
         if not same:
             raise SystemExit(f"{name}: records differ")
