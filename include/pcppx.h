@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PCPPX_ABI_VERSION 2
+#define PCPPX_ABI_VERSION 3
 /* the library is built with hidden visibility: exactly the functions declared here are exported */
 #define PCPPX_API __attribute__((visibility("default")))
 #define PCPPX_MAX_LAYERS 16     /* fixed depth cap; deeper chains set PCPPX_F_DEPTH_OVERFLOW */
@@ -265,16 +265,28 @@ PCPPX_API int pcppx_reasm_device(pcppx_ctx* ctx, const pcppx_batch* batch, const
 PCPPX_API int pcppx_parse_batch_device_reasm(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
                                    pcppx_records* out, pcppx_reasm_info* info, void* hip_stream);
 
-/* ---- host ingest: pcap files into packed batch buffers ---- */
+/* ---- host ingest: pcap / pcapng captures into packed batch buffers ---- */
 typedef struct pcppx_pcap pcppx_pcap;
-PCPPX_API int pcppx_pcap_open(const char* path, pcppx_pcap** out); /* PcapFileReaderDevice::open, PcapFileDevice.cpp:707-768 */
+/* Open a capture; the format comes from its first 4 bytes as IFileReaderDevice::createReader
+ * (Pcap++/src/PcapFileDevice.cpp:546-583): pcap as PcapFileReaderDevice::open (:707-768, incl. its version
+ * and snapshot-length checks), pcapng as PcapNgFileReaderDevice::open (:1157-1176, LightPcapNg). */
+PCPPX_API int pcppx_pcap_open(const char* path, pcppx_pcap** out);
+/* RawPacket::getLinkLayerType of the packets of the last batch returned (before the first batch: of the
+ * first packet). pcap: the file header's, LINKTYPE_INVALID (0xFFFF) outside LinkLayerType; pcapng: the
+ * packet's interface's. */
 PCPPX_API uint32_t pcppx_pcap_linktype(const pcppx_pcap* reader);
 /* Append up to max_packets records back to back into data[0, data_cap) (pinned memory feeds
  * pcppx_parse_batch_host without a staging copy); *n_out = packets read (0 at end of file). Record checks
- * as PcapFileReaderDevice::readNextPacket, PcapFileDevice.cpp:799-880. */
+ * as PcapFileReaderDevice::readNextPacket (PcapFileDevice.cpp:799-886) / light_get_next_packet. A batch
+ * holds one link type: it ends before a packet of another (pcapng interfaces). timestamps_ns may be NULL. */
 PCPPX_API int pcppx_pcap_read_batch(pcppx_pcap* reader, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
                           uint32_t* caplens, uint64_t* timestamps_ns, uint32_t max_packets, uint32_t* n_out,
                           uint64_t* bytes_out);
+/* as pcppx_pcap_read_batch, plus each packet's original (wire) length, RawPacket::getFrameLength
+ * (frame_lens may be NULL) */
+PCPPX_API int pcppx_pcap_read_batch_ex(pcppx_pcap* reader, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
+                          uint32_t* caplens, uint32_t* frame_lens, uint64_t* timestamps_ns, uint32_t max_packets,
+                          uint32_t* n_out, uint64_t* bytes_out);
 PCPPX_API void pcppx_pcap_close(pcppx_pcap* reader);
 PCPPX_API void* pcppx_host_alloc(size_t bytes); /* page-locked host memory (hipHostMalloc) */
 PCPPX_API void pcppx_host_free(void* p);

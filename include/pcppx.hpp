@@ -149,6 +149,7 @@ struct RawPacketVector
 	std::vector<uint64_t> offsets;
 	std::vector<uint32_t> caplens;
 	std::vector<uint64_t> timestampsNs;
+	std::vector<uint32_t> frameLens; /* RawPacket::getFrameLength (original wire length) */
 	uint16_t linkType = 1; /* LINKTYPE_ETHERNET */
 
 	size_t size() const { return caplens.size(); }
@@ -158,6 +159,7 @@ struct RawPacketVector
 		offsets.clear();
 		caplens.clear();
 		timestampsNs.clear();
+		frameLens.clear();
 	}
 	/* RawPacket::setRawData-style append (Packet++/header/RawPacket.h) */
 	void add(const uint8_t* bytes, uint32_t len, uint64_t tsNs = 0)
@@ -165,6 +167,7 @@ struct RawPacketVector
 		offsets.push_back(data.size());
 		caplens.push_back(len);
 		timestampsNs.push_back(tsNs);
+		frameLens.push_back(len);
 		data.insert(data.end(), bytes, bytes + len);
 	}
 	const uint8_t* packetData(size_t i) const { return data.data() + offsets[i]; }
@@ -176,7 +179,9 @@ struct RawPacketVector
 };
 using RawBatch = RawPacketVector;
 
-/* PcapFileReaderDevice (Pcap++/header/PcapFileDevice.h): open / getNextPackets / close */
+/* PcapFileReaderDevice / PcapNgFileReaderDevice (Pcap++/header/PcapFileDevice.h): open / getNextPackets / close.
+ * The format (pcap or pcapng) comes from the file's first bytes; a batch holds one link type (pcapng
+ * interfaces may differ), given by getLinkLayerType() after the batch is read. */
 class PcapFileReaderDevice
 {
 public:
@@ -206,15 +211,17 @@ public:
 		batch.offsets.resize(maxPackets);
 		batch.caplens.resize(maxPackets);
 		batch.timestampsNs.resize(maxPackets);
+		batch.frameLens.resize(maxPackets);
 		uint32_t n = 0;
 		uint64_t used = 0;
-		check(pcppx_pcap_read_batch(m_Reader, batch.data.data(), maxBytes, batch.offsets.data(), batch.caplens.data(),
-		                            batch.timestampsNs.data(), maxPackets, &n, &used),
-		      "pcppx_pcap_read_batch");
+		check(pcppx_pcap_read_batch_ex(m_Reader, batch.data.data(), maxBytes, batch.offsets.data(), batch.caplens.data(),
+		                               batch.frameLens.data(), batch.timestampsNs.data(), maxPackets, &n, &used),
+		      "pcppx_pcap_read_batch_ex");
 		batch.data.resize(used);
 		batch.offsets.resize(n);
 		batch.caplens.resize(n);
 		batch.timestampsNs.resize(n);
+		batch.frameLens.resize(n);
 		batch.linkType = (uint16_t)getLinkLayerType();
 		return (int)n;
 	}
@@ -223,6 +230,8 @@ private:
 	std::string m_FileName;
 	pcppx_pcap* m_Reader = nullptr;
 };
+using PcapNgFileReaderDevice = PcapFileReaderDevice;
+using IFileReaderDevice = PcapFileReaderDevice;
 
 /* One layer of a parsed packet: Layer::getProtocol / getOsiModelLayer / getData / getHeaderLen / getDataLen /
  * getLayerPayloadSize / isMemberOfProtocolFamily (Packet++/header/Layer.h) */

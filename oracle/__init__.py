@@ -66,6 +66,9 @@ def ref_lib() -> C.CDLL:
         lib.pcppx_ref_filter.restype = C.c_int
         lib.pcppx_ref_reasm.argtypes = [C.POINTER(abi.Batch), C.c_void_p]
         lib.pcppx_ref_reasm.restype = C.c_int
+        lib.ref_read_capture.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+        lib.ref_read_capture.restype = C.c_int
         _ref = lib
     return _ref
 
@@ -86,6 +89,29 @@ def oracle_parse(batch, opts: abi.Opts | None = None, threads: int = 1):
     if rc != 0:
         raise RuntimeError(f"oracle parse failed {rc}")
     return summary, layers[: batch.n * opts.max_layers].reshape(batch.n, opts.max_layers)
+
+
+def ref_read_capture(path) -> dict | None:
+    """Every packet of a capture as the reference's own file device reads it (PcapFileReaderDevice /
+    PcapNgFileReaderDevice getNextPacket, oracle/ref_ingest.cpp): None if the device does not open, else
+    {data, caplens, frame_lens, ts_ns, linktypes} (numpy arrays; data back to back)."""
+    lib = ref_lib()
+    size = max(Path(path).stat().st_size, 1)
+    cap_bytes, cap_n = 2 * size + 4096, size // 8 + 64
+    while True:
+        data = np.empty(cap_bytes, np.uint8)
+        cl, fl, lt = (np.empty(cap_n, np.uint32) for _ in range(3))
+        ts = np.empty(cap_n, np.uint64)
+        used = C.c_uint64(0)
+        n = lib.ref_read_capture(str(path).encode(), data.ctypes.data, cap_bytes, cl.ctypes.data, fl.ctypes.data,
+                                 ts.ctypes.data, lt.ctypes.data, cap_n, C.byref(used))
+        if n == -1:
+            return None
+        if n == -2:
+            cap_bytes, cap_n = cap_bytes * 4, cap_n * 4
+            continue
+        return {"data": data[: used.value].copy(), "caplens": cl[:n].copy(), "frame_lens": fl[:n].copy(),
+                "ts_ns": ts[:n].copy(), "linktypes": lt[:n].copy()}
 
 
 def ref_parse(batch, opts: abi.Opts | None = None):

@@ -696,3 +696,20 @@ extern "C"
 		return PCPPX_OK;
 	}
 }
+
+extern "C"
+{
+	void* pcppx_host_alloc(size_t bytes)
+	{
+		void* p = nullptr;
+		if (hipHostMalloc(&p, bytes ? bytes : 1) != hipSuccess)
+			return nullptr;
+		return p;
+	}
+
+	void pcppx_host_free(void* p)
+	{
+		if (p)
+			(void)hipHostFree(p);
+	}
+}

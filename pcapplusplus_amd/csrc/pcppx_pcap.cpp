@@ -1,17 +1,48 @@
-// pcppx_pcap.cpp — host ingest: pcap files straight into packed (optionally pinned) batch buffers.
+// pcppx_pcap.cpp — host ingest: pcap and pcapng captures straight into packed (optionally pinned) batches.
 //
-// Follows the reference reader's rules (Pcap++/src/PcapFileDevice.cpp): magic detection incl. the
-// swapped, nanosecond and Kuznetzov variants (:53-60, :667-705), the 24-B file header and 16-B record
-// header (:66-87), and readNextPacket's checks (:799-880): caplen > len, caplen > 256 KiB or an
-// out-of-range sub-second field end the stream; caplen beyond the snapshot length is truncated.
-// Unlike PcapFileReaderDevice::getNextPacket (:770-792: one heap allocation + copy per packet), records
-// are copied once from a memory-mapped file into the caller's batch buffers, back to back.
+// Plain C++ (no HIP): the same file builds into libpcppx.so and into the host-only sanitizer/fuzz
+// driver (tools/ingest_fuzz.cpp, -fsanitize=address,undefined).
+//
+// The format is detected from the first four bytes, as IFileReaderDevice::createReader does
+// (Pcap++/src/PcapFileDevice.cpp:283-325,404-458), and read as the device for that format would:
+//
+// pcap — PcapFileReaderDevice (PcapFileDevice.cpp):
+//   open (:707-768): 24-B file header; the six pcap magics (:53-60, :283-325; the Kuznetzov "modified"
+//   magics are accepted but, like the reference, read with the plain 16-B record header of :79-86);
+//   version_major 2 or 543 (:747); 0 < snaplen <= 1 MiB (:754-759); linktype through toLinkLayerType
+//   (:89-209: a value outside the LinkLayerType list becomes LINKTYPE_INVALID 0xFFFF).
+//   readNextPacket (:799-886): a short record header, caplen > len, caplen > 256 KiB, a sub-second
+//   field out of range, or packet bytes cut by the end of the file end the stream; caplen beyond the
+//   snapshot length keeps the first snaplen bytes and skips the rest (a skip that runs past the end of
+//   the file still delivers the packet: istream::ignore only sets eofbit).
+//
+// pcapng — PcapNgFileReaderDevice (:1157-1243) over LightPcapNg
+//   (3rdParty/LightPcapNg/LightPcapNg/src/light_pcapng.c, light_pcapng_ext.c):
+//   light_read_record (light_pcapng.c:341-423): type + total length + body + trailing length; a short
+//   read or a trailing length that differs ends the stream. The first block must be a section header
+//   (light_pcapng_ext.c:43-55), else the capture holds no packets.
+//   light_get_next_packet (light_pcapng_ext.c:380-479): blocks other than EPB/SPB are skipped; every
+//   interface description block met on the way is appended to one file-wide list (at most 32,
+//   MAX_SUPPORTED_INTERFACE_BLOCKS; sections do not reset it), with its link type (u16) and
+//   timestamp resolution from if_tsresol (:140-167: 10^v or 2^(v-128) ticks/s into a uint32, default
+//   10^6; options parsed as __parse_options, light_pcapng.c:36-93).
+//   EPB (light_pcapng.c:150-194): caplen clamped to block_total_length - 32 (GH #2180 patch); an
+//   interface id outside the list gives linktype 0xFFFF and timestamp 0; a timestamp whose seconds are
+//   0 or exceed UINT64_MAX / 1e9 is 0 (light_pcapng_ext.c:419-445).
+//   SPB (light_pcapng.c:196-211, light_pcapng_ext.c:451-466): caplen = original length, linktype of
+//   interface 0, timestamp 0.
+//   Where the reference's behaviour is undefined (it reads past its heap buffer), this reader ends the
+//   stream instead: a block total length below 12 (SPB: 16), an EPB/IDB body shorter than its fixed
+//   fields (a short section header only gives it a garbage version: it still opens the section), an SPB whose original length exceeds its body (we keep the body), or an SPB before any
+//   interface (the reference reads an uninitialised link type; we return 0xFFFF).
+//
+// Unlike getNextPacket (one heap allocation + copy per packet, :770-792), records are copied once from
+// a memory-mapped file into the caller's batch buffers, back to back. A batch holds packets of one link
+// type only (pcapng interfaces may differ): it ends before a packet of another link type.
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
-
-#include <hip/hip_runtime.h>
 
 #include <cstring>
 #include <new>
@@ -23,12 +54,67 @@ namespace
 constexpr uint32_t kMagic = 0xa1b2c3d4, kMagicSwapped = 0xd4c3b2a1;
 constexpr uint32_t kKuz = 0xa1b2cd34, kKuzSwapped = 0x34cdb2a1;
 constexpr uint32_t kNsec = 0xa1b23c4d, kNsecSwapped = 0x4d3cb2a1;
-constexpr uint32_t kMaxRecord = 256 * 1024;
+constexpr uint32_t kPcapNgMagic = 0x0A0D0D0A;  // section header block type (PcapFileDevice.cpp:331-335)
+constexpr uint32_t kMaxRecord = 256 * 1024;     // readNextPacket MAX_PACKET_SIZE (:832)
+constexpr uint32_t kMaxSnaplen = 1024 * 1024;   // open MAX_SNAPLEN (:754)
+constexpr uint32_t kLinkInvalid = 0xFFFF;       // LINKTYPE_INVALID (Packet++/header/RawPacket.h:250)
+
+// pcapng block types and options (light_pcapng.h)
+constexpr uint32_t kShb = 0x0A0D0D0A, kIdb = 0x00000001, kSpb = 0x00000003, kEpb = 0x00000006;
+constexpr uint16_t kOptTsresol = 9;
+constexpr uint32_t kMaxInterfaces = 32;  // MAX_SUPPORTED_INTERFACE_BLOCKS (light_pcapng_ext.h:46)
 
 uint32_t sw32(uint32_t v)
 {
 	return __builtin_bswap32(v);
 }
+
+uint32_t ld32(const uint8_t* p)
+{
+	uint32_t v;
+	std::memcpy(&v, p, 4);
+	return v;
+}
+
+uint16_t ld16(const uint8_t* p)
+{
+	uint16_t v;
+	std::memcpy(&v, p, 2);
+	return v;
+}
+
+// toLinkLayerType (PcapFileDevice.cpp:89-209): the LinkLayerType values of RawPacket.h:24-248
+bool known_linktype(uint32_t v)
+{
+	static const uint16_t kKnown[] = {
+		0,   1,   3,   6,   7,   8,   9,   10,  12,  14,  50,  51,  100, 101, 104, 105, 107, 108, 113, 114, 117,
+		119, 122, 123, 127, 129, 138, 139, 140, 141, 142, 143, 144, 147, 148, 149, 150, 151, 152, 153, 154, 155,
+		156, 157, 158, 159, 160, 161, 162, 163, 165, 166, 169, 170, 171, 177, 187, 189, 192, 195, 196, 197, 201,
+		202, 203, 204, 205, 206, 209, 215, 220, 224, 225, 226, 227, 228, 229, 230, 231, 235, 236, 237, 239, 240,
+		241, 242, 243, 244, 245, 247, 248, 249, 250, 251, 253, 254, 255, 256, 257, 258, 259, 260, 261, 262, 263,
+		264, 276,
+	};
+	for (uint16_t k : kKnown)
+		if (v == k)
+			return true;
+	return false;
+}
+
+uint64_t int_pow(uint64_t x, uint32_t y)
+{
+	uint64_t r = 1;
+	for (uint32_t i = 0; i < y; ++i)
+		r *= x;
+	return r;
+}
+
+struct Packet
+{
+	const uint8_t* bytes;
+	uint32_t keep, frame_len, linktype;
+	uint64_t ts_ns;
+	size_t next_pos;  // where the stream continues after this packet
+};
 }  // namespace
 
 struct pcppx_pcap
@@ -36,11 +122,158 @@ struct pcppx_pcap
 	const uint8_t* map = nullptr;
 	size_t size = 0;
 	size_t pos = 0;
+	bool ng = false;
 	bool swap = false, nsec = false;
-	uint32_t rec_hdr = 16;
 	uint32_t snaplen = 0;
-	uint32_t linktype = 0;
+	uint32_t linktype = 0;  // pcap: the file's; pcapng: of the last batch returned (before it: of the first packet)
 	bool done = false;
+	// pcapng: the file-wide interface list of light_pcapng_file_info
+	uint32_t n_if = 0;
+	uint16_t if_link[kMaxInterfaces];
+	uint32_t if_ticks[kMaxInterfaces];
+
+	// pcap record at pos (readNextPacket). false = the stream ends here.
+	bool next_pcap(Packet& pk) const
+	{
+		if (size - pos < 16)
+			return false;
+		uint32_t h[4];
+		std::memcpy(h, map + pos, 16);
+		if (swap)
+			for (uint32_t& x : h)
+				x = sw32(x);
+		const uint32_t sec = h[0], sub = h[1], cap = h[2], len = h[3];
+		if (cap > len || cap > kMaxRecord || sub >= (nsec ? 1000000000u : 1000000u))
+			return false;
+		const uint32_t keep = cap > snaplen ? snaplen : cap;
+		const size_t body = pos + 16;
+		if (size - body < keep)
+			return false;  // "Failed to read packet data"
+		pk.bytes = map + body;
+		pk.keep = keep;
+		pk.frame_len = len;
+		pk.linktype = linktype;
+		pk.ts_ns = (uint64_t)sec * 1000000000ull + (nsec ? sub : (uint64_t)sub * 1000ull);
+		pk.next_pos = (size - body < cap) ? size : body + cap;  // the skipped tail may run past the end
+		return true;
+	}
+
+	// light_read_record at p: block type, total length and body bounds; false = the stream ends.
+	bool ng_block(size_t p, uint32_t& type, uint32_t& total) const
+	{
+		if (size - p < 8)
+			return false;
+		type = ld32(map + p);
+		total = ld32(map + p + 4);
+		if (total < 12 || size - p < (size_t)total)
+			return false;
+		return ld32(map + p + total - 4) == total;
+	}
+
+	// __append_interface_block_to_file_info for the IDB at p (light_pcapng_ext.c:140-167)
+	bool ng_interface(size_t p, uint32_t total)
+	{
+		if (total < 20)
+			return false;  // link type + reserved + snaplen do not fit
+		const uint8_t* body = map + p + 8;
+		if (n_if >= kMaxInterfaces)
+			return true;
+		uint32_t ticks = 1000000;
+		// __parse_options (light_pcapng.c:36-93): max_len = total - 20 bytes of options; stop at the end
+		// option, a length that does not fit, or a zero-length option.
+		int32_t max_len = (int32_t)(total - 20);
+		const uint8_t* o = body + 8;
+		while (max_len > 4)
+		{
+			const uint16_t code = ld16(o), len = ld16(o + 2);
+			if ((int32_t)len > max_len - 4)
+				break;
+			const uint16_t actual = (len % 4) == 0 ? len : (uint16_t)((len / 4 + 1) * 4);
+			if (actual == 0 || (int32_t)actual > max_len - 4)
+				break;
+			if (code == kOptTsresol)
+			{
+				const uint8_t v = o[4];
+				ticks = (uint32_t)(v < 128 ? int_pow(10, v) : int_pow(2, v - 128u));
+				break;  // light_get_option returns the first match
+			}
+			if (code == 0)
+				break;
+			o += 4 + actual;
+			max_len = (uint16_t)(max_len - actual - 4);  // remaining_size is a uint16_t
+		}
+		if_link[n_if] = ld16(body);
+		if_ticks[n_if] = ticks;
+		++n_if;
+		return true;
+	}
+
+	// light_get_next_packet from pos: interface blocks on the way are appended (and pos moves past
+	// them, so a packet left for the next batch does not append them twice).
+	bool next_pcapng(Packet& pk)
+	{
+		for (;;)
+		{
+			uint32_t type, total;
+			if (!ng_block(pos, type, total))
+				return false;
+			if (type == kIdb)
+			{
+				if (!ng_interface(pos, total))
+					return false;
+				pos += total;
+				continue;
+			}
+			if (type == kEpb)
+			{
+				if (total < 32)
+					return false;  // the five fixed fields do not fit
+				const uint8_t* body = map + pos + 8;
+				const uint32_t ifid = ld32(body), hi = ld32(body + 4), lo = ld32(body + 8);
+				uint32_t cap = ld32(body + 12);
+				const uint32_t orig = ld32(body + 16);
+				const uint32_t max_cap = total > 32 ? total - 32 : 0;
+				if (cap > max_cap)
+					cap = max_cap;
+				pk.bytes = body + 20;
+				pk.keep = cap;
+				pk.frame_len = orig;
+				pk.ts_ns = 0;
+				pk.linktype = kLinkInvalid;
+				if (ifid < n_if)
+				{
+					const uint64_t t = ((uint64_t)hi << 32) + lo;
+					const uint64_t tps = if_ticks[ifid];
+					const uint64_t secs = tps != 0 ? t / tps : 0;
+					if (secs <= UINT64_MAX / 1000000000ull && secs != 0)
+						pk.ts_ns = secs * 1000000000ull + (1000000000ull * (t % tps)) / tps;
+					pk.linktype = if_link[ifid];
+				}
+				pk.next_pos = pos + total;
+				return true;
+			}
+			if (type == kSpb)
+			{
+				if (total < 16)
+					return false;
+				const uint8_t* body = map + pos + 8;
+				const uint32_t orig = ld32(body), avail = total - 16;
+				pk.bytes = body + 4;
+				pk.keep = orig < avail ? orig : avail;
+				pk.frame_len = orig;
+				pk.ts_ns = 0;
+				pk.linktype = n_if > 0 ? if_link[0] : kLinkInvalid;
+				pk.next_pos = pos + total;
+				return true;
+			}
+			pos += total;  // section header, statistics, name resolution, custom, unknown: skipped
+		}
+	}
+
+	bool next(Packet& pk)
+	{
+		return ng ? next_pcapng(pk) : next_pcap(pk);
+	}
 };
 
 extern "C"
@@ -54,7 +287,7 @@ extern "C"
 		if (fd < 0)
 			return PCPPX_E_INVAL;
 		struct stat st;
-		if (fstat(fd, &st) != 0 || st.st_size < 24)
+		if (fstat(fd, &st) != 0 || st.st_size < 4)
 		{
 			close(fd);
 			return PCPPX_E_INVAL;
@@ -72,26 +305,54 @@ extern "C"
 		}
 		r->map = static_cast<const uint8_t*>(m);
 		r->size = (size_t)st.st_size;
-		uint32_t magic;
-		std::memcpy(&magic, r->map, 4);
-		switch (magic)
-		{
-		case kMagic: break;
-		case kMagicSwapped: r->swap = true; break;
-		case kNsec: r->nsec = true; break;
-		case kNsecSwapped: r->nsec = r->swap = true; break;
-		case kKuz: r->rec_hdr = 24; break;
-		case kKuzSwapped: r->rec_hdr = 24; r->swap = true; break;
-		default:
+		auto fail = [&](int rc) {
 			munmap(m, r->size);
 			delete r;
-			return PCPPX_E_INVAL;
+			return rc;
+		};
+		const uint32_t magic = ld32(r->map);
+		if (magic == kPcapNgMagic)
+		{
+			// light_pcapng_open_read: the first record must be a well-formed section header, else the
+			// device opens with no packets (light_pcapng_ext.c:183-224, 43-55)
+			r->ng = true;
+			uint32_t type, total;
+			if (r->ng_block(0, type, total) && type == kShb)
+			{
+				r->pos = total;
+				Packet pk;
+				if (r->next_pcapng(pk))  // leaves pos at the first packet block (past the interfaces before it)
+					r->linktype = pk.linktype;  // the link type of the first batch
+			}
+			else
+				r->done = true;
+			*out = r;
+			return PCPPX_OK;
 		}
-		uint32_t snap, lt;
-		std::memcpy(&snap, r->map + 16, 4);
-		std::memcpy(&lt, r->map + 20, 4);
-		r->snaplen = r->swap ? sw32(snap) : snap;
-		r->linktype = (r->swap ? sw32(lt) : lt) & 0x0FFFFFFF;
+		switch (magic)
+		{
+		case kMagic: case kKuz: break;
+		case kMagicSwapped: case kKuzSwapped: r->swap = true; break;
+		case kNsec: r->nsec = true; break;
+		case kNsecSwapped: r->nsec = r->swap = true; break;
+		default: return fail(PCPPX_E_INVAL);  // not pcap / pcapng (snoop and zstd archives: not supported)
+		}
+		if (r->size < 24)
+			return fail(PCPPX_E_INVAL);  // "Cannot read pcap file header"
+		uint16_t vmaj = ld16(r->map + 4);
+		uint32_t snap = ld32(r->map + 16), lt = ld32(r->map + 20);
+		if (r->swap)
+		{
+			vmaj = (uint16_t)((vmaj >> 8) | (vmaj << 8));
+			snap = sw32(snap);
+			lt = sw32(lt);
+		}
+		if (vmaj != 2 && vmaj != 543)
+			return fail(PCPPX_E_INVAL);
+		if (snap == 0 || snap > kMaxSnaplen)
+			return fail(PCPPX_E_INVAL);
+		r->snaplen = snap;
+		r->linktype = known_linktype(lt) ? lt : kLinkInvalid;
 		r->pos = 24;
 		*out = r;
 		return PCPPX_OK;
@@ -102,41 +363,41 @@ extern "C"
 		return r ? r->linktype : 0;
 	}
 
-	int pcppx_pcap_read_batch(pcppx_pcap* r, uint8_t* data, uint64_t data_cap, uint64_t* offsets, uint32_t* caplens,
-	                          uint64_t* timestamps_ns, uint32_t max_packets, uint32_t* n_out, uint64_t* bytes_out)
+	int pcppx_pcap_read_batch_ex(pcppx_pcap* r, uint8_t* data, uint64_t data_cap, uint64_t* offsets, uint32_t* caplens,
+	                             uint32_t* frame_lens, uint64_t* timestamps_ns, uint32_t max_packets, uint32_t* n_out,
+	                             uint64_t* bytes_out)
 	{
 		if (r == nullptr || data == nullptr || offsets == nullptr || caplens == nullptr || n_out == nullptr)
 			return PCPPX_E_INVAL;
 		uint32_t n = 0;
 		uint64_t used = 0;
-		while (!r->done && n < max_packets && r->pos + r->rec_hdr <= r->size)
+		while (!r->done && n < max_packets)
 		{
-			uint32_t h[4];
-			std::memcpy(h, r->map + r->pos, 16);
-			if (r->swap)
-				for (uint32_t& x : h)
-					x = sw32(x);
-			const uint32_t sec = h[0], sub = h[1], cap = h[2], len = h[3];
-			if (cap > len || cap > kMaxRecord || sub >= (r->nsec ? 1000000000u : 1000000u) ||
-			    r->pos + r->rec_hdr + cap > r->size)
+			Packet pk;
+			if (!r->next(pk))
 			{
-				r->done = true;  // readNextPacket returns false: the stream ends here
+				r->done = true;  // readNextPacket / light_get_next_packet return false: the stream ends here
 				break;
 			}
-			const uint32_t keep = (r->snaplen != 0 && cap > r->snaplen) ? r->snaplen : cap;
-			if (used + keep > data_cap)
+			if (n > 0 && pk.linktype != r->linktype)
+				break;  // one link type per batch: the packet opens the next batch
+			if (used + pk.keep > data_cap)
 			{
 				if (n == 0)
 					return PCPPX_E_NOMEM;  // a single record does not fit the caller's buffer
 				break;
 			}
-			std::memcpy(data + used, r->map + r->pos + r->rec_hdr, keep);
+			r->linktype = pk.linktype;
+			if (pk.keep)
+				std::memcpy(data + used, pk.bytes, pk.keep);
 			offsets[n] = used;
-			caplens[n] = keep;
+			caplens[n] = pk.keep;
+			if (frame_lens)  // RawPacket::setRawData takes an int frameLength; -1 means "the captured length" (RawPacket.cpp:107)
+				frame_lens[n] = pk.frame_len == 0xFFFFFFFFu ? pk.keep : pk.frame_len;
 			if (timestamps_ns)
-				timestamps_ns[n] = (uint64_t)sec * 1000000000ull + (r->nsec ? sub : (uint64_t)sub * 1000ull);
-			used += keep;
-			r->pos += r->rec_hdr + cap;
+				timestamps_ns[n] = pk.ts_ns;
+			used += pk.keep;
+			r->pos = pk.next_pos;
 			++n;
 		}
 		*n_out = n;
@@ -145,25 +406,18 @@ extern "C"
 		return PCPPX_OK;
 	}
 
+	int pcppx_pcap_read_batch(pcppx_pcap* r, uint8_t* data, uint64_t data_cap, uint64_t* offsets, uint32_t* caplens,
+	                          uint64_t* timestamps_ns, uint32_t max_packets, uint32_t* n_out, uint64_t* bytes_out)
+	{
+		return pcppx_pcap_read_batch_ex(r, data, data_cap, offsets, caplens, nullptr, timestamps_ns, max_packets, n_out,
+		                                bytes_out);
+	}
+
 	void pcppx_pcap_close(pcppx_pcap* r)
 	{
 		if (r == nullptr)
 			return;
 		munmap(const_cast<uint8_t*>(r->map), r->size);
 		delete r;
-	}
-
-	void* pcppx_host_alloc(size_t bytes)
-	{
-		void* p = nullptr;
-		if (hipHostMalloc(&p, bytes ? bytes : 1) != hipSuccess)
-			return nullptr;
-		return p;
-	}
-
-	void pcppx_host_free(void* p)
-	{
-		if (p)
-			(void)hipHostFree(p);
 	}
 }

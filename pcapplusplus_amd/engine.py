@@ -115,8 +115,9 @@ class Engine:
 
 
 class PcapReader:
-    """Native pcap ingest (pcppx_pcap_*): records of a capture copied straight into packed batches.
-    Mirrors PcapFileReaderDevice (Pcap++/header/PcapFileDevice.h) open / getNextPackets / close."""
+    """Native capture ingest (pcppx_pcap_*): records of a pcap / pcapng capture copied straight into packed
+    batches. Mirrors IFileReaderDevice (Pcap++/header/PcapFileDevice.h) open / getNextPackets / close; each
+    batch carries one link type (RawPacket::getLinkLayerType), its timestamps and frame lengths."""
 
     def __init__(self, path: str, pinned: bool = False):
         self.lib = abi.load_engine()
@@ -130,14 +131,16 @@ class PcapReader:
         data = np.empty(data_cap, dtype=np.uint8)
         offsets = np.empty(max_packets, dtype=np.uint64)
         caplens = np.empty(max_packets, dtype=np.uint32)
+        frame_lens = np.empty(max_packets, dtype=np.uint32)
         ts = np.empty(max_packets, dtype=np.uint64)
         n, used = C.c_uint32(0), C.c_uint64(0)
-        abi.check(self.lib.pcppx_pcap_read_batch(self.handle, data.ctypes.data, data_cap, offsets.ctypes.data,
-                                                 caplens.ctypes.data, ts.ctypes.data, max_packets, C.byref(n),
-                                                 C.byref(used)), "pcppx_pcap_read_batch")
+        abi.check(self.lib.pcppx_pcap_read_batch_ex(self.handle, data.ctypes.data, data_cap, offsets.ctypes.data,
+                                                    caplens.ctypes.data, frame_lens.ctypes.data, ts.ctypes.data,
+                                                    max_packets, C.byref(n), C.byref(used)), "pcppx_pcap_read_batch_ex")
         k = n.value
+        self.linktype = int(self.lib.pcppx_pcap_linktype(self.handle))
         return PacketBatch(data[: used.value].copy(), offsets[:k].copy(), caplens[:k].copy(), self.linktype,
-                           timestamps_ns=ts[:k].copy())
+                           timestamps_ns=ts[:k].copy(), frame_lens=frame_lens[:k].copy())
 
     def close(self) -> None:
         if self.handle:
