@@ -8,7 +8,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -41,6 +43,103 @@ struct Slot
 	uint32_t first = 0, count = 0, ml = 0;
 };
 
+// memcpy split over persistent host threads (started with the host path, joined at pcppx_close): a single
+// core copies ~8-10 GB/s, below what the PCIe link takes. The caller copies part 0 itself.
+class CopyPool
+{
+public:
+	static constexpr unsigned kThreads = 16;
+
+	void start()
+	{
+		for (unsigned k = 1; k < kThreads; ++k)
+			m_threads.emplace_back([this, k] { work(k); });
+	}
+
+	void stop()
+	{
+		{
+			std::lock_guard<std::mutex> g(m_mu);
+			m_quit = true;
+		}
+		m_cv.notify_all();
+		for (auto& t : m_threads)
+			t.join();
+		m_threads.clear();
+		m_quit = false;
+	}
+
+	// one part per >= 4 MiB, at most kThreads parts
+	void copy(void* dst, const void* src, size_t bytes)
+	{
+		unsigned parts = (unsigned)(bytes >> 22);
+		parts = parts < 1 ? 1 : (parts > kThreads ? kThreads : parts);
+		if (parts == 1 || m_threads.empty())
+		{
+			std::memcpy(dst, src, bytes);
+			return;
+		}
+		const size_t per = ((bytes + parts - 1) / parts + 63) & ~(size_t)63;
+		{
+			std::lock_guard<std::mutex> g(m_mu);
+			m_dst = static_cast<uint8_t*>(dst);
+			m_src = static_cast<const uint8_t*>(src);
+			m_bytes = bytes;
+			m_per = per;
+			m_parts = parts;
+			m_left = 0;
+			for (unsigned k = 1; k < parts; ++k)
+				m_left += k * per < bytes ? 1 : 0;
+			++m_gen;
+		}
+		m_cv.notify_all();
+		std::memcpy(dst, src, per < bytes ? per : bytes);
+		std::unique_lock<std::mutex> g(m_mu);
+		m_done.wait(g, [&] { return m_left == 0; });
+	}
+
+private:
+	void work(unsigned k)
+	{
+		uint64_t seen = 0;
+		for (;;)
+		{
+			uint8_t* d;
+			const uint8_t* s;
+			size_t lo, len;
+			{
+				std::unique_lock<std::mutex> g(m_mu);
+				m_cv.wait(g, [&] { return m_quit || m_gen != seen; });
+				if (m_quit)
+					return;
+				seen = m_gen;
+				lo = k * m_per;
+				if (k >= m_parts || lo >= m_bytes)
+					continue;
+				len = m_bytes - lo < m_per ? m_bytes - lo : m_per;
+				d = m_dst + lo;
+				s = m_src + lo;
+			}
+			std::memcpy(d, s, len);
+			{
+				std::lock_guard<std::mutex> g(m_mu);
+				--m_left;
+			}
+			m_done.notify_one();
+		}
+	}
+
+	std::vector<std::thread> m_threads;
+	std::mutex m_mu;
+	std::condition_variable m_cv, m_done;
+	uint8_t* m_dst = nullptr;
+	const uint8_t* m_src = nullptr;
+	size_t m_bytes = 0, m_per = 0;
+	unsigned m_parts = 0, m_left = 0;
+	uint64_t m_gen = 0;
+	bool m_quit = false;
+};
+
 constexpr uint32_t kDefaultFlowSlots = 1u << 22;  // 64 MiB of flow table in HBM
 constexpr uint32_t kMaxSlots = 3;                   // host-path chunk slots in flight
 }  // namespace
@@ -52,6 +151,7 @@ struct pcppx_ctx
 	bool host_ready = false;
 	Slot slots[kMaxSlots];
 	uint32_t nslots = 0;  // slots allocated and used by the host paths
+	CopyPool copier;      // staging and drain copies of the host paths
 	// host filter path (pcppx_filter_reset / pcppx_filter_batch_host): the worker's flow table in HBM
 	uint64_t* d_keys = nullptr;
 	uint64_t* d_first = nullptr;
@@ -131,35 +231,9 @@ int init_host_path(pcppx_ctx* c)
 			return PCPPX_E_NOMEM;
 		}
 	}
+	c->copier.start();
 	c->host_ready = true;
 	return PCPPX_OK;
-}
-
-// memcpy split over host threads (one thread per >= 4 MiB, at most kCopyThreads): a single core copies
-// ~8-10 GB/s, below what the PCIe link takes
-constexpr unsigned kCopyThreads = 16;
-void par_copy(void* dst, const void* src, size_t bytes)
-{
-	unsigned t = (unsigned)(bytes >> 22);
-	t = t < 1 ? 1 : (t > kCopyThreads ? kCopyThreads : t);
-	if (t == 1)
-	{
-		std::memcpy(dst, src, bytes);
-		return;
-	}
-	const size_t per = ((bytes + t - 1) / t + 63) & ~(size_t)63;
-	std::vector<std::thread> th;
-	th.reserve(t);
-	for (unsigned k = 0; k < t; ++k)
-	{
-		const size_t lo = k * per;
-		if (lo >= bytes)
-			break;
-		const size_t len = bytes - lo < per ? bytes - lo : per;
-		th.emplace_back([=] { std::memcpy(static_cast<uint8_t*>(dst) + lo, static_cast<const uint8_t*>(src) + lo, len); });
-	}
-	for (auto& x : th)
-		x.join();
 }
 
 // true if p is page-locked host memory the GPU can DMA from directly
@@ -200,7 +274,8 @@ uint32_t contiguous_chunk(const pcppx_batch* b, uint32_t i, uint64_t* base, size
 // gather packets [i, j) of a host batch into the slot's pinned staging, rebasing offsets; returns j.
 // Contiguous runs are staged with one multi-threaded copy, or not at all when the caller's bytes are
 // already pinned (*direct is then the source of the H2D copy).
-uint32_t stage_chunk(Slot& s, const pcppx_batch* b, uint32_t i, size_t* pos_out, const uint8_t** direct, bool pinned_in)
+uint32_t stage_chunk(CopyPool& cp, Slot& s, const pcppx_batch* b, uint32_t i, size_t* pos_out, const uint8_t** direct,
+                     bool pinned_in)
 {
 	*direct = nullptr;
 	{
@@ -217,7 +292,7 @@ uint32_t stage_chunk(Slot& s, const pcppx_batch* b, uint32_t i, size_t* pos_out,
 			if (pinned_in)
 				*direct = b->data + base;
 			else
-				par_copy(s.h_data, b->data + base, bytes);
+				cp.copy(s.h_data, b->data + base, bytes);
 			*pos_out = bytes;
 			return j;
 		}
@@ -278,12 +353,16 @@ void abandon_slots(pcppx_ctx* c)
 	(void)hipGetLastError();
 }
 
-// copy a finished chunk's records from pinned memory to the caller's arrays
-void drain(Slot& s, pcppx_records* out)
+// copy a finished chunk's records from pinned memory to the caller's arrays (nothing to copy when the
+// caller's arrays are pinned: the chunk's D2H wrote them directly)
+void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out)
 {
-	par_copy(out->summary + s.first, s.h_sum, (size_t)s.count * sizeof(pcppx_summary));
-	if (s.ml && out->layers)
-		par_copy(out->layers + (size_t)s.first * s.ml, s.h_lay, (size_t)s.count * s.ml * sizeof(pcppx_layer));
+	if (!direct_out)
+	{
+		cp.copy(out->summary + s.first, s.h_sum, (size_t)s.count * sizeof(pcppx_summary));
+		if (s.ml && out->layers)
+			cp.copy(out->layers + (size_t)s.first * s.ml, s.h_lay, (size_t)s.count * s.ml * sizeof(pcppx_layer));
+	}
 	s.busy = false;
 }
 // pcppx_parse_batch_host's chunk pipeline (argument checks done; slots idle on entry)
@@ -292,6 +371,8 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 	int rc = PCPPX_OK;
 	const uint32_t ml = o->max_layers;
 	const bool pinned_in = is_pinned(b->data);
+	// a NIC ring / pcppx_host_alloc result buffer: records come back by DMA straight into the caller's arrays
+	const bool direct_out = is_pinned(r->summary) && (ml == 0 || r->layers == nullptr || is_pinned(r->layers));
 	uint32_t i = 0, k = 0;
 	while (i < b->n)
 	{
@@ -300,11 +381,11 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(s, r);
+			drain(c->copier, s, r, direct_out);
 		}
 		size_t pos = 0;
 		const uint8_t* direct = nullptr;
-		const uint32_t j = stage_chunk(s, b, i, &pos, &direct, pinned_in);
+		const uint32_t j = stage_chunk(c->copier, s, b, i, &pos, &direct, pinned_in);
 		const uint32_t cnt = j - i;
 		if (!upload_chunk(s, pos, cnt, direct))
 			return PCPPX_E_HIP;
@@ -313,9 +394,11 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		rc = pcppx::launch_parse(&db, o, &dr, s.st);
 		if (rc != PCPPX_OK)
 			return rc;
-		const bool good = ok(hipMemcpyAsync(s.h_sum, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
-		       (ml == 0 || ok(hipMemcpyAsync(s.h_lay, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer),
-		                                     hipMemcpyDeviceToHost, s.st))) &&
+		pcppx_summary* hs = direct_out ? r->summary + i : s.h_sum;
+		pcppx_layer* hl = direct_out && r->layers ? r->layers + (size_t)i * ml : s.h_lay;
+		const bool good = ok(hipMemcpyAsync(hs, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
+		       (ml == 0 || r->layers == nullptr ||
+		        ok(hipMemcpyAsync(hl, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer), hipMemcpyDeviceToHost, s.st))) &&
 		       ok(hipEventRecord(s.done, s.st));
 		if (!good)
 			return PCPPX_E_HIP;
@@ -331,7 +414,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(s, r);
+			drain(c->copier, s, r, direct_out);
 		}
 	return PCPPX_OK;
 }
@@ -359,7 +442,7 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 		}
 		size_t pos = 0;
 		const uint8_t* direct = nullptr;
-		const uint32_t j = stage_chunk(s, b, i, &pos, &direct, pinned_in);
+		const uint32_t j = stage_chunk(c->copier, s, b, i, &pos, &direct, pinned_in);
 		const uint32_t cnt = j - i;
 		if (!upload_chunk(s, pos, cnt, direct))
 			return PCPPX_E_HIP;
@@ -491,6 +574,8 @@ extern "C"
 			return;
 		(void)hipSetDevice(c->device);
 		(void)hipStreamSynchronize(c->stream);
+		if (c->host_ready)
+			c->copier.stop();
 		for (Slot& s : c->slots)
 		{
 			if (s.st)

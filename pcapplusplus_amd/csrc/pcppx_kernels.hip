@@ -1555,8 +1555,10 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // MarkFast (tools only): flags bit 0x8000 set on the packets the fast path took. FillTails: the staged layer rows
 // are zero-filled past n_layers and stored whole: full-line stores, 3.5% faster on config 3 than storing only the
 // chain's records (profiles/r02_ab_tails.txt).
+// GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
+// record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
-          bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true>
+          bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1671,7 +1673,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
 		const bool deep = et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
 		const uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
-		const bool more = live && !StreamOnly && deep && full > p.nch;
+		const bool more = live && !StreamOnly && (deep || GatherOnly) && full > p.nch;
 		if (__ballot(more))  // wave-uniform
 		{
 			m_nch[lane] = more ? (full | (p.nch << 8)) : 0u;
@@ -1683,7 +1685,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 	}
 	Fast f;
-	const bool fast = live && !StreamOnly && fast_walk(p, cap, prm, f);
+	const bool fast = live && !StreamOnly && !GatherOnly && fast_walk(p, cap, prm, f);
 
 	// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
 	const uint32_t ml = prm.max_layers;
@@ -1705,7 +1707,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		w.is_tcp = true;
 		w.l4pp = 0;
 	}
-	else if (live)
+	else if (live && !GatherOnly)
 	{
 		if (fast)
 		{
@@ -1843,12 +1845,12 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	else if (stage_layers)  // uniform
 	{
 		__syncthreads();  // every lane is done with the header stage
-		m_nch[lane] = fast ? (FillTails ? ml : w.n_layers) : 0u;  // records of the row to store
+		m_nch[lane] = (fast || GatherOnly) ? (FillTails ? ml : w.n_layers) : 0u;  // records of the row to store
 		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 		typedef __attribute__((address_space(3))) u32x2* lptr64w;
 		lptr64w rows = (lptr64w)(stage);
 		const uint32_t rs = ml + 1;  // padded row stride (records): breaks the power-of-two bank pattern
-		if (FillTails && fast)
+		if (FillTails && (fast || GatherOnly))
 			for (uint32_t k = 0; k < ml; ++k)
 				rows[lane * rs + k] = u32x2{ 0u, 0u };
 		if (fast)

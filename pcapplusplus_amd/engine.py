@@ -39,11 +39,18 @@ class Engine:
             pass
 
     # ---- host-resident batches ----
-    def parse_host(self, batch: PacketBatch, opts: abi.Opts | None = None):
-        """Parse a host batch; returns (summary[n], layers[n, max_layers]) numpy record arrays."""
+    def parse_host(self, batch: PacketBatch, opts: abi.Opts | None = None, out=None):
+        """Parse a host batch; returns (summary[n], layers[n, max_layers]) numpy record arrays. out: caller-owned
+        (summary, layers) arrays to fill (e.g. pinned_records(): the records then come back by DMA straight
+        into them), else fresh zeroed arrays."""
         opts = opts or abi.make_opts()
-        summary = np.zeros(batch.n, dtype=abi.SUMMARY_DTYPE)
-        layers = np.zeros(max(batch.n * opts.max_layers, 1), dtype=abi.LAYER_DTYPE)
+        if out is None:
+            summary = np.zeros(batch.n, dtype=abi.SUMMARY_DTYPE)
+            layers = np.zeros(max(batch.n * opts.max_layers, 1), dtype=abi.LAYER_DTYPE)
+        else:
+            summary, layers = out
+            if summary.shape[0] < batch.n or layers.size < batch.n * opts.max_layers:
+                raise ValueError("output arrays too small for the batch")
         rec = abi.Records(summary.ctypes.data, layers.ctypes.data if opts.max_layers else None)
         b = batch.c_batch()
         abi.check(self.lib.pcppx_parse_batch_host(self.ctx, C.byref(b), C.byref(opts), C.byref(rec)),
@@ -182,6 +189,14 @@ class PinnedBuffer:
             self.free()
         except Exception:
             pass
+
+
+def pinned_records(n: int, max_layers: int):
+    """(summary[n], layers[n * max_layers]) record arrays in page-locked memory, plus the buffers to keep alive:
+    pcppx_parse_batch_host then writes the records by DMA, with no host copy."""
+    sb = PinnedBuffer(n * abi.SUMMARY_DTYPE.itemsize)
+    lb = PinnedBuffer(max(1, n * max_layers) * abi.LAYER_DTYPE.itemsize)
+    return (sb.array.view(abi.SUMMARY_DTYPE)[:n], lb.array.view(abi.LAYER_DTYPE)[: max(1, n * max_layers)]), (sb, lb)
 
 
 def pinned_copy(batch: PacketBatch) -> tuple[PacketBatch, PinnedBuffer]:
