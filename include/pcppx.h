@@ -196,6 +196,10 @@ typedef struct pcppx_packet_stats { /* PacketStats, Examples/DpdkExample-FilterT
 	uint64_t needs_host_count;                  /* packets whose counters the host must complete: chains stopped
 	                                              before an out-of-scope L2/L3 layer (NEEDS_HOST_PROTO), bad
 	                                              records, or UDP tunnels (VXLAN, GTPv1) carrying inner packets */
+	uint64_t flow_table_full;                   /* matched packets whose flow found no free slot in the device flow
+	                                              table (capacity too small for the traffic's flows): the reference's
+	                                              unordered_map never fills, so when this is non-zero the
+	                                              matched_* counters and verdicts are no longer the reference's */
 } pcppx_packet_stats;
 
 PCPPX_API int pcppx_filter_device(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_records* records, uint8_t max_layers,

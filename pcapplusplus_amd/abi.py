@@ -114,7 +114,7 @@ class MatchSpec(C.Structure):
 
 STATS_FIELDS = ("packet_count", "eth_count", "arp_count", "ipv4_count", "ipv6_count", "tcp_count", "udp_count",
                 "http_count", "dns_count", "tls_count", "matched_tcp_flows", "matched_udp_flows", "matched_packets",
-                "needs_host_count")
+                "needs_host_count", "flow_table_full")
 
 
 class PacketStats(C.Structure):

@@ -2162,6 +2162,7 @@ __device__ __forceinline__ uint32_t flow_mix(uint32_t key)
 	return key * 0x9E3779B1u;
 }
 
+constexpr uint32_t kStatFlowTableFull = 14;  // pcppx_packet_stats::flow_table_full (u64 index)
 __global__ __launch_bounds__(kBlock) void filter_mark_kernel(FilterParams fp)
 {
 	const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -2191,6 +2192,7 @@ __global__ __launch_bounds__(kBlock) void filter_mark_kernel(FilterParams fp)
 		}
 		slot = (slot + 1) & m;
 	}
+	atomicAdd(&fp.stats[kStatFlowTableFull], 1ull);  // no free slot: results no longer the reference's (pcppx.h)
 }
 
 __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred)

@@ -236,3 +236,19 @@ def test_gpu_filter_mixed_settled_and_host(engine):
     for k in abi.STATS_FIELDS:
         assert gst[k] == ost[k], (k, gst[k], ost[k])
     assert ost["needs_host_count"] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_filter_table_full_is_counted(engine):
+    """A flow table too small for the matched flows cannot hold the reference's unordered_map: the packets whose
+    flow finds no free slot are counted in flow_table_full (pcppx.h), and with room to spare the count is 0."""
+    b = device_finishable([x for n, x in batches() if n == "pcap_lt1"][0])
+    spec = oracle.make_spec()
+    s, lay = oracle.oracle_parse(b, OPTS)
+    _, ost = oracle.oracle_filter(b, s, lay, spec)
+    _, big = gpu_filter(engine, b, spec)
+    assert big["flow_table_full"] == 0 and big["matched_packets"] == ost["matched_packets"]
+    _, small = gpu_filter(engine, b, spec, capacity=8)
+    flows = ost["matched_tcp_flows"] + ost["matched_udp_flows"]
+    assert flows > 8
+    assert 0 < small["flow_table_full"] <= ost["matched_packets"]

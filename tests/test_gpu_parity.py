@@ -124,10 +124,11 @@ def test_gpu_synthetic_configs(engine, cfg, n):
 
 
 def test_gpu_host_path_matches_device_path(engine):
-    """pcppx_parse_batch_host (chunked, double-buffered) equals the device path: packed pageable input
-    (multi-threaded staging), pinned input (DMA straight from the caller's bytes) and a gapped batch
-    (per-packet gather)."""
-    from pcapplusplus_amd.engine import pinned_copy
+    """pcppx_parse_batch_host (chunked, three slots) equals the device path: packed pageable input
+    (staged by the copy threads), pinned input (DMA straight from the caller's bytes), pinned input and
+    pinned record arrays (records DMA'd straight into them, no drain copy), and a gapped batch (per-packet
+    gather)."""
+    from pcapplusplus_amd.engine import pinned_copy, pinned_records
 
     b = synth.config(3, 600_000)
     opts = abi.make_opts(0, 8, True, 8)
@@ -137,6 +138,12 @@ def test_gpu_host_path_matches_device_path(engine):
     pb, buf = pinned_copy(b)
     hp = engine.parse_host(pb, opts)
     oracle.compare_exact(hp[0], hp[1], d[0], d[1])
+    out, keep = pinned_records(b.n, opts.max_layers)
+    hpo = engine.parse_host(pb, opts, out)
+    oracle.compare_exact(hpo[0], hpo[1], d[0], d[1])
+    del hpo, out
+    for k in keep:
+        k.free()
     buf.free()
     g = as_batch([b.packet(i) for i in range(20_000)], gaps=True, seed=3)
     hg = engine.parse_host(g, opts)
@@ -268,6 +275,27 @@ def test_gpu_flow_table_multi_batch_blocks_and_repeated_calls(engine):
     got, st = _device_flow_table(engine, s, b.caplens, b.n, 1 << 20, calls=2)
     want = _host_group_by(s, b.caplens, scale=2)
     zero = want.pop(0, (0, 0))
+    assert got == want
+    assert (int(st[0]), int(st[1]), int(st[2])) == (zero[0], zero[1], 0)
+
+
+def test_gpu_flow_table_many_batches_per_block(engine):
+    """9M packets with Zipf(1.1) flow keys over 1M flows (a synthetic summary: only hash5 and caplen are read):
+    each of the 256 persistent blocks aggregates 8-9 LDS batches of 4096 packets, so hot flows stay in LDS across
+    many flushes and cold keys ahead of them in their probe chains are cleared between batches. Per-flow counters
+    equal a host group-by exactly; key 0 goes to the stats counters."""
+    n = 9_000_000
+    rng = np.random.default_rng(5)
+    ranks = np.minimum(rng.zipf(1.1, n), 1_000_000).astype(np.uint64)
+    keys = ((ranks * 0x9E3779B1) & 0xFFFFFFFF).astype(np.uint32)  # distinct per rank, hot ranks first
+    keys[rng.random(n) < 0.001] = 0
+    s = np.zeros(n, dtype=abi.SUMMARY_DTYPE)
+    s["hash5"] = keys
+    caplens = rng.integers(60, 1515, n).astype(np.uint32)
+    got, st = _device_flow_table(engine, s, caplens, n, 1 << 21)
+    want = _host_group_by(s, caplens)
+    zero = want.pop(0, (0, 0))
+    assert len(want) > 100_000 and max(c for c, _ in want.values()) > n // 20
     assert got == want
     assert (int(st[0]), int(st[1]), int(st[2])) == (zero[0], zero[1], 0)
 
