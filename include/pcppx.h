@@ -18,9 +18,11 @@
  *                      (Packet++/header/Layer.h, ProtocolType.h:35-284)
  *   pcppx_summary <-> Packet::isPacketOfType (proto_mask, Packet.cpp:614-640), hash5Tuple(false/true),
  *                      hash2Tuple, the IPv4/L4 checksums.
- * Packets for which the reference would build a layer outside this engine's scope (L7 dissectors, ARP,
- * ICMP, PPPoE, ...) are flagged PCPPX_F_NEEDS_HOST_L7 / PCPPX_F_NEEDS_HOST_PROTO: their layer prefix is
- * exact, and the host owns the rest.
+ * Layers the engine builds: Ethernet II / 802.3 / LLC, VLAN, MPLS, IPv4, IPv6 (+ extensions), GREv0/v1,
+ * PPP_PPTP, ARP, TCP, UDP, Payload, Trailer, and the first layers of link types Ethernet, raw IP (RAW,
+ * DLT_RAW1/2, IPV4, IPV6), Linux SLL / SLL2 and Null/Loopback. Packets for which the reference would build a
+ * layer outside this scope (L7 dissectors, ICMP, PPPoE, NFLOG / Cisco HDLC first layers, ...) are flagged
+ * PCPPX_F_NEEDS_HOST_L7 / PCPPX_F_NEEDS_HOST_PROTO: their layer prefix is exact, and the host owns the rest.
  */
 #ifndef PCPPX_H
 #define PCPPX_H

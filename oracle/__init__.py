@@ -323,7 +323,7 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
 
 
 # protocols the engine builds itself (include/pcppx.h: everything else is a host layer)
-ENGINE_PROTOS = (1, 2, 3, 4, 5, 8, 9, 14, 15, 16, 17, 25, 30, 33, 44)
+ENGINE_PROTOS = (1, 2, 3, 4, 5, 8, 9, 14, 15, 16, 17, 19, 21, 25, 30, 33, 44, 52)
 
 
 def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:

@@ -30,11 +30,12 @@
 /* ---- ProtocolType ids (Packet++/header/ProtocolType.h:42-258) and OSI (:266-284) ---- */
 enum {
 	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14,
-	P_GREV0 = 15, P_GREV1 = 16, P_PPTP = 17, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44
+	P_GREV0 = 15, P_GREV1 = 16, P_PPTP = 17, P_SLL = 19, P_NULL = 21, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33,
+	P_LLC = 44, P_SLL2 = 52
 };
 
 enum kind { K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP,
-	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP };
+	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP, K_SLL, K_SLL2, K_NULL };
 
 static uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
@@ -357,6 +358,47 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		default: NEXT(K_PAYLOAD, po, pl); break;
 		}
 		break;
+	case K_SLL:  /* SllLayer::parseNextLayer, Packet++/src/SllLayer.cpp:49-102 (protocol_type at 14, SllLayer.h:15-32) */
+	case K_SLL2: /* Sll2Layer::parseNextLayer, Packet++/src/Sll2Layer.cpp:63-121 (protocol_type at 0, Sll2Layer.h:15-35) */
+		L.proto = k == K_SLL ? P_SLL : P_SLL2; L.osi = 2; L.hdr = k == K_SLL ? 16 : 20;
+		if (len <= L.hdr) break;
+		po = off + L.hdr; pl = len - L.hdr;
+		switch (be16(p + (k == K_SLL ? 14 : 0))) {
+		case 0x0800: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 0x86DD: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		case 0x0806: NEXT(K_ARP, po, pl); break;                  /* unchecked */
+		case 0x8100: case 0x88A8: NEXT(K_VLAN, po, pl); break;    /* unchecked */
+		case 0x8864: case 0x8863: NEXT(K_OUT, po, pl); *nosi = 2; break; /* PPPoE */
+		case 0x8847: NEXT(K_MPLS, po, pl); break;                 /* unchecked */
+		case 0x0004: /* Sll2ProtoTypeLLC, Sll2Layer.cpp:20,110-114 */
+			if (k == K_SLL2) { NEXT(llc_valid(pkt + po, pl) ? K_LLC : K_PAYLOAD, po, pl); break; }
+			NEXT(K_PAYLOAD, po, pl); break;
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	case K_NULL: { /* NullLoopbackLayer::getFamily :23-43, parseNextLayer :50-99 (no length check: a 4-byte packet
+	                * gets an empty next layer) */
+		L.proto = P_NULL; L.osi = 2; L.hdr = 4;
+		po = off + 4; pl = len - 4;
+		uint32_t fam = le32(p);
+		if (fam & 0xFFFF0000u) {
+			if ((fam & 0xFF000000u) == 0 && (fam & 0x00FF0000u) < 0x00060000u) fam >>= 16;
+			else fam = (fam >> 24) | ((fam >> 8) & 0xFF00u) | ((fam << 8) & 0xFF0000u) | (fam << 24);
+		} else if ((fam & 0xFFu) == 0 && (fam & 0xFF00u) < 0x0600u) {
+			/* BSWAP16 (:10) does not truncate to 16 bits: x >> 8 | x << 8 of a 32-bit value */
+			fam = ((fam & 0xFFFFu) >> 8) | ((fam & 0xFFFFu) << 8);
+		}
+		int v4 = 0, v6 = 0;
+		if (fam > 1500) { /* Ieee8023MaxLength: an EtherType */
+			v4 = (uint16_t)fam == 0x0800; v6 = (uint16_t)fam == 0x86DD;
+		} else {
+			v4 = fam == 2; v6 = fam == 24 || fam == 28 || fam == 30; /* BSD AF_INET / AF_INET6 variants */
+		}
+		if (v4) NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl);
+		else if (v6) NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl);
+		else NEXT(K_PAYLOAD, po, pl);
+		break;
+	}
 	case K_DOT3: /* EthDot3Layer::parseNextLayer, Packet++/src/EthDot3Layer.cpp:22-30 */
 		L.proto = P_DOT3; L.osi = 2; L.hdr = 14;
 		if (len <= 14) break;
@@ -561,7 +603,10 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 		break;
 	case 228: k = ipv4_valid(pkt, caplen) ? K_IPV4 : K_PAYLOAD; break; /* LINKTYPE_IPV4 */
 	case 229: k = ipv6_valid(pkt, caplen) ? K_IPV6 : K_PAYLOAD; break; /* LINKTYPE_IPV6 */
-	case 0: case 113: case 276: case 239: case 104: /* NULL, SLL, SLL2, NFLOG, C_HDLC: host dissectors */
+	case 113: k = K_SLL; break;                                   /* LINKTYPE_LINUX_SLL: unchecked */
+	case 276: k = caplen >= 20 ? K_SLL2 : K_PAYLOAD; break;        /* Sll2Layer::isDataValid, Sll2Layer.cpp:151-154 */
+	case 0: k = caplen >= 4 ? K_NULL : K_PAYLOAD; break;           /* NullLoopbackLayer::isDataValid, NullLoopbackLayer.h:86-89 */
+	case 239: case 104: /* NFLOG, C_HDLC: host dissectors */
 		sum->flags = PCPPX_F_NEEDS_HOST_PROTO;
 		return;
 	default: k = K_PAYLOAD; break;

@@ -30,14 +30,15 @@ constexpr int kBlock = 256;
 enum : uint32_t
 {
 	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_MPLS = 14, P_GREV0 = 15,
-	P_GREV1 = 16, P_PPTP = 17, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44
+	P_GREV1 = 16, P_PPTP = 17, P_SLL = 19, P_NULL = 21, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44,
+	P_SLL2 = 52
 };
 
 // next-layer kinds of the chain walk
 enum : uint32_t
 {
 	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
-	K_PAYLOAD, K_OUT, K_ARP,
+	K_PAYLOAD, K_OUT, K_ARP, K_SLL, K_SLL2, K_NULL,  // SLL / SLL2 / Null-Loopback: first layers only
 	// candidates: the layer a tryConstructNextLayerWithFallback would build if its isDataValid holds, else
 	// Payload (Layer.h:474-483); resolved from the candidate's own first bytes when the walk reaches it
 	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC
@@ -553,36 +554,38 @@ constexpr uint32_t kind_proto(uint32_t k)
 {
 	return k == K_ETH ? P_ETH : k == K_DOT3 ? P_DOT3 : k == K_LLC ? P_LLC : k == K_VLAN ? P_VLAN : k == K_MPLS ? P_MPLS
 	     : k == K_IPV4 ? P_IPV4 : k == K_IPV6 ? P_IPV6 : k == K_GRE0 ? P_GREV0 : k == K_GRE1 ? P_GREV1
-	     : k == K_PPTP ? P_PPTP : k == K_TCP ? P_TCP : k == K_UDP ? P_UDP : k == K_ARP ? P_ARP : P_PAYLOAD;
+	     : k == K_PPTP ? P_PPTP : k == K_TCP ? P_TCP : k == K_UDP ? P_UDP : k == K_ARP ? P_ARP : k == K_SLL ? P_SLL
+	     : k == K_SLL2 ? P_SLL2 : k == K_NULL ? P_NULL : P_PAYLOAD;
 }
 constexpr uint32_t kind_osi(uint32_t k)
 {
-	return (k == K_ETH || k == K_DOT3 || k == K_LLC || k == K_VLAN) ? 2
+	return (k == K_ETH || k == K_DOT3 || k == K_LLC || k == K_VLAN || k == K_SLL || k == K_SLL2 || k == K_NULL) ? 2
 	     : (k == K_MPLS || k == K_IPV4 || k == K_IPV6 || k == K_GRE0 || k == K_GRE1 || k == K_ARP) ? 3
 	     : k == K_PPTP ? 5 : (k == K_TCP || k == K_UDP) ? 4 : 7;
 }
 constexpr uint64_t pack_proto(uint32_t first)
 {
 	uint64_t t = 0;
-	for (uint32_t k = first; k < first + 10 && k <= K_ARP; ++k)
+	for (uint32_t k = first; k < first + 10 && k <= K_NULL; ++k)
 		t |= (uint64_t)kind_proto(k) << (6 * (k - first));
 	return t;
 }
 constexpr uint64_t pack_osi()
 {
 	uint64_t t = 0;
-	for (uint32_t k = 0; k <= K_ARP; ++k)
+	for (uint32_t k = 0; k <= K_NULL; ++k)
 		t |= (uint64_t)kind_osi(k) << (3 * k);
 	return t;
 }
 constexpr uint64_t kProtoLo = pack_proto(0), kProtoHi = pack_proto(10), kOsi = pack_osi();
-static_assert(K_ARP < 20 && 3 * K_ARP + 3 <= 64, "kind tables");
+static_assert(K_NULL < 20 && 3 * K_NULL + 3 <= 64 && P_SLL2 < 64, "kind tables");
 
 __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o, uint32_t len, const Peek& q)
 {
 	const bool isE = k == K_ETH, isD = k == K_DOT3, isL = k == K_LLC, isV = k == K_VLAN, isM = k == K_MPLS;
 	const bool is4 = k == K_IPV4, is6 = k == K_IPV6, isG = k == K_GRE0 || k == K_GRE1, isP = k == K_PPTP;
 	const bool isT = k == K_TCP, isU = k == K_UDP, isA = k == K_ARP;
+	const bool isS = k == K_SLL, isS2 = k == K_SLL2, isN = k == K_NULL;
 	// IPv6 extension headers (IPv6Layer::parseExtensions, no bound check against dataLen): IPv6 lanes only
 	uint32_t nh = q.b(6), ext = 0, last_ext = 0xFFFF;
 	if (is6)
@@ -627,6 +630,9 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	hdr = isT ? (q.b(12) >> 4) * 4 : hdr;
 	hdr = isU ? 8 : hdr;
 	hdr = isA ? 28 : hdr;
+	hdr = isS ? 16 : hdr;   // sll_header (SllLayer.h:15-32), even when the packet is shorter
+	hdr = isS2 ? 20 : hdr;  // sll2_header (Sll2Layer.h:15-35)
+	hdr = isN ? 4 : hdr;    // the family dword (NullLoopbackLayer.h:66-69)
 	// data length: IPv4 totalLength truncation (0 = TSO keeps it), IPv6 payloadLength + header, ARP 28
 	uint32_t dlen = len;
 	const uint32_t tl = q.be(2);
@@ -635,11 +641,13 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	const uint32_t total = q.be(4) + hdr;
 	dlen = (is6 && total < len) ? total : dlen;
 	dlen = isA ? 28 : dlen;
-	// successor: exists iff the layer's data runs past its header (every kind's "no next layer" rule)
-	const bool has_next = dlen > hdr;
+	// successor: exists iff the layer's data runs past its header (every kind's "no next layer" rule; Null/Loopback
+	// always builds one, empty for a 4-byte packet: NullLoopbackLayer.cpp:50-99 has no length check)
+	const bool has_next = dlen > hdr || isN;
 	const uint32_t po = o + hdr, pl = has_next ? dlen - hdr : 0;
-	// EtherType dispatch of Ethernet (EtherType at 12), VLAN and GRE (at 2); PPP protocol of PPP_PPTP (at 2)
-	const uint32_t et = isE ? q.be(12) : q.be(2);
+	// EtherType dispatch of Ethernet (EtherType at 12), VLAN and GRE (at 2), SLL (protocol_type at 14) and SLL2 (at
+	// 0: SllLayer.cpp:49-102, Sll2Layer.cpp:63-121); PPP protocol of PPP_PPTP (at 2)
+	const uint32_t et = isE ? q.be(12) : (isS ? q.be(14) : (isS2 ? q.be(0) : q.be(2)));
 	uint32_t ne = K_PAYLOAD;
 	ne = et == 0x0800 ? C_IPV4 : ne;
 	ne = et == 0x86DD ? C_IPV6 : ne;
@@ -652,6 +660,18 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	ne = (et < 1500 && isV) ? C_LLC : ne;
 	ne = (isE && pl < 4 && (ne == K_VLAN || ne == K_MPLS)) ? K_PAYLOAD : ne;
 	ne = isP ? (et == 0x21 ? C_IPV4 : (et == 0x57 ? C_IPV6 : K_PAYLOAD)) : ne;
+	ne = (isS2 && et == 0x0004) ? C_LLC : ne;  // Sll2ProtoTypeLLC (Sll2Layer.cpp:20,110-114)
+	// Null/Loopback: NullLoopbackLayer::getFamily (NullLoopbackLayer.cpp:23-43: a byte-order guess; its BSWAP16 keeps
+	// the shifted-out byte, :10) then an EtherType above 1500, else the BSD AF_INET / AF_INET6 values
+	uint32_t fam = q.q[0];
+	const uint32_t fsw = (fam >> 24) | ((fam & 0x00FF0000u) >> 8) | ((fam & 0x0000FF00u) << 8) | (fam << 24);
+	const uint32_t f16 = fam & 0xFFFFu;
+	fam = (fam & 0xFFFF0000u) ? (((fam & 0xFF000000u) == 0 && (fam & 0x00FF0000u) < 0x00060000u) ? fam >> 16 : fsw)
+	                          : (((fam & 0xFFu) == 0 && (fam & 0xFF00u) < 0x0600u) ? ((f16 >> 8) | (f16 << 8)) : fam);
+	const uint32_t fe = fam & 0xFFFFu;
+	const bool nv4 = fam > 1500 ? fe == 0x0800 : fam == 2;
+	const bool nv6 = fam > 1500 ? fe == 0x86DD : (fam == 24 || fam == 28 || fam == 30);
+	const uint32_t nn = nv4 ? C_IPV4 : (nv6 ? C_IPV6 : K_PAYLOAD);
 	// IP protocol / next-header dispatch (IPv4Layer.cpp:245-370, IPv6Layer.cpp:194-312)
 	const uint32_t ipp = is4 ? q.b(9) : nh;
 	uint32_t ni = K_PAYLOAD;
@@ -665,7 +685,8 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	const bool frag = (b6 & 0x20) || (((b6 & 0x1F) << 8) | q.b(7)) != 0;  // IPv4Layer.cpp:415-438
 	ni = ((is4 && frag) || (is6 && last_ext == 44)) ? K_PAYLOAD : ni;
 	uint32_t nk = K_PAYLOAD;
-	nk = (isE || isV || isG || isP) ? ne : nk;
+	nk = (isE || isV || isG || isP || isS || isS2) ? ne : nk;
+	nk = isN ? nn : nk;
 	nk = (is4 || is6) ? ni : nk;
 	nk = isM ? ((q.b(2) & 1) ? C_IPVER : K_MPLS) : nk;  // bottom of stack: IPv4/IPv6 by version nibble
 	nk = isD ? C_LLC : nk;
@@ -718,7 +739,10 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	case 101: case 12: case 14: k = C_IPVER; break;  // raw IP by version nibble
 	case 228: k = C_IPV4; break;
 	case 229: k = C_IPV6; break;
-	case 0: case 113: case 276: case 239: case 104: k = K_OUT; break;
+	case 113: k = K_SLL; break;                            // SllLayer: unchecked (Packet.cpp:849-852)
+	case 276: k = cap >= 20 ? K_SLL2 : K_PAYLOAD; break;  // Sll2Layer::isDataValid (Sll2Layer.cpp:151-154)
+	case 0: k = cap >= 4 ? K_NULL : K_PAYLOAD; break;     // NullLoopbackLayer::isDataValid (NullLoopbackLayer.h:86-89)
+	case 239: case 104: k = K_OUT; break;                  // NFLOG, Cisco HDLC: host dissectors
 	default: k = K_PAYLOAD; break;
 	}
 

@@ -265,3 +265,36 @@ def crafted_l7(seed: int = 13) -> list[bytes]:
             l4 = _udp(sp, dp, body)
             pk.append(_eth(0x0800) + _ipv4(17, len(l4)) + l4 + bytes(int(rng.integers(0, 3))))
     return pk
+
+
+def crafted_linklayers(seed: int = 23) -> dict[int, list[bytes]]:
+    """First layers of the non-Ethernet link types the engine builds, per link type: Linux SLL (113), SLL2 (276)
+    and Null/Loopback (0) at and around their length rules, every protocol / family encoding they dispatch on
+    (NullLoopbackLayer::getFamily's byte-order guesses, Packet++/src/NullLoopbackLayer.cpp:23-43), followed by valid
+    and broken IPv4 / IPv6 / VLAN / MPLS / ARP / LLC / PPPoE payloads."""
+    rng = np.random.default_rng(seed)
+    t4, u6 = _tcp(1234, 80, rng.bytes(20)), _udp(5000, 6000, rng.bytes(12))
+    ip4 = _ipv4(6, len(t4)) + t4
+    ip6 = _ipv6(17, len(u6)) + u6
+    inner = {0x0800: [ip4, ip4[:19], b"\x45" + ip4[1:10]], 0x86DD: [ip6, ip6[:39]], 0x8100: [b"\x00\x01\x08\x00" + ip4, b"\x00\x01"],
+             0x88A8: [b"\x00\x02\x86\xdd" + ip6], 0x8847: [b"\x00\x01\x41\x40" + ip4, b"\x00"], 0x0806: [bytes(28), bytes(10)],
+             0x8864: [bytes(20)], 0x0004: [b"\x42\x42\x03" + bytes(30), b"\xff\xff\x03", b"\xaa\xaa\x03\x00"],
+             0x1234: [rng.bytes(30)], 0x05DC: [rng.bytes(8)]}
+    out = {113: [], 276: [], 0: []}
+    for et, bodies in inner.items():
+        for body in bodies:
+            out[113].append(rng.bytes(14) + et.to_bytes(2, "big") + body)
+            out[276].append(et.to_bytes(2, "big") + rng.bytes(18) + body)
+    for n in range(0, 24):
+        out[113].append(rng.bytes(n))
+        out[276].append(rng.bytes(n))
+        out[0].append(rng.bytes(n))
+    fams = [2, 24, 28, 30, 7, 0x0800, 0x86DD, 0x1234, 1500, 1501]
+    for fam in fams:
+        for enc in (fam.to_bytes(4, "little"), fam.to_bytes(4, "big"), (fam << 16).to_bytes(4, "little"),
+                    (fam & 0xFFFF).to_bytes(2, "big") + b"\0\0"):
+            for body in (ip4, ip6, ip4[:19], b"", rng.bytes(5)):
+                out[0].append(enc + body)
+    for w in (0x00020000, 0x00050000, 0x00060000, 0x01000000, 0x00000200, 0x00000600, 0x00000002, 0x0000FF00):
+        out[0].append(w.to_bytes(4, "little") + ip4)
+    return out

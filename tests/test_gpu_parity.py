@@ -103,6 +103,26 @@ def test_gpu_permuted_descriptors(engine, order, kernel):
     oracle.compare_exact(g[0], g[1], o[0], o[1])
 
 
+@pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
+@pytest.mark.parametrize("linktype", [0, 113, 276])
+def test_gpu_link_layers(engine, linktype, kernel):
+    """Linux SLL / SLL2 / Null-Loopback first layers (Packet::createFirstLayer, Packet.cpp:827-923) on the generic
+    walk: crafted edge cases (lengths 0-23, every dispatch value and family encoding) and their mutations, packed
+    and with gaps, equal to the restatement (itself pinned to the reference in test_oracle_fuzz)."""
+    from mutate import crafted_linklayers
+
+    seeds = crafted_linklayers()[linktype]
+    pk = seeds + mutate(seeds, 3000, linktype + 1)
+    for gaps in (False, True):
+        b = as_batch(pk, gaps=gaps, seed=linktype)
+        b.linktype = linktype
+        for opts in (abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 2, True, 16),
+                     abi.make_opts(0, 8, False, 3)):
+            g = run(engine, b, opts, kernel)
+            o = oracle.oracle_parse(b, opts)
+            oracle.compare_exact(g[0], g[1], o[0], o[1])
+
+
 def test_gpu_edge_descriptors(engine):
     pk = [b"", b"\x01", bytes(13), bytes(14), bytes(70000), bytes(60)]
     b = from_packets(pk)

@@ -57,3 +57,26 @@ def test_mutations_vs_reference(seed):
         os_, ol = oracle.oracle_parse(b, opts)
         oracle.compare_engine_to_reference(os_, ol, rs, rl)
         oracle.check_flag_contract(os_, rs, rl)
+
+
+@pytest.mark.parametrize("linktype", [0, 113, 276])
+def test_link_layers_vs_reference(linktype):
+    """Linux SLL / SLL2 / Null-Loopback first layers (Packet::createFirstLayer, Packet.cpp:827-923): crafted edge
+    cases and mutations of the reference's own captures of that link type."""
+    from mutate import crafted_linklayers
+    from pcapplusplus_amd.pcap import from_packets
+
+    seeds = crafted_linklayers()[linktype]
+    g = [p for p in golden_files() if p.stem == f"pcap_lt{linktype}"]
+    if g:
+        gb, _ = load_golden(g[0])
+        seeds = seeds + [gb.packet(i) for i in range(gb.n)]
+    b = from_packets(seeds + mutate(seeds, 3000, linktype + 1), linktype)
+    for opts in OPTS[:4] + OPTS[5:]:
+        rs, rl = oracle.ref_parse(b, opts)
+        os_, ol = oracle.oracle_parse(b, opts)
+        oracle.compare_engine_to_reference(os_, ol, rs, rl)
+        if opts.max_layers >= 8:
+            oracle.check_flag_contract(os_, rs, rl)
+    s, _ = oracle.oracle_parse(b, OPTS[0])
+    assert ((s["flags"] & abi.F_NEEDS_HOST) == 0).mean() > 0.5
