@@ -986,27 +986,44 @@ __device__ __forceinline__ uint32_t ipv4_checksum(const Pkt& p, const Walk& w, u
 // {Tcp,Udp}Layer::calculateChecksum(false) (TcpLayer.cpp:271-311, UdpLayer.cpp:47-90) given the
 // residue of the L4 bytes as a stream: subtract the checksum field, add the pseudo header
 // (computePseudoHdrChecksum, PacketUtils.cpp:66-112), fold; UDP maps 0 to 0xFFFF.
-__device__ __forceinline__ uint32_t l4_checksum(const Pkt& p, const Walk& w, uint32_t l4_residue, uint32_t* stored)
+// the header-byte inputs of l4_checksum (read while the LDS window holds them): the checksum field as a
+// little-endian stream word, and the pseudo header's halves-sum (computePseudoHdrChecksum, PacketUtils.cpp:66-112)
+__device__ __forceinline__ void l4_inputs(const Pkt& p, const Walk& w, uint32_t* fw, uint32_t* ph)
 {
-	const uint32_t field = w.is_tcp ? 16 : 6;
-	const uint32_t fw = rd16(p, w.l4o + field);  // the field as a little-endian stream word
+	*fw = rd16(p, w.l4o + (w.is_tcp ? 16 : 6));
+	uint32_t h = 0;
+	if (w.l4pp == P_IPV4 || w.l4pp == P_IPV6)
+	{
+		const uint32_t as = w.l4pp == P_IPV4 ? w.l4ppo + 12 : w.l4ppo + 8;
+		const uint32_t nd = w.l4pp == P_IPV4 ? 2 : 8;  // dwords of src+dst
+		for (uint32_t j = 0; j < nd; ++j) h += halves(rd32(p, as + 4 * j));
+		h += ((w.l4dlen & 0xFF) << 8) | ((w.l4dlen >> 8) & 0xFF);  // htobe16(dataLen)
+		h += (w.is_tcp ? 6u : 17u) << 8;                              // htobe16(protocol)
+	}
+	*ph = h;
+}
+
+__device__ __forceinline__ uint32_t l4_checksum_from(const Walk& w, uint32_t l4_residue, uint32_t fw, uint32_t ph,
+                                                     uint32_t* stored)
+{
 	*stored = swap16(fw);
 	uint32_t res = 0;
 	if (w.l4pp == P_IPV4 || w.l4pp == P_IPV6)
 	{
 		uint32_t r = (l4_residue + 65535u - mod65535(fw)) % 65535u;
-		uint32_t ph = 0;
-		const uint32_t as = w.l4pp == P_IPV4 ? w.l4ppo + 12 : w.l4ppo + 8;
-		const uint32_t nd = w.l4pp == P_IPV4 ? 2 : 8;  // dwords of src+dst
-		for (uint32_t j = 0; j < nd; ++j) ph += halves(rd32(p, as + 4 * j));
-		ph += ((w.l4dlen & 0xFF) << 8) | ((w.l4dlen >> 8) & 0xFF);  // htobe16(dataLen)
-		ph += (w.is_tcp ? 6u : 17u) << 8;                              // htobe16(protocol)
 		r = (r + mod65535(ph)) % 65535u;
 		res = finish_checksum(r);
 	}
 	if (!w.is_tcp && res == 0)
 		res = 0xFFFF;
 	return res;
+}
+
+__device__ __forceinline__ uint32_t l4_checksum(const Pkt& p, const Walk& w, uint32_t l4_residue, uint32_t* stored)
+{
+	uint32_t fw, ph;
+	l4_inputs(p, w, &fw, &ph);
+	return l4_checksum_from(w, l4_residue, fw, ph, stored);
 }
 
 __device__ __forceinline__ void write_summary(pcppx_summary* out, uint32_t h5, uint32_t h5d, uint32_t h2,
@@ -1579,10 +1596,16 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // MarkFast (tools only): flags bit 0x8000 set on the packets the fast path took. FillTails: the staged layer rows
 // are zero-filled past n_layers and stored whole: full-line stores, 3.5% faster on config 3 than storing only the
 // chain's records (profiles/r02_ab_tails.txt).
+// Ring: the span stream writes every chunk's running prefix into a ring in the (by then free) header stage, and each
+// packet lane reads its two prefixes from it once per 4 stream groups, instead of pulling them (and its partial tail
+// chunk) from the owning lanes by ds_bpermute in every group; the header-window inputs of the L4 sum (edge chunks,
+// checksum field, pseudo header) are taken before the ring overwrites the stage, a tail chunk past the window by a
+// global load issued before the stream.
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
-          bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false>
+          bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
+          bool Ring = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1590,7 +1613,9 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	__shared__ uint32_t stage[kTile * kTSlotDw];
 	__shared__ uint64_t m_a0[kTile];
 	__shared__ uint32_t m_nch[kTile];  // gather range of each packet: chunks [bits 8-15, bits 0-7)
-	static_assert(kTile * (kRowMaxMl + 1) * 2 <= kTile * kTSlotDw, "stage too small for layer rows");
+	// layer rows staged in LDS up to this max_layers (a row = ml + 1 padded 8-B records); beyond, direct stores
+	constexpr uint32_t kRowMl = (uint32_t)kTSlotDw / 2 - 1 < kRowMaxMl ? (uint32_t)kTSlotDw / 2 - 1 : kRowMaxMl;
+	static_assert(kTile * (kRowMl + 1) * 2 <= kTile * kTSlotDw, "stage too small for layer rows");
 	static_assert(Chunks1 <= Chunks && Chunks < 256, "gather rounds");
 	const bool want_csum = Csum && prm.want_csum;  // uniform
 
@@ -1770,7 +1795,81 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		const bool tail = need && f0 <= f1 && f1 < ae;  // partial last chunk [f1, ae)
 		uint32_t fsum = 0, tsum = 0;
 		bool tail_done = false;
-		if (stream)
+		if constexpr (Ring)
+		{
+			// (a) header-window inputs, before the ring overwrites the stage
+			uint32_t head = 0, fw = 0, ph = 0;
+			uint4 tv = make_uint4(0, 0, 0, 0);
+			if (need)
+			{
+				head = f0 <= f1 ? edge_sum(p, as, f0) : edge_sum(p, as, ae);
+				l4_inputs(p, w, &fw, &ph);
+				if (tail)
+				{
+					if ((uint32_t)((f1 - p.a0) >> 4) < p.nch)
+					{
+						tsum = edge_sum(p, f1, ae);
+						tail_done = true;
+					}
+					else
+						tv = ld16(f1);  // lands during the stream
+				}
+			}
+			__syncthreads();  // every lane is done with the header stage
+			if (stream)
+			{
+				// (b) the span stream: per 64-chunk group a halves-sum, a DPP inclusive scan and the running prefix
+				// P into ring[c mod 512]; after each 4 groups the lanes whose P(c0-1) / P(c1-1) fell in them read it
+				lptr32w ring = (lptr32w)(stage);
+				constexpr uint32_t kRing = 4 * SWin < 512 ? 512u : 4u * SWin;  // 4 stream windows of prefixes
+				static_assert(kRing <= (uint32_t)(kTile * kTSlotDw), "ring");
+				const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
+				const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
+				uint32_t p0 = 0, p1 = 0, carry = 0;
+				const uint32_t nwin = (nchunks + SWin - 1) / SWin;
+				auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
+#pragma unroll
+					for (int k = 0; k < SWin / 64; ++k)
+					{
+						const uint32_t g = win * SWin + 64 * k;
+						const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+						const uint32_t x = wave_incl_scan(h);
+						ring[(g & (kRing - 1)) + lane] = carry + x;
+						carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+					}
+				};
+				load(vb, 1);
+				for (uint32_t wi = 0; wi < nwin; wi += 2)
+				{
+					process(va, wi);
+					load(va, wi + 2);
+					process(vb, wi + 1);
+					load(vb, wi + 3);
+					const int32_t lo = (int32_t)(wi * SWin), hi = lo + 2 * SWin;
+					const bool in0 = t0 >= lo && t0 < hi, in1 = t1 >= lo && t1 < hi;
+					const uint32_t r0 = ring[(uint32_t)(in0 ? t0 : 0) & (kRing - 1)];
+					const uint32_t r1 = ring[(uint32_t)(in1 ? t1 : 0) & (kRing - 1)];
+					p0 = in0 ? r0 : p0;
+					p1 = in1 ? r1 : p1;
+				}
+				if (full)
+					fsum = p1 - p0;
+			}
+			else if (full)
+				fsum = full_chunks_sum(f0, f1);
+			if (need)
+			{
+				if (tail && !tail_done)
+					tsum = chunk_sum(tv, f1, f1, ae);
+				uint32_t acc = mod65535(fsum) + head + (f0 <= f1 ? tsum : 0u);
+				uint32_t r = mod65535(acc);
+				if (as & 1)
+					r = (r * 256u) % 65535u;
+				l4c = l4_checksum_from(w, r, fw, ph, &l4s);
+				w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
+			}
+		}
+		else if (stream)
 		{
 			// Stream the tile span once, 4 x 1 KiB wave-loads per window, two register windows in
 			// flight. Per 64-chunk group: halves-sums -> DPP inclusive scan -> running prefix P; each
@@ -1828,7 +1927,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 		else if (full)
 			fsum = full_chunks_sum(f0, f1);
-		if (need)
+		if (!Ring && need)
 		{
 			uint32_t acc = mod65535(fsum);
 			if (f0 <= f1)
@@ -1858,7 +1957,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
 	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
-	if (stage_layers && ml > kRowMaxMl)  // uniform: deep records, each fast lane stores its own row
+	if (stage_layers && ml > kRowMl)  // uniform: deep records, each fast lane stores its own row
 	{
 		if (fast)
 		{

@@ -28,6 +28,10 @@ cases = {
     "tile/ml8/csum": (abi.make_opts(0, 8, True, 8), 0),
     "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
     "tile/chaintails": (abi.make_opts(0, 8, True, 8), 12),
+    "tile/ring": (abi.make_opts(0, 8, True, 8), 40),
+    "tile/ring-win256": (abi.make_opts(0, 8, True, 8), 41),
+    "tile/ring-w6c6": (abi.make_opts(0, 8, True, 8), 42),
+    "tile/ring-c6": (abi.make_opts(0, 8, True, 8), 43),
     "lane/ml8/csum": (abi.make_opts(0, 8, True, 8), 1),
     "tile/ml0/csum": (abi.make_opts(0, 8, True, 0), 0),
     "tile/ml8/nocsum": (abi.make_opts(0, 8, False, 8), 0),
