@@ -383,9 +383,10 @@ __device__ __forceinline__ uint32_t mod65535(uint32_t x)
 	return x == 0xFFFF ? 0 : x;
 }
 
-__device__ __forceinline__ uint32_t halves(uint32_t v)
+// v_sad_u16 against 0: |lo - 0| + |hi - 0| + acc, the sum of the two 16-bit halves in one instruction
+__device__ __forceinline__ uint32_t halves(uint32_t v, uint32_t acc = 0)
 {
-	return (v & 0xFFFF) + (v >> 16);
+	return __builtin_amdgcn_sad_u16(v, 0u, acc);
 }
 
 __device__ __forceinline__ uint32_t mask_dword(uint32_t v, uintptr_t b, uintptr_t lo, uintptr_t hi)
@@ -1832,7 +1833,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 					for (int k = 0; k < SWin / 64; ++k)
 					{
 						const uint32_t g = win * SWin + 64 * k;
-						const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+						const uint32_t h = halves(v[k].x, halves(v[k].y)) + halves(v[k].z, halves(v[k].w));
 						const uint32_t x = wave_incl_scan(h);
 						ring[(g & (kRing - 1)) + lane] = carry + x;
 						carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);

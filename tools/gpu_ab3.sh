@@ -10,6 +10,6 @@ if [ -z "$3" ]; then
     > "$OUT/${TAG}_gpu_tests.log" 2>&1 || { tail -30 "$OUT/${TAG}_gpu_tests.log"; exit 1; }
   tail -2 "$OUT/${TAG}_gpu_tests.log"
 fi
-AB_CASES=$2 timeout -k 10 400 python -u tools/ab_kernels.py 10000000 11 3 > $OUT/${TAG}_ab_cfg3.log 2>&1 || { tail -20 $OUT/${TAG}_ab_cfg3.log; exit 2; }
+AB_CASES=$2 timeout -k 10 400 python -u tools/ab_kernels.py 10000000 ${AB_ROUNDS:-11} 3 > $OUT/${TAG}_ab_cfg3.log 2>&1 || { tail -20 $OUT/${TAG}_ab_cfg3.log; exit 2; }
 cat $OUT/${TAG}_ab_cfg3.log
 echo "ab3 ok"
