@@ -158,11 +158,12 @@ struct pcppx_ctx
 	pcppx_packet_stats* d_stats = nullptr;
 	uint32_t flow_slots = 0;
 	uint64_t seq = 0;
-	// pcppx_flow_count_device: packed per-slot {packets, bytes} scratch (zero between calls), and an event
-	// after each call's last kernel: the next call (on whatever stream) waits for it before touching the
-	// scratch, so calls on one context are ordered even across streams
-	uint64_t* d_flow_packed = nullptr;
-	uint32_t flow_packed_slots = 0;
+	// pcppx_flow_count_device: the partitioned flush's record queues and queue lengths (zero between calls), and
+	// an event after each call's last kernel: the next call (on whatever stream) waits for it before touching
+	// the scratch, so calls on one context are ordered even across streams
+	void* d_flow_queues = nullptr;
+	uint64_t flow_queue_recs = 0;
+	uint32_t* d_flow_fill = nullptr;
 	hipEvent_t flow_done = nullptr;
 	bool flow_pending = false;
 };
@@ -583,7 +584,8 @@ extern "C"
 			free_slot(s);
 		}
 		free_filter(c);
-		(void)hipFree(c->d_flow_packed);
+		(void)hipFree(c->d_flow_queues);
+		(void)hipFree(c->d_flow_fill);
 		if (c->flow_done)
 			(void)hipEventDestroy(c->flow_done);
 		(void)hipStreamDestroy(c->stream);
@@ -754,25 +756,32 @@ extern "C"
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
 		hipStream_t st = static_cast<hipStream_t>(hip_stream);
-		if (c->flow_packed_slots < capacity)
+		const uint32_t parts = pcppx::flow_partitions(capacity);
+		const uint32_t rec_cap = pcppx::flow_queue_capacity(n, capacity);
+		if (c->flow_queue_recs < (uint64_t)parts * rec_cap)
 		{
 			// the previous scratch may still be in use by work queued on another stream
 			if (!ok(hipDeviceSynchronize()))
 				return PCPPX_E_HIP;
-			(void)hipFree(c->d_flow_packed);
-			c->d_flow_packed = nullptr;
-			c->flow_packed_slots = 0;
-			if (!ok(hipMalloc(reinterpret_cast<void**>(&c->d_flow_packed), (size_t)capacity * 8)) ||
-			    !ok(hipMemsetAsync(c->d_flow_packed, 0, (size_t)capacity * 8, st)))
+			(void)hipFree(c->d_flow_queues);
+			c->d_flow_queues = nullptr;
+			c->flow_queue_recs = 0;
+			if (!ok(hipMalloc(&c->d_flow_queues, (size_t)parts * rec_cap * 16)))
 				return PCPPX_E_NOMEM;
-			c->flow_packed_slots = capacity;
+			c->flow_queue_recs = (uint64_t)parts * rec_cap;
+		}
+		if (c->d_flow_fill == nullptr)
+		{
+			if (!ok(hipMalloc(reinterpret_cast<void**>(&c->d_flow_fill), 256 * sizeof(uint32_t))) ||
+			    !ok(hipMemsetAsync(c->d_flow_fill, 0, 256 * sizeof(uint32_t), st)))
+				return PCPPX_E_NOMEM;
 		}
 		if (c->flow_done == nullptr && !ok(hipEventCreateWithFlags(&c->flow_done, hipEventDisableTiming)))
 			return PCPPX_E_HIP;
 		if (c->flow_pending && !ok(hipStreamWaitEvent(st, c->flow_done, 0)))
 			return PCPPX_E_HIP;
-		const int rc =
-		    pcppx::launch_flow_count(summary, caplens, n, keys, packets, bytes, capacity, stats, c->d_flow_packed, st);
+		const int rc = pcppx::launch_flow_count_part(summary, caplens, n, keys, packets, bytes, capacity, stats,
+		                                             c->d_flow_queues, rec_cap, c->d_flow_fill, st);
 		if (rc != PCPPX_OK)
 			return rc;
 		if (!ok(hipEventRecord(c->flow_done, st)))

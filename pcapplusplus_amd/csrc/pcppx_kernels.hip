@@ -2056,13 +2056,58 @@ constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 // With `packed` (a zeroed u64 per slot, launches of < 2^24 packets) a flush adds {packets, bytes} as one
 // 64-bit atomic (packets << 40 | bytes: < 2^24 packets x < 2^16 B fit 40 bits) and flow_unpack_kernel
 // moves the sums into the table's own counters afterwards: one global atomic per distinct flow and flush.
-template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false>
+// Partitioned flush (kPart): the table is split into P = 2^log2p regions by the key's top hash bits, and instead of
+// global atomics on the table a block appends each distinct key of a batch, {key, packed count}, to its partition's
+// record queue (one global atomic per partition per batch reserves the space); flow_merge_kernel then gives every
+// partition to one block, which folds its queue in LDS and updates its own table region with plain loads and stores.
+// A full queue falls back to atomics on the region.
+struct FlowPart
+{
+	uint4* recs;       // P queues of rec_cap records {key, 0, packed lo, packed hi}
+	uint32_t rec_cap;
+	uint32_t* fill;    // P queue lengths (zero before the launch)
+	uint32_t log2p;    // partitions
+	uint32_t log2r;    // slots per region
+};
+
+__device__ __forceinline__ uint32_t flow_part(uint32_t key, uint32_t log2p)
+{
+	return log2p ? (key * 0x9E3779B1u) >> (32 - log2p) : 0u;
+}
+__device__ __forceinline__ uint32_t flow_region_slot(uint32_t key, uint32_t log2r)
+{
+	return (key * 0x85EBCA6Bu) & ((1u << log2r) - 1u);
+}
+// insert / find `key` in its region and add the counts with device atomics (the queue-overflow path); false: full
+__device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packets, unsigned long long* bytes,
+                                       const FlowPart& fp, uint32_t key, unsigned long long pk, unsigned long long by)
+{
+	const uint32_t rbase = flow_part(key, fp.log2p) << fp.log2r, rm = (1u << fp.log2r) - 1u;
+	uint32_t r = flow_region_slot(key, fp.log2r);
+	for (uint32_t probe = 0; probe <= rm; ++probe)
+	{
+		const uint32_t prev = atomicCAS(&keys[rbase + r], 0u, key);
+		if (prev == 0u || prev == key)
+		{
+			atomicAdd(&packets[rbase + r], pk);
+			atomicAdd(&bytes[rbase + r], by);
+			return true;
+		}
+		r = (r + 1) & rm;
+	}
+	return false;
+}
+
+template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
+          bool kPart = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
                                                             unsigned long long* bytes, uint32_t capacity,
-                                                            unsigned long long* stats, unsigned long long* packed)
+                                                            unsigned long long* stats, unsigned long long* packed,
+                                                            FlowPart fpart = FlowPart{})
 {
+	__shared__ uint32_t s_bin[kPart ? 256 : 1], s_base[kPart ? 256 : 1];  // per-partition counts / queue offsets
 	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
 	__shared__ uint32_t s_kept;
@@ -2074,6 +2119,9 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		s_key[j] = 0;
 		s_cnt[j] = 0;
 	}
+	if (kPart)
+		for (uint32_t j = t; j < 256; j += kFB)
+			s_bin[j] = 0;
 	__syncthreads();
 	// kPrefetch: the next batch's keys and lengths are loaded into registers before this batch's flush,
 	// so their latency overlaps the flush's HBM reads and atomics
@@ -2142,6 +2190,44 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		__syncthreads();
 		const bool keep_hot = !last && s_kept <= kFlowLds / 2 - kFlowBatch / 2;  // uniform
 		uint32_t fk[kPer], fs[kPer], fseen[kPer];
+		if constexpr (kPart)
+		{
+			// queue every distinct key: rank within its partition (LDS), one reservation per partition (global)
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; ++u)
+			{
+				const uint32_t j = u * kFB + t;
+				fk[u] = (keep_hot && ((hot >> u) & 1u)) ? 0u : s_key[j];
+				fs[u] = flow_part(fk[u], fpart.log2p);
+				fseen[u] = fk[u] ? atomicAdd(&s_bin[fs[u]], 1u) : 0u;
+			}
+			__syncthreads();
+			for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
+			{
+				const uint32_t c = s_bin[b];
+				s_base[b] = c ? atomicAdd(&fpart.fill[b], c) : 0u;
+				s_bin[b] = 0;
+			}
+			__syncthreads();
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; ++u)
+			{
+				const uint32_t j = u * kFB + t;
+				const uint32_t key = fk[u];
+				if (key == 0)
+					continue;
+				const uint32_t pos = s_base[fs[u]] + fseen[u];
+				const unsigned long long c = s_cnt[j];
+				if (pos < fpart.rec_cap)
+					fpart.recs[(size_t)fs[u] * fpart.rec_cap + pos] = make_uint4(key, 0u, (uint32_t)c, (uint32_t)(c >> 32));
+				else if (!flow_region_add_atomic(keys, packets, bytes, fpart, key, c >> 40, c & ((1ull << 40) - 1)))
+					lost += c >> 40;
+				s_key[j] = 0;
+				s_cnt[j] = 0;
+			}
+			__syncthreads();
+			continue;
+		}
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
 		{
@@ -2209,6 +2295,105 @@ __global__ __launch_bounds__(kBlock) void flow_unpack_kernel(unsigned long long*
 			packed[j] = 0;
 		}
 	}
+}
+
+// The merge step of the partitioned flush: block p folds partition p's queue in an LDS hash table (kPerT records per
+// thread per round; flushed whenever more than half full), then adds each distinct key's counts into its own table
+// region -- which no other block touches, so the counts take plain loads and stores (a CAS only claims a new key's
+// slot against the block's other threads). Resets the queue length for the next launch.
+template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT>
+__global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* keys, unsigned long long* packets,
+                                                         unsigned long long* bytes, unsigned long long* stats)
+{
+	__shared__ uint32_t s_key[kMLds];
+	__shared__ unsigned long long s_cnt[kMLds];
+	__shared__ uint32_t s_used;
+	static_assert(kMB * kPerT <= kMLds / 4 && (kMLds & (kMLds - 1)) == 0, "merge table");
+	const uint32_t t = threadIdx.x, p = blockIdx.x;
+	const uint32_t cnt = fp.fill[p] < fp.rec_cap ? fp.fill[p] : fp.rec_cap;
+	const uint4* q = fp.recs + (size_t)p * fp.rec_cap;
+	const uint32_t rbase = p << fp.log2r, rm = (1u << fp.log2r) - 1u;
+	for (uint32_t j = t; j < kMLds; j += kMB)
+	{
+		s_key[j] = 0;
+		s_cnt[j] = 0;
+	}
+	if (t == 0)
+		s_used = 0;
+	__syncthreads();
+	unsigned long long lost = 0;
+	for (uint32_t base = 0; base < cnt; base += kMB * kPerT)
+	{
+		uint4 rec[kPerT];
+#pragma unroll
+		for (uint32_t k = 0; k < kPerT; ++k)
+		{
+			const uint32_t idx = base + k * kMB + t;
+			rec[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < kPerT; ++k)
+		{
+			const uint32_t key = rec[k].x;
+			if (key == 0)
+				continue;
+			// a hash independent of the partition's (a partition's keys share the top bits of key * 0x9E3779B1)
+			uint32_t slot = (key * 0xC2B2AE35u) >> (32 - log2u(kMLds));
+			while (true)  // the table is at most 3/4 full: terminates
+			{
+				const uint32_t prev = atomicCAS(&s_key[slot], 0u, key);
+				if (prev == 0u || prev == key)
+				{
+					if (prev == 0u)
+						atomicAdd(&s_used, 1u);
+					atomicAdd(&s_cnt[slot], ((unsigned long long)rec[k].w << 32) | rec[k].z);
+					break;
+				}
+				slot = (slot + 1) & (kMLds - 1);
+			}
+		}
+		__syncthreads();
+		const bool flush = base + kMB * kPerT >= cnt || s_used > kMLds / 2;  // uniform
+		if (flush)
+		{
+			for (uint32_t j = t; j < kMLds; j += kMB)
+			{
+				const uint32_t key = s_key[j];
+				if (key == 0)
+					continue;
+				const unsigned long long c = s_cnt[j];
+				uint32_t r = flow_region_slot(key, fp.log2r);
+				bool done = false;
+				for (uint32_t probe = 0; probe <= rm; ++probe)
+				{
+					uint32_t prev = keys[rbase + r];
+					if (prev == 0u)
+						prev = atomicCAS(&keys[rbase + r], 0u, key);
+					if (prev == 0u || prev == key)
+					{
+						packets[rbase + r] += c >> 40;
+						bytes[rbase + r] += c & ((1ull << 40) - 1);
+						done = true;
+						break;
+					}
+					r = (r + 1) & rm;
+				}
+				if (!done)
+					lost += c >> 40;
+				s_key[j] = 0;
+				s_cnt[j] = 0;
+			}
+			__syncthreads();
+			if (t == 0)
+				s_used = 0;
+		}
+		__syncthreads();
+	}
+	lost = wave_sum_u64(lost);
+	if ((t & 63) == 0 && lost)
+		atomicAdd(&stats[2], lost);
+	if (t == 0)
+		fp.fill[p] = 0;
 }
 
 // ---- DpdkExample-FilterTraffic's worker on the device (AppWorkerThread.h:85-139) ----
@@ -2443,8 +2628,12 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 // the flow-table shape: 1024-thread blocks, 8192 LDS slots, 4096-packet batches with the next batch prefetched,
 // 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)
 #define PCPPX_FLOW_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true>
+// the partitioned flush (product): the same aggregation, then per-partition queues and one merge block per partition
+#define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true>
+#define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<1024, 8192, 2>
 constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 4096, kFlowBlocks = 256;
 constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed LDS/HBM counters hold
+constexpr uint32_t kFlowPartLog2 = 8;            // flow-table partitions (merge blocks) at most
 
 }  // namespace
 
@@ -2519,26 +2708,39 @@ int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, con
 	return check_launch("filter_apply_kernel", stream);
 }
 
-int launch_flow_count(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
-                      uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, uint64_t* packed,
-                      hipStream_t stream)
+uint32_t flow_partitions(uint32_t capacity)
+{
+	const uint32_t l = log2u(capacity);
+	return 1u << (l < kFlowPartLog2 ? l : kFlowPartLog2);
+}
+
+uint32_t flow_queue_capacity(uint32_t n, uint32_t capacity)
+{
+	const uint32_t per = kPackedMax < n ? kPackedMax : n;
+	const uint32_t parts = flow_partitions(capacity);
+	return 2 * ((per + parts - 1) / parts) + 4096;
+}
+
+int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
+                           uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, void* queues,
+                           uint32_t rec_cap, uint32_t* fill, hipStream_t stream)
 {
 	auto* pk = reinterpret_cast<unsigned long long*>(packets);
 	auto* by = reinterpret_cast<unsigned long long*>(bytes);
-	auto* pc = reinterpret_cast<unsigned long long*>(packed);
 	auto* st = reinterpret_cast<unsigned long long*>(stats);
+	const uint32_t l = log2u(capacity), lp = l < kFlowPartLog2 ? l : kFlowPartLog2;
+	const FlowPart fp{ static_cast<uint4*>(queues), rec_cap, fill, lp, l - lp };
 	for (uint32_t done = 0; done < n;)
 	{
 		const uint32_t cnt = n - done < kPackedMax ? n - done : kPackedMax;
 		const uint32_t batches = (cnt + kFlowBatchPk - 1) / kFlowBatchPk;
-		hipLaunchKernelGGL(PCPPX_FLOW_KERNEL, dim3(batches < kFlowBlocks ? batches : kFlowBlocks), dim3(kFlowThreads), 0,
-		                   stream, sum + done, caplens + done, cnt, keys, pk, by, capacity, st, pc);
-		int rc = check_launch("flow_count_kernel", stream);
+		hipLaunchKernelGGL(PCPPX_FLOW_PART_KERNEL, dim3(batches < kFlowBlocks ? batches : kFlowBlocks), dim3(kFlowThreads), 0,
+		                   stream, sum + done, caplens + done, cnt, keys, pk, by, capacity, st, nullptr, fp);
+		int rc = check_launch("flow_count_kernel(partitioned)", stream);
 		if (rc != PCPPX_OK)
 			return rc;
-		const uint32_t ub = (capacity + kBlock - 1) / kBlock;
-		hipLaunchKernelGGL(flow_unpack_kernel, dim3(ub < 2048 ? ub : 2048), dim3(kBlock), 0, stream, pk, by, pc, capacity);
-		rc = check_launch("flow_unpack_kernel", stream);
+		hipLaunchKernelGGL(PCPPX_FLOW_MERGE_KERNEL, dim3(1u << lp), dim3(kFlowThreads), 0, stream, fp, keys, pk, by, st);
+		rc = check_launch("flow_merge_kernel", stream);
 		if (rc != PCPPX_OK)
 			return rc;
 		done += cnt;
