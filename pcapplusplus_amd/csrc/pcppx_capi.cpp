@@ -772,8 +772,8 @@ extern "C"
 		}
 		if (c->d_flow_fill == nullptr)
 		{
-			if (!ok(hipMalloc(reinterpret_cast<void**>(&c->d_flow_fill), 256 * sizeof(uint32_t))) ||
-			    !ok(hipMemsetAsync(c->d_flow_fill, 0, 256 * sizeof(uint32_t), st)))
+			if (!ok(hipMalloc(reinterpret_cast<void**>(&c->d_flow_fill), 1024 * sizeof(uint32_t))) ||
+			    !ok(hipMemsetAsync(c->d_flow_fill, 0, 1024 * sizeof(uint32_t), st)))
 				return PCPPX_E_NOMEM;
 		}
 		if (c->flow_done == nullptr && !ok(hipEventCreateWithFlags(&c->flow_done, hipEventDisableTiming)))

@@ -2061,6 +2061,7 @@ constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 // record queue (one global atomic per partition per batch reserves the space); flow_merge_kernel then gives every
 // partition to one block, which folds its queue in LDS and updates its own table region with plain loads and stores.
 // A full queue falls back to atomics on the region.
+constexpr uint32_t kFlowMaxParts = 256;  // flow-table partitions (merge blocks) at most
 struct FlowPart
 {
 	uint4* recs;       // P queues of rec_cap records {key, 0, packed lo, packed hi}
@@ -2107,7 +2108,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
                                                             unsigned long long* stats, unsigned long long* packed,
                                                             FlowPart fpart = FlowPart{})
 {
-	__shared__ uint32_t s_bin[kPart ? 256 : 1], s_base[kPart ? 256 : 1];  // per-partition counts / queue offsets
+	__shared__ uint32_t s_bin[kPart ? kFlowMaxParts : 1], s_base[kPart ? kFlowMaxParts : 1];  // per-partition counts / offsets
 	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
 	__shared__ uint32_t s_kept;
@@ -2120,7 +2121,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		s_cnt[j] = 0;
 	}
 	if (kPart)
-		for (uint32_t j = t; j < 256; j += kFB)
+		for (uint32_t j = t; j < kFlowMaxParts; j += kFB)
 			s_bin[j] = 0;
 	__syncthreads();
 	// kPrefetch: the next batch's keys and lengths are loaded into registers before this batch's flush,
@@ -2322,15 +2323,24 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 		s_used = 0;
 	__syncthreads();
 	unsigned long long lost = 0;
+	// the next round's records are loaded before this round's inserts (their latency hides behind them)
+	uint4 nxt[kPerT];
+	auto fetch = [&](uint32_t base) {
+#pragma unroll
+		for (uint32_t k = 0; k < kPerT; ++k)
+		{
+			const uint32_t idx = base + k * kMB + t;
+			nxt[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
+		}
+	};
+	fetch(0);
 	for (uint32_t base = 0; base < cnt; base += kMB * kPerT)
 	{
 		uint4 rec[kPerT];
 #pragma unroll
 		for (uint32_t k = 0; k < kPerT; ++k)
-		{
-			const uint32_t idx = base + k * kMB + t;
-			rec[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
-		}
+			rec[k] = nxt[k];
+		fetch(base + kMB * kPerT);
 #pragma unroll
 		for (uint32_t k = 0; k < kPerT; ++k)
 		{
@@ -2356,17 +2366,29 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 		const bool flush = base + kMB * kPerT >= cnt || s_used > kMLds / 2;  // uniform
 		if (flush)
 		{
-			for (uint32_t j = t; j < kMLds; j += kMB)
+			// the home slot of every distinct key is read first (all loads in flight together), then claimed / added
+			constexpr uint32_t kPerF = kMLds / kMB;
+			uint32_t fkey[kPerF], fr[kPerF], fprev[kPerF];
+#pragma unroll
+			for (uint32_t u = 0; u < kPerF; ++u)
 			{
-				const uint32_t key = s_key[j];
+				fkey[u] = s_key[u * kMB + t];
+				fr[u] = flow_region_slot(fkey[u], fp.log2r);
+				fprev[u] = fkey[u] ? keys[rbase + fr[u]] : 0u;
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < kPerF; ++u)
+			{
+				const uint32_t j = u * kMB + t, key = fkey[u];
 				if (key == 0)
 					continue;
 				const unsigned long long c = s_cnt[j];
-				uint32_t r = flow_region_slot(key, fp.log2r);
+				uint32_t r = fr[u], prev = fprev[u];
 				bool done = false;
 				for (uint32_t probe = 0; probe <= rm; ++probe)
 				{
-					uint32_t prev = keys[rbase + r];
+					if (probe > 0)
+						prev = keys[rbase + r];
 					if (prev == 0u)
 						prev = atomicCAS(&keys[rbase + r], 0u, key);
 					if (prev == 0u || prev == key)
@@ -2630,10 +2652,11 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 #define PCPPX_FLOW_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true>
 // the partitioned flush (product): the same aggregation, then per-partition queues and one merge block per partition
 #define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true>
-#define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<1024, 8192, 2>
+#define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<kFlowMergeThreads, 8192, 2>
 constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 4096, kFlowBlocks = 256;
 constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed LDS/HBM counters hold
-constexpr uint32_t kFlowPartLog2 = 8;            // flow-table partitions (merge blocks) at most
+constexpr uint32_t kFlowPartLog2 = 8;            // flow-table partitions (merge blocks); at most kFlowMaxParts
+constexpr uint32_t kFlowMergeThreads = 1024;
 
 }  // namespace
 
@@ -2739,7 +2762,7 @@ int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* caplens, ui
 		int rc = check_launch("flow_count_kernel(partitioned)", stream);
 		if (rc != PCPPX_OK)
 			return rc;
-		hipLaunchKernelGGL(PCPPX_FLOW_MERGE_KERNEL, dim3(1u << lp), dim3(kFlowThreads), 0, stream, fp, keys, pk, by, st);
+		hipLaunchKernelGGL(PCPPX_FLOW_MERGE_KERNEL, dim3(1u << lp), dim3(kFlowMergeThreads), 0, stream, fp, keys, pk, by, st);
 		rc = check_launch("flow_merge_kernel", stream);
 		if (rc != PCPPX_OK)
 			return rc;
