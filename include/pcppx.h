@@ -164,9 +164,10 @@ PCPPX_API int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, c
 
 /* Per-flow counters keyed by hash5Tuple (Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:99-125).
  * Device pointers: summary[n] from a previous parse, caplens[n]. The table is open-addressed with
- * `capacity` slots (power of two); keys[i]==0 marks an empty slot — flow key 0 (non-5-tuple packets,
- * PacketUtils.cpp:141-148) is counted in stats[0] (packets) / stats[1] (bytes) instead, and packets
- * that found no free slot in stats[2]. Counts accumulate across calls. */
+ * `capacity` slots (power of two), split into min(capacity, 256) equal regions by the key's hash (a flow lives
+ * in its region); keys[i]==0 marks an empty slot — flow key 0 (non-5-tuple packets, PacketUtils.cpp:141-148)
+ * is counted in stats[0] (packets) / stats[1] (bytes) instead, and packets whose region had no free slot in
+ * stats[2]. Counts accumulate across calls; calls on one context are ordered (they share its scratch). */
 PCPPX_API int pcppx_flow_count_device(pcppx_ctx* ctx, const pcppx_summary* summary, const uint32_t* caplens,
                             uint32_t n, uint32_t* keys, uint64_t* packets, uint64_t* bytes,
                             uint32_t capacity, uint64_t* stats, void* hip_stream);

@@ -1602,11 +1602,13 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // chunk) from the owning lanes by ds_bpermute in every group; the header-window inputs of the L4 sum (edge chunks,
 // checksum field, pseudo header) are taken before the ring overwrites the stage, a tail chunk past the window by a
 // global load issued before the stream.
+// SkipGeneric (tools only, a diagnostic: wrong records): packets off the fast path are not walked -- the time the
+// generic walk costs the waves that hold such a packet.
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
-          bool Ring = false>
+          bool Ring = false, bool SkipGeneric = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1770,7 +1772,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
 			}
 		}
-		else
+		else if (!SkipGeneric)
 		{
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 			w = walk_chain(p, cap, prm, lay_out);

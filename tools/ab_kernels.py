@@ -58,6 +58,7 @@ cases.update({
     "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
     "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),
     "po/gather-only": (abi.make_opts(0, 8, False, _ml), 29),
+    "po/skip-generic": (abi.make_opts(0, 8, False, _ml), 44),
 })
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")
@@ -67,7 +68,7 @@ if only:
 ref_s = ref_l = None
 want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
-    if o.max_layers != next(iter(cases.values()))[0].max_layers or o.want_checksums != want_csum_ref or v in (2, 3, 4, 29):
+    if o.max_layers != next(iter(cases.values()))[0].max_layers or o.want_checksums != want_csum_ref or v in (2, 3, 4, 29, 44):
         continue
     summ.zero_()
     lay.zero_()
