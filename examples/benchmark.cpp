@@ -3,8 +3,9 @@
  * ==========================================================
  * The reference application (Examples/PcapPlusPlus-benchmark/benchmark.cpp:60-109), with one change: instead of
  * reading one RawPacket and building one Packet at a time, the reader fills a batch (getNextPackets, the reference's
- * IFileReaderDevice batch read) and the engine parses the whole batch on the GPU (the batch prepass). The
- * per-packet handler then runs over Packet views with pcpp::Packet's names, as before.
+ * IFileReaderDevice batch read) and the engine parses the whole batch on the GPU (the batch prepass); the next
+ * batch is read by a reader thread meanwhile. The per-packet handler then runs over Packet views with
+ * pcpp::Packet's names, as before.
  *
  *   benchmark <input-file> packet <repetitions> [--host-parser <lib.so>] [--dump]
  *
@@ -19,6 +20,7 @@
 #include <chrono>
 #include <cinttypes>
 #include <cstdio>
+#include <future>
 #include <iostream>
 #include <numeric>
 #include <string>
@@ -101,7 +103,7 @@ int main(int argc, char* argv[])
 		Engine engine(0);
 		if (!hostParser.empty())
 			engine.setHostParser(loadHostParser(hostParser));
-		RawPacketVector batch;
+		RawPacketVector bufs[2];  // batch k is parsed while batch k+1 is read (a reader thread; distinct buffers)
 		for (int i = 0; i < total_runs; ++i)
 		{
 			count = 0;
@@ -113,9 +115,13 @@ int main(int argc, char* argv[])
 				start = std::chrono::high_resolution_clock::now();
 				PacketParseOptions options(TCP);  // Packet(&rawPacket, pcpp::TCP)
 				options.computeChecksums = false;
-				while (reader.getNextPackets(batch, 1 << 20) > 0)
+				int cur = 0;
+				auto next = std::async(std::launch::async, [&] { return reader.getNextPackets(bufs[0], 1 << 20); });
+				while (next.get() > 0)
 				{
-					ParsedBatch parsed = engine.parse(batch, options);  // the batch prepass
+					next = std::async(std::launch::async,
+					                  [&, k = cur ^ 1] { return reader.getNextPackets(bufs[k], 1 << 20); });
+					ParsedBatch parsed = engine.parse(bufs[cur], options);  // the batch prepass
 					for (Packet packet : parsed)
 					{
 						handle_packet(packet);
@@ -123,6 +129,7 @@ int main(int argc, char* argv[])
 							dump(index, packet);
 						++index;
 					}
+					cur ^= 1;
 				}
 			}
 			auto end = std::chrono::high_resolution_clock::now();
