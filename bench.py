@@ -195,19 +195,22 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     flows = None
+    flow_keys = None
     if cfg == 4:  # per-GPU flow table: 2M slots for 1M flows, counters accumulate over all steps
         cap = 1 << 21
         flows = (torch.zeros(cap, dtype=torch.int32, device=dev), torch.zeros(cap, dtype=torch.int64, device=dev),
                  torch.zeros(cap, dtype=torch.int64, device=dev), torch.zeros(4, dtype=torch.int64, device=dev), cap)
+        # the parse also writes the dense hash5 column the flow table is keyed by (pcppx_records.flow_keys)
+        flow_keys = torch.empty(n, dtype=torch.int32, device=dev)
     mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if flows else None
 
     def step(k=None):
-        eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh)
+        eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh, flow_keys)
         if flows is not None:
             if k is not None:
                 mids[k].record(stream)
             keys, pk, by, st, cap = flows
-            eng.flow_count_device(summary, caplens, n, keys, pk, by, cap, st, sh)
+            eng.flow_count_keys_device(flow_keys, caplens, n, keys, pk, by, cap, st, sh)
 
     for _ in range(args.warmup):
         step()
@@ -249,7 +252,7 @@ def main() -> None:
         torch.cuda.synchronize(dev)
         read_bytes = algorithmic_read_bytes(batch, False, ext_sum, ext_lay, caplens, 16)
         del ext_sum, ext_lay
-    write_bytes = n * (32 + 8 * ml)
+    write_bytes = n * (32 + 8 * ml + (4 if flow_keys is not None else 0))
     achieved = read_bytes / (kern_ms * 1e-3) / 1e9
 
     # sanity: the records of the last step parse every packet cleanly (synthetic data has no L7 triggers)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PCPPX_ABI_VERSION 3
+#define PCPPX_ABI_VERSION 4
 /* the library is built with hidden visibility: exactly the functions declared here are exported */
 #define PCPPX_API __attribute__((visibility("default")))
 #define PCPPX_MAX_LAYERS 16     /* fixed depth cap; deeper chains set PCPPX_F_DEPTH_OVERFLOW */
@@ -127,6 +127,9 @@ typedef struct pcppx_records {
 	pcppx_layer* layers;    /* n * max_layers entries, or NULL when max_layers == 0; packet i's layer k is
 	                           layers[i * max_layers + k] for k < min(n_layers, max_layers); the entries past
 	                           n_layers are not written */
+	uint32_t* flow_keys;    /* optional (NULL): n entries, flow_keys[i] = summary[i].hash5 -- the dense column
+	                           FilterTraffic's flow table is keyed by (pcppx_flow_count_keys_device reads 8 B per
+	                           packet from it and caplens instead of 36 B through the summary) */
 } pcppx_records;
 
 /* The caller's own host parse of ONE packet — its Packet++ (`pcpp::Packet packet(&raw, parseUntil...)`) turned
@@ -168,6 +171,10 @@ PCPPX_API int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, c
  * in its region); keys[i]==0 marks an empty slot — flow key 0 (non-5-tuple packets, PacketUtils.cpp:141-148)
  * is counted in stats[0] (packets) / stats[1] (bytes) instead, and packets whose region had no free slot in
  * stats[2]. Counts accumulate across calls; calls on one context are ordered (they share its scratch). */
+/* The same over the dense key column a parse wrote (pcppx_records.flow_keys): keys_in[i] = hash5 of packet i. */
+PCPPX_API int pcppx_flow_count_keys_device(pcppx_ctx* ctx, const uint32_t* keys_in, const uint32_t* caplens, uint32_t n,
+                                           uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity,
+                                           uint64_t* stats, void* hip_stream);
 PCPPX_API int pcppx_flow_count_device(pcppx_ctx* ctx, const pcppx_summary* summary, const uint32_t* caplens,
                             uint32_t n, uint32_t* keys, uint64_t* packets, uint64_t* bytes,
                             uint32_t capacity, uint64_t* stats, void* hip_stream);

@@ -15,7 +15,7 @@ PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 ENGINE_SO = PKG_DIR / "libpcppx.so"
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_LAYERS = 16
 MAX_CAPLEN = 65535
 
@@ -103,7 +103,7 @@ class Opts(C.Structure):
 
 
 class Records(C.Structure):
-    _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p)]
+    _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p), ("flow_keys", C.c_void_p)]
 
 
 class MatchSpec(C.Structure):
@@ -158,6 +158,8 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_parse_batch_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records), P]
     lib.pcppx_parse_batch_host.argtypes = [P, C.POINTER(Batch), C.POINTER(Opts), C.POINTER(Records)]
     lib.pcppx_flow_count_device.argtypes = [P, P, P, C.c_uint32, P, P, P, C.c_uint32, P, P]
+    lib.pcppx_flow_count_keys_device.argtypes = [P, P, P, C.c_uint32, P, P, P, C.c_uint32, P, P]
+    lib.pcppx_flow_count_keys_device.restype = C.c_int
     lib.pcppx_filter_device.argtypes = [P, C.POINTER(Batch), C.POINTER(Records), C.c_uint8, C.POINTER(MatchSpec),
                                         C.c_uint64, P, P, C.c_uint32, P, P, P]
     lib.pcppx_filter_device.restype = C.c_int
@@ -197,7 +199,7 @@ _ENGINE: C.CDLL | None = None
 EXPORTED_SYMBOLS = (
     "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_runtime_info", "pcppx_open", "pcppx_close",
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
-    "pcppx_flow_count_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_parse_batch_device_reasm", "pcppx_pcap_open", "pcppx_pcap_linktype",
+    "pcppx_flow_count_device", "pcppx_flow_count_keys_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_parse_batch_device_reasm", "pcppx_pcap_open", "pcppx_pcap_linktype",
     "pcppx_pcap_read_batch", "pcppx_pcap_read_batch_ex", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
 )
 

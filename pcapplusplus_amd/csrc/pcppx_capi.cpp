@@ -341,6 +341,9 @@ void free_filter(pcppx_ctx* c)
 	c->seq = 0;
 }
 
+int flow_count(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* keys_in, const uint32_t* caplens, uint32_t n,
+               uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, void* hip_stream);
+
 // forget every slot's chunk without copying it out: after an error mid-call, and at the start of each host
 // call, so that a later call never drains a stale chunk into its own (possibly smaller) output arrays
 void abandon_slots(pcppx_ctx* c)
@@ -364,6 +367,9 @@ void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out)
 		if (s.ml && out->layers)
 			cp.copy(out->layers + (size_t)s.first * s.ml, s.h_lay, (size_t)s.count * s.ml * sizeof(pcppx_layer));
 	}
+	if (out->flow_keys)  // the dense hash5 column, from the host copy of the summaries
+		for (uint32_t k = 0; k < s.count; ++k)
+			out->flow_keys[s.first + k] = out->summary[s.first + k].hash5;
 	s.busy = false;
 }
 // pcppx_parse_batch_host's chunk pipeline (argument checks done; slots idle on entry)
@@ -391,7 +397,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		if (!upload_chunk(s, pos, cnt, direct))
 			return PCPPX_E_HIP;
 		pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
-		pcppx_records dr{ s.d_sum, ml ? s.d_lay : nullptr };
+		pcppx_records dr{ s.d_sum, ml ? s.d_lay : nullptr, nullptr };
 		rc = pcppx::launch_parse(&db, o, &dr, s.st);
 		if (rc != PCPPX_OK)
 			return rc;
@@ -451,7 +457,7 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 		if (prev != nullptr && !ok(hipStreamWaitEvent(s.st, prev->done, 0)))
 			return PCPPX_E_HIP;
 		pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
-		pcppx_records dr{ s.d_sum, s.d_lay };
+		pcppx_records dr{ s.d_sum, s.d_lay, nullptr };
 		rc = pcppx::launch_parse(&db, &o, &dr, s.st);
 		if (rc == PCPPX_OK)
 			rc = pcppx::launch_filter(&db, &dr, ml, spec, c->seq + i, c->d_keys, c->d_first, c->flow_slots,
@@ -746,12 +752,29 @@ extern "C"
 	                            uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity,
 	                            uint64_t* stats, void* hip_stream)
 	{
+		return flow_count(c, summary, nullptr, caplens, n, keys, packets, bytes, capacity, stats, hip_stream);
+	}
+
+	int pcppx_flow_count_keys_device(pcppx_ctx* c, const uint32_t* keys_in, const uint32_t* caplens, uint32_t n,
+	                                 uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity,
+	                                 uint64_t* stats, void* hip_stream)
+	{
+		return flow_count(c, nullptr, keys_in, caplens, n, keys, packets, bytes, capacity, stats, hip_stream);
+	}
+}
+
+namespace
+{
+// pcppx_flow_count_device / _keys_device: keys from the summaries or from a dense column (exactly one non-null)
+int flow_count(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* keys_in, const uint32_t* caplens, uint32_t n,
+               uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, void* hip_stream)
+{
 		if (c == nullptr || capacity == 0 || (capacity & (capacity - 1)) != 0)
 			return PCPPX_E_INVAL;
 		if (n == 0)
 			return PCPPX_OK;
-		if (summary == nullptr || caplens == nullptr || keys == nullptr || packets == nullptr || bytes == nullptr ||
-		    stats == nullptr)
+		if ((summary == nullptr) == (keys_in == nullptr) || caplens == nullptr || keys == nullptr || packets == nullptr ||
+		    bytes == nullptr || stats == nullptr)
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
@@ -780,7 +803,7 @@ extern "C"
 			return PCPPX_E_HIP;
 		if (c->flow_pending && !ok(hipStreamWaitEvent(st, c->flow_done, 0)))
 			return PCPPX_E_HIP;
-		const int rc = pcppx::launch_flow_count_part(summary, caplens, n, keys, packets, bytes, capacity, stats,
+		const int rc = pcppx::launch_flow_count_part(summary, keys_in, caplens, n, keys, packets, bytes, capacity, stats,
 		                                             c->d_flow_queues, rec_cap, c->d_flow_fill, st);
 		if (rc != PCPPX_OK)
 			return rc;

@@ -15,9 +15,9 @@ int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, con
 // the partitioned flow table (product): queues = P x rec_cap 16-B records, fill = P zeroed counters
 uint32_t flow_partitions(uint32_t capacity);
 uint32_t flow_queue_capacity(uint32_t n, uint32_t capacity);
-int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
-                           uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, void* queues,
-                           uint32_t rec_cap, uint32_t* fill, hipStream_t stream);
+int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* dkeys, const uint32_t* caplens, uint32_t n,
+                           uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats,
+                           void* queues, uint32_t rec_cap, uint32_t* fill, hipStream_t stream);
 int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
                        hipStream_t stream);
 int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcppx_reasm_info* info, hipStream_t stream);

@@ -705,6 +705,7 @@ struct Params
 	uint64_t data_len;
 	pcppx_summary* summary;
 	pcppx_layer* layers;
+	uint32_t* flow_keys;  // optional dense hash5 column
 	uint32_t n;
 	uint32_t family;
 	uint32_t until_osi;
@@ -1957,6 +1958,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	}
 	else if (in)
 		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
+	if (in && prm.flow_keys != nullptr)
+		__builtin_nontemporal_store(h5, prm.flow_keys + i);
 
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
 	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
@@ -2101,14 +2104,15 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 	return false;
 }
 
+// kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false>
+          bool kPart = false, bool kDense = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
                                                             unsigned long long* bytes, uint32_t capacity,
                                                             unsigned long long* stats, unsigned long long* packed,
-                                                            FlowPart fpart = FlowPart{})
+                                                            FlowPart fpart = FlowPart{}, const uint32_t* dkeys = nullptr)
 {
 	__shared__ uint32_t s_bin[kPart ? kFlowMaxParts : 1], s_base[kPart ? kFlowMaxParts : 1];  // per-partition counts / offsets
 	__shared__ uint32_t s_key[kFlowLds];
@@ -2136,7 +2140,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		for (uint32_t r = 0; r < kR; ++r)
 		{
 			const uint64_t i = b + r * kFB + t;
-			pkey[r] = i < n ? sum[i].hash5 : 0u;
+			pkey[r] = i < n ? (kDense ? dkeys[i] : sum[i].hash5) : 0u;
 			plen[r] = i < n ? caplens[i] : 0u;
 			pvalid |= (i < n ? 1u : 0u) << r;
 		}
@@ -2151,7 +2155,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 			const uint64_t i = base + r * kFB + t;
 			if (kPrefetch ? !((pvalid >> r) & 1u) : i >= n)
 				break;
-			const uint32_t key = kPrefetch ? pkey[r] : sum[i].hash5;
+			const uint32_t key = kPrefetch ? pkey[r] : (kDense ? dkeys[i] : sum[i].hash5);
 			const uint32_t len = kPrefetch ? plen[r] : caplens[i];
 			if (key == 0)
 			{
@@ -2624,6 +2628,7 @@ Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, 
 	prm.caplens = b->caplens;
 	prm.data_len = b->data_len;
 	prm.summary = r->summary;
+	prm.flow_keys = r->flow_keys;
 	prm.layers = o->max_layers ? r->layers : nullptr;
 	prm.n = b->n;
 	prm.family = o->parse_until_family;
@@ -2654,6 +2659,7 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 #define PCPPX_FLOW_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true>
 // the partitioned flush (product): the same aggregation, then per-partition queues and one merge block per partition
 #define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true>
+#define PCPPX_FLOW_PART_DENSE_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true>
 #define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<kFlowMergeThreads, 8192, 2>
 constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 4096, kFlowBlocks = 256;
 constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed LDS/HBM counters hold
@@ -2746,9 +2752,9 @@ uint32_t flow_queue_capacity(uint32_t n, uint32_t capacity)
 	return 2 * ((per + parts - 1) / parts) + 4096;
 }
 
-int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n, uint32_t* keys,
-                           uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, void* queues,
-                           uint32_t rec_cap, uint32_t* fill, hipStream_t stream)
+int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* dkeys, const uint32_t* caplens, uint32_t n,
+                           uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats,
+                           void* queues, uint32_t rec_cap, uint32_t* fill, hipStream_t stream)
 {
 	auto* pk = reinterpret_cast<unsigned long long*>(packets);
 	auto* by = reinterpret_cast<unsigned long long*>(bytes);
@@ -2759,8 +2765,13 @@ int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* caplens, ui
 	{
 		const uint32_t cnt = n - done < kPackedMax ? n - done : kPackedMax;
 		const uint32_t batches = (cnt + kFlowBatchPk - 1) / kFlowBatchPk;
-		hipLaunchKernelGGL(PCPPX_FLOW_PART_KERNEL, dim3(batches < kFlowBlocks ? batches : kFlowBlocks), dim3(kFlowThreads), 0,
-		                   stream, sum + done, caplens + done, cnt, keys, pk, by, capacity, st, nullptr, fp);
+		const dim3 grid(batches < kFlowBlocks ? batches : kFlowBlocks);
+		if (dkeys != nullptr)
+			hipLaunchKernelGGL(PCPPX_FLOW_PART_DENSE_KERNEL, grid, dim3(kFlowThreads), 0, stream, nullptr, caplens + done, cnt,
+			                   keys, pk, by, capacity, st, nullptr, fp, dkeys + done);
+		else
+			hipLaunchKernelGGL(PCPPX_FLOW_PART_KERNEL, grid, dim3(kFlowThreads), 0, stream, sum + done, caplens + done, cnt,
+			                   keys, pk, by, capacity, st, nullptr, fp, nullptr);
 		int rc = check_launch("flow_count_kernel(partitioned)", stream);
 		if (rc != PCPPX_OK)
 			return rc;

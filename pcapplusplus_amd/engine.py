@@ -59,11 +59,12 @@ class Engine:
 
     # ---- device-resident batches (torch tensors on this GPU) ----
     def parse_device(self, data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers=None,
-                     stream: int | None = None) -> None:
+                     stream: int | None = None, flow_keys=None) -> None:
         """Queue a parse of device tensors on `stream` (a hipStream_t handle, e.g.
         torch.cuda.current_stream().cuda_stream). summary: uint8 tensor of n*32 bytes; layers: n*max_layers*8."""
         b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
-        rec = abi.Records(abi.ptr(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None)
+        rec = abi.Records(abi.ptr(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None,
+                          abi.ptr(flow_keys) if flow_keys is not None else None)
         abi.check(self.lib.pcppx_parse_batch_device(self.ctx, C.byref(b), C.byref(opts), C.byref(rec),
                                                     C.c_void_p(stream or 0)), "pcppx_parse_batch_device")
 
@@ -72,6 +73,13 @@ class Engine:
         abi.check(self.lib.pcppx_flow_count_device(self.ctx, abi.ptr(summary), abi.ptr(caplens), n, abi.ptr(keys),
                                                    abi.ptr(packets), abi.ptr(bytes_), capacity, abi.ptr(stats),
                                                    C.c_void_p(stream or 0)), "pcppx_flow_count_device")
+
+    def flow_count_keys_device(self, flow_keys, caplens, n: int, keys, packets, bytes_, capacity: int, stats,
+                               stream: int | None = None) -> None:
+        """pcppx_flow_count_keys_device: the flow table over the dense hash5 column a parse wrote (flow_keys)."""
+        abi.check(self.lib.pcppx_flow_count_keys_device(self.ctx, abi.ptr(flow_keys), abi.ptr(caplens), n, abi.ptr(keys),
+                                                        abi.ptr(packets), abi.ptr(bytes_), capacity, abi.ptr(stats),
+                                                        C.c_void_p(stream or 0)), "pcppx_flow_count_keys_device")
 
     def filter_device(self, data, offsets, caplens, n: int, linktype: int, summary, layers, max_layers: int,
                       spec: abi.MatchSpec, seq_base: int, flow_keys, flow_first, capacity: int, matched, stats,

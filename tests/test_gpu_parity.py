@@ -320,6 +320,53 @@ def test_gpu_flow_table_many_batches_per_block(engine):
     assert (int(st[0]), int(st[1]), int(st[2])) == (zero[0], zero[1], 0)
 
 
+def test_gpu_flow_keys_column(engine):
+    """pcppx_records.flow_keys: the parse writes every packet's hash5 into the dense column (device and host paths), and
+    pcppx_flow_count_keys_device over it builds exactly the table pcppx_flow_count_device builds from the summaries."""
+    import torch
+
+    from pcapplusplus_amd.engine import to_device
+
+    b = synth.imix(1_500_000, 9, corrupt_frac=0.0, flows=100_000)
+    dev = "cuda:0"
+    data, offs, caps = to_device(b, dev)
+    n = b.n
+    summ = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    fk = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    st0 = torch.cuda.current_stream().cuda_stream
+    for csum in (False, True):
+        engine.parse_device(data, offs, caps, n, b.linktype, abi.make_opts(0, 8, csum, 0), summ, None, st0, fk)
+        torch.cuda.synchronize()
+        s = summ.cpu().numpy().view(abi.SUMMARY_DTYPE)
+        assert np.array_equal(fk.cpu().numpy().view(np.uint32), s["hash5"])
+    cap = 1 << 18
+    tabs = []
+    for dense in (False, True):
+        keys = torch.zeros(cap, dtype=torch.int32, device=dev)
+        pk = torch.zeros(cap, dtype=torch.int64, device=dev)
+        by = torch.zeros(cap, dtype=torch.int64, device=dev)
+        stt = torch.zeros(4, dtype=torch.int64, device=dev)
+        for _ in range(2):
+            if dense:
+                engine.flow_count_keys_device(fk, caps, n, keys, pk, by, cap, stt, st0)
+            else:
+                engine.flow_count_device(summ, caps, n, keys, pk, by, cap, stt, st0)
+        torch.cuda.synchronize()
+        k = keys.cpu().numpy().view(np.uint32)
+        tabs.append((k.copy(), pk.cpu().numpy(), by.cpu().numpy(), stt.cpu().numpy()))
+    for a, z in zip(tabs[0], tabs[1]):
+        assert np.array_equal(a, z)
+    sub = b.slice(0, 200_000)
+    opts = abi.make_opts(0, 8, True, 0)
+    out = (np.zeros(sub.n, dtype=abi.SUMMARY_DTYPE), np.zeros(1, dtype=abi.LAYER_DTYPE))
+    hk = np.zeros(sub.n, dtype=np.uint32)
+    rec = abi.Records(out[0].ctypes.data, None, hk.ctypes.data)
+    bb = sub.c_batch()
+    import ctypes as C
+    abi.check(engine.lib.pcppx_parse_batch_host(engine.ctx, C.byref(bb), C.byref(opts), C.byref(rec)), "host")
+    assert np.array_equal(hk, out[0]["hash5"]) and hk.any()
+
+
 def test_gpu_flow_table_full_conserves_packets(engine):
     """A table far smaller than the flow count: a key once stored is never displaced, so every stored
     flow's counters are exact, and stored + lost (stats[2]) + key-0 packets account for every packet."""

@@ -220,7 +220,7 @@ PCPPX_AB_API int pcppx_ab_flow_count_device(const pcppx_summary* sum, const uint
 		const uint32_t batches = (n + batch - 1) / batch;
 		const uint32_t cap = grid ? grid : def_grid;
 		hipLaunchKernelGGL(kern, dim3(batches < cap ? batches : cap), dim3(threads), 0, stream, sum, caplens, n, keys, pk,
-		                   by, capacity, st, pc, FlowPart{});
+		                   by, capacity, st, pc, FlowPart{}, nullptr);
 	};
 	switch (shape)
 	{
