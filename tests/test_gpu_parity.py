@@ -353,9 +353,10 @@ def test_gpu_flow_keys_column(engine):
                 engine.flow_count_device(summ, caps, n, keys, pk, by, cap, stt, st0)
         torch.cuda.synchronize()
         k = keys.cpu().numpy().view(np.uint32)
-        tabs.append((k.copy(), pk.cpu().numpy(), by.cpu().numpy(), stt.cpu().numpy()))
-    for a, z in zip(tabs[0], tabs[1]):
-        assert np.array_equal(a, z)
+        used = k != 0  # slot positions depend on the claim order: compare by key
+        tabs.append((dict(zip(k[used].tolist(), zip(pk.cpu().numpy()[used].tolist(), by.cpu().numpy()[used].tolist()))),
+                     stt.cpu().numpy().tolist()))
+    assert tabs[0] == tabs[1] and len(tabs[0][0]) > 50_000
     sub = b.slice(0, 200_000)
     opts = abi.make_opts(0, 8, True, 0)
     out = (np.zeros(sub.n, dtype=abi.SUMMARY_DTYPE), np.zeros(1, dtype=abi.LAYER_DTYPE))
