@@ -31,6 +31,8 @@ def lib() -> C.CDLL:
         l.pcppx_ab_parse_device.restype = C.c_int
         l.pcppx_ab_flow_count_device.argtypes = [P, P, C.c_uint32, P, P, P, C.c_uint32, P, P, P, C.c_int, C.c_uint32]
         l.pcppx_ab_flow_count_device.restype = C.c_int
+        l.pcppx_ab_flow_part.argtypes = [P, P, C.c_uint32, P, P, P, C.c_uint32, P, P, C.c_uint32, P, P, C.c_int]
+        l.pcppx_ab_flow_part.restype = C.c_int
         _lib = l
     return _lib
 

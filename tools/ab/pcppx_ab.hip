@@ -199,6 +199,38 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	return check_launch("pcppx_ab_parse_device", stream);
 }
 
+/* The partitioned flow table over a dense key column with count-kernel shape `shape` (0: the product's
+ * 1024 threads / 8192 LDS slots / 4096-packet batches / 256 blocks; 1: 512 / 4096 / 2048 / 768; 2: 256 / 2048 / 1024 /
+ * 1536; 3: 1024 / 8192 / 4096 / 512), then the product's merge. queues / fill: scratch as pcppx_capi.cpp sizes it. */
+PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caplens, uint32_t n, uint32_t* keys,
+                                    uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, void* queues,
+                                    uint32_t rec_cap, uint32_t* fill, void* hip_stream, int shape)
+{
+	hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+	auto* pk = reinterpret_cast<unsigned long long*>(packets);
+	auto* by = reinterpret_cast<unsigned long long*>(bytes);
+	auto* st = reinterpret_cast<unsigned long long*>(stats);
+	const uint32_t l = log2u(capacity), lp = l < kFlowPartLog2 ? l : kFlowPartLog2;
+	const FlowPart fp{ static_cast<uint4*>(queues), rec_cap, fill, lp, l - lp };
+	auto go = [&](auto kern, uint32_t threads, uint32_t batch, uint32_t blocks) {
+		const uint32_t batches = (n + batch - 1) / batch;
+		hipLaunchKernelGGL(kern, dim3(batches < blocks ? batches : blocks), dim3(threads), 0, stream, nullptr, caplens, n,
+		                   keys, pk, by, capacity, st, nullptr, fp, dkeys);
+	};
+	switch (shape)
+	{
+	case 1: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true, true, true>, 512, 2048, 768); break;
+	case 2: go(flow_count_kernel<256, 2048, 1024, kFlowHot, true, true, true>, 256, 1024, 1536); break;
+	case 3: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 512); break;
+	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 256); break;
+	}
+	int rc = check_launch("pcppx_ab_flow_part", stream);
+	if (rc != PCPPX_OK)
+		return rc;
+	hipLaunchKernelGGL(PCPPX_FLOW_MERGE_KERNEL, dim3(1u << lp), dim3(kFlowMergeThreads), 0, stream, fp, keys, pk, by, st);
+	return check_launch("flow_merge_kernel", stream);
+}
+
 /* Flow-table shapes 0-12 of profiles/r01_ab_flow_shape.txt (9 = the product's); grid 0 = the shape's default
  * persistent grid. packed: zeroed u64[capacity] scratch (the product's packed accumulator) or NULL. */
 PCPPX_AB_API int pcppx_ab_flow_count_device(const pcppx_summary* sum, const uint32_t* caplens, uint32_t n,

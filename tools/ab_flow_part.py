@@ -1,0 +1,66 @@
+"""Interleaved A/B of the partitioned flow table's count-kernel shapes (tools/ab pcppx_ab_flow_part) on config 4's
+12.5M packets over their dense hash5 column; every shape's table must equal shape 0's by key.
+
+  python tools/ab_flow_part.py [rounds]
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch  # noqa: E402
+
+from pcapplusplus_amd import abi, synth  # noqa: E402
+from pcapplusplus_amd.engine import Engine, to_device  # noqa: E402
+from tools import ab  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+b = synth.imix(12_500_000, 4, flows=1_000_000, corrupt_frac=0.0)
+n = b.n
+dev = "cuda:0"
+data, offs, caps = to_device(b, dev)
+st = torch.cuda.current_stream()
+eng = Engine(0)
+summ = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+fk = torch.empty(n, dtype=torch.int32, device=dev)
+eng.parse_device(data, offs, caps, n, b.linktype, abi.make_opts(0, 8, False, 0), summ, None, st.cuda_stream, fk)
+cap = 1 << 21
+parts = 256
+rec_cap = 2 * ((n + parts - 1) // parts) + 4096
+queues = torch.empty(parts * rec_cap * 4, dtype=torch.int32, device=dev)
+fill = torch.zeros(1024, dtype=torch.int32, device=dev)
+
+
+def run(shape):
+    t = (torch.zeros(cap, dtype=torch.int32, device=dev), torch.zeros(cap, dtype=torch.int64, device=dev),
+         torch.zeros(cap, dtype=torch.int64, device=dev), torch.zeros(4, dtype=torch.int64, device=dev))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    abi.check(ab.lib().pcppx_ab_flow_part(abi.ptr(fk), abi.ptr(caps), n, abi.ptr(t[0]), abi.ptr(t[1]), abi.ptr(t[2]), cap,
+                                          abi.ptr(t[3]), abi.ptr(queues), rec_cap, abi.ptr(fill), st.cuda_stream, shape),
+              "pcppx_ab_flow_part")
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1), t
+
+
+shapes = (0, 1, 2, 3)
+ref = None
+for s in shapes:
+    _, t = run(s)
+    k = t[0].cpu().numpy().view(np.uint32)
+    used = k != 0
+    d = dict(zip(k[used].tolist(), zip(t[1].cpu().numpy()[used].tolist(), t[2].cpu().numpy()[used].tolist())))
+    if ref is None:
+        ref = d
+    print(f"shape {s}: table equal to shape 0: {d == ref} ({len(d)} flows)", flush=True)
+times = {s: [] for s in shapes}
+for r in range(rounds):
+    for s in shapes:
+        ms, _ = run(s)
+        if r:
+            times[s].append(ms)
+for s in shapes:
+    t = np.array(times[s])
+    print(f"shape {s}: median {np.median(t):.4f} ms  min {t.min():.4f} ms (count + merge)")
