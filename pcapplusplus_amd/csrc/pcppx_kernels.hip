@@ -2641,12 +2641,16 @@ Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, 
 	return prm;
 }
 
-// the parse kernel's shape: 5 waves/SIMD (96 VGPRs, 8 KiB LDS), 2 x 2 KiB span-stream windows, 112-B header
-// windows, non-temporal span loads and record stores -- the fastest of the measured shapes
+// the parse kernel's shape: 5 waves/SIMD (87 VGPRs, 7 KiB LDS), 2 x 2 KiB span-stream windows, non-temporal span
+// loads and record stores -- the fastest of the measured shapes
 // (profiles/r01_ab_occupancy.txt, r01_ab_windows.txt, r01_ab_window160.txt, r01_ab_nontemporal.txt; the
 // other shapes are built only into tools/ab/libpcppx_ab.so)
 constexpr int kParseWaves = 5, kParseSWin = 128;
-#define PCPPX_PARSE_KERNEL parse_tile_kernel<kParseWaves, kParseSWin, kTStageChunks, true>
+// 96-B header windows since round 2: every Eth / VLAN / IPv4|IPv6 / TCP|UDP stack fits (deeper stacks take the generic
+// walk's HBM peeks past the window); 1.5% faster than 112 B on config 3 in two interleaved A/Bs, and a two-round
+// 96 + 16 B gather is slower (profiles/r02_ab_windows96.txt)
+constexpr int kParseChunks = 6;
+#define PCPPX_PARSE_KERNEL parse_tile_kernel<kParseWaves, kParseSWin, kParseChunks, true>
 // parse-only launches (no checksums): no span stream; a 144-B window reached in two gather rounds (96 B for every
 // packet, the rest only for the deep stacks the first window cannot hold): 99.7% of config 5's deep stacks take the
 // fast path; 16 waves/CU of LDS (144 B: 0.88 ms on config 5, 160 B: 1.00 ms at 14 waves/CU, 112 B: 1.17 ms with
