@@ -191,6 +191,8 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 45: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96-B windows
 	case 46: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, false, true, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96-B windows, 6 waves
 	case 47: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96 + 16 B two-round
+	case 48: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 6, true>), grid, dim3(kTile), 0, stream, prm); break;  // 1-KiB windows, 6 waves
+	case 49: hipLaunchKernelGGL((parse_tile_kernel<5, 64, 6, true>), grid, dim3(kTile), 0, stream, prm); break;   // 1-KiB windows
 	case 44: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // skip-generic diagnostic
 	case 29: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // gather-only diagnostic
 	case 28: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 5, false, false>), grid, dim3(kTile), 0, stream, prm); break;

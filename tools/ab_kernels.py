@@ -35,6 +35,8 @@ cases = {
     "tile/c6": (abi.make_opts(0, 8, True, 8), 45),
     "tile/c6w6": (abi.make_opts(0, 8, True, 8), 46),
     "tile/c7r6": (abi.make_opts(0, 8, True, 8), 47),
+    "tile/c6w6win64": (abi.make_opts(0, 8, True, 8), 48),
+    "tile/c6win64": (abi.make_opts(0, 8, True, 8), 49),
     "lane/ml8/csum": (abi.make_opts(0, 8, True, 8), 1),
     "tile/ml0/csum": (abi.make_opts(0, 8, True, 0), 0),
     "tile/ml8/nocsum": (abi.make_opts(0, 8, False, 8), 0),
