@@ -171,7 +171,10 @@ def stats_settled(batch, summary, layers):
     fl = summary["flags"].astype(np.int64)
     settled = ((fl & (abi.F_NEEDS_HOST_PROTO | abi.F_OVERSIZE | abi.F_BAD_DESC)) == 0) & \
         (((fl & abi.F_NEEDS_HOST_L7) == 0) | ((fl & abi.F_L7_KNOWN) != 0))
-    l7 = (((fl & abi.F_L7_HTTP) != 0) * 1 | ((fl & abi.F_L7_DNS) != 0) * 2 | ((fl & abi.F_L7_SSL) != 0) * 4).astype(np.int32)
+    m = summary["proto_mask"].astype(np.uint64)
+    bit = lambda p: ((m >> np.uint64(p)) & np.uint64(1)) != 0  # noqa: E731  (layers the parse built)
+    l7 = ((((fl & abi.F_L7_HTTP) != 0) | bit(6) | bit(7)) * 1 | (((fl & abi.F_L7_DNS) != 0) | bit(13)) * 2 |
+          (((fl & abi.F_L7_SSL) != 0) | bit(18)) * 4).astype(np.int32)
     return settled, l7
 
 
@@ -322,8 +325,9 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
     return stats
 
 
-# protocols the engine builds itself (include/pcppx.h: everything else is a host layer)
-ENGINE_PROTOS = (1, 2, 3, 4, 5, 8, 9, 14, 15, 16, 17, 19, 21, 25, 30, 33, 44, 52)
+# protocols the engine builds itself (include/pcppx.h: everything else is a host layer); HTTPRequest /
+# HTTPResponse (6/7), DNS (13) and SSL (18) as a classified first L7 layer and the layers behind it
+ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 14, 15, 16, 17, 18, 19, 21, 25, 30, 33, 44, 52)
 
 
 def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:

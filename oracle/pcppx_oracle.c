@@ -220,14 +220,125 @@ static uint16_t tcp_l7(const uint8_t* d, uint32_t n, uint16_t sp, uint16_t dp)
 static uint16_t udp_l7(uint32_t n, uint16_t sp, uint16_t dp, int sip)
 {
 	if (!udp_l7_port(sp, dp) && !sip) return 0;
+	int dhcp = (sp == 68 && dp == 67) || (sp == 67 && dp == 68) || (sp == 67 && dp == 67);
+	/* DnsLayer after DHCP and VXLAN (UdpLayer.cpp:103-115): 12 bytes (DnsLayer.h:481-485) and a DNS port */
+	if (!dhcp && dp != 4789 && n >= 12 && (dns_port(sp) || dns_port(dp)))
+		return PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN | PCPPX_F_L7_DNS;
 	/* VXLAN (dst 4789, VxlanLayer.h:119-122) and GTPv1 (2152/2123, GtpLayer.h:386-389) carry a whole inner
 	 * packet whose layers only the host sees */
 	if (dp == 4789 || sp == 2152 || dp == 2152 || sp == 2123 || dp == 2123) return PCPPX_F_NEEDS_HOST_L7;
-	uint16_t cls = PCPPX_F_L7_KNOWN;
-	int dhcp = (sp == 68 && dp == 67) || (sp == 67 && dp == 68) || (sp == 67 && dp == 67);
-	/* DnsLayer after DHCP and VXLAN (UdpLayer.cpp:103-115): 12 bytes (DnsLayer.h:481-485) and a DNS port */
-	if (!dhcp && n >= 12 && (dns_port(sp) || dns_port(dp))) cls |= PCPPX_F_L7_DNS;
-	return PCPPX_F_NEEDS_HOST_L7 | cls;
+	return PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN;
+}
+
+/* ---- the classified first L7 layers the engine builds itself (HTTP, SSL, DNS) ----
+ * With no parse-until family, a payload classified HTTP / SSL / DNS above (the layer the reference builds is then
+ * certain) gets the reference's layers instead of NEEDS_HOST_L7. Each layer's data runs to the end of the L4
+ * payload, so the trailer rule is the plain Payload's. */
+enum { P_HTTP_REQ = 6, P_HTTP_RESP = 7, P_DNS = 13, P_SSL = 18 };
+typedef struct {
+	uint8_t proto, osi;
+	uint32_t off, hdr, dlen;
+} lay;
+/* HeaderField::HeaderField size, TextBasedProtocol.cpp:448-461: through the first '\n', else strnlen to the end */
+static uint32_t tbp_field(const uint8_t* d, uint32_t a, uint32_t n)
+{
+	const uint8_t* e = (const uint8_t*)memchr(d + a, '\n', n - a);
+	if (e) return (uint32_t)(e - (d + a)) + 1;
+	return (uint32_t)strnlen((const char*)d + a, n - a);
+}
+/* TextBasedProtocolMessage::parseFields + getHeaderLen (TextBasedProtocol.cpp:87-139,436-439): fields from the
+ * end of the first line until an end-of-header field (size 0, or starting '\r' / '\n'), the end of the data, or
+ * an empty field; the header ends with the last field kept */
+static uint32_t tbp_header_len(const uint8_t* d, uint32_t fl, uint32_t n)
+{
+	uint32_t off = fl, s = tbp_field(d, off, n);
+	int end = s == 0 || d[off] == '\r' || d[off] == '\n';
+	while (!end && off + s < n) {
+		uint32_t s2 = tbp_field(d, off + s, n);
+		if (s2 == 0) break;
+		off += s;
+		s = s2;
+		end = d[off] == '\r' || d[off] == '\n';
+	}
+	return off + s;
+}
+/* HttpRequestFirstLine (HttpLayer.cpp:166-213, parseVersion :287-320, cross_platform_memmem GeneralUtils.cpp:86-113):
+ * the first " HTTP/" after the method's space; with room for "x.y" the line ends at the next '\n', else (or with
+ * no version) at the end of the data */
+static uint32_t http_request_line(const uint8_t* d, uint32_t n)
+{
+	uint32_t sp = 0;
+	while (d[sp] != ' ') ++sp; /* exists: http_request() */
+	for (uint32_t v = sp + 1; v + 6 <= n; ++v) {
+		if (memcmp(d + v, " HTTP/", 6) != 0) continue;
+		if (v + 9 > n) return n;
+		const uint8_t* e = (const uint8_t*)memchr(d + v + 6, '\n', n - v - 6);
+		return e ? (uint32_t)(e - d) + 1 : n;
+	}
+	return n;
+}
+/* HttpResponseFirstLine (HttpLayer.cpp:897-920): through the first '\n' */
+static uint32_t http_response_line(const uint8_t* d, uint32_t n)
+{
+	const uint8_t* e = (const uint8_t*)memchr(d, '\n', n);
+	return e ? (uint32_t)(e - d) + 1 : n;
+}
+/* The layers of a classified L7 payload at [off, off+n) behind the L4 layer l4, appended at index count:
+ *   HTTP: HttpRequestLayer / HttpResponseLayer (HttpLayer.cpp:62-68,666-672), a Payload for the body
+ *         (TextBasedProtocolMessage::parseNextLayer, TextBasedProtocol.cpp:427-434);
+ *   SSL:  one SSLLayer per record (SSLLayer::getHeaderLen / parseNextLayer, SSLLayer.cpp:88-106; every record type
+ *         has protocol SSL, OSI presentation, SSLLayer.h:246-249) while the rest is another record header;
+ *   DNS:  DnsLayer / DnsOverTcpLayer, header = the whole data, no next layer (DnsLayer.h:353-372).
+ * Each layer passes the stop rules of Packet::parsePacket (Packet.cpp:134-155) before it is kept; the first one
+ * that fails is rolled back (:168-175) and ends the chain (*stopped). Returns the new count; *last is the last
+ * layer kept. */
+static int family_member(uint32_t fam, uint8_t p);
+static int l7_layers(const uint8_t* pkt, uint32_t off, uint32_t n, uint16_t cls, const lay* l4, const pcppx_opts* opts,
+                     int* found, int* stopped, pcppx_layer* layers, int cap, int count, uint64_t* mask, lay* last)
+{
+	const uint8_t* d = pkt + off;
+	lay L = { 0, 7, off, 0, n };
+#define EMIT() do { \
+		int member_ = family_member(opts->parse_until_family, L.proto); \
+		int fail_ = L.osi > opts->parse_until_osi; \
+		if (!fail_) { \
+			if (opts->parse_until_family != 0 && member_) *found = 1; \
+			if (*found && !member_) fail_ = 1; \
+		} \
+		if (fail_) { *stopped = 1; goto done; } \
+		if (layers && count < cap) { \
+			pcppx_layer* o = &layers[count]; \
+			o->proto = L.proto; o->osi = L.osi; \
+			o->offset = (uint16_t)L.off; o->hdr_len = (uint16_t)L.hdr; o->data_len = (uint16_t)L.dlen; \
+		} \
+		*mask |= (uint64_t)1 << L.proto; *last = L; ++count; } while (0)
+	if (cls & PCPPX_F_L7_HTTP) {
+		const int req = http_port(be16(pkt + l4->off + 2)) && http_request(d, n); /* tcp_l7's order */
+		L.proto = req ? P_HTTP_REQ : P_HTTP_RESP;
+		L.hdr = tbp_header_len(d, req ? http_request_line(d, n) : http_response_line(d, n), n);
+		EMIT();
+		if (n > L.hdr) {
+			L.proto = P_PAYLOAD; L.off = off + L.hdr; L.dlen = n - L.hdr; L.hdr = L.dlen;
+			EMIT();
+		}
+	} else if (cls & PCPPX_F_L7_SSL) {
+		uint32_t ro = off, rem = n;
+		for (;;) {
+			uint32_t hl = 5u + be16(pkt + ro + 3);
+			if (hl > rem) hl = rem;
+			L.proto = P_SSL; L.osi = 6; L.off = ro; L.hdr = hl; L.dlen = rem;
+			EMIT();
+			if (rem <= hl || !ssl_record(pkt + ro + hl, rem - hl)) break;
+			ro += hl;
+			rem -= hl;
+		}
+	} else {
+		L.proto = P_DNS; L.hdr = n;
+		EMIT();
+	}
+#undef EMIT
+done:
+	return count;
 }
 
 /* ---- parse-until roll-back of a layer this path does not build (Packet.cpp:134-155, 168-175) ----
@@ -317,11 +428,6 @@ static uint32_t fnv_update(uint32_t h, const uint8_t* p, uint32_t n)
 	return h;
 }
 uint32_t pcppx_oracle_fnv1(const uint8_t* buf, uint32_t len) { return fnv_update(2166136261u, buf, len); }
-
-typedef struct {
-	uint8_t proto, osi;
-	uint32_t off, hdr, dlen;
-} lay;
 
 /* ProtocolTypeFamily membership, ProtocolType.h:293-298 + Layer.cpp:47-50 */
 static int family_member(uint32_t fam, uint8_t p)
@@ -625,6 +731,14 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 	const int fam_engine_only = family_engine_only(opts->parse_until_family);
 	while (k != K_NONE) {
 		if (k == K_OUT || k == K_L7) {
+			/* a classified HTTP / SSL / DNS layer: the engine builds it and the layers behind it, each under the
+			 * stop rules */
+			if (k == K_L7 && (kcls & (PCPPX_F_L7_HTTP | PCPPX_F_L7_SSL | PCPPX_F_L7_DNS))) {
+				const lay l4l = last;
+				count = l7_layers(pkt, off, len, kcls, &l4l, opts, &found, &stopped_by_rule, layers, cap, count,
+				                  &mask, &last);
+				break;
+			}
 			/* the host would build this layer, then the stop rules would roll it back (see above) */
 			if (count > 0 && (kosi > opts->parse_until_osi || (found && fam_engine_only))) {
 				stopped_by_rule = 1;

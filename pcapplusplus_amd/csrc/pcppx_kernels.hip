@@ -324,11 +324,14 @@ __device__ uint32_t l7_flags(const Pkt& p, bool tcp, uint32_t o, uint32_t n, uin
 	const uint32_t known = PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN;
 	if (!tcp)
 	{
-		// VXLAN (VxlanLayer.h:119-122) and GTPv1 (GtpLayer.h:386-389) bring an inner packet only the host parses
+		// DNS after DHCP and VXLAN (UdpLayer.cpp:103-115); then VXLAN (VxlanLayer.h:119-122) and GTPv1
+		// (GtpLayer.h:386-389) bring an inner packet only the host parses
+		const bool dhcp = (sp == 68 && dp == 67) || (sp == 67 && (dp == 68 || dp == 67));
+		if (!dhcp && dp != 4789 && n >= 12 && (dns_port(sp) || dns_port(dp)))
+			return known | PCPPX_F_L7_DNS;
 		if (dp == 4789 || sp == 2152 || dp == 2152 || sp == 2123 || dp == 2123)
 			return PCPPX_F_NEEDS_HOST_L7;
-		const bool dhcp = (sp == 68 && dp == 67) || (sp == 67 && (dp == 68 || dp == 67));
-		return known | ((!dhcp && n >= 12 && (dns_port(sp) || dns_port(dp))) ? PCPPX_F_L7_DNS : 0u);
+		return known;
 	}
 	if (http_port(dp) && http_request(p, o, n))
 		return known | PCPPX_F_L7_HTTP;
@@ -343,6 +346,157 @@ __device__ uint32_t l7_flags(const Pkt& p, bool tcp, uint32_t o, uint32_t n, uin
 	// payload; nothing after DNS builds an HTTP, DNS or SSL layer
 	const bool sbs = sp == 5060 || sp == 5061 || sp == 179 || sp == 22 || dp == 5060 || dp == 5061 || dp == 179 || dp == 22;
 	return known | ((!sbs && n >= 14 && (dns_port(sp) || dns_port(dp))) ? PCPPX_F_L7_DNS : 0u);
+}
+
+// ---- the layers of a classified first L7 layer, built on the device (restated in oracle/pcppx_oracle.c:
+// l7_layers): with no parse-until family, an HTTP / SSL / DNS class names the layer the reference builds, and its
+// rules are short length walks. Each layer's data runs to the end of the L4 payload (no effect on the trailer). ----
+constexpr uint32_t P_HTTP_REQ = 6, P_HTTP_RESP = 7, P_DNS = 13, P_SSL = 18;
+constexpr uint32_t kL7Built = PCPPX_F_L7_HTTP | PCPPX_F_L7_SSL | PCPPX_F_L7_DNS;
+
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v)
+{
+	return (v - 0x01010101u) & ~v & 0x80808080u;  // the lowest flagged byte is the first zero byte
+}
+// the first '\n' in payload bytes [a, n) of the payload at o (n if none), dword-wise; *nul: the first NUL before it
+__device__ uint32_t scan_nl(const Pkt& p, uint32_t o, uint32_t a, uint32_t n, uint32_t* nul)
+{
+	uint32_t z = n;
+	for (uint32_t j = a; j < n; j += 4)
+	{
+		uint32_t w;
+		if (j + 4 <= n)
+			w = rd32(p, o + j);
+		else
+		{
+			w = 0x01010101u;  // past the payload: neither '\n' nor NUL
+			for (uint32_t k = 0; j + k < n; ++k)
+				w = (w & ~(0xFFu << (8 * k))) | (rb(p, o + j + k) << (8 * k));
+		}
+		const uint32_t zl = zero_bytes(w ^ 0x0A0A0A0Au), z0 = zero_bytes(w);
+		if (z == n && z0)
+			z = j + (__builtin_ctz(z0) >> 3);
+		if (zl)
+		{
+			const uint32_t e = j + (__builtin_ctz(zl) >> 3);
+			*nul = z < e ? z : n;
+			return e;
+		}
+	}
+	*nul = z;
+	return n;
+}
+// HeaderField size (TextBasedProtocol.cpp:448-461): through the first '\n', else strnlen to the end
+__device__ __forceinline__ uint32_t tbp_field(const Pkt& p, uint32_t o, uint32_t a, uint32_t n)
+{
+	uint32_t nul;
+	const uint32_t e = scan_nl(p, o, a, n, &nul);
+	return e < n ? e - a + 1 : nul - a;
+}
+// TextBasedProtocolMessage::parseFields + getHeaderLen (TextBasedProtocol.cpp:87-139,436-439)
+__device__ uint32_t tbp_header_len(const Pkt& p, uint32_t o, uint32_t fl, uint32_t n)
+{
+	uint32_t off = fl, s = tbp_field(p, o, off, n);
+	bool end = s == 0;
+	if (!end)
+	{
+		const uint32_t c = rb(p, o + off);
+		end = c == '\r' || c == '\n';
+	}
+	while (!end && off + s < n)
+	{
+		const uint32_t s2 = tbp_field(p, o, off + s, n);
+		if (s2 == 0)
+			break;
+		off += s;
+		s = s2;
+		const uint32_t c = rb(p, o + off);
+		end = c == '\r' || c == '\n';
+	}
+	return off + s;
+}
+// HttpRequestFirstLine's end (HttpLayer.cpp:166-213, parseVersion :287-320): the first " HTTP/" after the method's
+// space; with room for "x.y" the line ends after the next '\n', else (or with no version) at the end
+__device__ uint32_t http_request_line(const Pkt& p, uint32_t o, uint32_t n)
+{
+	uint32_t sp = 0;
+	while (rb(p, o + sp) != ' ')  // exists, < 8 (http_request)
+		++sp;
+	for (uint32_t v = sp + 1; v + 6 <= n; ++v)
+	{
+		if (rb(p, o + v) != ' ' || rb(p, o + v + 1) != 'H' || rb(p, o + v + 2) != 'T' || rb(p, o + v + 3) != 'T' ||
+		    rb(p, o + v + 4) != 'P' || rb(p, o + v + 5) != '/')
+			continue;
+		if (v + 9 > n)
+			return n;
+		uint32_t nul;
+		const uint32_t e = scan_nl(p, o, v + 6, n, &nul);
+		return e < n ? e + 1 : n;
+	}
+	return n;
+}
+// a member of the parse-until family (ProtocolTypeFamily: up to four protocol bytes)
+__device__ __forceinline__ bool family_has(uint32_t family, uint32_t proto)
+{
+	return family != 0 && (proto == (family & 0xFF) || (proto << 8) == (family & 0xFF00) ||
+	                       (proto << 16) == (family & 0xFF0000) || (proto << 24) == (family & 0xFF000000u));
+}
+// The layers of a classified L7 payload at [o, o+n) (HTTP: HttpRequestLayer / HttpResponseLayer + a Payload body,
+// HttpLayer.cpp:62-68,666-672,897-920; SSL: one SSLLayer per record, SSLLayer.cpp:88-106; DNS: DnsLayer, header =
+// data, DnsLayer.h:353-372), appended at index `count`, each kept only if it passes the stop rules (Packet.cpp:
+// 134-155; the first that fails is rolled back and ends the chain); stops counting once past cap_layers (every
+// further layer is another SSL record: same mask, same DEPTH_OVERFLOW).
+__device__ uint32_t l7_build(const Pkt& p, uint32_t lf, uint32_t o, uint32_t n, uint32_t dp, uint32_t count, uint32_t ml,
+                             uint32_t cap_layers, uint32_t family, uint32_t until_osi, uint32_t& found,
+                             uint32_t& stopped, uint64_t& mask, uint2* lay_out)
+{
+	auto emit = [&](uint32_t proto, uint32_t osi, uint32_t lo, uint32_t hdr, uint32_t dlen) -> bool {
+		const bool member = family_has(family, proto);
+		const bool osi_fail = osi > until_osi;
+		found = (!osi_fail && member) ? 1u : found;
+		if (osi_fail || (found && !member))
+		{
+			stopped = 1;
+			return false;
+		}
+		if (lay_out && count < ml)
+			lay_out[count] = make_uint2(proto | (osi << 8) | (lo << 16), (hdr & 0xFFFF) | (dlen << 16));
+		mask |= 1ull << proto;
+		++count;
+		return true;
+	};
+	if (lf & PCPPX_F_L7_HTTP)
+	{
+		const bool req = http_port(dp) && http_request(p, o, n);  // l7_flags' order
+		uint32_t fl;
+		if (req)
+			fl = http_request_line(p, o, n);
+		else
+		{
+			uint32_t nul;
+			const uint32_t e = scan_nl(p, o, 0, n, &nul);
+			fl = e < n ? e + 1 : n;
+		}
+		const uint32_t h = tbp_header_len(p, o, fl, n);
+		if (emit(req ? P_HTTP_REQ : P_HTTP_RESP, 7, o, h, n) && n > h)
+			emit(P_PAYLOAD, 7, o + h, n - h, n - h);
+	}
+	else if (lf & PCPPX_F_L7_SSL)
+	{
+		uint32_t ro = o, rem = n;
+		for (;;)
+		{
+			uint32_t hl = 5 + ((rb(p, ro + 3) << 8) | rb(p, ro + 4));
+			hl = hl < rem ? hl : rem;
+			if (!emit(P_SSL, 6, ro, hl, rem) || rem <= hl || count > cap_layers || !ssl_record(p, ro + hl, rem - hl))
+				break;
+			ro += hl;
+			rem -= hl;
+		}
+	}
+	else
+		emit(P_DNS, 7, o, n, n);
+	return count;
 }
 
 // Smallest OSI layer among the layers the host would build on an L4 payload the port / SIP triggers hand to
@@ -839,25 +993,28 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		const bool sip = !l7_tcp && l7_pl >= 4 && sip_key(__builtin_bswap32(rd32(p, l7_o + 8)));
 		const bool trig = l7_tcp ? tcp_l7(sp, dp) : (udp_l7(sp, dp) || sip);
 		uint32_t lf = trig ? l7_flags(p, l7_tcp, l7_end - l7_pl, l7_pl, sp, dp, sip, true) : 0u;
-		// parse-until options: the dissector's layer is rolled back (Packet.cpp:134-155,168-175) when every
-		// candidate lies above parseUntilLayer, or the family was found and holds only engine-built protocols
-		if (lf && (prm.family != 0 || prm.until_osi < 8))  // uniform
+		// parse-until options and a layer left to the host: it is rolled back (Packet.cpp:134-155,168-175)
+		// when every candidate lies above parseUntilLayer, or the family was found and holds only engine-built
+		// protocols (a classified layer is built below, under the stop rules themselves)
+		if (lf && !(lf & kL7Built) && (prm.family != 0 || prm.until_osi < 8))  // uniform
 		{
-			// a classified first L7 layer has its own OSI layer (HTTP / DNS application, SSL presentation)
-			const uint32_t osi = (lf & PCPPX_F_L7_SSL) ? 6u
-			                   : (lf & (PCPPX_F_L7_HTTP | PCPPX_F_L7_DNS)) ? 7u : l7_min_osi(l7_tcp, sp, dp, sip);
-			if (osi > prm.until_osi || (found && prm.fam_engine_only))
+			if (l7_min_osi(l7_tcp, sp, dp, sip) > prm.until_osi || (found && prm.fam_engine_only))
 				lf = 0;
 		}
 		if (lf)
 		{
-			flags |= lf;
 			if (count > l7_next)  // the tentative Payload was recorded
 			{
 				count = l7_next;
 				mask &= ~(1ull << P_PAYLOAD);
 				last_end = l7_end;
 			}
+			// a classified HTTP / SSL / DNS layer: built here with the layers behind it; anything else is the host's
+			if (lf & kL7Built)
+				count = l7_build(p, lf, l7_end - l7_pl, l7_pl, dp, count, ml, cap_layers, prm.family, prm.until_osi,
+				                 found, stopped, mask, lay_out);
+			else
+				flags |= lf;
 		}
 	}
 
@@ -1738,7 +1895,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 	}
 	Fast f;
-	const bool fast = live && !StreamOnly && !GatherOnly && fast_walk(p, cap, prm, f);
+	bool fast = live && !StreamOnly && !GatherOnly && fast_walk(p, cap, prm, f);
 
 	// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
 	const uint32_t ml = prm.max_layers;
@@ -1766,6 +1923,10 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		{
 			fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
 			fast_l7(p, f, cap);
+			fast = !(f.l7() & kL7Built);  // a classified HTTP / SSL / DNS payload: the generic walk builds its layers
+		}
+		if (fast)
+		{
 			w = fast_to_walk(f, ml);
 			if (want_csum && w.v4 >= 0)
 			{
@@ -2557,7 +2718,10 @@ __global__ __launch_bounds__(kBlock) void filter_apply_kernel(FilterParams fp)
 		// out-of-scope L2/L3 layer, a bad record, or an L7 layer the parse could not classify (PCPPX_F_L7_KNOWN)
 		settled = (flags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC)) == 0 &&
 		          (!(flags & PCPPX_F_NEEDS_HOST_L7) || (flags & PCPPX_F_L7_KNOWN));
-		l7 = ((flags & PCPPX_F_L7_HTTP) ? 1u : 0u) | ((flags & PCPPX_F_L7_DNS) ? 2u : 0u) | ((flags & PCPPX_F_L7_SSL) ? 4u : 0u);
+		// isPacketOfType(HTTP / DNS / SSL): the built layers (proto_mask), else the class of a host-owned first L7 layer
+		l7 = ((flags & PCPPX_F_L7_HTTP) || (mask & ((1ull << P_HTTP_REQ) | (1ull << P_HTTP_RESP))) ? 1u : 0u) |
+		     ((flags & PCPPX_F_L7_DNS) || (mask & (1ull << P_DNS)) ? 2u : 0u) |
+		     ((flags & PCPPX_F_L7_SSL) || (mask & (1ull << P_SSL)) ? 4u : 0u);
 		const bool own = filter_is_matched(fp, i, mask, nl);
 		const unsigned long long key = (1ull << 32) | sm.hash5;
 		const uint64_t seq = fp.seq_base + i;

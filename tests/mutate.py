@@ -251,6 +251,24 @@ def crafted_l7(seed: int = 13) -> list[bytes]:
               bytes([20, 0x7f, 0x1c, 0, 1, 1]), bytes([21, 0xfb, 0x1a, 0, 2]), bytes([22, 3, 5, 0, 9]),
               bytes([22, 3, 0, 1, 0]), bytes([22, 3]), b"", b"x" * 11, b"x" * 12, b"x" * 13, b"x" * 14,
               b"INVITE sip:a SIP/2.0\r\n", rng.bytes(40)]
+    # the layers built behind a classified first L7 layer: HTTP header fields (TextBasedProtocol.cpp:87-139,
+    # 448-461) and first-line ends, SSL record chains (SSLLayer.cpp:88-106), DNS lengths
+    bodies += [b"GET /a HTTP/1.1\r\nHost: x\r\nA: b\r\n\r\nbody", b"GET /a HTTP/1.1\r\nHost: x\r\n\r\n",
+               b"GET /a HTTP/1.1\nHost: x\n\nbody", b"GET /a HTTP/1.1\r\nHost: x", b"GET /a HTTP/1.1\r\nHost: x\r\n",
+               b"GET /a HTTP/1.1\r\nHo\0st: x", b"GET /a HTTP/1.1\r\n\0Host", b"GET /a HTTP/1.1\r\nHo\0st: x\r\n\r\n",
+               b"GET /a HTTP/1.1\r\n\r\n", b"GET /a HTTP/1.1\r\n\n", b"GET /a HTTP/1.1\r\n\rX\r\nA: b\r\n",
+               b"GET /a HTT", b"GET /a HTTP/1", b"GET /a HTTP/1.", b"GET /a HTTP/1.1", b"GET /a HTTP/7.7\r\nA: b\r\n\r\nz",
+               b"GET /a\r\nA: b HTTP/1.1\r\nC: d\r\n\r\n", b"GET  HTTP/1.0\nX", b"POST /p HTTP/1.0\r\nL: 3\r\n\r\nabc" * 3,
+               b"HTTP/1.1 200 OK\r\nServer: s\r\nContent-Length: 4\r\n\r\nbody", b"HTTP/1.1 200 OK\r\nA: b",
+               b"HTTP/1.1 200 OK\r\n\r\n", b"HTTP/1.1 200 OK\r\nA:\0b\r\n\r\nq", b"HTTP/1.1 404 Not Found\nA: b\n\nzz",
+               b"HTTP/1.1 200 OK\r\n" + b"X-Long: " + b"v" * 300 + b"\r\n\r\n" + b"b" * 100,
+               bytes([22, 3, 1, 0, 2, 1, 2, 20, 3, 3, 0, 1, 1, 23, 3, 3, 0, 3, 9, 9, 9]),
+               bytes([22, 3, 1, 0, 2, 1, 2, 20, 3, 3, 0, 1, 1, 99, 3, 3, 0, 1, 1]), bytes([22, 3, 1, 0, 2, 1, 2, 23, 3]),
+               bytes([22, 3, 1, 0, 2, 1, 2, 23, 3, 3, 0, 0]), bytes([22, 3, 1, 0, 2, 1, 2, 23, 3, 3, 0, 9, 1]),
+               bytes([23, 3, 3, 0, 40]) + b"e" * 10, bytes([21, 3, 3, 0, 2, 1, 0]) * 12,
+               bytes([23, 3, 4, 0, 1, 7]) * 30, bytes([22, 3, 3, 0, 4, 1, 0, 0, 0, 22, 0x7f, 0x10, 0, 1, 1, 22, 3, 6, 0, 1, 1]),
+               b"\x12\x34\x01\x00\x00\x01\x00\x00\x00\x00\x00\x00\x03www\x01a\x00\x00\x01\x00\x01",
+               b"\x00\x1d\x12\x34\x01\x00\x00\x01\x00\x00\x00\x00\x00\x00\x03www\x01a\x00\x00\x01\x00\x01"]
     tcp_ports = [(40000, 80), (80, 40000), (8080, 8080), (443, 40000), (40000, 993), (80, 443), (53, 40000),
                  (40000, 5353), (22, 80), (443, 179), (5060, 80), (102, 443), (21, 8080), (40000, 40001), (2123, 53)]
     udp_ports = [(40000, 53), (53, 40000), (5355, 5355), (68, 67), (67, 53), (40000, 4789), (2152, 53), (53, 2123),

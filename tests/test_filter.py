@@ -218,9 +218,12 @@ def test_l7_counters_cover_every_class():
     assert settled.all()
     for bit in (1, 2, 4):
         assert ((l7 & bit) != 0).sum() > 50, bit
-    http_resp = [i for i in np.nonzero(l7 & 1)[0] if b.packet(int(i))[int(lay[i, int(s["n_layers"][i]) - 1]["offset"])
+    http_resp = [i for i in np.nonzero(l7 & 1)[0] if b.packet(int(i))[int(lay[i, int(s["l4_layer"][i])]["offset"])
                                                                         :][:2] == b"\x00\x50"]
     assert http_resp, "no HTTP response among the fixtures"
+    # with no parse-until family the parse builds those layers itself: HTTPRequest / HTTPResponse, SSL, DNS
+    for proto in (6, 7, 13, 18):
+        assert (lay["proto"] == proto).any(), proto
 
 
 @pytest.mark.gpu

@@ -61,8 +61,12 @@ def test_gpu_crafted_l7_payloads(engine, gaps, kernel):
     """The L7 content checks (HTTP request / response first line, SSL record header, DNS lengths) at their edges,
     on the fast path (Eth/IPv4) and the generic walk (VLAN/IPv6), payload bytes in and past the LDS window."""
     b = as_batch(crafted_l7(), gaps=gaps, seed=17)
+    # parse-until variants around the built HTTP / SSL / DNS layers: TCP, HTTP (request|response), SSL, DNS and
+    # UDP families, OSI 4 / 6 / 7
     for opts in (abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 4, True, 16),
-                 abi.make_opts(0, 8, False, 0)):
+                 abi.make_opts(0, 8, False, 0), abi.make_opts(0x607, 8, True, 16), abi.make_opts(18, 8, True, 16),
+                 abi.make_opts(13, 8, True, 16), abi.make_opts(5, 8, True, 16), abi.make_opts(0, 6, True, 16),
+                 abi.make_opts(0, 7, True, 8)):
         g = run(engine, b, opts, kernel)
         o = oracle.oracle_parse(b, opts)
         oracle.compare_exact(g[0], g[1], o[0], o[1])

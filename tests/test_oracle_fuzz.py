@@ -17,7 +17,8 @@ pytestmark = pytest.mark.skipif(not oracle.ref_available(), reason="reference li
 OPTS = [abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 3, True, 16),
         abi.make_opts(0x203, 8, True, 4), abi.make_opts(0, 8, True, 0), abi.make_opts(0, 4, True, 16),
         abi.make_opts(0, 5, True, 16), abi.make_opts(0, 6, True, 16), abi.make_opts(5, 8, True, 16),
-        abi.make_opts(0x607, 8, True, 16)]
+        abi.make_opts(0x607, 8, True, 16), abi.make_opts(18, 8, True, 16), abi.make_opts(13, 8, True, 16),
+        abi.make_opts(0, 7, True, 8), abi.make_opts(0x1219, 8, True, 16)]
 
 
 def _seed_packets():

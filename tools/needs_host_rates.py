@@ -4,7 +4,8 @@ The engine's flags equal the C restatement's on every packet (GPU parity tests),
 here on the CPU with the restatement (oracle/liboracle.so) over the reference's own captures, read by the
 engine's ingest (pcppx_pcap_*). For each capture and option variant: packets, packets flagged
 PCPPX_F_NEEDS_HOST (a host parse completes them), of those how many the device classified to their first
-L7 layer (PCPPX_F_L7_KNOWN: HTTP / SSL / DNS for FilterTraffic's collectStats), and the split by reason.
+L7 layer (PCPPX_F_L7_KNOWN: HTTP / SSL / DNS for FilterTraffic's collectStats), the split by reason, and the
+packets whose HTTP / SSL / DNS layers the device built itself (not flagged).
 
   python tools/needs_host_rates.py > profiles/r02_needs_host_rates.md
 """
@@ -58,17 +59,19 @@ def main() -> None:
         cells = []
         for fam, osi in VARIANTS.values():
             opts = abi.make_opts(fam, osi, False, 0)
-            flags = []
+            flags, masks = [], []
             for b in batches:
                 s, _ = oracle.oracle_parse(b, opts)
-                flags.append(np.asarray(s).view(np.uint32).reshape(-1, 8)[:, 3] & 0xFFFF)
-            fl = np.concatenate(flags)
+                flags.append(s["flags"].astype(np.uint32))
+                masks.append(s["proto_mask"].astype(np.uint64))
+            fl, m = np.concatenate(flags), np.concatenate(masks)
             host = (fl & abi.F_NEEDS_HOST) != 0
             l7 = host & ((fl & abi.F_NEEDS_HOST_L7) != 0)
             known = l7 & ((fl & abi.F_L7_KNOWN) != 0)
             proto = host & ((fl & abi.F_NEEDS_HOST_PROTO) != 0)
+            built = (m & np.uint64((1 << 6) | (1 << 7) | (1 << 13) | (1 << 18))) != 0
             cells.append(f"{host.sum()} ({100 * host.mean():.1f}%): L7 {l7.sum()} [{known.sum()} classified], "
-                         f"L2/L3 {proto.sum()}")
+                         f"L2/L3 {proto.sum()}; HTTP/SSL/DNS built {built.sum()}")
         lt = sorted({b.linktype for b in batches})
         print(f"| `{rel.split('/')[-1]}` (link {','.join(map(str, lt))}) | {n} | " + " | ".join(cells) + " |")
 
