@@ -9,9 +9,9 @@
  *   - where the reference would hand an L4 payload to an L7 dissector (port/content triggers of
  *     TcpLayer.cpp:372-491 and UdpLayer.cpp:103-178, incl. the SIP content heuristic
  *     SipLayer.cpp:127-160) the chain stops after the TCP/UDP layer and PCPPX_F_NEEDS_HOST_L7 is set;
- *   - where it would build an out-of-scope L2/L3 layer (PPPoE, WoL, ICMP, IGMP, AH, ESP, VRRP,
- *     ICMPv6, STP, SLL/SLL2/NULL/NFLOG/C_HDLC first layers) the chain stops before it and
- *     PCPPX_F_NEEDS_HOST_PROTO is set;
+ *   - except that a classified HTTP / SSL / DNS first L7 layer is built, with the layers behind it;
+ *   - where it would build an out-of-scope L2/L3 layer (PPPoE, WoL, IGMP, AH, ESP, VRRP, ICMPv6, STP,
+ *     NFLOG/C_HDLC first layers) the chain stops before it and PCPPX_F_NEEDS_HOST_PROTO is set;
  *   - no trailer is appended to a flagged chain; hashes and checksums are computed over the emitted chain.
  * For unflagged packets every field equals the reference; for flagged packets the emitted layers are an
  * exact prefix of the reference chain.
@@ -35,7 +35,7 @@ enum {
 };
 
 enum kind { K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP,
-	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP, K_SLL, K_SLL2, K_NULL };
+	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP, K_SLL, K_SLL2, K_NULL, K_ICMP };
 
 static uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
@@ -56,6 +56,20 @@ static int llc_valid(const uint8_t* p, uint32_t n) { return n >= 3 && !(p[0] == 
 static int ipv4_valid(const uint8_t* p, uint32_t n) { return n >= 20 && (p[0] >> 4) == 4 && (p[0] & 0xF) >= 5; }
 /* IPv6Layer::isDataValid, Packet++/header/IPv6Layer.h:245-249 */
 static int ipv6_valid(const uint8_t* p, uint32_t n) { return n >= 40 && (p[0] >> 4) == 6; }
+/* IcmpLayer::isDataValid, Packet++/header/IcmpLayer.h:619-660: the type's message struct fits (icmphdr 4 B; timestamp
+ * 20; address mask 12; unreachable / redirect / time exceeded / source quench / param problem / router
+ * advertisement 8); other types are not ICMP */
+static int icmp_valid(const uint8_t* p, uint32_t n)
+{
+	if (n < 4) return 0;
+	switch (p[0]) {
+	case 8: case 0: case 10: case 15: case 16: return 1;
+	case 13: case 14: return n >= 20;
+	case 17: case 18: return n >= 12;
+	case 3: case 5: case 4: case 11: case 12: case 9: return n >= 8;
+	default: return 0;
+	}
+}
 /* TcpLayer::isDataValid, Packet++/header/TcpLayer.h:596-601 */
 static int tcp_valid(const uint8_t* p, uint32_t n) { return n >= 20 && (p[12] >> 4) >= 5 && n >= (uint32_t)(p[12] >> 4) * 4; }
 
@@ -391,7 +405,9 @@ static int engine_proto(uint32_t p)
 {
 	switch (p) {
 	case P_ETH: case P_IPV4: case P_IPV6: case P_TCP: case P_UDP: case P_ARP: case P_VLAN: case P_MPLS:
-	case P_GREV0: case P_GREV1: case P_PPTP: case P_TRAILER: case P_DOT3: case P_LLC: return 1;
+	case P_GREV0: case P_GREV1: case P_PPTP: case P_TRAILER: case P_DOT3: case P_LLC: case P_ICMP: return 1;
+	/* a classified first L7 layer is built, an unclassified one is none of these */
+	case P_HTTP_REQ: case P_HTTP_RESP: case P_DNS: case P_SSL: return 1;
 	default: return 0;
 	}
 }
@@ -574,7 +590,8 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 			else NEXT(K_PAYLOAD, po, pl);
 			break;
 		case 41: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
-		case 1: case 2: case 51: case 50: case 112: NEXT(K_OUT, po, pl); *nosi = 3; break; /* ICMP IGMP AH ESP VRRP */
+		case 1: NEXT(icmp_valid(pkt + po, pl) ? K_ICMP : K_PAYLOAD, po, pl); break; /* tryConstruct, :272-274 */
+		case 2: case 51: case 50: case 112: NEXT(K_OUT, po, pl); *nosi = 3; break; /* IGMP AH ESP VRRP */
 		default: NEXT(K_PAYLOAD, po, pl); break;
 		}
 		break;
@@ -675,6 +692,24 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 			*nosi = l7_osi(*ncls, udp_l7_min_osi(be16(p), be16(p + 2), sip));
 		}
 		break;
+	case K_ICMP: { /* IcmpLayer (OSI network, IcmpLayer.h:611-614): getHeaderLen by message type, IcmpLayer.cpp:589-620
+	                * (getMessageType :36-43); parseNextLayer :562-587: the error messages carry the offending IPv4
+	                * header (tryConstruct IPv4, else a Payload, even an empty one), the rest a Payload past the header */
+		L.proto = P_ICMP; L.osi = 3;
+		int err = 0;
+		switch (p[0]) {
+		case 0: case 8: L.hdr = len; break;
+		case 13: case 14: L.hdr = 20; break;
+		case 17: case 18: L.hdr = 12; break;
+		case 3: case 4: case 5: case 11: case 12: L.hdr = 8; err = 1; break;
+		case 9: { uint32_t ra = 8u + 8u * p[4]; L.hdr = ra > len ? len : ra; break; }
+		default: L.hdr = 4; break; /* 10, 15, 16 */
+		}
+		po = off + L.hdr; pl = len - L.hdr;
+		if (err) NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl);
+		else if (len > L.hdr) NEXT(K_PAYLOAD, po, pl);
+		break;
+	}
 	case K_ARP: /* ArpLayer: dataLen := sizeof(arphdr) = 28 whatever remains, no next (ArpLayer.h:151-155,242-273) */
 		L.proto = P_ARP; L.osi = 3; L.hdr = 28; L.dlen = 28;
 		break;
@@ -807,7 +842,7 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 	int has_ip = have_ipv4 || have_ipv6;
 	for (int dir = 0; dir < 2; ++dir) {
 		uint32_t h = 0;
-		if (has_ip && l4_idx >= 0) {
+		if (has_ip && l4_idx >= 0 && !(mask & ((uint64_t)1 << P_ICMP))) { /* ICMP: 0, PacketUtils.cpp:144-145 */
 			const uint8_t* lp = pkt + l4.off;
 			uint16_t sp = le16(lp), dp = le16(lp + 2); /* raw network-order values */
 			int s = 0;

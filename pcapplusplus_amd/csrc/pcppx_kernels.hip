@@ -29,7 +29,7 @@ constexpr int kBlock = 256;
 // ProtocolType ids (Packet++/header/ProtocolType.h:42-258)
 enum : uint32_t
 {
-	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_MPLS = 14, P_GREV0 = 15,
+	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14, P_GREV0 = 15,
 	P_GREV1 = 16, P_PPTP = 17, P_SLL = 19, P_NULL = 21, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44,
 	P_SLL2 = 52
 };
@@ -39,9 +39,10 @@ enum : uint32_t
 {
 	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
 	K_PAYLOAD, K_OUT, K_ARP, K_SLL, K_SLL2, K_NULL,  // SLL / SLL2 / Null-Loopback: first layers only
+	K_ICMP,
 	// candidates: the layer a tryConstructNextLayerWithFallback would build if its isDataValid holds, else
 	// Payload (Layer.h:474-483); resolved from the candidate's own first bytes when the walk reaches it
-	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC
+	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC, C_ICMP
 };
 
 // explicit address spaces: keep packet reads as global_load / ds_read, never flat
@@ -682,12 +683,19 @@ __device__ __forceinline__ uint32_t resolve(uint32_t k, const Peek& q, uint32_t 
 	const uint32_t et = q.be(12);
 	const uint32_t ke = len < 14 ? K_PAYLOAD : (et >= 0x0600 ? K_ETH : (et <= 0x05DC ? K_DOT3 : K_PAYLOAD));
 	const bool okl = len >= 3 && !(b0 == 0xFF && q.b(1) == 0xFF);
+	// IcmpLayer::isDataValid (IcmpLayer.h:619-660): the message type's struct fits; other types are no ICMP
+	uint32_t need = 0xFFFFu;
+	need = (b0 == 8 || b0 == 0 || b0 == 10 || b0 == 15 || b0 == 16) ? 4u : need;
+	need = (b0 == 13 || b0 == 14) ? 20u : need;
+	need = (b0 == 17 || b0 == 18) ? 12u : need;
+	need = (b0 == 3 || b0 == 4 || b0 == 5 || b0 == 9 || b0 == 11 || b0 == 12) ? 8u : need;
 	k = k == C_IPV4 ? (ok4 ? K_IPV4 : K_PAYLOAD) : k;
 	k = k == C_IPV6 ? (ok6 ? K_IPV6 : K_PAYLOAD) : k;
 	k = k == C_TCP ? (okt ? K_TCP : K_PAYLOAD) : k;
 	k = k == C_GRE ? kg : k;
 	k = k == C_ETHG ? ke : k;
 	k = k == C_LLC ? (okl ? K_LLC : K_PAYLOAD) : k;
+	k = k == C_ICMP ? (len >= need ? K_ICMP : K_PAYLOAD) : k;
 	return k;
 }
 
@@ -710,37 +718,37 @@ constexpr uint32_t kind_proto(uint32_t k)
 	return k == K_ETH ? P_ETH : k == K_DOT3 ? P_DOT3 : k == K_LLC ? P_LLC : k == K_VLAN ? P_VLAN : k == K_MPLS ? P_MPLS
 	     : k == K_IPV4 ? P_IPV4 : k == K_IPV6 ? P_IPV6 : k == K_GRE0 ? P_GREV0 : k == K_GRE1 ? P_GREV1
 	     : k == K_PPTP ? P_PPTP : k == K_TCP ? P_TCP : k == K_UDP ? P_UDP : k == K_ARP ? P_ARP : k == K_SLL ? P_SLL
-	     : k == K_SLL2 ? P_SLL2 : k == K_NULL ? P_NULL : P_PAYLOAD;
+	     : k == K_SLL2 ? P_SLL2 : k == K_NULL ? P_NULL : k == K_ICMP ? P_ICMP : P_PAYLOAD;
 }
 constexpr uint32_t kind_osi(uint32_t k)
 {
 	return (k == K_ETH || k == K_DOT3 || k == K_LLC || k == K_VLAN || k == K_SLL || k == K_SLL2 || k == K_NULL) ? 2
-	     : (k == K_MPLS || k == K_IPV4 || k == K_IPV6 || k == K_GRE0 || k == K_GRE1 || k == K_ARP) ? 3
+	     : (k == K_MPLS || k == K_IPV4 || k == K_IPV6 || k == K_GRE0 || k == K_GRE1 || k == K_ARP || k == K_ICMP) ? 3
 	     : k == K_PPTP ? 5 : (k == K_TCP || k == K_UDP) ? 4 : 7;
 }
 constexpr uint64_t pack_proto(uint32_t first)
 {
 	uint64_t t = 0;
-	for (uint32_t k = first; k < first + 10 && k <= K_NULL; ++k)
+	for (uint32_t k = first; k < first + 10 && k <= K_ICMP; ++k)
 		t |= (uint64_t)kind_proto(k) << (6 * (k - first));
 	return t;
 }
 constexpr uint64_t pack_osi()
 {
 	uint64_t t = 0;
-	for (uint32_t k = 0; k <= K_NULL; ++k)
+	for (uint32_t k = 0; k <= K_ICMP; ++k)
 		t |= (uint64_t)kind_osi(k) << (3 * k);
 	return t;
 }
 constexpr uint64_t kProtoLo = pack_proto(0), kProtoHi = pack_proto(10), kOsi = pack_osi();
-static_assert(K_NULL < 20 && 3 * K_NULL + 3 <= 64 && P_SLL2 < 64, "kind tables");
+static_assert(K_ICMP < 20 && 3 * K_ICMP + 3 <= 64 && P_SLL2 < 64, "kind tables");
 
 __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o, uint32_t len, const Peek& q)
 {
 	const bool isE = k == K_ETH, isD = k == K_DOT3, isL = k == K_LLC, isV = k == K_VLAN, isM = k == K_MPLS;
 	const bool is4 = k == K_IPV4, is6 = k == K_IPV6, isG = k == K_GRE0 || k == K_GRE1, isP = k == K_PPTP;
 	const bool isT = k == K_TCP, isU = k == K_UDP, isA = k == K_ARP;
-	const bool isS = k == K_SLL, isS2 = k == K_SLL2, isN = k == K_NULL;
+	const bool isS = k == K_SLL, isS2 = k == K_SLL2, isN = k == K_NULL, isI = k == K_ICMP;
 	// IPv6 extension headers (IPv6Layer::parseExtensions, no bound check against dataLen): IPv6 lanes only
 	uint32_t nh = q.b(6), ext = 0, last_ext = 0xFFFF;
 	if (is6)
@@ -788,6 +796,17 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	hdr = isS ? 16 : hdr;   // sll_header (SllLayer.h:15-32), even when the packet is shorter
 	hdr = isS2 ? 20 : hdr;  // sll2_header (Sll2Layer.h:15-35)
 	hdr = isN ? 4 : hdr;    // the family dword (NullLoopbackLayer.h:66-69)
+	// ICMP by message type (IcmpLayer::getHeaderLen, IcmpLayer.cpp:589-620): echo = the whole data; timestamp 20;
+	// address mask 12; the error messages 8; router advertisement 8 + 8 per address, at most the data; else 4
+	const uint32_t it = f0;
+	const bool ierr = it == 3 || it == 4 || it == 5 || it == 11 || it == 12;
+	uint32_t ih = (it == 0 || it == 8) ? len : 4u;
+	ih = (it == 13 || it == 14) ? 20u : ih;
+	ih = (it == 17 || it == 18) ? 12u : ih;
+	ih = ierr ? 8u : ih;
+	const uint32_t ra = 8 + 8 * q.b(4);
+	ih = it == 9 ? (ra < len ? ra : len) : ih;
+	hdr = isI ? ih : hdr;
 	// data length: IPv4 totalLength truncation (0 = TSO keeps it), IPv6 payloadLength + header, ARP 28
 	uint32_t dlen = len;
 	const uint32_t tl = q.be(2);
@@ -798,7 +817,8 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	dlen = isA ? 28 : dlen;
 	// successor: exists iff the layer's data runs past its header (every kind's "no next layer" rule; Null/Loopback
 	// always builds one, empty for a 4-byte packet: NullLoopbackLayer.cpp:50-99 has no length check)
-	const bool has_next = dlen > hdr || isN;
+	// (an ICMP error message always builds one, empty when the quote is: IcmpLayer.cpp:562-587)
+	const bool has_next = dlen > hdr || isN || (isI && ierr);
 	const uint32_t po = o + hdr, pl = has_next ? dlen - hdr : 0;
 	// EtherType dispatch of Ethernet (EtherType at 12), VLAN and GRE (at 2), SLL (protocol_type at 14) and SLL2 (at
 	// 0: SllLayer.cpp:49-102, Sll2Layer.cpp:63-121); PPP protocol of PPP_PPTP (at 2)
@@ -835,7 +855,8 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	ni = ipp == 4 ? C_IPVER : ni;
 	ni = ipp == 47 ? C_GRE : ni;
 	ni = (ipp == 41 && is4) ? C_IPV6 : ni;
-	ni = (ipp == 51 || ipp == 50 || ipp == 112 || (is4 && (ipp == 1 || ipp == 2)) || (!is4 && ipp == 58)) ? K_OUT : ni;
+	ni = (ipp == 1 && is4) ? C_ICMP : ni;  // IPv4Layer.cpp:272-274
+	ni = (ipp == 51 || ipp == 50 || ipp == 112 || (is4 && ipp == 2) || (!is4 && ipp == 58)) ? K_OUT : ni;
 	const uint32_t b6 = q.b(6);
 	const bool frag = (b6 & 0x20) || (((b6 & 0x1F) << 8) | q.b(7)) != 0;  // IPv4Layer.cpp:415-438
 	ni = ((is4 && frag) || (is6 && last_ext == 44)) ? K_PAYLOAD : ni;
@@ -846,6 +867,7 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	nk = isM ? ((q.b(2) & 1) ? C_IPVER : K_MPLS) : nk;  // bottom of stack: IPv4/IPv6 by version nibble
 	nk = isD ? C_LLC : nk;
 	nk = isL ? ((f0 == 0x42 && f1 == 0x42) ? K_OUT : K_PAYLOAD) : nk;
+	nk = isI ? (ierr ? C_IPV4 : K_PAYLOAD) : nk;  // the quoted IPv4 header (tryConstruct), else a Payload
 	// TCP/UDP: a tentative Payload; walk_chain decides afterwards whether an L7 dissector takes it
 	nk = has_next ? nk : K_NONE;
 	return Step{ proto, osi, hdr, dlen, nk, has_next ? po : 0, pl };
@@ -927,7 +949,7 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		{
 			// an out-of-scope layer: rolled back by the stop rules when every candidate fails one
 			// (oracle/pcppx_oracle.c, family_engine_only): L2 candidates (PPPoE, WoL, STP) have OSI 2, the
-			// IP-protocol ones (ICMP, IGMP, AH, ESP, VRRP, ICMPv6) 3
+			// IP-protocol ones (IGMP, AH, ESP, VRRP, ICMPv6) 3
 			const uint32_t pp = prev & 0xFFu;
 			const uint32_t kosi = (pp == P_IPV4 || pp == P_IPV6) ? 3u : 2u;
 			if (!(count > 0 && (kosi > prm.until_osi || (found && prm.fam_engine_only))))
@@ -1124,7 +1146,7 @@ __device__ __forceinline__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5
 		s[k] = (uint32_t)k < na ? rd32(p, so + 4 * k) : 0;
 		d[k] = (uint32_t)k < na ? rd32(p, dofs + 4 * k) : 0;
 	}
-	const bool has_l4 = w.l4i >= 0;
+	const bool has_l4 = w.l4i >= 0 && !(w.mask & (1ull << P_ICMP));  // ICMP: no 5-tuple (PacketUtils.cpp:144-145)
 	const uint32_t pw = has_l4 ? rd32(p, w.l4o) : 0;
 	tuple_hashes(s, d, na, has_l4, pw, rb(p, ipo + (v4 ? 9 : 6)), h5, h5d, h2);
 }
@@ -2777,7 +2799,9 @@ bool family_engine_only(uint32_t fam)
 		const uint32_t b = (fam >> (8 * k)) & 0xFFu;
 		const bool own = b == P_ETH || b == P_IPV4 || b == P_IPV6 || b == P_TCP || b == P_UDP || b == P_ARP ||
 		                 b == P_VLAN || b == P_MPLS || b == P_GREV0 || b == P_GREV1 || b == P_PPTP ||
-		                 b == P_TRAILER || b == P_DOT3 || b == P_LLC;
+		                 b == P_TRAILER || b == P_DOT3 || b == P_LLC || b == P_ICMP ||
+		                 // a classified first L7 layer is built, an unclassified one is none of these
+		                 b == P_HTTP_REQ || b == P_HTTP_RESP || b == P_DNS || b == P_SSL;
 		if (b != 0 && !own)
 			return false;
 	}

@@ -144,6 +144,31 @@ def crafted(seed: int = 7) -> list[bytes]:
     pk.append(_eth(0x0800) + _ipv4(17, 8 + 12) + _udp(53, 50001, pay(12)))
     pk.append(_eth(0x0806) + pay(28))
     pk.append(_eth(0x0800) + _ipv4(1, 8) + pay(8))
+    # ICMP (IcmpLayer.cpp:562-620, IcmpLayer.h:619-660): every type 0-20 at and around its message size, error
+    # messages quoting an IPv4 header (+ TCP / UDP, cut short), router advertisements with counts past the data,
+    # behind a VLAN, GRE, an IPv4 fragment and IPv6 (next header 1 is no ICMP there), padded for a trailer
+    inner = [b"", _ipv4(6, 20)[:12], _ipv4(6, 8) + _tcp(1, 2, b"")[:8], _ipv4(17, 8) + _udp(53, 9, b""),
+             _ipv4(1, 8) + bytes([8, 0, 0, 0]) + pay(4), _ipv4(6, 40) + _tcp(80, 3, pay(20))]
+    for t in range(21):
+        for n in (3, 4, 7, 8, 11, 12, 19, 20, 24, 40):
+            body = bytes([t, 0, 0, 0]) + pay(max(0, n - 4))
+            body = body[:n]
+            pk.append(_eth(0x0800) + _ipv4(1, len(body)) + body)
+        if t in (3, 4, 5, 11, 12):
+            for inn in inner:
+                body = bytes([t, 1, 0, 0]) + pay(4) + inn
+                pk.append(_eth(0x0800) + _ipv4(1, len(body)) + body)
+                pk.append(_eth(0x0800) + _ipv4(1, len(body)) + body + b"\x00" * 6)
+    for cnt, extra in ((0, 0), (1, 8), (2, 8), (3, 30), (255, 16)):
+        body = bytes([9, 0, 0, 0, cnt, 2, 0, 30]) + pay(extra)
+        pk.append(_eth(0x0800) + _ipv4(1, len(body)) + body)
+    echo = bytes([8, 0, 0, 0]) + pay(36)
+    pk.append(_eth(0x8100) + struct.pack(">HH", 4, 0x0800) + _ipv4(1, len(echo)) + echo)
+    gre = bytes([0, 0]) + struct.pack(">H", 0x0800) + _ipv4(1, len(echo)) + echo
+    pk.append(_eth(0x0800) + _ipv4(47, len(gre)) + gre)
+    pk.append(_eth(0x0800) + _ipv4(1, len(echo), frag=0x2000) + echo)
+    pk.append(_eth(0x86DD) + _ipv6(1, len(echo)) + echo)
+    pk.append(_eth(0x0800) + _ipv4(1, len(echo)) + echo + b"\xee" * 9)
     return pk
 
 
