@@ -19,9 +19,10 @@
  *   pcppx_summary <-> Packet::isPacketOfType (proto_mask, Packet.cpp:614-640), hash5Tuple(false/true),
  *                      hash2Tuple, the IPv4/L4 checksums.
  * Layers the engine builds: Ethernet II / 802.3 / LLC, VLAN, MPLS, IPv4, IPv6 (+ extensions), GREv0/v1,
- * PPP_PPTP, ARP, ICMP (+ the IPv4 header an error message quotes), TCP, UDP, Payload, Trailer, the first
- * layers of link types Ethernet, raw IP (RAW, DLT_RAW1/2, IPV4, IPV6), Linux SLL / SLL2 and Null/Loopback,
- * and the first L7 layers it can name: HTTPRequest / HTTPResponse (+ the Payload body), SSL records and DNS.
+ * PPP_PPTP, ARP, ICMP (+ the IPv4 header an error message quotes), TCP, UDP, the VXLAN and GTPv1 tunnels
+ * (+ the inner packet), Payload, Trailer, the first layers of link types Ethernet, raw IP (RAW, DLT_RAW1/2,
+ * IPV4, IPV6), Linux SLL / SLL2 and Null/Loopback, and the first L7 layers it can name: HTTPRequest /
+ * HTTPResponse (+ the Payload body), SSL records and DNS.
  * Packets for which the reference would build a layer outside this scope (other L7 dissectors, IGMP, PPPoE,
  * NFLOG / Cisco HDLC first layers, ...) are flagged PCPPX_F_NEEDS_HOST_L7 / PCPPX_F_NEEDS_HOST_PROTO: their
  * layer prefix is exact, and the host owns the rest.
@@ -68,8 +69,9 @@ extern "C" {
  * TcpLayer.cpp:372-415 / UdpLayer.cpp:103-116 it restates): with PCPPX_F_L7_KNOWN set, the packet's chain holds
  * an HTTPRequest/HTTPResponse, SSL or DNS layer exactly when the matching bit is set, i.e.
  * Packet::isPacketOfType(HTTP / SSL / DNS) is decided. Not set for tunnels (VXLAN, GTPv1) whose inner packet only
- * the host parses. An HTTP / SSL / DNS layer the device builds itself is in the records and proto_mask
- * instead, with none of these bits: the packet is not NEEDS_HOST_L7. */
+ * the host parses (the VXLAN / GTPv1 tunnels the device builds itself are not NEEDS_HOST_L7). An HTTP / SSL /
+ * DNS layer the device builds itself is in the records and proto_mask instead, with none of these bits: the
+ * packet is not NEEDS_HOST_L7. */
 #define PCPPX_F_L7_KNOWN 0x0400
 #define PCPPX_F_L7_HTTP 0x0800
 #define PCPPX_F_L7_SSL 0x1000

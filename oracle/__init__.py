@@ -327,7 +327,7 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
 
 # protocols the engine builds itself (include/pcppx.h: everything else is a host layer); HTTPRequest /
 # HTTPResponse (6/7), DNS (13) and SSL (18) as a classified first L7 layer and the layers behind it
-ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16, 17, 18, 19, 21, 25, 30, 33, 44, 52)
+ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16, 17, 18, 19, 21, 25, 26, 30, 32, 33, 44, 52)
 
 
 def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:

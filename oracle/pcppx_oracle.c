@@ -9,7 +9,8 @@
  *   - where the reference would hand an L4 payload to an L7 dissector (port/content triggers of
  *     TcpLayer.cpp:372-491 and UdpLayer.cpp:103-178, incl. the SIP content heuristic
  *     SipLayer.cpp:127-160) the chain stops after the TCP/UDP layer and PCPPX_F_NEEDS_HOST_L7 is set;
- *   - except that a classified HTTP / SSL / DNS first L7 layer is built, with the layers behind it;
+ *   - except that a classified HTTP / SSL / DNS first L7 layer is built, with the layers behind it, and so
+ *     are the VXLAN and GTPv1 tunnels over UDP with the packet they carry;
  *   - where it would build an out-of-scope L2/L3 layer (PPPoE, WoL, IGMP, AH, ESP, VRRP, ICMPv6, STP,
  *     NFLOG/C_HDLC first layers) the chain stops before it and PCPPX_F_NEEDS_HOST_PROTO is set;
  *   - no trailer is appended to a flagged chain; hashes and checksums are computed over the emitted chain.
@@ -31,11 +32,11 @@
 enum {
 	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14,
 	P_GREV0 = 15, P_GREV1 = 16, P_PPTP = 17, P_SLL = 19, P_NULL = 21, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33,
-	P_LLC = 44, P_SLL2 = 52
+	P_LLC = 44, P_SLL2 = 52, P_VXLAN = 26, P_GTPV1 = 32
 };
 
 enum kind { K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP,
-	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP, K_SLL, K_SLL2, K_NULL, K_ICMP };
+	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP, K_SLL, K_SLL2, K_NULL, K_ICMP, K_VXLAN, K_GTP1 };
 
 static uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
@@ -406,6 +407,7 @@ static int engine_proto(uint32_t p)
 	switch (p) {
 	case P_ETH: case P_IPV4: case P_IPV6: case P_TCP: case P_UDP: case P_ARP: case P_VLAN: case P_MPLS:
 	case P_GREV0: case P_GREV1: case P_PPTP: case P_TRAILER: case P_DOT3: case P_LLC: case P_ICMP: return 1;
+	case P_VXLAN: case P_GTPV1: return 1; /* decided exactly at the UDP layer, never a host candidate */
 	/* a classified first L7 layer is built, an unclassified one is none of these */
 	case P_HTTP_REQ: case P_HTTP_RESP: case P_DNS: case P_SSL: return 1;
 	default: return 0;
@@ -686,12 +688,74 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		if (len <= 8) break;
 		po = off + 8; pl = len - 8;
 		{
+			/* the tunnels, decided here as UdpLayer::parseNextLayer does (:103-131): VXLAN by destination port
+			 * (tryConstruct, VxlanLayer.h:97-100: 8 bytes), GTPv1 by port and GtpV1Layer::isGTPv1 (GtpLayer.cpp:
+			 * 199-207) where no earlier dissector takes the payload: DHCP, DNS, SIP (by port), RADIUS (by port and
+			 * RadiusLayer::isDataValid, RadiusLayer.cpp:238-247: 20 <= length field <= data) */
+			const uint16_t sp = be16(p), dp = be16(p + 2);
+			if (dp == 4789) { NEXT(pl >= 8 ? K_VXLAN : K_PAYLOAD, po, pl); break; }
+			int dhcp = (sp == 68 && dp == 67) || (sp == 67 && dp == 68) || (sp == 67 && dp == 67);
+			int dnsb = pl >= 12 && (dns_port(sp) || dns_port(dp));
+			int sipp = 0, radp = 0;
+			for (int k = 0; k < 2; ++k) {
+				uint16_t x = k ? dp : sp;
+				if (x == 5060 || x == 5061) sipp = 1;
+				if (x == 1812 || x == 1813 || x == 3799) radp = 1;
+			}
+			int rad = radp && pl >= 20 && be16(pkt + po + 2) >= 20 && be16(pkt + po + 2) <= pl;
+			int gport = sp == 2152 || dp == 2152 || sp == 2123 || dp == 2123;
+			if (gport && !dhcp && !dnsb && !sipp && !rad && pl >= 8 && (pkt[po] & 0xE0) == 0x20) {
+				NEXT(K_GTP1, po, pl);
+				break;
+			}
 			int sip = sip_heuristic(pkt + po, pl);
-			*ncls = udp_l7(pl, be16(p), be16(p + 2), sip);
+			*ncls = udp_l7(pl, sp, dp, sip);
 			NEXT(*ncls ? K_L7 : K_PAYLOAD, po, pl);
 			*nosi = l7_osi(*ncls, udp_l7_min_osi(be16(p), be16(p + 2), sip));
 		}
 		break;
+	case K_VXLAN: /* VxlanLayer (OSI data link, VxlanLayer.h:130-144): 8-byte header; parseNextLayer VxlanLayer.cpp:50-58:
+	               * Ethernet (tryConstruct), else a Payload */
+		L.proto = P_VXLAN; L.osi = 2; L.hdr = 8;
+		if (len <= 8) break;
+		po = off + 8; pl = len - 8;
+		NEXT(eth_valid(pkt + po, pl) ? K_ETH : K_PAYLOAD, po, pl);
+		break;
+	case K_GTP1: { /* GtpV1Layer (OSI transport, GtpLayer.h:408-411): getHeaderLen GtpLayer.cpp:602-632, the extension
+	                * chain GtpExtension :60-120 and :323-350; parseNextLayer :560-600 (G-PDU only) */
+		L.proto = P_GTPV1; L.osi = 4; L.hdr = 8;
+		const uint8_t fl = p[0], mt = p[1];
+		if (mt != 0xFF) {
+			uint32_t ml = be16(p + 2);
+			L.hdr += ml > len - 8 ? len - 8 : ml;
+			break; /* GTP-C: the last layer */
+		}
+		if (len >= 12 && (fl & 7)) {
+			L.hdr += 4; /* gtpv1_header_extra */
+			uint32_t nt = p[11];
+			if ((fl & 4) && nt != 0 && len > 12) {
+				uint32_t ed = 12, erem = len - 12;
+				for (;;) {
+					uint32_t tl = 4u * p[ed];
+					if (tl > erem) tl = erem;
+					L.hdr += tl;
+					nt = tl >= 4 ? p[ed + tl - 1] : 0;
+					if (nt == 0 || erem <= tl + 1) break;
+					ed += tl;
+					erem -= tl;
+				}
+			}
+		}
+		if (len <= L.hdr) break;
+		po = off + L.hdr; pl = len - L.hdr;
+		{
+			uint8_t sub = pkt[po];
+			if (sub >= 0x45 && sub <= 0x4e) NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl);
+			else if ((sub & 0xf0) == 0x60) NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl);
+			else NEXT(K_PAYLOAD, po, pl);
+		}
+		break;
+	}
 	case K_ICMP: { /* IcmpLayer (OSI network, IcmpLayer.h:611-614): getHeaderLen by message type, IcmpLayer.cpp:589-620
 	                * (getMessageType :36-43); parseNextLayer :562-587: the error messages carry the offending IPv4
 	                * header (tryConstruct IPv4, else a Payload, even an empty one), the rest a Payload past the header */

@@ -31,7 +31,7 @@ enum : uint32_t
 {
 	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14, P_GREV0 = 15,
 	P_GREV1 = 16, P_PPTP = 17, P_SLL = 19, P_NULL = 21, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44,
-	P_SLL2 = 52
+	P_SLL2 = 52, P_VXLAN = 26, P_GTPV1 = 32
 };
 
 // next-layer kinds of the chain walk
@@ -39,10 +39,10 @@ enum : uint32_t
 {
 	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
 	K_PAYLOAD, K_OUT, K_ARP, K_SLL, K_SLL2, K_NULL,  // SLL / SLL2 / Null-Loopback: first layers only
-	K_ICMP,
+	K_ICMP, K_VXLAN, K_GTP1,
 	// candidates: the layer a tryConstructNextLayerWithFallback would build if its isDataValid holds, else
 	// Payload (Layer.h:474-483); resolved from the candidate's own first bytes when the walk reaches it
-	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC, C_ICMP
+	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC, C_ICMP, C_ETH, C_IPGTP
 };
 
 // explicit address spaces: keep packet reads as global_load / ds_read, never flat
@@ -674,6 +674,8 @@ __device__ __forceinline__ uint32_t resolve(uint32_t k, const Peek& q, uint32_t 
 {
 	const uint32_t b0 = q.b(0), ver = b0 >> 4;
 	k = k == C_IPVER ? (ver == 4 ? C_IPV4 : (ver == 6 ? C_IPV6 : K_PAYLOAD)) : k;
+	// GtpV1Layer::parseNextLayer's sub-protocol byte (GtpLayer.cpp:585-599): 0x45-0x4e IPv4, 0x6_ IPv6
+	k = k == C_IPGTP ? ((b0 >= 0x45 && b0 <= 0x4e) ? C_IPV4 : (ver == 6 ? C_IPV6 : K_PAYLOAD)) : k;
 	const bool ok4 = len >= 20 && ver == 4 && (b0 & 0xF) >= 5;
 	const bool ok6 = len >= 40 && ver == 6;
 	const uint32_t d = q.b(12) >> 4;
@@ -696,6 +698,7 @@ __device__ __forceinline__ uint32_t resolve(uint32_t k, const Peek& q, uint32_t 
 	k = k == C_ETHG ? ke : k;
 	k = k == C_LLC ? (okl ? K_LLC : K_PAYLOAD) : k;
 	k = k == C_ICMP ? (len >= need ? K_ICMP : K_PAYLOAD) : k;
+	k = k == C_ETH ? ((len >= 14 && et >= 0x0600) ? K_ETH : K_PAYLOAD) : k;  // VXLAN: Ethernet, else Payload
 	return k;
 }
 
@@ -710,7 +713,39 @@ __device__ __forceinline__ uint32_t resolve(uint32_t k, const Peek& q, uint32_t 
 struct Step
 {
 	uint32_t proto, osi, hdr, dlen, nk, po, pl;
+	bool l7done;  // a TCP/UDP payload whose next layer this step decided (a tunnel): no L7 decision after the walk
 };
+
+// GtpV1Layer::getHeaderLen (GtpLayer.cpp:602-632): 8 B; GTP-C adds its message length (at most the data); a
+// G-PDU with any of the E / S / PN flags adds gtpv1_header_extra (4 B) and, with E, the extension chain
+// (GtpExtension, :60-120,323-350: 4 * length byte, at most the rest; the next type is its last byte)
+__device__ uint32_t gtp1_header_len(const Pkt& p, uint32_t o, uint32_t len, const Peek& q)
+{
+	const uint32_t fl = q.b(0);
+	if (q.b(1) != 0xFF)
+	{
+		const uint32_t ml = q.be(2);
+		return 8 + (ml > len - 8 ? len - 8 : ml);
+	}
+	if (len < 12 || !(fl & 7))
+		return 8;
+	uint32_t res = 12, nt = q.b(11);
+	if (!(fl & 4) || nt == 0 || len <= 12)
+		return res;
+	uint32_t ed = 12, erem = len - 12;
+	for (;;)
+	{
+		uint32_t tl = 4 * rb(p, o + ed);
+		tl = tl <= erem ? tl : erem;
+		res += tl;
+		nt = tl >= 4 ? rb(p, o + ed + tl - 1) : 0u;
+		if (nt == 0 || erem <= tl + 1)
+			break;
+		ed += tl;
+		erem -= tl;
+	}
+	return res;
+}
 
 // per-kind ProtocolType (6 bits) and OsiModelLayer (3 bits); kinds without a layer map to Payload / 7
 constexpr uint32_t kind_proto(uint32_t k)
@@ -778,8 +813,12 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	}
 	// protocol / OSI layer (ProtocolType.h) of kind k, read from per-kind tables packed into 64-bit
 	// constants (two shifts instead of a select chain over every kind)
-	const uint32_t proto = (uint32_t)((k < 10 ? (kProtoLo >> (6 * k)) : (kProtoHi >> (6 * (k - 10)))) & 63u);
-	const uint32_t osi = (uint32_t)((kOsi >> (3 * k)) & 7u);
+	const uint32_t kt = k < 20 ? k : 0u;  // the packed tables hold kinds 0-19; VXLAN / GTPv1 are set below
+	const bool isVx = k == K_VXLAN, isG1 = k == K_GTP1;
+	uint32_t proto = (uint32_t)((kt < 10 ? (kProtoLo >> (6 * kt)) : (kProtoHi >> (6 * (kt - 10)))) & 63u);
+	uint32_t osi = (uint32_t)((kOsi >> (3 * kt)) & 7u);
+	proto = isVx ? P_VXLAN : (isG1 ? P_GTPV1 : proto);
+	osi = isVx ? 2u : (isG1 ? 4u : osi);  // VxlanLayer.h:141-144, GtpLayer.h:408-411
 	// header length
 	const uint32_t f0 = q.b(0), f1 = q.b(1);
 	const uint32_t greh = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
@@ -807,6 +846,9 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	const uint32_t ra = 8 + 8 * q.b(4);
 	ih = it == 9 ? (ra < len ? ra : len) : ih;
 	hdr = isI ? ih : hdr;
+	hdr = isVx ? 8 : hdr;  // vxlan_header (VxlanLayer.h:14-60)
+	if (isG1)
+		hdr = gtp1_header_len(p, o, len, q);
 	// data length: IPv4 totalLength truncation (0 = TSO keeps it), IPv6 payloadLength + header, ARP 28
 	uint32_t dlen = len;
 	const uint32_t tl = q.be(2);
@@ -818,7 +860,7 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	// successor: exists iff the layer's data runs past its header (every kind's "no next layer" rule; Null/Loopback
 	// always builds one, empty for a 4-byte packet: NullLoopbackLayer.cpp:50-99 has no length check)
 	// (an ICMP error message always builds one, empty when the quote is: IcmpLayer.cpp:562-587)
-	const bool has_next = dlen > hdr || isN || (isI && ierr);
+	const bool has_next = (dlen > hdr || isN || (isI && ierr)) && !(isG1 && q.b(1) != 0xFF);  // GTP-C: last
 	const uint32_t po = o + hdr, pl = has_next ? dlen - hdr : 0;
 	// EtherType dispatch of Ethernet (EtherType at 12), VLAN and GRE (at 2), SLL (protocol_type at 14) and SLL2 (at
 	// 0: SllLayer.cpp:49-102, Sll2Layer.cpp:63-121); PPP protocol of PPP_PPTP (at 2)
@@ -868,9 +910,26 @@ __device__ __forceinline__ Step step_layer(const Pkt& p, uint32_t k, uint32_t o,
 	nk = isD ? C_LLC : nk;
 	nk = isL ? ((f0 == 0x42 && f1 == 0x42) ? K_OUT : K_PAYLOAD) : nk;
 	nk = isI ? (ierr ? C_IPV4 : K_PAYLOAD) : nk;  // the quoted IPv4 header (tryConstruct), else a Payload
+	// UDP tunnels, decided as UdpLayer::parseNextLayer does (:103-131): VXLAN by destination port (8 bytes,
+	// VxlanLayer.h:97-100), GTPv1 by port and isGTPv1 (GtpLayer.cpp:199-207) where no earlier dissector takes the
+	// payload: DHCP, DNS, SIP (port), RADIUS (port and RadiusLayer::isDataValid, RadiusLayer.cpp:238-247)
+	const uint32_t usp = q.be(0), udp = q.be(2);
+	const bool vx = isU && udp == 4789;
+	const bool dhcp = (usp == 68 && udp == 67) || (usp == 67 && (udp == 68 || udp == 67));
+	const bool dnsb = pl >= 12 && (dns_port(usp) || dns_port(udp));
+	const bool sipp = usp == 5060 || usp == 5061 || udp == 5060 || udp == 5061;
+	const bool radp = usp == 1812 || usp == 1813 || usp == 3799 || udp == 1812 || udp == 1813 || udp == 3799;
+	const uint32_t rlen = q.be(10);  // the RADIUS length field (payload bytes 2-3)
+	const bool rad = radp && pl >= 20 && rlen >= 20 && rlen <= pl;
+	const bool gport = usp == 2152 || udp == 2152 || usp == 2123 || udp == 2123;
+	const bool gtp = isU && gport && !vx && !dhcp && !dnsb && !sipp && !rad && pl >= 8 && (q.b(8) & 0xE0) == 0x20;
+	nk = vx ? (pl >= 8 ? K_VXLAN : K_PAYLOAD) : nk;
+	nk = gtp ? K_GTP1 : nk;
+	nk = isVx ? C_ETH : nk;
+	nk = isG1 ? C_IPGTP : nk;
 	// TCP/UDP: a tentative Payload; walk_chain decides afterwards whether an L7 dissector takes it
 	nk = has_next ? nk : K_NONE;
-	return Step{ proto, osi, hdr, dlen, nk, has_next ? po : 0, pl };
+	return Step{ proto, osi, hdr, dlen, nk, has_next ? po : 0, pl, vx || gtp };
 }
 
 struct Params
@@ -992,7 +1051,7 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 		udpA = (udpA & ~mU) | (a_new & mU);
 		udpB = (udpB & ~mU) | (b_new & mU);
 		const uint32_t mP = (mT & 0xFFu) | (mU & 0xFF00u) | ((mT | mU) & 0xFFFF0000u);
-		const uint32_t p_new = (prev & 0xFFu) * 0x101u | (s.pl << 16);
+		const uint32_t p_new = (prev & 0xFFu) * 0x101u | ((s.l7done ? 0u : s.pl) << 16);
 		pps = (pps & ~mP) | (p_new & mP);
 		prev = proto | (o << 16);
 		last_end = o + s.dlen;
@@ -1945,7 +2004,10 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		{
 			fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
 			fast_l7(p, f, cap);
-			fast = !(f.l7() & kL7Built);  // a classified HTTP / SSL / DNS payload: the generic walk builds its layers
+			// a classified HTTP / SSL / DNS payload or a UDP tunnel (VXLAN, GTPv1: an unclassified L7 flag): the
+			// generic walk builds their layers
+			const uint32_t l7 = f.l7();
+			fast = !(l7 & kL7Built) && !((l7 & PCPPX_F_NEEDS_HOST_L7) && !(l7 & PCPPX_F_L7_KNOWN));
 		}
 		if (fast)
 		{

@@ -169,6 +169,46 @@ def crafted(seed: int = 7) -> list[bytes]:
     pk.append(_eth(0x0800) + _ipv4(1, len(echo), frag=0x2000) + echo)
     pk.append(_eth(0x86DD) + _ipv6(1, len(echo)) + echo)
     pk.append(_eth(0x0800) + _ipv4(1, len(echo)) + echo + b"\xee" * 9)
+    # tunnels over UDP (UdpLayer.cpp:103-131): VXLAN (VxlanLayer.cpp:50-58) and GTPv1 (GtpLayer.cpp:199-207,
+    # 560-632) with inner stacks, extension chains, GTP-C lengths, and the port combinations that keep an earlier
+    # dissector (DHCP, DNS, SIP, RADIUS) in front
+    t4 = _tcp(1000, 2000, pay(10))
+    in4 = _ipv4(6, len(t4)) + t4
+    u53 = _udp(3000, 53, pay(20))
+    in6 = _ipv6(17, len(u53)) + u53
+    vx = bytes([8, 0, 0, 0, 0, 1, 2, 0])
+    for inner in (_eth(0x0800) + in4, _eth(0x86DD) + in6, _eth(0x0800)[:13], bytes(12) + b"\x05\xdc" + pay(8), b"",
+                  _eth(0x0800) + _ipv4(17, 16) + _udp(5, 4789, vx + _eth(0x0800) + in4)[:24], pay(3)):
+        for v in (vx, vx[:7]):
+            u = _udp(40000, 4789, v + inner)
+            pk.append(_eth(0x0800) + _ipv4(17, len(u)) + u)
+            pk.append(_eth(0x86DD) + _ipv6(17, len(u)) + u + b"\x00" * 3)
+    u = _udp(4789, 40000, vx + _eth(0x0800) + in4)  # source port only: no VXLAN
+    pk.append(_eth(0x0800) + _ipv4(17, len(u)) + u)
+
+    def gtp(fl, mt, body, extra=b""):
+        return bytes([fl, mt]) + struct.pack(">HI", len(extra) + len(body), 0x1234) + extra + body
+    exts = [b"", bytes([1, 0x12, 0, 0]), bytes([1, 0x12, 0, 0x85]) + bytes([2, 1, 2, 3, 4, 5, 6, 0]),
+            bytes([1, 0, 0, 0x85]), bytes([0, 9, 9, 9]), bytes([3, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 0]),
+            bytes([9, 1, 2, 3]), bytes([1, 2, 3, 0x40]) + bytes([1, 2, 3, 0])]
+    for fl in (0x30, 0x32, 0x34, 0x31, 0x36, 0x37, 0x20, 0x50, 0x10):
+        for ext in exts:
+            nt = ext[0] if False else (0x85 if ext else 0)
+            extra = (b"\x00\x01\x00" + bytes([nt]) + ext) if fl & 7 else b""
+            for body in (in4, in6, bytes([0x4f]) + in4[1:], bytes([0x44]) + in4[1:], in4[:19], pay(6), b""):
+                g = gtp(fl, 0xFF, body, extra)
+                u = _udp(2152, 2152, g)
+                pk.append(_eth(0x0800) + _ipv4(17, len(u)) + u)
+    for ports in ((2123, 40000), (40000, 2123), (2152, 53), (53, 2152), (2152, 5060), (1812, 2152), (67, 2152),
+                  (2152, 4789), (2152, 40000)):
+        for mt, ml in ((0xFF, None), (1, 4), (1, 400), (16, 0)):
+            g = gtp(0x32, mt, in4, b"\x00\x01\x00\x00")
+            if ml is not None:
+                g = g[:2] + struct.pack(">H", ml) + g[4:]
+            u = _udp(ports[0], ports[1], g)
+            pk.append(_eth(0x0800) + _ipv4(17, len(u)) + u)
+        u = _udp(ports[0], ports[1], gtp(0x30, 0xFF, in4)[:7])
+        pk.append(_eth(0x0800) + _ipv4(17, len(u)) + u)
     return pk
 
 
