@@ -10,9 +10,11 @@ from pcapplusplus_amd import abi
 
 AB_SO = Path(__file__).resolve().parent / "libpcppx_ab.so"
 R01_SO = Path(__file__).resolve().parent / "r01" / "libpcppx_r01.so"
+PREV_SO = Path(__file__).resolve().parent / "prev" / "libpcppx_prev.so"
 _lib = None
-_r01 = None
+_r01 = {}
 R01 = -1  # parse_device variant: the round-1 product kernel (tools/ab/r01, rebuilt from git history)
+PREV = -2  # parse_device variant: the r02m product kernel before device-built L7 / ICMP / tunnels (tools/ab/prev)
 
 # pcppx_ab_parse_device variants (tools/ab/pcppx_ab.hip)
 LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ, TILE_W5_WIN256, TILE_W1_WIN128, TILE_W1_WIN256, TILE_CACHED = \
@@ -37,25 +39,25 @@ def lib() -> C.CDLL:
     return _lib
 
 
-def r01_lib() -> C.CDLL:
-    global _r01
-    if _r01 is None:
-        if not R01_SO.exists():
-            raise RuntimeError(f"{R01_SO} missing: run `make -C tools/ab/r01`")
+def r01_lib(so: Path = R01_SO) -> C.CDLL:
+    """a product kernel rebuilt from git history (round 1, or tools/ab/prev's revision)"""
+    if so not in _r01:
+        if not so.exists():
+            raise RuntimeError(f"{so} missing: run `make -C {so.parent}`")
         abi.load_engine()
-        l = C.CDLL(str(R01_SO))
+        l = C.CDLL(str(so))
         l.pcppx_r01_parse_device.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Opts), C.POINTER(abi.Records), C.c_void_p]
         l.pcppx_r01_parse_device.restype = C.c_int
-        _r01 = l
-    return _r01
+        _r01[so] = l
+    return _r01[so]
 
 
 def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers, stream: int,
                  variant: int) -> None:
     b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
     rec = abi.Records(abi.ptr(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None)
-    if variant == R01:  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
-        abi.check(r01_lib().pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
+    if variant in (R01, PREV):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
+        abi.check(r01_lib(R01_SO if variant == R01 else PREV_SO).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
                   "pcppx_r01_parse_device")
         return
     abi.check(lib().pcppx_ab_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0), variant),

@@ -27,6 +27,7 @@ read_bytes = int(b.caplens.sum(dtype=np.int64)) + 12 * n  # the checksum runs' a
 cases = {
     "tile/ml8/csum": (abi.make_opts(0, 8, True, 8), 0),
     "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
+    "prev/ml8/csum": (abi.make_opts(0, 8, True, 8), -2),
     "tile/chaintails": (abi.make_opts(0, 8, True, 8), 12),
     "tile/ring": (abi.make_opts(0, 8, True, 8), 40),
     "tile/ring-win256": (abi.make_opts(0, 8, True, 8), 41),
@@ -59,6 +60,7 @@ cases.update({
     "po/w10r5": (abi.make_opts(0, 8, False, _ml), 24),
     "po/w7r5": (abi.make_opts(0, 8, False, _ml), 25),
     "po/r01": (abi.make_opts(0, 8, False, _ml), -1),
+    "po/prev": (abi.make_opts(0, 8, False, _ml), -2),
     "po/chaintails": (abi.make_opts(0, 8, False, _ml), 26),
     "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
     "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),
@@ -73,7 +75,7 @@ if only:
 ref_s = ref_l = None
 want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
-    if o.max_layers != next(iter(cases.values()))[0].max_layers or o.want_checksums != want_csum_ref or v in (2, 3, 4, 29, 44):
+    if o.max_layers != next(iter(cases.values()))[0].max_layers or o.want_checksums != want_csum_ref or v in (2, 3, 4, 29, 44, -2):  # -2: L7 records of an older contract
         continue
     summ.zero_()
     lay.zero_()
