@@ -55,6 +55,9 @@ def parse_args():
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py; default profiles/traffic_cfg<N>.json); "
                          "used only if it was measured on this kernel source, config, size and record options")
     ap.add_argument("--no-traffic", action="store_true", help="do not report PMC traffic (the PMC passes themselves)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="gloo: a multi-rank rehearsal on fewer GPUs than ranks (ranks share cards round-robin); "
+                         "the timed numbers of such a run are not a scaling measurement")
     return ap.parse_args()
 
 
@@ -163,10 +166,15 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.dist_backend == "gloo":
+        local = local % torch.cuda.device_count()  # rehearsal: ranks share the card(s)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
     dev = f"cuda:{local}"
     torch.cuda.set_device(dev)
 
@@ -235,7 +243,7 @@ def main() -> None:
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, mids)])) if mids else step_ms
     flow_ms = step_ms - kern_ms if mids else None
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, kern_max = float(t[0]), float(t[1])

@@ -1823,6 +1823,58 @@ __device__ uint32_t full_chunks_sum(uintptr_t c0, uintptr_t c1)
 	return acc;
 }
 
+// The header extent of a deep stack, from the first gather window: where fast_walk stops reading (the L4 layer's
+// first 20 bytes: TCP's fixed header, UDP's header + the SIP heuristic's 4 payload bytes) for up to three MPLS
+// labels, IPv6 extension headers and GREv0 + an inner IP layer -- the same steps as fast_walk, without its validity
+// checks (a too-short window only sends a packet to the generic walk, which reads on from HBM). Any stack it cannot
+// follow inside the window, or one that does not end in TCP / UDP / a fragment, asks for the whole window (0xFFFF).
+// et / o: the EtherType and offset after the VLAN tags.
+__device__ __forceinline__ uint32_t deep_extent(const Pkt& p, uint32_t et, uint32_t o)
+{
+#pragma unroll
+	for (int t = 0; t < 3; ++t)
+	{
+		const bool ml = et == 0x8847 && o + 5 <= p.lim;
+		const uint32_t w = lds_u32(p, ml ? o : 0), nb = (lds_u32(p, ml ? o + 4 : 0) & 0xFF) >> 4;
+		const uint32_t nxt = ((w >> 16) & 1) ? (nb == 4 ? 0x0800u : (nb == 6 ? 0x86DDu : 0xFFFFu)) : 0x8847u;
+		et = ml ? nxt : et;
+		o = ml ? o + 4 : o;
+	}
+	const bool v6 = et == 0x86DD;
+	bool ok = (et == 0x0800 || v6) && o + (v6 ? 40 : 20) <= p.lim;
+	const uint32_t w0 = lds_u32(p, ok ? o : 0), w1 = lds_u32(p, ok ? o + 4 : 0), w2 = lds_u32(p, ok ? o + 8 : 0);
+	uint32_t hdr = v6 ? 40u : (w0 & 0xF) * 4;
+	uint32_t nh = v6 ? (w1 >> 16) & 0xFF : (w2 >> 8) & 0xFF;
+	bool frag = !v6 && ((w1 & 0xFF3F0000u) != 0);  // IPv4 MF / fragment offset (bytes 6-7)
+	constexpr uint64_t kExt = (1ull << 0) | (1ull << 43) | (1ull << 44) | (1ull << 51) | (1ull << 60);
+#pragma unroll
+	for (int t = 0; t < 3; ++t)
+	{
+		const bool e = ok && v6 && nh < 64 && ((kExt >> nh) & 1ull) && o + hdr + 2 <= p.lim;
+		const uint32_t two = lds_u32(p, e ? o + hdr : 0) & 0xFFFFu;
+		const uint32_t el = nh == 51 ? 4u * ((two >> 8) + 2) : 8u * ((two >> 8) + 1);
+		frag = frag || (e && nh == 44);
+		frag = frag && !(e && nh != 44);  // only a LAST Fragment extension makes the rest a Payload
+		nh = e ? (two & 0xFFu) : nh;
+		hdr += e ? el : 0u;
+	}
+	ok = ok && !(v6 && nh < 64 && ((kExt >> nh) & 1ull));
+	uint32_t l4 = o + hdr;
+	const bool g = ok && !frag && nh == 47;
+	ok = ok && (!g || l4 + 4 <= p.lim);
+	const uint32_t gw = lds_u32(p, g && ok ? l4 : 0);
+	const uint32_t f0 = gw & 0xFF, f1 = (gw >> 8) & 0xFF, get = swap16(gw >> 16);
+	const uint32_t gh = 4 + ((f0 & 0xC0) ? 4 : 0) + ((f0 & 0x20) ? 4 : 0) + ((f0 & 0x10) ? 4 : 0) + ((f1 & 0x80) ? 4 : 0);
+	const uint32_t o2 = l4 + gh;
+	const bool v6b = get == 0x86DD;
+	ok = ok && (!g || ((get == 0x0800 || v6b) && o2 + 10 <= p.lim));
+	const uint32_t i0 = lds_u32(p, g && ok ? o2 : 0), i1 = lds_u32(p, g && ok ? o2 + 4 : 0), i2 = lds_u32(p, g && ok ? o2 + 8 : 0);
+	l4 = g ? o2 + (v6b ? 40u : (i0 & 0xF) * 4) : l4;
+	nh = g ? (v6b ? (i1 >> 16) & 0xFF : (i2 >> 8) & 0xFF) : nh;
+	ok = ok && (frag || nh == 6 || nh == 17);
+	return ok ? l4 + 20 : 0xFFFFu;
+}
+
 constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_layers; beyond, direct stores
 
 // MinWaves: __launch_bounds__ minimum waves per SIMD (1 = compiler's choice). LDS is 8 KiB per block
@@ -1843,11 +1895,13 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // global load issued before the stream.
 // SkipGeneric (tools only, a diagnostic: wrong records): packets off the fast path are not walked -- the time the
 // generic walk costs the waves that hold such a packet.
+// TightR2: the second gather round reads only up to the deep stack's header extent (deep_extent) instead of the
+// whole window (false: tools/ab variant 50).
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
-          bool Ring = false, bool SkipGeneric = false>
+          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1963,8 +2017,15 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 8 <= p.lim ? o + 8 : 0);
 		const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
 		const bool deep = et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
-		const uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
-		const bool more = live && !StreamOnly && (deep || GatherOnly) && full > p.nch;
+		uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
+		bool more = live && !StreamOnly && (deep || GatherOnly) && full > p.nch;
+		if (TightR2 && !GatherOnly && __ballot(more))  // wave-uniform: waves without a deep stack skip the extent
+		{
+			// only as far as the fast path reads: the deep stack's header extent, when the first window names it
+			const uint32_t xc = (p.mis + deep_extent(p, et, o) + 15) >> 4;
+			full = xc < full ? xc : full;
+			more = more && full > p.nch;
+		}
 		if (__ballot(more))  // wave-uniform
 		{
 			m_nch[lane] = more ? (full | (p.nch << 8)) : 0u;

@@ -180,6 +180,7 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 21: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 10>), grid, dim3(kTile), 0, stream, prm); break;
 	case 22: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 23: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	case 50: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // whole-window second round
 	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 26: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // chain records only
