@@ -1896,12 +1896,13 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // SkipGeneric (tools only, a diagnostic: wrong records): packets off the fast path are not walked -- the time the
 // generic walk costs the waves that hold such a packet.
 // TightR2: the second gather round reads only up to the deep stack's header extent (deep_extent) instead of the
-// whole window (false: tools/ab variant 50).
+// whole window (false: tools/ab variant 50). Realign: a deep stack that ends past the window is re-gathered from a
+// dword-aligned start (mis <= 3 instead of <= 15) so that it fits (false: tools/ab variant 51).
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
-          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true>
+          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -2019,16 +2020,31 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		const bool deep = et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
 		uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
 		bool more = live && !StreamOnly && (deep || GatherOnly) && full > p.nch;
+		uint32_t from = p.nch;  // the second round gathers chunks [from, full)
 		if (TightR2 && !GatherOnly && __ballot(more))  // wave-uniform: waves without a deep stack skip the extent
 		{
 			// only as far as the fast path reads: the deep stack's header extent, when the first window names it
-			const uint32_t xc = (p.mis + deep_extent(p, et, o) + 15) >> 4;
+			const uint32_t ext = deep_extent(p, et, o);
+			uint32_t xc = (p.mis + ext + 15) >> 4;
+			// a known stack ending past the 16-B-aligned window (up to 15 B of it lie before the packet): this lane
+			// re-gathers its whole window from a dword-aligned start instead, so the fast path still takes it
+			const bool realign = Realign && more && ext != 0xFFFFu && xc > (uint32_t)Chunks;
+			if (realign)
+			{
+				p.a0 = (uintptr_t)p.g & ~(uintptr_t)3;
+				p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+				m_a0[lane] = p.a0;
+				const uint32_t need4 = (p.mis + cap + 15) >> 4;
+				full = need4 < (uint32_t)Chunks ? need4 : (uint32_t)Chunks;
+				xc = (p.mis + ext + 15) >> 4;
+				from = 0;
+			}
 			full = xc < full ? xc : full;
-			more = more && full > p.nch;
+			more = more && full > from;
 		}
 		if (__ballot(more))  // wave-uniform
 		{
-			m_nch[lane] = more ? (full | (p.nch << 8)) : 0u;
+			m_nch[lane] = more ? (full | (from << 8)) : 0u;
 			__syncthreads();
 			gather();
 			__syncthreads();

@@ -181,6 +181,7 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 22: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 23: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 50: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // whole-window second round
+	case 51: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, false>), grid, dim3(kTile), 0, stream, prm); break;  // tight second round, no realign
 	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 26: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // chain records only
@@ -199,7 +200,7 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 28: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 5, false, false>), grid, dim3(kTile), 0, stream, prm); break;
 	// the product shapes with flags bit 0x8000 marking the packets the fast path took (records otherwise equal)
 	case 30: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 7, true>), grid, dim3(kTile), 0, stream, prm); break;
-	case 31: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 6, true>), grid, dim3(kTile), 0, stream, prm); break;
+	case 31: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, true>), grid, dim3(kTile), 0, stream, prm); break;
 	default: return launch_parse(b, o, r, stream);
 	}
 	return check_launch("pcppx_ab_parse_device", stream);

@@ -62,6 +62,7 @@ cases.update({
     "po/r01": (abi.make_opts(0, 8, False, _ml), -1),
     "po/prev": (abi.make_opts(0, 8, False, _ml), -2),
     "po/r2full": (abi.make_opts(0, 8, False, _ml), 50),
+    "po/norealign": (abi.make_opts(0, 8, False, _ml), 51),
     "po/chaintails": (abi.make_opts(0, 8, False, _ml), 26),
     "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
     "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),

@@ -29,3 +29,5 @@ for variant, csum in ((30, True), (31, False)):
     print(f"variant {variant} (checksums {csum}): fast {fast.mean():.4f} of {b.n}")
     for k, v in slow.most_common(12):
         print(f"   slow {v:7d} of {stacks[k]:7d}  {k}")
+    mis = (b.offsets & 15)[~fast]
+    print("   slow packets by start offset mod 16:", np.bincount(mis.astype(np.int64), minlength=16).tolist())
