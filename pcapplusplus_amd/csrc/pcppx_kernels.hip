@@ -2026,9 +2026,11 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// only as far as the fast path reads: the deep stack's header extent, when the first window names it
 			const uint32_t ext = deep_extent(p, et, o);
 			uint32_t xc = (p.mis + ext + 15) >> 4;
-			// a known stack ending past the 16-B-aligned window (up to 15 B of it lie before the packet): this lane
-			// re-gathers its whole window from a dword-aligned start instead, so the fast path still takes it
-			const bool realign = Realign && more && ext != 0xFFFFu && xc > (uint32_t)Chunks;
+			// a stack ending past the 16-B-aligned window (up to 15 B of it lie before the packet), or one whose end the
+			// first window does not show: this lane re-gathers its whole window from a dword-aligned start instead, so
+			// that the fast path still takes it
+			const bool past = ext != 0xFFFFu ? xc > (uint32_t)Chunks : (need > (uint32_t)Chunks && p.mis > 3);
+			const bool realign = Realign && more && past;
 			if (realign)
 			{
 				p.a0 = (uintptr_t)p.g & ~(uintptr_t)3;

@@ -199,7 +199,7 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 29: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // gather-only diagnostic
 	case 28: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 5, false, false>), grid, dim3(kTile), 0, stream, prm); break;
 	// the product shapes with flags bit 0x8000 marking the packets the fast path took (records otherwise equal)
-	case 30: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 7, true>), grid, dim3(kTile), 0, stream, prm); break;
+	case 30: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, true>), grid, dim3(kTile), 0, stream, prm); break;
 	case 31: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, true>), grid, dim3(kTile), 0, stream, prm); break;
 	default: return launch_parse(b, o, r, stream);
 	}
