@@ -55,6 +55,8 @@ def parse_args():
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py; default profiles/traffic_cfg<N>.json); "
                          "used only if it was measured on this kernel source, config, size and record options")
     ap.add_argument("--no-traffic", action="store_true", help="do not report PMC traffic (the PMC passes themselves)")
+    ap.add_argument("--window", choices=("default", "deep"), default="default",
+                    help="checksum launches' header window (pcppx_opts.window): deep = two-round 144 B for deep stacks")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: a multi-rank rehearsal on fewer GPUs than ranks (ranks share cards round-robin); "
                          "the timed numbers of such a run are not a scaling measurement")
@@ -194,7 +196,7 @@ def main() -> None:
         batch = synth.small64(npk, seed)
     gen_s = time.time() - t0
     want_csum = args.checksums == "on" or (args.checksums == "auto" and cfg == 3)
-    opts = abi.make_opts(0, 8, want_csum, ml)
+    opts = abi.make_opts(0, 8, want_csum, ml, abi.WINDOW_DEEP if args.window == "deep" else abi.WINDOW_DEFAULT)
     n = batch.n
     eng = Engine(local)
     data, offsets, caplens = to_device(batch, dev)
@@ -347,6 +349,7 @@ def main() -> None:
                 "packets_per_gpu": n,
                 "wire_bytes_per_gpu": wire,
                 "checksums": want_csum,
+                "window": args.window,
                 "max_layers": ml,
                 "parallelism": f"shard{world} (no collective)",
                 "wire_GBps": round(wire * world * args.steps / wall_max / 1e9, 2),

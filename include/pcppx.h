@@ -124,8 +124,13 @@ typedef struct pcppx_opts {
 	uint8_t parse_until_osi;     /* pcpp::OsiModelLayer; 8 = OsiModelLayerUnknown */
 	uint8_t want_checksums;      /* compute IPv4 / L4 checksums */
 	uint8_t max_layers;          /* 0 = do not write layers; else layers stride per packet (1..16) */
-	uint8_t reserved;            /* must be 0 */
+	uint8_t window;              /* PCPPX_WINDOW_*: the header window of checksum launches (records are identical
+	                                either way; parse-only launches always gather a two-round deep window) */
 } pcppx_opts;
+#define PCPPX_WINDOW_DEFAULT 0 /* 96-B header window, 5 waves/SIMD: the fastest for Eth / VLAN / IP / L4 traffic */
+#define PCPPX_WINDOW_DEEP 1    /* + a second gather round up to 144 B for stacks deeper than the first window
+                                  (QinQ, MPLS, GRE, IPv6 extensions): those packets stay on the fast path instead of
+                                  the generic walk; 4 waves/SIMD */
 
 /* Output arrays (same memory space as the batch for the _device call, host for the _host call). */
 typedef struct pcppx_records {

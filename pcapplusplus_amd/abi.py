@@ -18,6 +18,7 @@ ENGINE_SO = PKG_DIR / "libpcppx.so"
 ABI_VERSION = 4
 MAX_LAYERS = 16
 MAX_CAPLEN = 65535
+WINDOW_DEFAULT, WINDOW_DEEP = 0, 1  # pcppx_opts.window (PCPPX_WINDOW_*)
 
 # error codes
 OK, E_INVAL, E_NODEV, E_HIP, E_NOMEM, E_LINKTYPE = 0, -1, -2, -3, -4, -5
@@ -98,7 +99,7 @@ class Opts(C.Structure):
         ("parse_until_osi", C.c_uint8),
         ("want_checksums", C.c_uint8),
         ("max_layers", C.c_uint8),
-        ("reserved", C.c_uint8),
+        ("window", C.c_uint8),
     ]
 
 
@@ -132,11 +133,14 @@ def ipv4_to_int(dotted: str) -> int:
 
 
 def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checksums: bool = True,
-              max_layers: int = MAX_LAYERS) -> Opts:
-    """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection."""
+              max_layers: int = MAX_LAYERS, window: int = 0) -> Opts:
+    """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection; window:
+    WINDOW_DEFAULT / WINDOW_DEEP (the checksum launch's header window, records identical)."""
     if not 0 <= max_layers <= MAX_LAYERS:
         raise ValueError(f"max_layers must be in [0, {MAX_LAYERS}]")
-    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, 0)
+    if window not in (WINDOW_DEFAULT, WINDOW_DEEP):
+        raise ValueError("window must be WINDOW_DEFAULT or WINDOW_DEEP")
+    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, window)
 
 
 def _declare(lib: C.CDLL) -> C.CDLL:

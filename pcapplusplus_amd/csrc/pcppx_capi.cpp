@@ -177,7 +177,7 @@ bool ok(hipError_t e)
 
 int valid_opts(const pcppx_opts* o)
 {
-	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->reserved != 0)
+	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->window > PCPPX_WINDOW_DEEP)
 		return PCPPX_E_INVAL;
 	return PCPPX_OK;
 }
@@ -549,7 +549,7 @@ extern "C"
 		o->parse_until_osi = 8;     // OsiModelLayerUnknown
 		o->want_checksums = 1;
 		o->max_layers = PCPPX_MAX_LAYERS;
-		o->reserved = 0;
+		o->window = PCPPX_WINDOW_DEFAULT;
 	}
 
 	int pcppx_open(int device, pcppx_ctx** out)

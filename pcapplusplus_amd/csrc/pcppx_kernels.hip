@@ -581,7 +581,7 @@ __device__ uint32_t range_residue(const Pkt& p, uint32_t lo, uint32_t hi)
 	for (; c < ahi; c += 16)
 	{
 		uint32_t ci = (uint32_t)((c - p.a0) >> 4);
-		if (ci >= p.nch)
+		if (ci >= p.nch || (p.a0 & 15) != 0)  // a re-gathered deep window starts at a dword: not memory chunks
 			break;
 		lptr32 w = reinterpret_cast<lptr32>(p.s) + ci * 4;
 		uint4 v = make_uint4(w[0], w[1], w[2], w[3]);
@@ -1793,7 +1793,7 @@ __device__ __forceinline__ uint32_t edge_sum(const Pkt& p, uintptr_t lo, uintptr
 	const uintptr_t c = lo & ~(uintptr_t)15;
 	const uint32_t ci = (uint32_t)((c - p.a0) >> 4);
 	uint4 v;
-	if (ci < p.nch)
+	if (ci < p.nch && (p.a0 & 15) == 0)  // a re-gathered deep window starts at a dword: its chunks are not memory's
 	{
 		lptr32 w = reinterpret_cast<lptr32>(p.s) + ci * 4;
 		v = make_uint4(w[0], w[1], w[2], w[3]);
@@ -2134,7 +2134,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				l4_inputs(p, w, &fw, &ph);
 				if (tail)
 				{
-					if ((uint32_t)((f1 - p.a0) >> 4) < p.nch)
+					if ((p.a0 & 15) == 0 && (uint32_t)((f1 - p.a0) >> 4) < p.nch)
 					{
 						tsum = edge_sum(p, f1, ae);
 						tail_done = true;
@@ -2986,6 +2986,9 @@ constexpr int kParseChunks = 6;
 // 22% of the packets on the generic walk; gpurun_out r02l_ab_cfg5 -> profiles/r02_ab_parse_only.txt)
 constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 #define PCPPX_PARSE_ONLY_KERNEL parse_tile_kernel<1, 64, kParseOnlyChunks, true, false, false, kParseOnlyChunks1>
+// checksum launches with opts.window = PCPPX_WINDOW_DEEP: the parse-only instance's two-round 144-B window (tight second
+// round, dword-aligned re-gather) with the span stream; LDS 10 KiB, 4 waves/SIMD
+#define PCPPX_PARSE_DEEP_KERNEL parse_tile_kernel<4, kParseSWin, kParseOnlyChunks, true, false, true, kParseOnlyChunks1>
 
 // the flow-table shape: 1024-thread blocks, 8192 LDS slots, 4096-packet batches with the next batch prefetched,
 // 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)
@@ -3018,7 +3021,9 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 		return PCPPX_OK;
 	const Params prm = make_params(b, o, r, nullptr);
 	const dim3 grid((b->n + kTile - 1) / kTile);
-	if (o->want_checksums)
+	if (o->want_checksums && o->window == PCPPX_WINDOW_DEEP)
+		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else if (o->want_checksums)
 		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	else
 		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
@@ -3032,7 +3037,9 @@ int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records*
 		return PCPPX_OK;
 	const Params prm = make_params(b, o, r, info);
 	const dim3 grid((b->n + kTile - 1) / kTile);
-	if (o->want_checksums)
+	if (o->want_checksums && o->window == PCPPX_WINDOW_DEEP)
+		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else if (o->want_checksums)
 		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	else
 		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);

@@ -46,7 +46,8 @@ def test_gpu_golden(engine, path, kernel):
 def test_gpu_crafted_deep_stacks(engine, gaps, kernel):
     b = as_batch(crafted(), gaps=gaps, seed=11)
     for opts in (abi.make_opts(), abi.make_opts(4, 8, True, 16), abi.make_opts(0, 3, True, 5),
-                 abi.make_opts(0, 8, True, 0), abi.make_opts(0, 8, False, 16)):
+                 abi.make_opts(0, 8, True, 0), abi.make_opts(0, 8, False, 16),
+                 abi.make_opts(0, 8, True, 16, abi.WINDOW_DEEP), abi.make_opts(4, 8, True, 16, abi.WINDOW_DEEP)):
         g = run(engine, b, opts, kernel)
         o = oracle.oracle_parse(b, opts)
         oracle.compare_exact(g[0], g[1], o[0], o[1])
@@ -403,3 +404,34 @@ def test_gpu_flag_contract_parse_until(engine, path):
         gsum, glay = parse_on_device(engine, batch, opts)
         oracle.compare_engine_to_reference(gsum, glay, rsum, rlay)
         oracle.check_flag_contract(gsum, rsum, rlay)
+
+
+def test_gpu_deep_window_with_checksums(engine):
+    """opts.window = PCPPX_WINDOW_DEEP (the checksum launch with the two-round 144-B header window, the tight second
+    round and the dword-aligned re-gather of stacks past the window): records identical to the default window and
+    to the restatement, on config-5 deep stacks with checksums (packed, so the span stream runs, and gapped, so every
+    start alignment and the HBM edge-chunk path are hit) and on every golden set under its option variants."""
+    b = synth.config(5, 200_000)
+    deep = abi.make_opts(0, 8, True, 12, abi.WINDOW_DEEP)
+    d = parse_on_device(engine, b, deep)
+    dflt = parse_on_device(engine, b, abi.make_opts(0, 8, True, 12))
+    oracle.compare_exact(d[0], d[1], dflt[0], dflt[1])
+    has_l4 = d[0]["l4_layer"] != 0xFF  # IPv6 stacks ending in a Fragment extension carry a Payload, no L4 layer
+    assert has_l4.mean() > 0.9 and ((d[0]["flags"][has_l4] & abi.F_L4_CSUM) != 0).all()
+    idx = np.arange(0, b.n, 7)
+    sub = from_packets([b.packet(int(i)) for i in idx])
+    o = oracle.oracle_parse(sub, deep, threads=8)
+    oracle.compare_exact(d[0][idx], d[1][idx], o[0], o[1])
+    g = as_batch([b.packet(i) for i in range(30_000)], gaps=True, seed=5)
+    gd = parse_on_device(engine, g, deep)
+    og = oracle.oracle_parse(g, deep, threads=8)
+    oracle.compare_exact(gd[0], gd[1], og[0], og[1])
+    for path in golden_files():
+        batch, variants = load_golden(path)
+        for v, (opts, rsum, rlay) in variants.items():
+            if not opts.want_checksums:
+                continue
+            od = abi.make_opts(opts.parse_until_family, opts.parse_until_osi, True, opts.max_layers, abi.WINDOW_DEEP)
+            gs, gl = parse_on_device(engine, batch, od)
+            os_, ol = oracle.oracle_parse(batch, od)
+            oracle.compare_exact(gs, gl, os_, ol)
