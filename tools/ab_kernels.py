@@ -28,6 +28,7 @@ cases = {
     "tile/ml8/csum": (abi.make_opts(0, 8, True, 8), 0),
     "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
     "prev/ml8/csum": (abi.make_opts(0, 8, True, 8), -2),
+    "tile/deepwin": (abi.make_opts(0, 8, True, 8, abi.WINDOW_DEEP), 0),
     "tile/chaintails": (abi.make_opts(0, 8, True, 8), 12),
     "tile/ring": (abi.make_opts(0, 8, True, 8), 40),
     "tile/ring-win256": (abi.make_opts(0, 8, True, 8), 41),
