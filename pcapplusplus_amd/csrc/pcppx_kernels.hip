@@ -1898,11 +1898,12 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // TightR2: the second gather round reads only up to the deep stack's header extent (deep_extent) instead of the
 // whole window (false: tools/ab variant 50). Realign: a deep stack that ends past the window is re-gathered from a
 // dword-aligned start (mis <= 3 instead of <= 15) so that it fits (false: tools/ab variant 51).
+// LateGeneric: packets off the fast path are walked after the span stream ((4b)); tools/ab variant 53.
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
-          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true>
+          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -2097,7 +2098,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
 			}
 		}
-		else if (!SkipGeneric)
+		else if (!SkipGeneric && !LateGeneric)
 		{
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 			w = walk_chain(p, cap, prm, lay_out);
@@ -2266,6 +2267,26 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			if (as & 1)
 				r = (r * 256u) % 65535u;
 			l4c = l4_checksum(p, w, r, &l4s);
+			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
+		}
+	}
+
+	// ---- (4b) LateGeneric: the packets off the fast path are walked after the span stream (the LDS window is still
+	// intact), so the stream's registers and the generic walk's are never live together; their L4 sums come from the
+	// window and HBM (range_residue) instead of the stream's prefixes. Same records. ----
+	if (LateGeneric && live && !fast && !StreamOnly && !GatherOnly && !SkipGeneric)
+	{
+		uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
+		w = walk_chain(p, cap, prm, lay_out);
+		hashes(p, w, h5, h5d, h2);
+		if (want_csum && w.v4 >= 0)
+		{
+			ipc = ipv4_checksum(p, w, &ips);
+			w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+		}
+		if (want_csum && w.l4i >= 0)
+		{
+			l4c = l4_checksum(p, w, range_residue(p, w.l4o, w.l4o + w.l4dlen), &l4s);
 			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
 		}
 	}

@@ -29,6 +29,8 @@ cases = {
     "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
     "prev/ml8/csum": (abi.make_opts(0, 8, True, 8), -2),
     "tile/deepwin": (abi.make_opts(0, 8, True, 8, abi.WINDOW_DEEP), 0),
+    "tile/skip-generic": (abi.make_opts(0, 8, True, 8), 52),
+    "tile/late-generic": (abi.make_opts(0, 8, True, 8), 53),
     "tile/chaintails": (abi.make_opts(0, 8, True, 8), 12),
     "tile/ring": (abi.make_opts(0, 8, True, 8), 40),
     "tile/ring-win256": (abi.make_opts(0, 8, True, 8), 41),
