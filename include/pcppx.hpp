@@ -123,6 +123,7 @@ struct PacketParseOptions
 	OsiModelLayer parseUntilLayer = OsiModelLayerUnknown;
 	bool computeChecksums = true; /* IPv4 header + TCP/UDP checksum verification */
 	uint8_t maxLayers = PCPPX_MAX_LAYERS;
+	bool deepWindow = false; /* PCPPX_WINDOW_DEEP: two-round 144-B header window for checksum launches over deep stacks */
 
 	PacketParseOptions() = default;
 	PacketParseOptions(ProtocolTypeFamily until, OsiModelLayer layer = OsiModelLayerUnknown)
@@ -137,6 +138,7 @@ struct PacketParseOptions
 		o.parse_until_osi = parseUntilLayer;
 		o.want_checksums = computeChecksums ? 1 : 0;
 		o.max_layers = maxLayers;
+		o.window = deepWindow ? PCPPX_WINDOW_DEEP : PCPPX_WINDOW_DEFAULT;
 		return o;
 	}
 };
