@@ -435,3 +435,53 @@ def test_gpu_deep_window_with_checksums(engine):
             gs, gl = parse_on_device(engine, batch, od)
             os_, ol = oracle.oracle_parse(batch, od)
             oracle.compare_exact(gs, gl, os_, ol)
+
+
+def test_gpu_config4_full_size_flow_table(engine):
+    """BASELINE config 4 at its full per-GPU size through bench.py's own path: 12.5M IMIX packets with Zipf(1.1)
+    5-tuples over 1M flows (rank 0's shard), a parse writing the summary and the dense hash5 column, then three
+    pcppx_flow_count_keys_device calls into one 2M-slot table (three bench steps). Every flow's {packets, bytes}
+    equals three times a host group-by of the device keys, key 0 goes to the stats counters, nothing is lost; the
+    keys themselves equal the restatement's hash5Tuple on a 100k-packet sample."""
+    import torch
+
+    from pcapplusplus_amd import shard
+    from pcapplusplus_amd.engine import to_device
+
+    n = 12_500_000
+    b = synth.imix(n, shard.shard_seed(4, 0), flows=1_000_000, corrupt_frac=0.0)
+    dev = "cuda:0"
+    data, offs, caps = to_device(b, dev)
+    st = torch.cuda.current_stream().cuda_stream
+    summ = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    fk = torch.empty(n, dtype=torch.int32, device=dev)
+    opts = abi.make_opts(0, 8, False, 0)
+    engine.parse_device(data, offs, caps, n, b.linktype, opts, summ, None, st, fk)
+    cap = 1 << 21
+    keys = torch.zeros(cap, dtype=torch.int32, device=dev)
+    pk = torch.zeros(cap, dtype=torch.int64, device=dev)
+    by = torch.zeros(cap, dtype=torch.int64, device=dev)
+    stt = torch.zeros(4, dtype=torch.int64, device=dev)
+    for _ in range(3):
+        engine.flow_count_keys_device(fk, caps, n, keys, pk, by, cap, stt, st)
+    torch.cuda.synchronize()
+    k = keys.cpu().numpy().view(np.uint32)
+    used = k != 0
+    got = dict(zip(k[used].tolist(), zip(pk.cpu().numpy()[used].tolist(), by.cpu().numpy()[used].tolist())))
+    hk = fk.cpu().numpy().view(np.uint32)
+    del data, offs, caps, summ, fk, keys, pk, by
+    uk, inv = np.unique(hk, return_inverse=True)
+    cnt = np.bincount(inv)
+    byt = np.bincount(inv, weights=b.caplens.astype(np.float64)).astype(np.int64)
+    want = {int(x): (3 * int(c), 3 * int(y)) for x, c, y in zip(uk.tolist(), cnt.tolist(), byt.tolist()) if x != 0}
+    z = int(cnt[0]) if uk[0] == 0 else 0
+    zb = int(byt[0]) if uk[0] == 0 else 0
+    assert len(want) > 500_000
+    assert got == want
+    s = stt.cpu().numpy()
+    assert (int(s[0]), int(s[1]), int(s[2])) == (3 * z, 3 * zb, 0)
+    rng = np.random.default_rng(4)
+    idx = np.sort(rng.choice(n, size=100_000, replace=False))
+    sub = from_packets([b.packet(int(i)) for i in idx])
+    o = oracle.oracle_parse(sub, opts, threads=8)
+    assert np.array_equal(hk[idx], o[0]["hash5"])
