@@ -2031,14 +2031,16 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// first window does not show: this lane re-gathers its whole window from a dword-aligned start instead, so
 			// that the fast path still takes it
 			const bool past = ext != 0xFFFFu ? xc > (uint32_t)Chunks : (need > (uint32_t)Chunks && p.mis > 3);
-			const bool realign = Realign && more && past;
+			// the re-gathered window holds only 16-B pieces that lie wholly inside the packet: a piece starting at a
+			// dword could otherwise run past the end of the batch buffer (the packet's tail stays readable from HBM)
+			const uint32_t mis4 = (uint32_t)((uintptr_t)p.g & 3), whole4 = (mis4 + cap) >> 4;
+			const bool realign = Realign && more && past && whole4 >= (uint32_t)Chunks;
 			if (realign)
 			{
-				p.a0 = (uintptr_t)p.g & ~(uintptr_t)3;
-				p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+				p.a0 = (uintptr_t)p.g - mis4;
+				p.mis = mis4;
 				m_a0[lane] = p.a0;
-				const uint32_t need4 = (p.mis + cap + 15) >> 4;
-				full = need4 < (uint32_t)Chunks ? need4 : (uint32_t)Chunks;
+				full = (uint32_t)Chunks;
 				xc = (p.mis + ext + 15) >> 4;
 				from = 0;
 			}
