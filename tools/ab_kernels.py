@@ -66,6 +66,7 @@ cases.update({
     "po/prev": (abi.make_opts(0, 8, False, _ml), -2),
     "po/r2full": (abi.make_opts(0, 8, False, _ml), 50),
     "po/norealign": (abi.make_opts(0, 8, False, _ml), 51),
+    "po/c6w5": (abi.make_opts(0, 8, False, _ml), 45),  # the checksum instance's single 96-B window, 5 waves/SIMD
     "po/chaintails": (abi.make_opts(0, 8, False, _ml), 26),
     "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
     "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),
