@@ -422,6 +422,8 @@ def test_gpu_deep_window_with_checksums(engine):
     sub = from_packets([b.packet(int(i)) for i in idx])
     o = oracle.oracle_parse(sub, deep, threads=8)
     oracle.compare_exact(d[0][idx], d[1][idx], o[0], o[1])
+    h = engine.parse_host(b, deep)  # the host path's chunked launches pick the same instance
+    oracle.compare_exact(h[0], h[1], d[0], d[1])
     g = as_batch([b.packet(i) for i in range(30_000)], gaps=True, seed=5)
     gd = parse_on_device(engine, g, deep)
     og = oracle.oracle_parse(g, deep, threads=8)
