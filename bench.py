@@ -157,8 +157,57 @@ def cpu_baseline(batch, opts, sample: int, min_seconds: float) -> dict:
                       f"{' + IPv4/L4 checksums' if opts.want_checksums else ''}, {threads} threads = {core_note}"}
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(gpus: int, argv: list[str], port: int) -> list[str]:
+    """The child command that runs `bench.py <argv>` as `gpus` ranks, one process per GPU on this node
+    (the reference's one-worker-per-core launch, Pcap++/src/DpdkDeviceList.cpp:346-440)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def check_world(gpus: int, env) -> int | None:
+    """None when this process is a rank of a `gpus`-rank job (or a 1-GPU run); otherwise an exit code.
+    A rank whose WORLD_SIZE differs from --gpus would report a GPU count nobody asked for."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return None if gpus == 1 else 0  # 0: not a rank yet; the caller launches the ranks
+    if int(ws) != gpus:
+        print(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}: refusing to report a {ws}-rank run as {gpus} GPUs",
+              file=sys.stderr, flush=True)
+        return 2
+    return None
+
+
+def launch_ranks(gpus: int, argv: list[str]) -> int:
+    """Parent of an N-GPU run: starts the N ranks as a child torch.distributed.run and forwards their output
+    and exit code. This process never imports torch or touches the GPU (no exec after GPU initialisation)."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = launcher_cmd(gpus, argv, free_port())
+    print("bench.py: launching " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    assert proc.stdout is not None
+    for line in proc.stdout:  # rank 0's JSON line (and anything else the ranks print), as it arrives
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
 def main() -> None:
     args = parse_args()
+    rc = check_world(args.gpus, os.environ)
+    if rc is not None:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]) if rc == 0 else rc)
     import torch
     import torch.distributed as dist
 
@@ -170,6 +219,10 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.dist_backend == "gloo":
         local = local % torch.cuda.device_count()  # rehearsal: ranks share the card(s)
+    elif world > 1 and world > torch.cuda.device_count():
+        print(f"bench.py: {world} ranks over RCCL need {world} GPUs, this node has {torch.cuda.device_count()} "
+              f"(--dist-backend gloo rehearses more ranks than GPUs)", file=sys.stderr, flush=True)
+        sys.exit(2)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -245,10 +298,14 @@ def main() -> None:
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, mids)])) if mids else step_ms
     flow_ms = step_ms - kern_ms if mids else None
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+    tdev = dev if args.dist_backend == "nccl" else "cpu"
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=tdev)
+    per_rank = [t.clone() for _ in range(world)]
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max, kern_max = float(t[0]), float(t[1])
+        dist.all_gather(per_rank, t)  # after the timed region: each rank's wall and kernel time
+    per_rank = [[float(v) for v in x.cpu()] for x in per_rank]
+    wall_max = max(p[0] for p in per_rank)
+    kern_max = max(p[1] for p in per_rank)
     total_packets = n * world * args.steps
     mpps = total_packets / wall_max / 1e6
     wire = int(batch.caplens.sum(dtype=np.int64))
@@ -324,7 +381,12 @@ def main() -> None:
             flow_check = {"merged_flows": int(len(merged["keys"])), "ranks_merged": len(tables),
                           "per_rank_flows": [int(len(t["keys"])) for t in tables],
                           "packets_counted": counted, "expected": expected, "conserved": counted == expected,
+                          # exact: no packet fell to the no-free-slot count, i.e. the table is the reference's map
+                          "exact": merged["dropped"] == 0,
                           "table_full_drops": merged["dropped"], "flow_kernel_ms": round(flow_ms, 4)}
+            if merged["dropped"]:
+                print(f"bench.py: flow table lost {merged['dropped']} packets (no free slot): per-flow counters are "
+                      f"not the reference's", file=sys.stderr, flush=True)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -352,6 +414,10 @@ def main() -> None:
                 "window": args.window,
                 "max_layers": ml,
                 "parallelism": f"shard{world} (no collective)",
+                "ranks": world,
+                "dist_backend": args.dist_backend if world > 1 else None,
+                "per_rank_kernel_ms": [round(p[1], 4) for p in per_rank],
+                "per_rank_wall_ms_per_step": [round(p[0] * 1e3 / args.steps, 4) for p in per_rank],
                 "wire_GBps": round(wire * world * args.steps / wall_max / 1e9, 2),
                 "kernel_ms": round(kern_max, 4),
                 "step_kernel_ms": round(step_ms, 4),

@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <iomanip>
 #include <iostream>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -154,18 +155,29 @@ public:
 		const uint32_t hdr[6] = { 0xa1b2c3d4u, 2u | (4u << 16), 0, 0, 262144, m_LinkType };
 		return std::fwrite(hdr, 4, 6, m_F) == 6;
 	}
-	void writePacket(const pcppx::RawPacketVector& b, size_t i)
+	/* PcapFileWriterDevice::writePacket (Pcap++/src/PcapFileDevice.cpp:1026-1039): a file holds one link type, a
+	 * packet of another is refused (a pcapng input can switch link types between interfaces) */
+	bool writePacket(const pcppx::RawPacketVector& b, size_t i)
 	{
+		if (b.linkType != m_LinkType)
+		{
+			if (m_Dropped++ == 0)
+				std::cerr << "Cannot write a packet with a different link type\n";
+			return false;
+		}
 		const uint64_t ts = b.timestampsNs[i];
 		const uint32_t h[4] = { (uint32_t)(ts / 1000000000ull), (uint32_t)(ts % 1000000000ull / 1000ull), b.caplens[i],
 			                    b.caplens[i] };
 		std::fwrite(h, 4, 4, m_F);
 		std::fwrite(b.packetData(i), 1, b.caplens[i], m_F);
+		return true;
 	}
+	uint64_t droppedPackets() const { return m_Dropped; }
 
 private:
 	std::string m_Path;
 	uint32_t m_LinkType;
+	uint64_t m_Dropped = 0;
 	FILE* m_F = nullptr;
 };
 
@@ -391,10 +403,10 @@ int main(int argc, char* argv[])
 			std::cerr << "cannot open " << in << "\n";
 			return 1;
 		}
-		PcapFileWriterDevice* pcapWriter = nullptr;
+		std::unique_ptr<PcapFileWriterDevice> pcapWriter;
 		if (!out.empty())
 		{
-			pcapWriter = new PcapFileWriterDevice(out, reader.getLinkLayerType());
+			pcapWriter = std::make_unique<PcapFileWriterDevice>(out, reader.getLinkLayerType());
 			if (!pcapWriter->open())
 			{
 				std::cerr << "Couldn't open pcap writer device\n";
@@ -403,10 +415,13 @@ int main(int argc, char* argv[])
 		}
 		AppWorkerThread worker(engine, matchingEngine, burst);
 		if (deviceWorker)
-			worker.runOnDevice(reader, pcapWriter);
+			worker.runOnDevice(reader, pcapWriter.get());
 		else
-			worker.run(reader, pcapWriter);
-		delete pcapWriter;
+			worker.run(reader, pcapWriter.get());
+		if (pcapWriter && pcapWriter->droppedPackets())
+			std::cerr << pcapWriter->droppedPackets() << " matched packets not written: link type differs from the "
+			          << "output file's\n";
+		pcapWriter.reset();
 		printStats(worker.getStats(), deviceWorker ? "GPU worker" : "Worker");
 	}
 	catch (const pcppx::Error& e)

@@ -178,10 +178,12 @@ PCPPX_API int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, c
 
 /* Per-flow counters keyed by hash5Tuple (Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:99-125).
  * Device pointers: summary[n] from a previous parse, caplens[n]. The table is open-addressed with
- * `capacity` slots (power of two), split into min(capacity, 256) equal regions by the key's hash (a flow lives
- * in its region); keys[i]==0 marks an empty slot — flow key 0 (non-5-tuple packets, PacketUtils.cpp:141-148)
- * is counted in stats[0] (packets) / stats[1] (bytes) instead, and packets whose region had no free slot in
- * stats[2]. Counts accumulate across calls; calls on one context are ordered (they share its scratch). */
+ * `capacity` slots (power of two), split into min(256, max(1, capacity / 4096)) equal regions by the key's hash (a
+ * flow lives in its region; every region has at least 4096 slots, or is the whole table); keys[i]==0 marks an
+ * empty slot — flow key 0 (non-5-tuple packets, PacketUtils.cpp:141-148) is counted in stats[0] (packets) /
+ * stats[1] (bytes) instead, and packets whose region had no free slot in stats[2]. Counts accumulate across
+ * calls; calls on one context are ordered (they share its scratch). HBM scratch held by the context: record
+ * queues of 16 B x min(n, 2^24) x ~1.25 (grown in stream order, freed by pcppx_close). */
 /* The same over the dense key column a parse wrote (pcppx_records.flow_keys): keys_in[i] = hash5 of packet i. */
 PCPPX_API int pcppx_flow_count_keys_device(pcppx_ctx* ctx, const uint32_t* keys_in, const uint32_t* caplens, uint32_t n,
                                            uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity,

@@ -590,8 +590,14 @@ extern "C"
 			free_slot(s);
 		}
 		free_filter(c);
-		(void)hipFree(c->d_flow_queues);
-		(void)hipFree(c->d_flow_fill);
+		if (c->flow_pending)
+			(void)hipEventSynchronize(c->flow_done);
+		// the flow scratch is stream-ordered memory (hipMallocAsync): released on the context's stream
+		if (c->d_flow_queues)
+			(void)hipFreeAsync(c->d_flow_queues, c->stream);
+		if (c->d_flow_fill)
+			(void)hipFreeAsync(c->d_flow_fill, c->stream);
+		(void)hipStreamSynchronize(c->stream);
 		if (c->flow_done)
 			(void)hipEventDestroy(c->flow_done);
 		(void)hipStreamDestroy(c->stream);
@@ -781,28 +787,29 @@ int flow_count(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* keys_
 		hipStream_t st = static_cast<hipStream_t>(hip_stream);
 		const uint32_t parts = pcppx::flow_partitions(capacity);
 		const uint32_t rec_cap = pcppx::flow_queue_capacity(n, capacity);
+		if (c->flow_done == nullptr && !ok(hipEventCreateWithFlags(&c->flow_done, hipEventDisableTiming)))
+			return PCPPX_E_HIP;
+		// the context's previous flow work (possibly queued on another stream) owns the scratch until flow_done
+		if (c->flow_pending && !ok(hipStreamWaitEvent(st, c->flow_done, 0)))
+			return PCPPX_E_HIP;
 		if (c->flow_queue_recs < (uint64_t)parts * rec_cap)
 		{
-			// the previous scratch may still be in use by work queued on another stream
-			if (!ok(hipDeviceSynchronize()))
+			// grow in stream order: the old queues are released behind that wait, on this stream; nothing else on
+			// the device is stalled
+			if (c->d_flow_queues != nullptr && !ok(hipFreeAsync(c->d_flow_queues, st)))
 				return PCPPX_E_HIP;
-			(void)hipFree(c->d_flow_queues);
 			c->d_flow_queues = nullptr;
 			c->flow_queue_recs = 0;
-			if (!ok(hipMalloc(&c->d_flow_queues, (size_t)parts * rec_cap * 16)))
+			if (!ok(hipMallocAsync(&c->d_flow_queues, (size_t)parts * rec_cap * 16, st)))
 				return PCPPX_E_NOMEM;
 			c->flow_queue_recs = (uint64_t)parts * rec_cap;
 		}
 		if (c->d_flow_fill == nullptr)
 		{
-			if (!ok(hipMalloc(reinterpret_cast<void**>(&c->d_flow_fill), 1024 * sizeof(uint32_t))) ||
+			if (!ok(hipMallocAsync(reinterpret_cast<void**>(&c->d_flow_fill), 1024 * sizeof(uint32_t), st)) ||
 			    !ok(hipMemsetAsync(c->d_flow_fill, 0, 1024 * sizeof(uint32_t), st)))
 				return PCPPX_E_NOMEM;
 		}
-		if (c->flow_done == nullptr && !ok(hipEventCreateWithFlags(&c->flow_done, hipEventDisableTiming)))
-			return PCPPX_E_HIP;
-		if (c->flow_pending && !ok(hipStreamWaitEvent(st, c->flow_done, 0)))
-			return PCPPX_E_HIP;
 		const int rc = pcppx::launch_flow_count_part(summary, keys_in, caplens, n, keys, packets, bytes, capacity, stats,
 		                                             c->d_flow_queues, rec_cap, c->d_flow_fill, st);
 		if (rc != PCPPX_OK)

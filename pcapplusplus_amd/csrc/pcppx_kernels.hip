@@ -1915,6 +1915,11 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	constexpr uint32_t kRowMl = (uint32_t)kTSlotDw / 2 - 1 < kRowMaxMl ? (uint32_t)kTSlotDw / 2 - 1 : kRowMaxMl;
 	static_assert(kTile * (kRowMl + 1) * 2 <= kTile * kTSlotDw, "stage too small for layer rows");
 	static_assert(Chunks1 <= Chunks && Chunks < 256, "gather rounds");
+#ifndef PCPPX_TOOLS_AB
+	// the diagnostic switches write wrong or marked records: only tools/ab/libpcppx_ab.so (built with PCPPX_TOOLS_AB)
+	// may instantiate them, never libpcppx.so
+	static_assert(!MarkFast && !GatherOnly && !SkipGeneric && !StreamOnly, "tools-only parse_tile_kernel switch");
+#endif
 	const bool want_csum = Csum && prm.want_csum;  // uniform
 
 	const uint32_t lane = threadIdx.x;
@@ -3023,6 +3028,7 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 4096, kFlowBlocks = 256;
 constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed LDS/HBM counters hold
 constexpr uint32_t kFlowPartLog2 = 8;            // flow-table partitions (merge blocks); at most kFlowMaxParts
+constexpr uint32_t kFlowMinRegionLog2 = 12;      // slots per partition at least (capacity 2^20+ -> 256 partitions)
 constexpr uint32_t kFlowMergeThreads = 1024;
 
 }  // namespace
@@ -3102,17 +3108,33 @@ int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, con
 	return check_launch("filter_apply_kernel", stream);
 }
 
-uint32_t flow_partitions(uint32_t capacity)
+// log2 of the partitions: every region keeps at least 2^kFlowMinRegionLog2 slots, so a flow is only lost when its
+// region is full, not while a small table still has free slots elsewhere (a single region = the plain
+// open-addressed table)
+uint32_t flow_partitions_log2(uint32_t capacity)
 {
 	const uint32_t l = log2u(capacity);
-	return 1u << (l < kFlowPartLog2 ? l : kFlowPartLog2);
+	const uint32_t lp = l > kFlowMinRegionLog2 ? l - kFlowMinRegionLog2 : 0u;
+	return lp < kFlowPartLog2 ? lp : kFlowPartLog2;
 }
 
+uint32_t flow_partitions(uint32_t capacity)
+{
+	return 1u << flow_partitions_log2(capacity);
+}
+
+// Records per partition queue. A launch queues at most one record per packet in total (a record carries at least
+// one packet no earlier record carried), so one partition needs `per` and P partitions need per/P each for keys
+// spread evenly by the hash, plus a quarter and a constant for the spread; a full queue falls back to atomics on
+// the region (correct, slower).
 uint32_t flow_queue_capacity(uint32_t n, uint32_t capacity)
 {
 	const uint32_t per = kPackedMax < n ? kPackedMax : n;
 	const uint32_t parts = flow_partitions(capacity);
-	return 2 * ((per + parts - 1) / parts) + 4096;
+	if (parts == 1)
+		return per;
+	const uint32_t even = (per + parts - 1) / parts;
+	return even + even / 4 + 4096;
 }
 
 int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* dkeys, const uint32_t* caplens, uint32_t n,
@@ -3122,7 +3144,7 @@ int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* dkeys, cons
 	auto* pk = reinterpret_cast<unsigned long long*>(packets);
 	auto* by = reinterpret_cast<unsigned long long*>(bytes);
 	auto* st = reinterpret_cast<unsigned long long*>(stats);
-	const uint32_t l = log2u(capacity), lp = l < kFlowPartLog2 ? l : kFlowPartLog2;
+	const uint32_t l = log2u(capacity), lp = flow_partitions_log2(capacity);
 	const FlowPart fp{ static_cast<uint4*>(queues), rec_cap, fill, lp, l - lp };
 	for (uint32_t done = 0; done < n;)
 	{

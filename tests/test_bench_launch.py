@@ -1,0 +1,77 @@
+"""bench.py's own N-GPU launch (no external launcher), on CPU.
+
+`python bench.py --gpus N` must run N ranks itself — a child `torch.distributed.run` started before anything
+touches the GPU — and a rank must refuse to run when WORLD_SIZE differs from --gpus, so a line's n_gpus is
+always the GPU count that was asked for. Mirrors the reference's self-contained one-worker-per-core launch
+(Pcap++/src/DpdkDeviceList.cpp:346-440, Examples/DpdkExample-FilterTraffic/main.cpp:279-287).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+
+def test_launcher_command_line():
+    argv = ["--gpus", "8", "--config", "4", "--steps", "3"]
+    cmd = bench.launcher_cmd(8, argv, 29555)
+    assert cmd[0] == sys.executable
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    i = cmd.index(str((ROOT / "bench.py").resolve()))
+    assert cmd[i + 1:] == argv  # the ranks get the same arguments
+
+
+def test_check_world():
+    assert bench.check_world(1, {}) is None                      # plain 1-GPU run
+    assert bench.check_world(4, {}) == 0                         # parent: launch 4 ranks
+    assert bench.check_world(4, {"WORLD_SIZE": "4"}) is None     # a rank of the 4-rank job
+    assert bench.check_world(1, {"WORLD_SIZE": "1"}) is None
+    assert bench.check_world(8, {"WORLD_SIZE": "2"}) == 2        # mismatch
+    assert bench.check_world(1, {"WORLD_SIZE": "8"}) == 2
+
+
+def test_world_mismatch_exits_nonzero_before_gpu():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2" in r.stderr and r.stdout == ""
+
+
+def test_parent_forwards_rank_output_and_exit_code(tmp_path):
+    """launch_ranks streams the child's stdout and returns its exit code (child stubbed by a tiny script)."""
+    fake = tmp_path / "fake_rank.py"
+    fake.write_text("import sys\nprint('{\"n_gpus\": 2}')\nsys.exit(3)\n")
+    r = subprocess.run([sys.executable, "-c",
+                        "import sys; sys.path.insert(0, %r); import bench; "
+                        "bench.launcher_cmd = lambda g, a, p: [sys.executable, %r]; "
+                        "sys.exit(bench.launch_ranks(2, []))" % (str(ROOT), str(fake))],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3
+    assert r.stdout.strip() == '{"n_gpus": 2}'
+
+
+def test_real_launcher_starts_n_ranks(tmp_path):
+    """The exact torch.distributed.run command line bench.py builds starts N ranks with WORLD_SIZE = N (a stub rank
+    script in place of bench.py; gloo rendezvous over 127.0.0.1, no GPU)."""
+    stub = tmp_path / "rank.py"
+    stub.write_text("import os, sys\n"
+                    "import torch.distributed as dist\n"
+                    "dist.init_process_group('gloo')\n"
+                    "ws = dist.get_world_size()\n"
+                    "dist.barrier()\n"
+                    "if dist.get_rank() == 0:\n"
+                    "    print('ranks', ws, os.environ['WORLD_SIZE'], ' '.join(sys.argv[1:]), flush=True)\n"
+                    "dist.destroy_process_group()\n")
+    cmd = bench.launcher_cmd(2, ["--config", "4"], bench.free_port())
+    cmd[cmd.index(str((ROOT / "bench.py").resolve()))] = str(stub)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "ranks 2 2 --config 4" in r.stdout
