@@ -57,6 +57,13 @@ def parse_args():
     ap.add_argument("--no-traffic", action="store_true", help="do not report PMC traffic (the PMC passes themselves)")
     ap.add_argument("--window", choices=("default", "deep"), default="default",
                     help="checksum launches' header window (pcppx_opts.window): deep = two-round 144 B for deep stacks")
+    ap.add_argument("--layout", choices=("auto", "fixed", "packed"), default="auto",
+                    help="layer-record layout (pcppx_opts.layout): fixed = max_layers entries per packet; packed = only the "
+                         "chain's entries, dense per 64-packet tile (the same entries; auto: " + ", ".join(
+                             f"config {c} {v}" for c, v in sorted(CONFIG_LAYOUT.items())) + ")")
+    ap.add_argument("--records", choices=("auto", "summary", "tuples"), default="auto",
+                    help="per-packet record: the 32-B summary, or the 48-B 5-tuple extract (pcppx_tuple) alone "
+                         "(auto: tuples for config 2's 5-tuple extract, else summary)")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: a multi-rank rehearsal on fewer GPUs than ranks (ranks share cards round-robin); "
                          "the timed numbers of such a run are not a scaling measurement")
@@ -65,6 +72,7 @@ def parse_args():
 
 CONFIG_PACKETS = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000_000}
 CONFIG_MAX_LAYERS = {2: 0, 3: 8, 4: 0, 5: 12}
+CONFIG_LAYOUT = {3: "packed", 5: "packed"}  # configs with layer records
 KERNEL_SRC = ROOT / "pcapplusplus_amd" / "csrc" / "pcppx_kernels.hip"
 
 
@@ -75,7 +83,8 @@ def kernel_sha() -> str:
     return hashlib.sha256(KERNEL_SRC.read_bytes()).hexdigest()[:16]
 
 
-def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool) -> tuple[int | None, str]:
+def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool, layout: str = "fixed",
+                 records: str = "summary") -> tuple[int | None, str]:
     """(HBM bytes per parse launch, note) from a PMC traffic file, only if it matches this run exactly."""
     if not path.exists():
         return None, f"no PMC measurement ({path.name})"
@@ -83,8 +92,9 @@ def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool) -> tuple[int
         tj = json.loads(path.read_text())
     except (ValueError, OSError) as e:
         return None, f"unreadable {path.name}: {e}"
-    want = {"config": cfg, "packets": n, "max_layers": ml, "checksums": csum, "kernel_sha": kernel_sha()}
-    got = {k: tj.get(k) for k in want}
+    want = {"config": cfg, "packets": n, "max_layers": ml, "checksums": csum, "layout": layout, "records": records,
+            "kernel_sha": kernel_sha()}
+    got = {k: tj.get(k, {"layout": "fixed", "records": "summary"}.get(k)) for k in want}
     if got != want:
         return None, f"stale {path.name}: measured {got}, this run {want}"
     return int(tj["hbm_bytes_per_launch"]), f"{path.name} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
@@ -107,11 +117,11 @@ def cpu_cores() -> tuple[int, str]:
         return quota, f"{quota} of {aff} affinity cores (cgroup cpu.max quota)"
     return aff, f"all {aff} cores of the affinity mask"
 WORKLOADS = {
-    2: "config 2: 64 B Eth/IPv4/{TCP,UDP} 50/50; parse + hash5Tuple/hash2Tuple (5-tuple extract)",
+    2: "config 2: 64 B Eth/IPv4/{TCP,UDP} 50/50; parse + hash5Tuple, 5-tuple extract",
     3: "config 3: IMIX 64/512/1500 B 7:4:1, 25% VLAN, 70/30 IPv4/IPv6, TCP/UDP 50/50, 1% bad checksums; "
        "parse + hashes + IPv4/L4 checksum verify",
     4: "config 4: IMIX as config 3 with 5-tuples Zipf(1.1) over 1M flows, both directions; parse + hash5Tuple + "
-       "per-flow {packets, bytes} counters (FilterTraffic flow table)",
+       "per-flow {packets, bytes} counters (FilterTraffic flow table) + collectStats protocol histogram",
     5: "config 5: deep encapsulation (QinQ, 1-3 MPLS labels, GREv0 C/K/S over IPv4|IPv6, IPv6 1-3 extension "
        "headers) then TCP/UDP, 64/512/1500 B; parse + hashes",
 }
@@ -249,26 +259,36 @@ def main() -> None:
         batch = synth.small64(npk, seed)
     gen_s = time.time() - t0
     want_csum = args.checksums == "on" or (args.checksums == "auto" and cfg == 3)
-    opts = abi.make_opts(0, 8, want_csum, ml, abi.WINDOW_DEEP if args.window == "deep" else abi.WINDOW_DEFAULT)
+    layout = args.layout if args.layout != "auto" else CONFIG_LAYOUT.get(cfg, "fixed")
+    rec_kind = args.records if args.records != "auto" else ("tuples" if cfg == 2 else "summary")
+    if rec_kind == "tuples" and ml:
+        sys.exit("bench.py: --records tuples writes no layer records (use --max-layers 0)")
+    opts = abi.make_opts(0, 8, want_csum, ml, abi.WINDOW_DEEP if args.window == "deep" else abi.WINDOW_DEFAULT,
+                         abi.LAYOUT_PACKED if layout == "packed" else abi.LAYOUT_FIXED)
     n = batch.n
     eng = Engine(local)
     data, offsets, caplens = to_device(batch, dev)
-    summary = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    summary = torch.empty(n * 32, dtype=torch.uint8, device=dev) if rec_kind == "summary" else None
+    tuples = torch.empty(n * 48, dtype=torch.uint8, device=dev) if rec_kind == "tuples" else None
     layers = torch.empty(max(n * ml, 1) * 8, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     flows = None
     flow_keys = None
+    proto_stats = None
     if cfg == 4:  # per-GPU flow table: 2M slots for 1M flows, counters accumulate over all steps
         cap = 1 << 21
         flows = (torch.zeros(cap, dtype=torch.int32, device=dev), torch.zeros(cap, dtype=torch.int64, device=dev),
                  torch.zeros(cap, dtype=torch.int64, device=dev), torch.zeros(4, dtype=torch.int64, device=dev), cap)
-        # the parse also writes the dense hash5 column the flow table is keyed by (pcppx_records.flow_keys)
+        # the parse also writes the dense hash5 column the flow table is keyed by (pcppx_records.flow_keys) and the
+        # collectStats protocol counters (pcppx_records.proto_stats, accumulated over every launch)
         flow_keys = torch.empty(n, dtype=torch.int32, device=dev)
+        proto_stats = torch.zeros(abi.PROTO_STATS, dtype=torch.int64, device=dev)
     mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if flows else None
 
     def step(k=None):
-        eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh, flow_keys)
+        eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh, flow_keys, tuples,
+                         proto_stats)
         if flows is not None:
             if k is not None:
                 mids[k].record(stream)
@@ -294,7 +314,7 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - w0
     step_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
-    # the parse kernel is the dominant kernel of every config; config 4 also runs the flow-table kernel
+    # the parse kernel is the dominant kernel of every config; config 4 also runs the flow-table kernels
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, mids)])) if mids else step_ms
     flow_ms = step_ms - kern_ms if mids else None
 
@@ -309,28 +329,44 @@ def main() -> None:
     total_packets = n * world * args.steps
     mpps = total_packets / wall_max / 1e6
     wire = int(batch.caplens.sum(dtype=np.int64))
-    if want_csum or ml >= 8:
-        read_bytes = algorithmic_read_bytes(batch, want_csum, summary, layers, caplens, ml)
-    else:
-        # the header extents come from the layer records: one untimed parse with full records
-        ext_sum = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-        ext_lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device=dev)
-        eng.parse_device(data, offsets, caplens, n, batch.linktype, abi.make_opts(0, 8, False, 16), ext_sum, ext_lay, sh)
-        torch.cuda.synchronize(dev)
-        read_bytes = algorithmic_read_bytes(batch, False, ext_sum, ext_lay, caplens, 16)
-        del ext_sum, ext_lay
-    write_bytes = n * (32 + 8 * ml + (4 if flow_keys is not None else 0))
+    # untimed reference parse with full FIXED records: the header extents (parse-only byte model), the chain lengths
+    # (packed write bytes) and the flag check
+    ext_sum = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    ext_lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device=dev)
+    eng.parse_device(data, offsets, caplens, n, batch.linktype, abi.make_opts(0, 8, want_csum, 16), ext_sum, ext_lay, sh)
+    torch.cuda.synchronize(dev)
+    read_bytes = algorithmic_read_bytes(batch, want_csum, ext_sum, ext_lay, caplens, 16)
+    nl16 = ext_sum.view(n, 32)[:, 14].to(torch.int64)
+    chain_entries = int(torch.clamp(nl16, max=ml).sum().item()) if ml else 0
+    del ext_lay
+    per_pkt = (32 if summary is not None else 0) + (48 if tuples is not None else 0) + \
+        (4 if flow_keys is not None else 0)
+    write_bytes = n * per_pkt + 8 * (chain_entries if layout == "packed" else n * ml)
     achieved = read_bytes / (kern_ms * 1e-3) / 1e9
 
-    # sanity: the records of the last step parse every packet cleanly (synthetic data has no L7 triggers)
-    s = summary.view(torch.int32).view(n, 8)
+    # sanity: every packet parses cleanly (synthetic data has no L7 triggers)
+    s = ext_sum.view(torch.int32).view(n, 8)
     flags = (s[:, 3] & 0xFFFF)
     flagged = int(((flags & abi.F_NEEDS_HOST) != 0).sum().item())
+    if tuples is not None:  # the timed output itself: every packet carries its 5-tuple, hash5 as the summary's
+        tv = tuples.view(torch.int32).view(n, 12)
+        tuple_check = {"with_5tuple": int(((tv[:, 9] >> 24) & 0xFF).eq(1).sum().item()),
+                       "hash5_equal_summary": bool(torch.equal(tv[:, 10], s[:, 0]))}
+    else:
+        tuple_check = None
+    stats_line = None
+    if proto_stats is not None:  # collectStats over every launch (warmup + timed): the histogram of one pass
+        launches = args.warmup + args.steps
+        tot = proto_stats.cpu().numpy()
+        stats_line = {f: int(tot[k]) // launches for k, f in enumerate(abi.PROTO_STATS_FIELDS)}
+        stats_line["launches"] = launches
+        stats_line["consistent"] = bool((tot % launches == 0).all() and stats_line["packet_count"] == n)
+    del ext_sum
 
     traffic, traffic_note = None, "not requested"
     if not args.no_traffic:
         tp = Path(args.traffic) if args.traffic else ROOT / "profiles" / f"traffic_cfg{cfg}.json"
-        traffic, traffic_note = load_traffic(tp, cfg, n, ml, want_csum)
+        traffic, traffic_note = load_traffic(tp, cfg, n, ml, want_csum, layout, rec_kind)
 
     e2e = None
     if not args.no_e2e and rank == 0 and world == 1:
@@ -413,6 +449,8 @@ def main() -> None:
                 "checksums": want_csum,
                 "window": args.window,
                 "max_layers": ml,
+                "layout": layout,
+                "records": rec_kind,
                 "parallelism": f"shard{world} (no collective)",
                 "ranks": world,
                 "dist_backend": args.dist_backend if world > 1 else None,
@@ -441,6 +479,10 @@ def main() -> None:
             line["e2e_host_to_host"] = e2e
         if flow_check is not None:
             line["config"]["flow_table"] = flow_check
+        if stats_line is not None:
+            line["config"]["collect_stats"] = stats_line
+        if tuple_check is not None:
+            line["config"]["tuples"] = tuple_check
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

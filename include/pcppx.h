@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PCPPX_ABI_VERSION 4
+#define PCPPX_ABI_VERSION 5
 /* the library is built with hidden visibility: exactly the functions declared here are exported */
 #define PCPPX_API __attribute__((visibility("default")))
 #define PCPPX_MAX_LAYERS 16     /* fixed depth cap; deeper chains set PCPPX_F_DEPTH_OVERFLOW */
@@ -126,21 +126,75 @@ typedef struct pcppx_opts {
 	uint8_t max_layers;          /* 0 = do not write layers; else layers stride per packet (1..16) */
 	uint8_t window;              /* PCPPX_WINDOW_*: the header window of checksum launches (records are identical
 	                                either way; parse-only launches always gather a two-round deep window) */
+	uint8_t layout;              /* PCPPX_LAYOUT_*: how pcppx_records.layers is laid out */
+	uint8_t reserved[3];
 } pcppx_opts;
 #define PCPPX_WINDOW_DEFAULT 0 /* 96-B header window, 5 waves/SIMD: the fastest for Eth / VLAN / IP / L4 traffic */
 #define PCPPX_WINDOW_DEEP 1    /* + a second gather round up to 144 B for stacks deeper than the first window
                                   (QinQ, MPLS, GRE, IPv6 extensions): those packets stay on the fast path instead of
                                   the generic walk; 4 waves/SIMD */
 
+/* pcppx_records.layers layouts (pcppx_opts.layout). Both hold the same pcppx_layer entries, bit for bit:
+ *   FIXED:  packet i's layer k is layers[i * max_layers + k], k < min(n_layers, max_layers); entries past
+ *           n_layers are unspecified.
+ *   PACKED: only the chain's entries are written, densely per 64-packet tile: the entries of tile t (packets
+ *           64t .. 64t+63) start at layers[64 * t * max_layers], and packet i's entries follow those of the packets
+ *           before it in its tile: layers[64 * t * max_layers + sum_{64t <= j < i} min(n_layers_j, max_layers) + k].
+ *           The buffer is sized as for FIXED (n * max_layers entries); the summary is required (its n_layers
+ *           decode the positions: pcppx_unpack_layers, include/pcppx.hpp). The write traffic is the chain, not
+ *           max_layers rows per packet. max_layers <= PCPPX_PACKED_MAX_LAYERS. Device path only. */
+#define PCPPX_LAYOUT_FIXED 0
+#define PCPPX_LAYOUT_PACKED 1
+#define PCPPX_PACKED_MAX_LAYERS 12
+
+/* The 5-tuple extract (the compact record of the bandwidth runs), 48 bytes per packet: exactly the
+ * fields pcpp::hash5Tuple reads (Packet++/src/PacketUtils.cpp:139-210), from the same layers as the summary's
+ * hashes -- the first IPv4 layer, else the first IPv6 layer (getLayerOfType<IPv4Layer>() / <IPv6Layer>()), and
+ * the last TCP layer, else the last UDP layer (getLayerOfType<TcpLayer>(true) / <UdpLayer>(true)). */
+typedef struct pcppx_tuple {
+	uint8_t src_ip[16]; /* IPv4: getSrcIPv4Address() bytes in packet order, then 12 zero bytes; IPv6: ipSrc; none: 0 */
+	uint8_t dst_ip[16];
+	uint16_t src_port;  /* the port layer's getSrcPort() (host order); 0 without a TCP/UDP layer */
+	uint16_t dst_port;  /* getDstPort() */
+	uint8_t ip_version; /* 4 or 6: which layer the addresses come from; 0 = no IP layer */
+	uint8_t ip_proto;   /* that layer's protocol (IPv4) / nextHeader (IPv6) byte: hash5Tuple's last byte */
+	uint8_t l4_proto;   /* pcpp::TCP (4) / pcpp::UDP (5): the port layer; 0 = none */
+	uint8_t has_5tuple; /* 1 iff hash5Tuple hashes these fields: an IP layer, a TCP/UDP layer and no ICMP layer
+	                       (PacketUtils.cpp:141-148); 0: hash5 == 0 */
+	uint32_t hash5;     /* pcpp::hash5Tuple(&packet, false) (= pcppx_summary.hash5) */
+	uint16_t flags;     /* pcppx_summary.flags (PCPPX_F_NEEDS_HOST*: the fields of a flagged packet are those of the
+	                       chain prefix the device built) */
+	uint8_t n_layers;   /* pcppx_summary.n_layers */
+	uint8_t reserved;
+} pcppx_tuple;
+
+/* PacketStats::collectStats (Examples/DpdkExample-FilterTraffic/Common.h:83-104) over a parsed batch: word k of
+ * pcppx_records.proto_stats (device memory, PCPPX_PROTO_STATS words, accumulated by += across calls) counts */
+#define PCPPX_PS_PACKETS 0    /* packets of the batch */
+#define PCPPX_PS_ETH 1        /* isPacketOfType(Ethernet) */
+#define PCPPX_PS_ARP 2        /* isPacketOfType(ARP) */
+#define PCPPX_PS_IPV4 3       /* isPacketOfType(IPv4) */
+#define PCPPX_PS_IPV6 4       /* isPacketOfType(IPv6) */
+#define PCPPX_PS_TCP 5        /* isPacketOfType(TCP) */
+#define PCPPX_PS_UDP 6        /* isPacketOfType(UDP) */
+#define PCPPX_PS_HTTP 7       /* isPacketOfType(HTTP), over the packets the device settles (below) */
+#define PCPPX_PS_DNS 8        /* isPacketOfType(DNS), the same */
+#define PCPPX_PS_SSL 9        /* isPacketOfType(SSL) (collectStats' tlsCount), the same */
+#define PCPPX_PS_NEEDS_HOST 10 /* packets whose HTTP/DNS/SSL answer the host must complete: a chain stopped before an
+                                 out-of-scope layer (NEEDS_HOST_PROTO), a bad record, or an L7 payload the device could
+                                 not classify -- as pcppx_packet_stats.needs_host_count */
+#define PCPPX_PROTO_STATS 16  /* words (11-15 are zero) */
+
 /* Output arrays (same memory space as the batch for the _device call, host for the _host call). */
 typedef struct pcppx_records {
-	pcppx_summary* summary; /* n entries */
-	pcppx_layer* layers;    /* n * max_layers entries, or NULL when max_layers == 0; packet i's layer k is
-	                           layers[i * max_layers + k] for k < min(n_layers, max_layers); the entries past
-	                           n_layers are not written */
+	pcppx_summary* summary; /* n entries; may be NULL on the device path when tuples is set and layout is FIXED */
+	pcppx_layer* layers;    /* n * max_layers entries in pcppx_opts.layout, or NULL when max_layers == 0 */
 	uint32_t* flow_keys;    /* optional (NULL): n entries, flow_keys[i] = summary[i].hash5 -- the dense column
 	                           FilterTraffic's flow table is keyed by (pcppx_flow_count_keys_device reads 8 B per
 	                           packet from it and caplens instead of 36 B through the summary) */
+	pcppx_tuple* tuples;    /* optional (NULL): n 5-tuple extracts. Device path only */
+	uint64_t* proto_stats;  /* optional (NULL): PCPPX_PROTO_STATS counters, accumulated (collectStats). Device path
+	                           only; calls that set it on one context are ordered (they share its scratch) */
 } pcppx_records;
 
 /* The caller's own host parse of ONE packet — its Packet++ (`pcpp::Packet packet(&raw, parseUntil...)`) turned
@@ -172,7 +226,8 @@ PCPPX_API int pcppx_parse_batch_device(pcppx_ctx* ctx, const pcppx_batch* batch,
                              pcppx_records* out, void* hip_stream);
 
 /* Host-to-host parse: batch and records hold host pointers. The context stages the bytes through pinned
- * buffers in chunks, overlapping H2D copies, kernels and D2H copies; returns when out is filled. */
+ * buffers in chunks, overlapping H2D copies, kernels and D2H copies; returns when out is filled. The FIXED layout
+ * only; records.tuples and records.proto_stats must be NULL (device-path outputs). */
 PCPPX_API int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
                            pcppx_records* out);
 

@@ -455,6 +455,24 @@ public:
 	std::vector<pcppx_layer> layers;
 };
 
+/* PCPPX_LAYOUT_PACKED entries (include/pcppx.h) -> the FIXED layout: packet i's chain starts at its tile's base
+ * 64 * t * maxLayers plus the chains of the packets before it in the tile (summary n_layers, capped at maxLayers).
+ * fixed: n * maxLayers entries; entries past a chain are zeroed. */
+inline void unpackLayers(const pcppx_summary* summary, const pcppx_layer* packed, size_t n, uint32_t maxLayers,
+                         pcppx_layer* fixed)
+{
+	size_t pos = 0;
+	for (size_t i = 0; i < n; ++i)
+	{
+		if (i % 64 == 0)
+			pos = i * maxLayers;
+		const uint32_t cnt = summary[i].n_layers < maxLayers ? summary[i].n_layers : maxLayers;
+		for (uint32_t k = 0; k < maxLayers; ++k)
+			fixed[i * maxLayers + k] = k < cnt ? packed[pos + k] : pcppx_layer{};
+		pos += cnt;
+	}
+}
+
 /* PacketMatchingEngine's criteria (Examples/DpdkExample-FilterTraffic/PacketMatchingEngine.h:28-41) */
 struct MatchSpec
 {

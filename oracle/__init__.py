@@ -66,6 +66,8 @@ def ref_lib() -> C.CDLL:
         lib.pcppx_ref_filter.restype = C.c_int
         lib.pcppx_ref_reasm.argtypes = [C.POINTER(abi.Batch), C.c_void_p]
         lib.pcppx_ref_reasm.restype = C.c_int
+        lib.pcppx_ref_tuples.argtypes = [C.POINTER(abi.Batch), C.c_void_p]
+        lib.pcppx_ref_tuples.restype = C.c_int
         lib.ref_read_capture.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
         lib.ref_read_capture.restype = C.c_int
@@ -89,6 +91,63 @@ def oracle_parse(batch, opts: abi.Opts | None = None, threads: int = 1):
     if rc != 0:
         raise RuntimeError(f"oracle parse failed {rc}")
     return summary, layers[: batch.n * opts.max_layers].reshape(batch.n, opts.max_layers)
+
+
+def oracle_parse_tuples(batch, opts: abi.Opts | None = None, threads: int = 1):
+    """Restatement records plus the 5-tuple extracts: (summary[n], layers[n, max_layers], tuples[n])."""
+    opts = opts or abi.make_opts()
+    summary, layers, rec = _alloc(batch.n, opts)
+    tuples = np.zeros(max(batch.n, 1), dtype=abi.TUPLE_DTYPE)
+    rec.tuples = tuples.ctypes.data
+    b = batch.c_batch()
+    rc = oracle_lib().pcppx_oracle_parse_batch(C.byref(b), C.byref(opts), C.byref(rec), threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle parse failed {rc}")
+    return summary, layers[: batch.n * opts.max_layers].reshape(batch.n, opts.max_layers), tuples[: batch.n]
+
+
+def ref_tuples(batch):
+    """The 5-tuple extract through the real reference's accessors (oracle/ref_harness.cpp pcppx_ref_tuples) under
+    Packet(&raw): tuples[n] with flags 0 and the uncapped chain length in n_layers."""
+    out = np.zeros(max(batch.n, 1), dtype=abi.TUPLE_DTYPE)
+    b = batch.c_batch()
+    rc = ref_lib().pcppx_ref_tuples(C.byref(b), out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"reference tuples failed {rc}")
+    return out[: batch.n]
+
+
+def proto_stats(summary) -> dict:
+    """collectStats totals (PacketStats::collectStats, Common.h:83-104) of engine-format summaries, as the device's
+    pcppx_records.proto_stats counts them: the protocol counters from proto_mask for every packet; HTTP / DNS / SSL
+    over the settled packets (stats_settled); needs_host = the others."""
+    settled, l7 = stats_settled(None, summary, None)
+    m = summary["proto_mask"].astype(np.uint64)
+    bit = lambda p: int((((m >> np.uint64(p)) & np.uint64(1)) != 0).sum())  # noqa: E731
+    return {"packet_count": len(summary), "eth_count": bit(P_ETH), "arp_count": bit(P_ARP), "ipv4_count": bit(P_IPV4),
+            "ipv6_count": bit(P_IPV6), "tcp_count": bit(P_TCP), "udp_count": bit(P_UDP),
+            "http_count": int((settled & ((l7 & 1) != 0)).sum()), "dns_count": int((settled & ((l7 & 2) != 0)).sum()),
+            "tls_count": int((settled & ((l7 & 4) != 0)).sum()), "needs_host_count": int((~settled).sum())}
+
+
+def compare_tuples(eng, ref, eng_summary=None) -> dict:
+    """Engine 5-tuple extracts against the reference's (ref_tuples): every field of every unflagged packet (flags
+    aside; n_layers where the chain fits 16 layers). Flagged packets (PCPPX_F_NEEDS_HOST) are the host's."""
+    fl = eng["flags"] if eng_summary is None else eng_summary["flags"]
+    ok = (fl & abi.F_NEEDS_HOST) == 0
+    for f in ("src_ip", "dst_ip", "src_port", "dst_port", "ip_version", "ip_proto", "l4_proto", "has_5tuple", "hash5"):
+        a, b = eng[f], ref[f]
+        diff = (a != b).reshape(len(a), -1).any(axis=1)
+        bad = np.nonzero(ok & diff)[0]
+        if len(bad):
+            i = int(bad[0])
+            raise AssertionError(f"tuple.{f} differs on {len(bad)} unflagged packets; first #{i}: {eng[i]} vs {ref[i]}")
+    deep = ref["n_layers"] <= abi.MAX_LAYERS
+    bad = np.nonzero(ok & deep & (eng["n_layers"] != ref["n_layers"]))[0]
+    if len(bad):
+        i = int(bad[0])
+        raise AssertionError(f"tuple.n_layers differs on {len(bad)} packets; first #{i}: {eng[i]} vs {ref[i]}")
+    return {"n": len(eng), "exact": int(ok.sum()), "with_5tuple": int((ok & (eng["has_5tuple"] != 0)).sum())}
 
 
 def ref_read_capture(path) -> dict | None:

@@ -786,14 +786,58 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 	return L;
 }
 
+/* the 5-tuple extract (include/pcppx.h pcppx_tuple): the fields hash5Tuple reads, PacketUtils.cpp:139-210 -- the first
+ * IPv4 layer (getLayerOfType<IPv4Layer>()), else the first IPv6 layer: ipSrc / ipDst and protocol / nextHeader
+ * (:177-201); the last TCP layer, else the last UDP layer (getLayerOfType<TcpLayer>(true) / <UdpLayer>(true),
+ * :157-169): getSrcPort / getDstPort (TcpLayer.cpp:54-62, UdpLayer.cpp:37-45: be16toh of the header fields); 5-tuple
+ * iff an IP layer, a port layer and no ICMP layer (:141-148) */
+static void fill_tuple(const uint8_t* pkt, const pcppx_summary* sum, int have_ipv4, const lay* ip4, int have_ipv6,
+                       const lay* ip6, int l4_idx, int l4_is_tcp, const lay* l4, pcppx_tuple* t)
+{
+	memset(t, 0, sizeof(*t));
+	if (have_ipv4) {
+		const uint8_t* ip = pkt + ip4->off;
+		memcpy(t->src_ip, ip + 12, 4);
+		memcpy(t->dst_ip, ip + 16, 4);
+		t->ip_version = 4;
+		t->ip_proto = ip[9];
+	} else if (have_ipv6) {
+		const uint8_t* ip = pkt + ip6->off;
+		memcpy(t->src_ip, ip + 8, 16);
+		memcpy(t->dst_ip, ip + 24, 16);
+		t->ip_version = 6;
+		t->ip_proto = ip[6];
+	}
+	if (l4_idx >= 0) {
+		const uint8_t* lp = pkt + l4->off;
+		t->src_port = be16(lp);
+		t->dst_port = be16(lp + 2);
+		t->l4_proto = l4_is_tcp ? P_TCP : P_UDP;
+	}
+	t->has_5tuple = (have_ipv4 || have_ipv6) && l4_idx >= 0 && !(sum->proto_mask & ((uint64_t)1 << P_ICMP));
+	t->hash5 = sum->hash5;
+	t->flags = sum->flags;
+	t->n_layers = sum->n_layers;
+}
+
+static void parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t linktype, const pcppx_opts* opts,
+                         pcppx_summary* sum, pcppx_layer* layers, pcppx_tuple* tup);
+
 void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t linktype, const pcppx_opts* opts,
                                pcppx_summary* sum, pcppx_layer* layers)
 {
+	parse_packet(pkt, caplen, linktype, opts, sum, layers, NULL);
+}
+
+static void parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t linktype, const pcppx_opts* opts,
+                         pcppx_summary* sum, pcppx_layer* layers, pcppx_tuple* tup)
+{
+	if (tup) memset(tup, 0, sizeof(*tup));
 	memset(sum, 0, sizeof(*sum));
 	sum->l4_layer = 0xFF;
 	int cap = opts->max_layers ? opts->max_layers : PCPPX_MAX_LAYERS;
 	uint16_t flags = 0;
-	if (caplen > PCPPX_MAX_CAPLEN) { sum->flags = PCPPX_F_OVERSIZE; return; }
+	if (caplen > PCPPX_MAX_CAPLEN) { sum->flags = PCPPX_F_OVERSIZE; if (tup) tup->flags = PCPPX_F_OVERSIZE; return; }
 	if (caplen == 0) return; /* createFirstLayer returns nullptr, Packet.cpp:829-831 */
 
 	/* first layer: Packet::createFirstLayer, Packet++/src/Packet.cpp:827-923 */
@@ -813,6 +857,7 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 	case 0: k = caplen >= 4 ? K_NULL : K_PAYLOAD; break;           /* NullLoopbackLayer::isDataValid, NullLoopbackLayer.h:86-89 */
 	case 239: case 104: /* NFLOG, C_HDLC: host dissectors */
 		sum->flags = PCPPX_F_NEEDS_HOST_PROTO;
+		if (tup) tup->flags = PCPPX_F_NEEDS_HOST_PROTO;
 		return;
 	default: k = K_PAYLOAD; break;
 	}
@@ -1009,6 +1054,8 @@ void pcppx_oracle_parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t lin
 		}
 	}
 	sum->flags = flags;
+	if (tup)
+		fill_tuple(pkt, sum, have_ipv4, &chain_first_ipv4, have_ipv6, &chain_first_ipv6, l4_idx, l4_is_tcp, &l4, tup);
 }
 
 /* ---- reassembly front ends, from a packet's engine-format records ---- */
@@ -1135,13 +1182,15 @@ static void* run_job(void* arg)
 		pcppx_summary* sp = j->r ? &j->r->summary[i] : &s;
 		pcppx_layer scratch[PCPPX_MAX_LAYERS];
 		pcppx_layer* lp = (j->r && j->r->layers && ml) ? j->r->layers + (size_t)i * ml : (ml ? scratch : NULL);
+		pcppx_tuple* tp = (j->r && j->r->tuples) ? &j->r->tuples[i] : NULL;
 		if (j->b->offsets[i] + j->b->caplens[i] > j->b->data_len) {
 			memset(sp, 0, sizeof(*sp));
 			sp->l4_layer = 0xFF;
 			sp->flags = PCPPX_F_BAD_DESC;
+			if (tp) { memset(tp, 0, sizeof(*tp)); tp->flags = PCPPX_F_BAD_DESC; }
 			continue;
 		}
-		pcppx_oracle_parse_packet(j->b->data + j->b->offsets[i], j->b->caplens[i], j->b->linktype, j->o, sp, lp);
+		parse_packet(j->b->data + j->b->offsets[i], j->b->caplens[i], j->b->linktype, j->o, sp, lp, tp);
 		acc += sp->hash5 + sp->hash5_dir + sp->hash2 + sp->l4_csum_calc + sp->ip_csum_calc + sp->n_layers;
 	}
 	j->acc = acc;

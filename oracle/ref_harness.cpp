@@ -306,6 +306,63 @@ extern "C"
 		return PCPPX_OK;
 	}
 
+	// The 5-tuple extract (include/pcppx.h pcppx_tuple) through the reference's own accessors, for every packet of a
+	// host batch parsed as Packet(&raw): the first IPv4 layer (getLayerOfType<IPv4Layer>()) else the first IPv6
+	// layer, their getSrc/DstIPv4Address / getSrc/DstIPv6Address and protocol / nextHeader; the port layer
+	// hash5Tuple takes (getLayerOfType<TcpLayer>(true), else <UdpLayer>(true), PacketUtils.cpp:157-169) and its
+	// getSrcPort / getDstPort; has_5tuple = isPacketOfType(IPv4|IPv6) && !ICMP && (TCP|UDP) (PacketUtils.cpp:141-148);
+	// hash5 = hash5Tuple(&packet). flags is left 0 (the engine's own), n_layers = the chain length.
+	int pcppx_ref_tuples(const pcppx_batch* b, pcppx_tuple* out)
+	{
+		if (b == nullptr || out == nullptr)
+			return PCPPX_E_INVAL;
+		pcpp::Logger::getInstance().suppressLogs();
+		Prepared p;
+		prepare(b, p);
+		for (uint32_t i = 0; i < b->n; ++i)
+		{
+			pcppx_tuple& t = out[i];
+			std::memset(&t, 0, sizeof(t));
+			pcpp::Packet packet(&p.raws[i]);
+			if (auto* v4 = packet.getLayerOfType<pcpp::IPv4Layer>())
+			{
+				const uint32_t s4 = v4->getSrcIPv4Address().toInt(), d4 = v4->getDstIPv4Address().toInt();
+				std::memcpy(t.src_ip, &s4, 4);
+				std::memcpy(t.dst_ip, &d4, 4);
+				t.ip_version = 4;
+				t.ip_proto = v4->getIPv4Header()->protocol;
+			}
+			else if (auto* v6 = packet.getLayerOfType<pcpp::IPv6Layer>())
+			{
+				std::memcpy(t.src_ip, v6->getSrcIPv6Address().toBytes(), 16);
+				std::memcpy(t.dst_ip, v6->getDstIPv6Address().toBytes(), 16);
+				t.ip_version = 6;
+				t.ip_proto = v6->getIPv6Header()->nextHeader;
+			}
+			if (auto* tcp = packet.getLayerOfType<pcpp::TcpLayer>(true))
+			{
+				t.src_port = tcp->getSrcPort();
+				t.dst_port = tcp->getDstPort();
+				t.l4_proto = pcpp::TCP;
+			}
+			else if (auto* udp = packet.getLayerOfType<pcpp::UdpLayer>(true))
+			{
+				t.src_port = udp->getSrcPort();
+				t.dst_port = udp->getDstPort();
+				t.l4_proto = pcpp::UDP;
+			}
+			t.has_5tuple = (packet.isPacketOfType(pcpp::IPv4) || packet.isPacketOfType(pcpp::IPv6)) &&
+			               !packet.isPacketOfType(pcpp::ICMP) &&
+			               (packet.isPacketOfType(pcpp::TCP) || packet.isPacketOfType(pcpp::UDP));
+			t.hash5 = pcpp::hash5Tuple(&packet);
+			int nl = 0;
+			for (pcpp::Layer* l = packet.getFirstLayer(); l != nullptr; l = l->getNextLayer())
+				++nl;
+			t.n_layers = static_cast<uint8_t>(nl > 255 ? 255 : nl);
+		}
+		return PCPPX_OK;
+	}
+
 	// Parse a host batch with the reference Packet++ and fill host records.
 	int pcppx_ref_parse_batch(const pcppx_batch* b, const pcppx_opts* opts, pcppx_records* out)
 	{

@@ -15,10 +15,13 @@ PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 ENGINE_SO = PKG_DIR / "libpcppx.so"
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_LAYERS = 16
 MAX_CAPLEN = 65535
 WINDOW_DEFAULT, WINDOW_DEEP = 0, 1  # pcppx_opts.window (PCPPX_WINDOW_*)
+LAYOUT_FIXED, LAYOUT_PACKED = 0, 1  # pcppx_opts.layout (PCPPX_LAYOUT_*)
+PACKED_MAX_LAYERS = 12
+TILE = 64  # packets per tile of the PACKED layout
 
 # error codes
 OK, E_INVAL, E_NODEV, E_HIP, E_NOMEM, E_LINKTYPE = 0, -1, -2, -3, -4, -5
@@ -72,7 +75,18 @@ REASM_DTYPE = np.dtype(
     [("ip_key", "<u4"), ("frag_id", "<u4"), ("frag_offset", "<u2"), ("ip_status", "u1"), ("tcp_status", "u1"),
      ("tcp_payload", "<u4")]
 )
+TUPLE_DTYPE = np.dtype(
+    [("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,)), ("src_port", "<u2"), ("dst_port", "<u2"), ("ip_version", "u1"),
+     ("ip_proto", "u1"), ("l4_proto", "u1"), ("has_5tuple", "u1"), ("hash5", "<u4"), ("flags", "<u2"),
+     ("n_layers", "u1"), ("reserved", "u1")]
+)
 assert SUMMARY_DTYPE.itemsize == 32 and LAYER_DTYPE.itemsize == 8 and REASM_DTYPE.itemsize == 16
+assert TUPLE_DTYPE.itemsize == 48
+
+# pcppx_records.proto_stats words (PCPPX_PS_*): PacketStats::collectStats, Common.h:83-104
+PROTO_STATS = 16
+PROTO_STATS_FIELDS = ("packet_count", "eth_count", "arp_count", "ipv4_count", "ipv6_count", "tcp_count", "udp_count",
+                      "http_count", "dns_count", "tls_count", "needs_host_count")
 
 # pcppx_reasm_info status codes (low nibble) and flags
 IPR_NON_IP, IPR_NON_FRAGMENT, IPR_MALFORMED, IPR_FRAGMENT, IPR_HOST = 0, 1, 2, 3, 15
@@ -100,11 +114,14 @@ class Opts(C.Structure):
         ("want_checksums", C.c_uint8),
         ("max_layers", C.c_uint8),
         ("window", C.c_uint8),
+        ("layout", C.c_uint8),
+        ("reserved", C.c_uint8 * 3),
     ]
 
 
 class Records(C.Structure):
-    _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p), ("flow_keys", C.c_void_p)]
+    _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p), ("flow_keys", C.c_void_p), ("tuples", C.c_void_p),
+                ("proto_stats", C.c_void_p)]
 
 
 class MatchSpec(C.Structure):
@@ -133,14 +150,45 @@ def ipv4_to_int(dotted: str) -> int:
 
 
 def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checksums: bool = True,
-              max_layers: int = MAX_LAYERS, window: int = 0) -> Opts:
+              max_layers: int = MAX_LAYERS, window: int = 0, layout: int = LAYOUT_FIXED) -> Opts:
     """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection; window:
-    WINDOW_DEFAULT / WINDOW_DEEP (the checksum launch's header window, records identical)."""
+    WINDOW_DEFAULT / WINDOW_DEEP (the checksum launch's header window, records identical); layout: LAYOUT_FIXED /
+    LAYOUT_PACKED (the layer entries, bit for bit the same; unpack_layers)."""
     if not 0 <= max_layers <= MAX_LAYERS:
         raise ValueError(f"max_layers must be in [0, {MAX_LAYERS}]")
     if window not in (WINDOW_DEFAULT, WINDOW_DEEP):
         raise ValueError("window must be WINDOW_DEFAULT or WINDOW_DEEP")
-    return Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, window)
+    if layout not in (LAYOUT_FIXED, LAYOUT_PACKED) or (layout == LAYOUT_PACKED and max_layers > PACKED_MAX_LAYERS):
+        raise ValueError(f"layout must be LAYOUT_FIXED, or LAYOUT_PACKED with max_layers <= {PACKED_MAX_LAYERS}")
+    o = Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, window)
+    o.layout = layout
+    return o
+
+
+def packed_positions(n_layers: np.ndarray, max_layers: int) -> np.ndarray:
+    """Start entry of every packet's chain in a PACKED layer array (include/pcppx.h PCPPX_LAYOUT_PACKED): the tile's
+    base 64 * t * max_layers plus the chains of the packets before it in its 64-packet tile."""
+    cnt = np.minimum(n_layers.astype(np.int64), max_layers)
+    n = len(cnt)
+    tile = np.arange(n) // TILE
+    csum = np.cumsum(cnt) - cnt  # exclusive prefix over the whole batch
+    first = tile * TILE
+    return tile * TILE * max_layers + csum - csum[first] if n else csum
+
+
+def unpack_layers(summary: np.ndarray, packed: np.ndarray, max_layers: int) -> np.ndarray:
+    """PACKED layer entries -> the FIXED [n, max_layers] array (entries past a chain zero)."""
+    n = len(summary)
+    out = np.zeros((n, max_layers), dtype=LAYER_DTYPE)
+    if n == 0 or max_layers == 0:
+        return out
+    cnt = np.minimum(summary["n_layers"].astype(np.int64), max_layers)
+    start = packed_positions(summary["n_layers"], max_layers)
+    flat = packed.reshape(-1)
+    for k in range(max_layers):
+        m = cnt > k
+        out[m, k] = flat[start[m] + k]
+    return out
 
 
 def _declare(lib: C.CDLL) -> C.CDLL:

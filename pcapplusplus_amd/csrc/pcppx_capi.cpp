@@ -166,6 +166,12 @@ struct pcppx_ctx
 	uint32_t* d_flow_fill = nullptr;
 	hipEvent_t flow_done = nullptr;
 	bool flow_pending = false;
+	// pcppx_records.proto_stats: the parse's per-wave collectStats records (16 B per 64 packets), summed into the
+	// caller's counters by a second kernel; ordered across calls like the flow scratch
+	void* d_wave_stats = nullptr;
+	uint64_t wave_stats_bytes = 0;
+	hipEvent_t stats_done = nullptr;
+	bool stats_pending = false;
 };
 
 namespace
@@ -177,8 +183,68 @@ bool ok(hipError_t e)
 
 int valid_opts(const pcppx_opts* o)
 {
-	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->window > PCPPX_WINDOW_DEEP)
+	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->window > PCPPX_WINDOW_DEEP ||
+	    o->layout > PCPPX_LAYOUT_PACKED || (o->layout == PCPPX_LAYOUT_PACKED && o->max_layers > PCPPX_PACKED_MAX_LAYERS))
 		return PCPPX_E_INVAL;
+	return PCPPX_OK;
+}
+
+// the device path's record arguments: layers when max_layers > 0; a summary unless only the 5-tuples are wanted
+// (a PACKED layout is decoded through the summary's n_layers)
+bool valid_device_records(const pcppx_opts* o, const pcppx_records* r)
+{
+	if (o->max_layers != 0 && r->layers == nullptr)
+		return false;
+	if (r->summary == nullptr && (r->tuples == nullptr || o->max_layers != 0))
+		return false;
+	return true;
+}
+
+// Scratch owned by a context and shared by its calls: a call waits (on its own stream) for the previous call's
+// `done` event before touching it, and a larger size is reallocated in stream order behind that wait -- no call
+// stalls the device or another stream.
+int ensure_scratch(hipStream_t st, void** ptr, uint64_t* have, uint64_t want, hipEvent_t* done, bool pending)
+{
+	if (*done == nullptr && !ok(hipEventCreateWithFlags(done, hipEventDisableTiming)))
+		return PCPPX_E_HIP;
+	if (pending && !ok(hipStreamWaitEvent(st, *done, 0)))
+		return PCPPX_E_HIP;
+	if (*have < want)
+	{
+		if (*ptr != nullptr && !ok(hipFreeAsync(*ptr, st)))
+			return PCPPX_E_HIP;
+		*ptr = nullptr;
+		*have = 0;
+		if (!ok(hipMallocAsync(ptr, want, st)))
+			return PCPPX_E_NOMEM;
+		*have = want;
+	}
+	return PCPPX_OK;
+}
+
+// launch a device parse (plain or with the fused reassembly output) with the collectStats reduction when
+// r->proto_stats is set
+int device_parse(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
+                 hipStream_t st)
+{
+	void* ws = nullptr;
+	if (r->proto_stats != nullptr)
+	{
+		const int rc = ensure_scratch(st, &c->d_wave_stats, &c->wave_stats_bytes, (uint64_t)pcppx::parse_waves(b->n) * 16,
+		                              &c->stats_done, c->stats_pending);
+		if (rc != PCPPX_OK)
+			return rc;
+		ws = c->d_wave_stats;
+	}
+	int rc = info ? pcppx::launch_parse_reasm(b, o, r, info, st, ws) : pcppx::launch_parse(b, o, r, st, ws);
+	if (rc != PCPPX_OK || ws == nullptr)
+		return rc;
+	rc = pcppx::launch_proto_stats_reduce(ws, b->n, r->proto_stats, st);
+	if (rc != PCPPX_OK)
+		return rc;
+	if (!ok(hipEventRecord(c->stats_done, st)))
+		return PCPPX_E_HIP;
+	c->stats_pending = true;
 	return PCPPX_OK;
 }
 
@@ -550,6 +616,8 @@ extern "C"
 		o->want_checksums = 1;
 		o->max_layers = PCPPX_MAX_LAYERS;
 		o->window = PCPPX_WINDOW_DEFAULT;
+		o->layout = PCPPX_LAYOUT_FIXED;
+		o->reserved[0] = o->reserved[1] = o->reserved[2] = 0;
 	}
 
 	int pcppx_open(int device, pcppx_ctx** out)
@@ -592,14 +660,20 @@ extern "C"
 		free_filter(c);
 		if (c->flow_pending)
 			(void)hipEventSynchronize(c->flow_done);
-		// the flow scratch is stream-ordered memory (hipMallocAsync): released on the context's stream
+		if (c->stats_pending)
+			(void)hipEventSynchronize(c->stats_done);
+		// the flow / stats scratch is stream-ordered memory (hipMallocAsync): released on the context's stream
 		if (c->d_flow_queues)
 			(void)hipFreeAsync(c->d_flow_queues, c->stream);
 		if (c->d_flow_fill)
 			(void)hipFreeAsync(c->d_flow_fill, c->stream);
+		if (c->d_wave_stats)
+			(void)hipFreeAsync(c->d_wave_stats, c->stream);
 		(void)hipStreamSynchronize(c->stream);
 		if (c->flow_done)
 			(void)hipEventDestroy(c->flow_done);
+		if (c->stats_done)
+			(void)hipEventDestroy(c->stats_done);
 		(void)hipStreamDestroy(c->stream);
 		delete c;
 	}
@@ -625,12 +699,11 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (b->n == 0)
 			return PCPPX_OK;
-		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || r->summary == nullptr ||
-		    (o->max_layers != 0 && r->layers == nullptr))
+		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || !valid_device_records(o, r))
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
-		return pcppx::launch_parse(b, o, r, static_cast<hipStream_t>(hip_stream));
+		return device_parse(c, b, o, r, nullptr, static_cast<hipStream_t>(hip_stream));
 	}
 
 	int pcppx_parse_batch_host(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r)
@@ -641,6 +714,9 @@ extern "C"
 			return PCPPX_OK;
 		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || r->summary == nullptr ||
 		    (o->max_layers != 0 && r->layers == nullptr))
+			return PCPPX_E_INVAL;
+		// device-path-only outputs
+		if (r->tuples != nullptr || r->proto_stats != nullptr || o->layout != PCPPX_LAYOUT_FIXED)
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
@@ -675,7 +751,8 @@ extern "C"
 	int pcppx_parse_batch_device_reasm(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r,
 	                                   pcppx_reasm_info* info, void* hip_stream)
 	{
-		if (c == nullptr || b == nullptr || r == nullptr || valid_opts(o) != PCPPX_OK || o->max_layers == 0)
+		if (c == nullptr || b == nullptr || r == nullptr || valid_opts(o) != PCPPX_OK || o->max_layers == 0 ||
+		    o->layout != PCPPX_LAYOUT_FIXED)
 			return PCPPX_E_INVAL;
 		if (b->n == 0)
 			return PCPPX_OK;
@@ -684,7 +761,7 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
-		return pcppx::launch_parse_reasm(b, o, r, info, static_cast<hipStream_t>(hip_stream));
+		return device_parse(c, b, o, r, info, static_cast<hipStream_t>(hip_stream));
 	}
 
 	int pcppx_reasm_device(pcppx_ctx* c, const pcppx_batch* b, const pcppx_records* r, uint8_t max_layers,
@@ -787,23 +864,14 @@ int flow_count(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* keys_
 		hipStream_t st = static_cast<hipStream_t>(hip_stream);
 		const uint32_t parts = pcppx::flow_partitions(capacity);
 		const uint32_t rec_cap = pcppx::flow_queue_capacity(n, capacity);
-		if (c->flow_done == nullptr && !ok(hipEventCreateWithFlags(&c->flow_done, hipEventDisableTiming)))
-			return PCPPX_E_HIP;
-		// the context's previous flow work (possibly queued on another stream) owns the scratch until flow_done
-		if (c->flow_pending && !ok(hipStreamWaitEvent(st, c->flow_done, 0)))
-			return PCPPX_E_HIP;
-		if (c->flow_queue_recs < (uint64_t)parts * rec_cap)
-		{
-			// grow in stream order: the old queues are released behind that wait, on this stream; nothing else on
-			// the device is stalled
-			if (c->d_flow_queues != nullptr && !ok(hipFreeAsync(c->d_flow_queues, st)))
-				return PCPPX_E_HIP;
-			c->d_flow_queues = nullptr;
-			c->flow_queue_recs = 0;
-			if (!ok(hipMallocAsync(&c->d_flow_queues, (size_t)parts * rec_cap * 16, st)))
-				return PCPPX_E_NOMEM;
-			c->flow_queue_recs = (uint64_t)parts * rec_cap;
-		}
+		// the context's previous flow work (possibly queued on another stream) owns the scratch until flow_done; a
+		// larger one is allocated in stream order behind that wait
+		uint64_t have = c->flow_queue_recs * 16;
+		const int src = ensure_scratch(st, &c->d_flow_queues, &have, (uint64_t)parts * rec_cap * 16, &c->flow_done,
+		                               c->flow_pending);
+		c->flow_queue_recs = have / 16;
+		if (src != PCPPX_OK)
+			return src;
 		if (c->d_flow_fill == nullptr)
 		{
 			if (!ok(hipMallocAsync(reinterpret_cast<void**>(&c->d_flow_fill), 1024 * sizeof(uint32_t), st)) ||

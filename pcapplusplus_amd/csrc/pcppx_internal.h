@@ -8,7 +8,11 @@
 namespace pcppx
 {
 int check_launch(const char* what, hipStream_t stream);
-int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream);
+// wave_stats: null, or parse_waves(n) 16-B per-wave collectStats records, summed by launch_proto_stats_reduce
+int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream,
+                 void* wave_stats = nullptr);
+uint32_t parse_waves(uint32_t n);
+int launch_proto_stats_reduce(const void* wave_stats, uint32_t n, uint64_t* out, hipStream_t stream);
 int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, const pcppx_match_spec* spec,
                   uint64_t seq_base, uint64_t* keys, uint64_t* first, uint32_t capacity, uint8_t* matched,
                   pcppx_packet_stats* stats, hipStream_t stream);
@@ -19,6 +23,6 @@ int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* dkeys, cons
                            uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats,
                            void* queues, uint32_t rec_cap, uint32_t* fill, hipStream_t stream);
 int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
-                       hipStream_t stream);
+                       hipStream_t stream, void* wave_stats = nullptr);
 int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcppx_reasm_info* info, hipStream_t stream);
 }  // namespace pcppx

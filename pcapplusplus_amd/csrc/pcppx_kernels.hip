@@ -949,6 +949,9 @@ struct Params
 	uint32_t linktype;
 	uint32_t fam_engine_only;  // family != 0 and every protocol of it is one the engine builds (host-computed)
 	pcppx_reasm_info* reasm;  // fused reassembly front ends (pcppx_parse_batch_device_reasm), or null
+	pcppx_tuple* tuples;      // optional 5-tuple extracts (pcppx_records.tuples)
+	uint4* wave_stats;        // optional per-wave collectStats counters (16 x u8), reduced by proto_stats_reduce_kernel
+	uint32_t packed;          // PCPPX_LAYOUT_PACKED: the chain's layer entries dense per 64-packet tile
 };
 
 // Everything the summary needs after the chain walk.
@@ -1274,6 +1277,55 @@ __device__ __forceinline__ void write_summary(pcppx_summary* out, uint32_t h5, u
 	uint4 s1 = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), ipc | (ips << 16), l4c | (l4s << 16));
 	reinterpret_cast<uint4*>(out)[0] = s0;
 	reinterpret_cast<uint4*>(out)[1] = s1;
+}
+
+// the 5-tuple extract (pcppx_tuple): the fields hash5Tuple reads (PacketUtils.cpp:139-210) -- the first IPv4, else first
+// IPv6 layer's addresses and protocol / next-header byte, the port layer's (last TCP, else last UDP) ports -- read the
+// way hashes() reads them (the LDS window where staged, else HBM); three 16-B stores
+__device__ __forceinline__ void write_tuple(const Pkt& p, const Walk& w, uint32_t h5, pcppx_tuple* out)
+{
+	const bool v4 = w.v4 >= 0, ip = v4 || w.v6 >= 0;
+	const uint32_t ipo = v4 ? (uint32_t)w.v4 : (uint32_t)w.v6;
+	const uint32_t na = ip ? (v4 ? 1u : 4u) : 0u;
+	const uint32_t so = ipo + (v4 ? 12 : 8), dofs = ipo + (v4 ? 16 : 24);
+	uint32_t s[4], d[4];
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+	{
+		s[k] = (uint32_t)k < na ? rd32(p, so + 4 * k) : 0u;
+		d[k] = (uint32_t)k < na ? rd32(p, dofs + 4 * k) : 0u;
+	}
+	const bool l4 = w.l4i >= 0;
+	const uint32_t pw = l4 ? rd32(p, w.l4o) : 0u;  // raw network-order ports, LE-loaded
+	const uint32_t ports = swap16(pw) | (swap16(pw >> 16) << 16);  // getSrcPort / getDstPort (host order)
+	const uint32_t ipp = ip ? rb(p, ipo + (v4 ? 9 : 6)) : 0u;
+	const bool has5 = ip && l4 && !(w.mask & (1ull << P_ICMP));  // PacketUtils.cpp:141-148
+	const uint32_t meta = (ip ? (v4 ? 4u : 6u) : 0u) | (ipp << 8) | ((l4 ? (w.is_tcp ? P_TCP : P_UDP) : 0u) << 16) |
+	                      ((has5 ? 1u : 0u) << 24);
+	uint4* o = reinterpret_cast<uint4*>(out);
+	o[0] = make_uint4(s[0], s[1], s[2], s[3]);
+	o[1] = make_uint4(d[0], d[1], d[2], d[3]);
+	o[2] = make_uint4(ports, meta, h5, (w.flags & 0xFFFFu) | ((w.n_layers & 0xFFu) << 16));
+}
+
+// PacketStats::collectStats (Examples/DpdkExample-FilterTraffic/Common.h:83-104) of one wave of packets: 11 ballot counts
+// (<= 64 each) packed as bytes into one 16-B record per wave (PCPPX_PS_* order), written by lane 0. Same rules as
+// filter_apply_kernel: HTTP / DNS / SSL only for the packets the device settles.
+__device__ __forceinline__ void wave_proto_stats(bool in, uint64_t mask, uint32_t flags, uint4* out)
+{
+	const bool settled = (flags & (PCPPX_F_NEEDS_HOST_PROTO | PCPPX_F_OVERSIZE | PCPPX_F_BAD_DESC)) == 0 &&
+	                     (!(flags & PCPPX_F_NEEDS_HOST_L7) || (flags & PCPPX_F_L7_KNOWN));
+	const bool http = (flags & PCPPX_F_L7_HTTP) || (mask & ((1ull << P_HTTP_REQ) | (1ull << P_HTTP_RESP)));
+	const bool dns = (flags & PCPPX_F_L7_DNS) || (mask & (1ull << P_DNS));
+	const bool ssl = (flags & PCPPX_F_L7_SSL) || (mask & (1ull << P_SSL));
+	auto cnt = [&](bool pr) { return (uint32_t)__popcll(__ballot(in && pr)); };
+	const uint32_t x = cnt(true) | (cnt((mask >> P_ETH) & 1) << 8) | (cnt((mask >> P_ARP) & 1) << 16) |
+	                   (cnt((mask >> P_IPV4) & 1) << 24);
+	const uint32_t y = cnt((mask >> P_IPV6) & 1) | (cnt((mask >> P_TCP) & 1) << 8) | (cnt((mask >> P_UDP) & 1) << 16) |
+	                   (cnt(settled && http) << 24);
+	const uint32_t z = cnt(settled && dns) | (cnt(settled && ssl) << 8) | (cnt(!settled) << 16);
+	if ((threadIdx.x & 63) == 0)
+		*out = make_uint4(x, y, z, 0u);
 }
 
 // descriptor checks shared by both kernels: returns 0 if the packet is parseable, else its flags
@@ -2298,7 +2350,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 	}
 
-	if (in && NT)
+	if (in && NT && prm.summary != nullptr)
 	{
 		const uint32_t l4b = w.l4i >= 0 ? (uint32_t)w.l4i : 0xFFu;
 		u32x4 s0, s1;
@@ -2308,14 +2360,46 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		__builtin_nontemporal_store(s0, so);
 		__builtin_nontemporal_store(s1, so + 1);
 	}
-	else if (in)
+	else if (in && prm.summary != nullptr)
 		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
 	if (in && prm.flow_keys != nullptr)
 		__builtin_nontemporal_store(h5, prm.flow_keys + i);
+	if (in && prm.tuples != nullptr)  // the LDS window is still intact here (the rows below reuse it)
+		write_tuple(p, w, h5, prm.tuples + i);
+	if (prm.wave_stats != nullptr)  // uniform
+		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + blockIdx.x);
 
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
 	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
-	if (stage_layers && ml > kRowMl)  // uniform: deep records, each fast lane stores its own row
+	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+	typedef __attribute__((address_space(3))) u32x2* lptr64w;
+	// PCPPX_LAYOUT_PACKED: the tile's chains dense in LDS (entry excl + k of the lane's exclusive prefix), stored as one
+	// contiguous run of entries from the tile's base; needs kTile * PCPPX_PACKED_MAX_LAYERS entries of stage
+	constexpr bool kPackedOk = kTSlotDw >= 2 * PCPPX_PACKED_MAX_LAYERS;
+	if (kPackedOk && stage_layers && prm.packed)  // uniform
+	{
+		const uint32_t cnt = in ? (w.n_layers < ml ? w.n_layers : ml) : 0u;
+		const uint32_t incl = wave_incl_scan(cnt);
+		const uint32_t excl = incl - cnt;
+		const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)blockIdx.x * kTile * ml;
+		__syncthreads();  // every lane is done with the header stage
+		lptr64w rows = (lptr64w)(stage);
+		if (fast)
+			fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) {
+				u32x2 e;
+				e.x = r.x;
+				e.y = r.y;
+				rows[excl + k] = e;
+			});
+		else
+			for (uint32_t k = 0; k < cnt; ++k)  // the generic walk wrote this lane's chain at its fixed-layout slot
+				rows[excl + k] = dst[lane * ml + k];
+		__syncthreads();
+		for (uint32_t r = lane; r < total; r += kTile)
+			__builtin_nontemporal_store(rows[r], &dst[r]);
+	}
+	else if (stage_layers && ml > kRowMl)  // uniform: deep records, each fast lane stores its own row
 	{
 		if (fast)
 		{
@@ -2327,8 +2411,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	{
 		__syncthreads();  // every lane is done with the header stage
 		m_nch[lane] = (fast || GatherOnly) ? (FillTails ? ml : w.n_layers) : 0u;  // records of the row to store
-		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-		typedef __attribute__((address_space(3))) u32x2* lptr64w;
 		lptr64w rows = (lptr64w)(stage);
 		const uint32_t rs = ml + 1;  // padded row stride (records): breaks the power-of-two bank pattern
 		if (FillTails && (fast || GatherOnly))
@@ -2398,6 +2480,44 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		else
 			r = reasm_one(w.flags, w.n_layers, prm.layers + (size_t)i * ml, ml, prm.data + off);
 		reinterpret_cast<uint4*>(prm.reasm)[i] = r;
+	}
+}
+
+// ---- collectStats totals: the per-wave counters of a parse (wave_proto_stats) summed into the caller's
+// PCPPX_PROTO_STATS words (one 64-bit atomic per counter and block) ----
+__global__ __launch_bounds__(kBlock) void proto_stats_reduce_kernel(const uint4* __restrict__ part, uint32_t nw,
+                                                                  unsigned long long* out)
+{
+	constexpr int kC = 11;  // PCPPX_PS_PACKETS .. PCPPX_PS_NEEDS_HOST
+	uint32_t a[kC];
+#pragma unroll
+	for (int k = 0; k < kC; ++k)
+		a[k] = 0;
+	for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < nw; j += gridDim.x * kBlock)
+	{
+		const uint4 v = part[j];
+		const uint32_t w[3] = { v.x, v.y, v.z };
+#pragma unroll
+		for (int k = 0; k < kC; ++k)
+			a[k] += (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+	}
+	__shared__ unsigned long long s_part[kBlock / 64][kC];
+	const uint32_t wv = threadIdx.x >> 6;
+#pragma unroll
+	for (int k = 0; k < kC; ++k)
+	{
+		const unsigned long long t = wave_sum_u64(a[k]);
+		if ((threadIdx.x & 63) == 0)
+			s_part[wv][k] = t;
+	}
+	__syncthreads();
+	if (threadIdx.x < (uint32_t)kC)
+	{
+		unsigned long long t = 0;
+		for (uint32_t q = 0; q < kBlock / 64; ++q)
+			t += s_part[q][threadIdx.x];
+		if (t)
+			atomicAdd(&out[threadIdx.x], t);
 	}
 }
 
@@ -2995,6 +3115,9 @@ Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, 
 	prm.linktype = b->linktype;
 	prm.fam_engine_only = family_engine_only(o->parse_until_family) ? 1u : 0u;
 	prm.reasm = info;
+	prm.tuples = r->tuples;
+	prm.wave_stats = nullptr;
+	prm.packed = o->layout == PCPPX_LAYOUT_PACKED ? 1u : 0u;
 	return prm;
 }
 
@@ -3044,11 +3167,12 @@ int check_launch(const char* what, hipStream_t /*stream*/)
 	return PCPPX_OK;
 }
 
-int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream)
+int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream, void* wave_stats)
 {
 	if (b->n == 0)
 		return PCPPX_OK;
-	const Params prm = make_params(b, o, r, nullptr);
+	Params prm = make_params(b, o, r, nullptr);
+	prm.wave_stats = static_cast<uint4*>(wave_stats);
 	const dim3 grid((b->n + kTile - 1) / kTile);
 	if (o->want_checksums && o->window == PCPPX_WINDOW_DEEP)
 		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
@@ -3060,11 +3184,12 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 }
 
 int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
-                       hipStream_t stream)
+                       hipStream_t stream, void* wave_stats)
 {
 	if (b->n == 0)
 		return PCPPX_OK;
-	const Params prm = make_params(b, o, r, info);
+	Params prm = make_params(b, o, r, info);
+	prm.wave_stats = static_cast<uint4*>(wave_stats);
 	const dim3 grid((b->n + kTile - 1) / kTile);
 	if (o->want_checksums && o->window == PCPPX_WINDOW_DEEP)
 		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
@@ -3073,6 +3198,22 @@ int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records*
 	else
 		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel(reasm)", stream);
+}
+
+uint32_t parse_waves(uint32_t n)
+{
+	return (n + kTile - 1) / kTile;
+}
+
+int launch_proto_stats_reduce(const void* wave_stats, uint32_t n, uint64_t* out, hipStream_t stream)
+{
+	if (n == 0)
+		return PCPPX_OK;
+	const uint32_t nw = parse_waves(n);
+	const uint32_t blocks = (nw + kBlock - 1) / kBlock;
+	hipLaunchKernelGGL(proto_stats_reduce_kernel, dim3(blocks < 128 ? blocks : 128), dim3(kBlock), 0, stream,
+	                   static_cast<const uint4*>(wave_stats), nw, reinterpret_cast<unsigned long long*>(out));
+	return check_launch("proto_stats_reduce_kernel", stream);
 }
 
 int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, const pcppx_match_spec* spec,

@@ -59,12 +59,15 @@ class Engine:
 
     # ---- device-resident batches (torch tensors on this GPU) ----
     def parse_device(self, data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers=None,
-                     stream: int | None = None, flow_keys=None) -> None:
+                     stream: int | None = None, flow_keys=None, tuples=None, proto_stats=None) -> None:
         """Queue a parse of device tensors on `stream` (a hipStream_t handle, e.g.
-        torch.cuda.current_stream().cuda_stream). summary: uint8 tensor of n*32 bytes; layers: n*max_layers*8."""
+        torch.cuda.current_stream().cuda_stream). summary: uint8 tensor of n*32 bytes (or None with tuples and no
+        layers); layers: n*max_layers*8; tuples: n*48 bytes (5-tuple extracts); proto_stats: 16 x int64,
+        accumulated (collectStats)."""
         b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
-        rec = abi.Records(abi.ptr(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None,
-                          abi.ptr(flow_keys) if flow_keys is not None else None)
+        opt = lambda t: abi.ptr(t) if t is not None else None  # noqa: E731
+        rec = abi.Records(opt(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None,
+                          opt(flow_keys), opt(tuples), opt(proto_stats))
         abi.check(self.lib.pcppx_parse_batch_device(self.ctx, C.byref(b), C.byref(opts), C.byref(rec),
                                                     C.c_void_p(stream or 0)), "pcppx_parse_batch_device")
 
@@ -236,6 +239,41 @@ def records_from_device(summary_t, layers_t, n: int, max_layers: int):
         return s, np.zeros((n, 0), dtype=abi.LAYER_DTYPE)
     lay = layers_t.cpu().numpy().view(abi.LAYER_DTYPE)[: n * max_layers].reshape(n, max_layers)
     return s, lay
+
+
+def parse_on_device_ex(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = None, device: str = "cuda:0",
+                       summary: bool = True, tuples: bool = False, proto_stats: bool = False):
+    """parse_on_device with the optional outputs: {"summary", "layers" (FIXED [n, max_layers], decoded when the
+    layout is PACKED), "packed" (the raw PACKED entries), "tuples", "proto_stats" (dict)}."""
+    import torch
+
+    opts = opts or abi.make_opts()
+    data, offsets, caplens = to_device(batch, device)
+    n = batch.n
+    st = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device=device) if summary else None
+    lay = torch.zeros(max(n * opts.max_layers, 1) * 8, dtype=torch.uint8, device=device)
+    tp = torch.zeros(max(n, 1) * 48, dtype=torch.uint8, device=device) if tuples else None
+    ps = torch.zeros(abi.PROTO_STATS, dtype=torch.int64, device=device) if proto_stats else None
+    eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, st, lay if opts.max_layers else None,
+                     torch.cuda.current_stream(device).cuda_stream, tuples=tp, proto_stats=ps)
+    torch.cuda.synchronize(device)
+    out = {}
+    if st is not None:
+        out["summary"] = st.cpu().numpy().view(abi.SUMMARY_DTYPE)[:n]
+    if opts.max_layers and st is not None:
+        raw = lay.cpu().numpy().view(abi.LAYER_DTYPE)[: n * opts.max_layers]
+        if opts.layout == abi.LAYOUT_PACKED:
+            out["packed"] = raw
+            out["layers"] = abi.unpack_layers(out["summary"], raw, opts.max_layers)
+        else:
+            out["layers"] = raw.reshape(n, opts.max_layers)
+    if tp is not None:
+        out["tuples"] = tp.cpu().numpy().view(abi.TUPLE_DTYPE)[:n]
+    if ps is not None:
+        v = ps.cpu().numpy()
+        out["proto_stats"] = {f: int(v[k]) for k, f in enumerate(abi.PROTO_STATS_FIELDS)}
+        out["proto_stats_raw"] = v
+    return out
 
 
 def parse_on_device(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = None, device: str = "cuda:0"):

@@ -2,10 +2,12 @@
 # PMC HBM traffic of the parse kernel for each bench config (GPU box, repo root): two rocprofv3 --pmc passes
 # (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) over bench.py itself, so the numbers belong to exactly the
 # launch bench.py times; then gpurun_out/<tag>_traffic_cfg<N>.json, keyed by config / size / records / kernel sha.
-#   tools/measure_traffic.sh <tag> "<configs>"
+#   tools/measure_traffic.sh <tag> "<configs>" [extra bench.py args, e.g. --layout packed]
 set -o pipefail
 TAG=${1:-tr}
 CFGS=${2:-"3"}
+shift 2 2>/dev/null
+EXTRA="$*"
 OUT=gpurun_out
 ROOT=$(pwd)
 mkdir -p "$OUT"
@@ -14,12 +16,10 @@ for c in $CFGS; do
   mkdir -p "$OUT/${TAG}_pmc_cfg$c"
   for ctr in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $ctr -d "$ROOT/$OUT/${TAG}_pmc_cfg$c/$ctr" -o p --output-format csv -- \
-      python3 "$ROOT/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-traffic \
+      python3 "$ROOT/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-traffic $EXTRA \
       > "$ROOT/$OUT/${TAG}_pmc_cfg$c/$ctr.json" 2> "$ROOT/$OUT/${TAG}_pmc_cfg$c.$ctr.err") || exit 1
   done
-  line=$(tail -1 "$OUT/${TAG}_pmc_cfg$c/FETCH_SIZE.json")
-  read -r n ml cs < <(python3 -c "import json,sys; d=json.loads(sys.argv[1]); c=d['config']; print(c['packets_per_gpu'], c['max_layers'], int(c['checksums']))" "$line")
-  python3 tools/pmc_traffic.py "$OUT/${TAG}_pmc_cfg$c/FETCH_SIZE" "$OUT/${TAG}_pmc_cfg$c/WRITE_SIZE" "$c" "$n" "$ml" "$cs" \
-    "$OUT/${TAG}_traffic_cfg$c.json" || exit 2
+  python3 tools/pmc_traffic.py "$OUT/${TAG}_pmc_cfg$c/FETCH_SIZE" "$OUT/${TAG}_pmc_cfg$c/WRITE_SIZE" \
+    "$OUT/${TAG}_pmc_cfg$c/FETCH_SIZE.json" "$OUT/${TAG}_traffic_cfg$c.json" || exit 2
 done
 echo "traffic ok"

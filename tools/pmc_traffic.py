@@ -3,10 +3,11 @@
 gfx950 correction (/opt/skills/guides/MI355X_MICROARCH.md §HBM): FETCH_SIZE reports exactly half of the
 bytes of a wide (16 B/lane) coalesced streaming read; WRITE_SIZE is exact for 16-B-per-lane stores. Both
 are in KiB. Our reads are dwordx4 (16 B/lane) loads, so hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024.
-The result is keyed by everything bench.py checks before using it: config, packets, max_layers, checksums and the
-sha of the kernel source it was measured on (bench.kernel_sha).
+The result is keyed by everything bench.py checks before using it: config, packets, max_layers, checksums, layer
+layout, record kind (taken from the bench line the profiled run printed) and the sha of the kernel source it was
+measured on (bench.kernel_sha).
 
-  python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <packets> <max_layers> <checksums 0|1> <out.json>
+  python tools/pmc_traffic.py <fetch_dir> <write_dir> <bench line .json> <out.json>
 """
 import csv
 import json
@@ -31,13 +32,16 @@ def per_launch(d: str, counter: str) -> tuple[float, int]:
 
 fetch_kib, nf = per_launch(sys.argv[1], "FETCH_SIZE")
 write_kib, nw = per_launch(sys.argv[2], "WRITE_SIZE")
+line = json.loads(Path(sys.argv[3]).read_text().strip().splitlines()[-1])
+c = line["config"]
 out = {
-    "config": int(sys.argv[3]), "packets": int(sys.argv[4]), "max_layers": int(sys.argv[5]),
-    "checksums": sys.argv[6] == "1", "kernel_sha": kernel_sha(),
+    "config": int(c["workload"].split("config ")[1].split(":")[0]), "packets": int(c["packets_per_gpu"]),
+    "max_layers": int(c["max_layers"]), "checksums": bool(c["checksums"]), "layout": c.get("layout", "fixed"),
+    "records": c.get("records", "summary"), "kernel_sha": kernel_sha(),
     "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "launches": [nf, nw],
     "read_bytes_corrected": 2 * fetch_kib * 1024, "write_bytes": write_kib * 1024,
     "hbm_bytes_per_launch": int(2 * fetch_kib * 1024 + write_kib * 1024),
     "correction": "gfx950 FETCH_SIZE = half the bytes of 16B/lane streaming reads (MI355X_MICROARCH.md §HBM)",
 }
-Path(sys.argv[7]).write_text(json.dumps(out, indent=1) + "\n")
+Path(sys.argv[4]).write_text(json.dumps(out, indent=1) + "\n")
 print(json.dumps(out))
