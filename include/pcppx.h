@@ -369,6 +369,14 @@ PCPPX_API int pcppx_pcap_read_batch(pcppx_pcap* reader, uint8_t* data, uint64_t 
 PCPPX_API int pcppx_pcap_read_batch_ex(pcppx_pcap* reader, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
                           uint32_t* caplens, uint32_t* frame_lens, uint64_t* timestamps_ns, uint32_t max_packets,
                           uint32_t* n_out, uint64_t* bytes_out);
+/* Zero-copy: the next batch's packets stay where they are in the reader's memory-mapped file. *data = the map
+ * base, *data_len = the file size, offsets[i] = the position of packet i's bytes in it (caplens / frame_lens /
+ * timestamps_ns as pcppx_pcap_read_batch_ex; the same records and batch boundaries). The file's record headers lie
+ * between the packets -- a gapped, ascending batch, which pcppx_parse_batch_host stages as near-contiguous ranges.
+ * The bytes stay valid until pcppx_pcap_close. */
+PCPPX_API int pcppx_pcap_map_batch(pcppx_pcap* reader, const uint8_t** data, uint64_t* data_len, uint64_t* offsets,
+                                   uint32_t* caplens, uint32_t* frame_lens, uint64_t* timestamps_ns, uint32_t max_packets,
+                                   uint32_t* n_out);
 PCPPX_API void pcppx_pcap_close(pcppx_pcap* reader);
 PCPPX_API void* pcppx_host_alloc(size_t bytes); /* page-locked host memory (hipHostMalloc) */
 PCPPX_API void pcppx_host_free(void* p);

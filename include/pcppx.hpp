@@ -514,7 +514,7 @@ public:
 	{
 		const pcppx_batch b = batch.toC();
 		const pcppx_opts o = options.toC();
-		pcppx_records r{ out.summaries.data(), options.maxLayers ? out.layers.data() : nullptr, nullptr };
+		pcppx_records r{ out.summaries.data(), options.maxLayers ? out.layers.data() : nullptr, nullptr, nullptr, nullptr };
 		check(pcppx_parse_batch_host(m_Ctx, &b, &o, &r), "pcppx_parse_batch_host");
 		out.hostParsed = 0;
 		if (m_HostParser == nullptr || options.maxLayers == 0)

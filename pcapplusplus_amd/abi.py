@@ -233,6 +233,9 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_pcap_read_batch_ex.argtypes = [P, P, C.c_uint64, P, P, P, P, C.c_uint32, C.POINTER(C.c_uint32),
                                              C.POINTER(C.c_uint64)]
     lib.pcppx_pcap_read_batch_ex.restype = C.c_int
+    lib.pcppx_pcap_map_batch.argtypes = [P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), P, P, P, P, C.c_uint32,
+                                         C.POINTER(C.c_uint32)]
+    lib.pcppx_pcap_map_batch.restype = C.c_int
     lib.pcppx_pcap_close.argtypes = [P]
     lib.pcppx_pcap_close.restype = None
     lib.pcppx_host_alloc.argtypes = [C.c_size_t]
@@ -252,7 +255,7 @@ EXPORTED_SYMBOLS = (
     "pcppx_abi_version", "pcppx_strerror", "pcppx_device_count", "pcppx_runtime_info", "pcppx_open", "pcppx_close",
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
     "pcppx_flow_count_device", "pcppx_flow_count_keys_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_parse_batch_device_reasm", "pcppx_pcap_open", "pcppx_pcap_linktype",
-    "pcppx_pcap_read_batch", "pcppx_pcap_read_batch_ex", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
+    "pcppx_pcap_read_batch", "pcppx_pcap_read_batch_ex", "pcppx_pcap_map_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
 )
 
 

@@ -315,8 +315,10 @@ bool is_pinned(const void* p)
 	return a.type == hipMemoryTypeHost;
 }
 
-// Packets [i, j) of a host batch as one contiguous byte range [*base, *base + *bytes) (the layout pcap
-// ingest and packed captures have): returns j, or i if the next chunk is not contiguous and in bounds.
+// Packets [i, j) of a host batch as one byte range [*base, *base + *bytes): ascending, each starting at most kMaxGap
+// bytes after the previous one ends (packed batches; a memory-mapped capture's packets with their record headers
+// between them, pcppx_pcap_map_batch): returns j, or i if packet i does not start such a run.
+constexpr uint64_t kMaxGap = 256;
 uint32_t contiguous_chunk(const pcppx_batch* b, uint32_t i, uint64_t* base, size_t* bytes)
 {
 	uint64_t end = b->offsets[i];
@@ -326,17 +328,17 @@ uint32_t contiguous_chunk(const pcppx_batch* b, uint32_t i, uint64_t* base, size
 	{
 		const uint64_t off = b->offsets[j];
 		const uint32_t cap = b->caplens[j];
-		if (off != end || off + cap > b->data_len || off + cap < off)
+		if (off < end || off - end > kMaxGap || off + cap > b->data_len || off + cap < off)
 			break;
-		if (end + cap - *base > kChunkBytes)
+		if (off + cap - *base > kChunkBytes)
 			break;
-		end += cap;
+		end = off + cap;
 		++j;
 	}
-	// a chunk stops at a non-contiguous packet only if it holds some packets; else the gather path runs
 	*bytes = (size_t)(end - *base);
 	return j;
 }
+constexpr uint32_t kMinRun = 4096;  // a shorter run that stops at a discontinuity is gathered per packet instead
 
 // gather packets [i, j) of a host batch into the slot's pinned staging, rebasing offsets; returns j.
 // Contiguous runs are staged with one multi-threaded copy, or not at all when the caller's bytes are
@@ -349,7 +351,7 @@ uint32_t stage_chunk(CopyPool& cp, Slot& s, const pcppx_batch* b, uint32_t i, si
 		uint64_t base = 0;
 		size_t bytes = 0;
 		const uint32_t j = contiguous_chunk(b, i, &base, &bytes);
-		if (j > i && (j == b->n || j - i == kChunkPackets || bytes + b->caplens[j] > kChunkBytes))
+		if (j > i && (j == b->n || j - i >= kMinRun || b->offsets[j] + b->caplens[j] - base > kChunkBytes))
 		{
 			for (uint32_t k = i; k < j; ++k)
 			{

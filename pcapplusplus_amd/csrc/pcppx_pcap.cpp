@@ -406,6 +406,42 @@ extern "C"
 		return PCPPX_OK;
 	}
 
+	// The same records without the copy: the batch points into the reader's map (offsets relative to *data = the map
+	// base; the file's record headers / block framing lie between the packets).
+	int pcppx_pcap_map_batch(pcppx_pcap* r, const uint8_t** data, uint64_t* data_len, uint64_t* offsets,
+	                         uint32_t* caplens, uint32_t* frame_lens, uint64_t* timestamps_ns, uint32_t max_packets,
+	                         uint32_t* n_out)
+	{
+		if (r == nullptr || data == nullptr || data_len == nullptr || offsets == nullptr || caplens == nullptr ||
+		    n_out == nullptr)
+			return PCPPX_E_INVAL;
+		*data = r->map;
+		*data_len = r->size;
+		uint32_t n = 0;
+		while (!r->done && n < max_packets)
+		{
+			Packet pk;
+			if (!r->next(pk))
+			{
+				r->done = true;
+				break;
+			}
+			if (n > 0 && pk.linktype != r->linktype)
+				break;  // one link type per batch
+			r->linktype = pk.linktype;
+			offsets[n] = (uint64_t)(pk.bytes - r->map);
+			caplens[n] = pk.keep;
+			if (frame_lens)
+				frame_lens[n] = pk.frame_len == 0xFFFFFFFFu ? pk.keep : pk.frame_len;
+			if (timestamps_ns)
+				timestamps_ns[n] = pk.ts_ns;
+			r->pos = pk.next_pos;
+			++n;
+		}
+		*n_out = n;
+		return PCPPX_OK;
+	}
+
 	int pcppx_pcap_read_batch(pcppx_pcap* r, uint8_t* data, uint64_t data_cap, uint64_t* offsets, uint32_t* caplens,
 	                          uint64_t* timestamps_ns, uint32_t max_packets, uint32_t* n_out, uint64_t* bytes_out)
 	{

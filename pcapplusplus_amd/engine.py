@@ -160,6 +160,21 @@ class PcapReader:
         return PacketBatch(data[: used.value].copy(), offsets[:k].copy(), caplens[:k].copy(), self.linktype,
                            timestamps_ns=ts[:k].copy(), frame_lens=frame_lens[:k].copy())
 
+    def map_batch(self, max_packets: int = 1 << 20):
+        """Zero-copy next batch (pcppx_pcap_map_batch): (map address, file size, offsets, caplens, frame_lens, ts);
+        the bytes stay in the reader's memory map until close()."""
+        offsets = np.empty(max_packets, dtype=np.uint64)
+        caplens = np.empty(max_packets, dtype=np.uint32)
+        frame_lens = np.empty(max_packets, dtype=np.uint32)
+        ts = np.empty(max_packets, dtype=np.uint64)
+        base, size, n = C.c_void_p(), C.c_uint64(0), C.c_uint32(0)
+        abi.check(self.lib.pcppx_pcap_map_batch(self.handle, C.byref(base), C.byref(size), offsets.ctypes.data,
+                                                caplens.ctypes.data, frame_lens.ctypes.data, ts.ctypes.data,
+                                                max_packets, C.byref(n)), "pcppx_pcap_map_batch")
+        k = n.value
+        self.linktype = int(self.lib.pcppx_pcap_linktype(self.handle))
+        return base.value, size.value, offsets[:k].copy(), caplens[:k].copy(), frame_lens[:k].copy(), ts[:k].copy()
+
     def close(self) -> None:
         if self.handle:
             self.lib.pcppx_pcap_close(self.handle)

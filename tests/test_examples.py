@@ -6,6 +6,7 @@ parse (pcppx_host_parse_fn); here that is the real reference, oracle/_ref/libpcp
 are compared with the reference."""
 from __future__ import annotations
 
+import json
 import re
 import subprocess
 
@@ -199,3 +200,22 @@ def test_benchmark_synthetic_imix(built, tmp_path):
     assert r.returncode == 0, r.stderr
     count, _ms = (int(x) for x in r.stdout.split())
     assert count == b.n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [[], ["--copy"]], ids=["map", "copy"])
+def test_pcap_parse_file_to_records(built, tmp_path, mode):
+    """examples/bin/pcap_parse (capture file -> zero-copy map batches or copied page-locked batches ->
+    pcppx_parse_batch_host): every packet of a 150k-packet IMIX pcap and of example2.pcap parsed, the records' hash5
+    digest equal to the restatement's (batches of 40k packets, so several batches and chunk boundaries)."""
+    b = synth.config(3, 150_000)
+    ex, _ = capture("example2.pcap")
+    for batch in (b, ex):
+        f = tmp_path / "in.pcap"
+        write_pcap(f, batch)
+        r = run([built / "pcap_parse", f, "--batch", "40000", "--reps", "1", *mode])
+        assert r.returncode == 0, r.stderr
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        s, _ = oracle.oracle_parse(batch, abi.make_opts(0, 8, True, 8), threads=8)
+        assert line["packets"] == batch.n
+        assert line["hash5_digest"] == int(s["hash5"].astype(np.uint64).sum())

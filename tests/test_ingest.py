@@ -52,6 +52,34 @@ def native_read_all(path, max_packets=777, data_cap=1 << 20):
             "ts_ns": cat(ts, np.uint64), "linktypes": np.array(lt, np.uint32)}
 
 
+def native_map_all(path, max_packets=777):
+    """Every packet through the zero-copy pcppx_pcap_map_batch (the bytes read out of the reader's map)."""
+    import ctypes as C
+
+    from pcapplusplus_amd.engine import PcapReader
+
+    try:
+        r = PcapReader(path)
+    except RuntimeError:
+        return None
+    pk, cl, fl, ts, lt = [], [], [], [], []
+    with r:
+        while True:
+            base, size, off, cap, flen, t = r.map_batch(max_packets)
+            if len(cap) == 0:
+                break
+            assert len(cap) <= max_packets and (off + cap <= size).all()
+            assert (np.diff(off.astype(np.int64)) > 0).all()  # ascending: the host path stages near-contiguous runs
+            pk += [C.string_at(base + int(o), int(c)) for o, c in zip(off, cap)]
+            cl.append(cap)
+            fl.append(flen)
+            ts.append(t)
+            lt += [r.linktype] * len(cap)
+    cat = lambda xs, t: np.concatenate(xs).astype(t) if xs else np.zeros(0, t)  # noqa: E731
+    return {"packets": pk, "caplens": cat(cl, np.uint32), "frame_lens": cat(fl, np.uint32),
+            "ts_ns": cat(ts, np.uint64), "linktypes": np.array(lt, np.uint32)}
+
+
 def _golden():
     g = np.load(GOLD / "expected.npz")
     starts = np.concatenate([[0], np.cumsum(g["counts"])])
@@ -118,6 +146,32 @@ def test_reader_equals_reference(tmp_path, kind):
         assert checked > 50
     elif checked == 0:
         pytest.skip("/root/reference absent: the large reference captures are checked where it exists")
+
+
+@pytest.mark.parametrize("kind", ["fixture", "crafted", "mutation"])
+def test_zero_copy_reader_equals_reference(tmp_path, kind):
+    """pcppx_pcap_map_batch: the same packets, lengths, timestamps and link types as the reference readers, read in
+    place from the memory-mapped capture."""
+    g, starts = _golden()
+    data = _case_bytes(g)
+    checked = 0
+    for k, name in enumerate(g["names"]):
+        if g["kinds"][k] != kind:
+            continue
+        b = data[str(name)]
+        f = tmp_path / "case"
+        f.write_bytes(b)
+        got = native_map_all(f, max_packets=1 + (k * 53) % 400)
+        assert (got is not None) == bool(g["opened"][k]), f"{name}: open"
+        if got is None:
+            continue
+        s, e = starts[k], starts[k + 1]
+        assert len(got["caplens"]) == e - s, f"{name}: packet count"
+        for key in ("caplens", "frame_lens", "ts_ns", "linktypes"):
+            assert np.array_equal(got[key], g[key][s:e]), f"{name}: {key}"
+        assert np.array_equal(ic.digest(got["packets"]), g["digests"][s:e]), f"{name}: packet bytes"
+        checked += 1
+    assert checked > 50
 
 
 def test_reader_equals_live_reference_on_large_captures(tmp_path):

@@ -1,0 +1,111 @@
+"""End-to-end rates from capture files (GPU box, repo root): packets start in a pcap file and end as parse records in
+host memory (north_star: "the rate including the H2D/D2H copies must also be measured").
+
+1. file -> records: BASELINE config 3's 10M-packet IMIX batch written as a pcap into /dev/shm (tmpfs), then
+   examples/bin/pcap_parse -- the engine's reader (zero-copy map batches, or the copying reader into page-locked
+   buffers with --copy) overlapped with pcppx_parse_batch_host (chunked H2D, parse on the GPU, D2H into page-locked
+   record arrays) -- for 8 layer rows + checksums and for summaries only.
+2. the drop-in benchmark: examples/bin/benchmark (the reference's PcapPlusPlus-benchmark loop with the batch prepass)
+   beside oracle/_ref/benchmark_ref (the reference's benchmark.cpp compiled unchanged, one core) on the config-1 10k
+   pcap, the reference's example.pcap (frozen in tests/golden/capture_example.npz) and the 10M IMIX pcap.
+
+  python tools/e2e_file.py --out gpurun_out/r03_e2e_file.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+from pcapplusplus_amd import synth  # noqa: E402
+from pcapplusplus_amd.pcap import write_pcap  # noqa: E402
+
+
+def run(cmd, timeout=600) -> str:
+    r = subprocess.run([str(c) for c in cmd], capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise SystemExit(f"{cmd} failed ({r.returncode}): {r.stderr[-2000:]}")
+    return r.stdout
+
+
+def bench_pair(pcap: Path, reps: tuple[int, int], n: int) -> dict:
+    """Per-run time of the reference benchmark and of the engine's drop-in, from two repetition counts (process
+    start-up, file open and HIP initialisation cancel out), as tools/config1.py does."""
+    out = {"packets": n, "pcap_bytes": pcap.stat().st_size}
+    for name, exe, rr in (("reference_benchmark", ROOT / "oracle" / "_ref" / "benchmark_ref", reps),
+                          ("engine_benchmark", ROOT / "examples" / "bin" / "benchmark", reps)):
+        if not exe.exists():
+            continue
+        walls = []
+        for r in rr:
+            t = time.perf_counter()
+            last = run([exe, pcap, "packet", r], timeout=1200).strip().splitlines()[-1]
+            walls.append(time.perf_counter() - t)
+        ms = (walls[1] - walls[0]) / (rr[1] - rr[0]) * 1e3
+        out[name] = {"ms_per_run": round(ms, 4), "Mpackets_per_s": round(n / ms / 1e3, 2), "stdout": last,
+                     "threads": 1 if name == "reference_benchmark" else "1 host thread + reader thread + GPU",
+                     "reps": list(rr)}
+    if "reference_benchmark" in out and "engine_benchmark" in out:
+        out["speedup"] = round(out["reference_benchmark"]["ms_per_run"] / out["engine_benchmark"]["ms_per_run"], 2)
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--packets", type=int, default=10_000_000)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--shm", default="/dev/shm")
+    args = ap.parse_args()
+    res = {"cores": len(os.sched_getaffinity(0))}
+    big = Path(args.shm) / f"pcppx_e2e_{os.getpid()}.pcap"
+    try:
+        t = time.time()
+        b = synth.config(3, args.packets)
+        write_pcap(big, b)
+        res["imix_pcap"] = {"packets": b.n, "bytes": big.stat().st_size, "wire_bytes": int(b.caplens.sum()),
+                            "gen_write_seconds": round(time.time() - t, 1), "where": "tmpfs (/dev/shm)"}
+        del b
+        print(json.dumps(res["imix_pcap"]), flush=True)
+        runs = {}
+        for tag, extra in (("map_l8_csum", []), ("copy_l8_csum", ["--copy"]),
+                           ("map_summary", ["--layers", "0", "--checksums", "0"]),
+                           ("copy_summary", ["--copy", "--layers", "0", "--checksums", "0"])):
+            line = run([ROOT / "examples" / "bin" / "pcap_parse", big, "--reps", "3", *extra], timeout=900)
+            runs[tag] = json.loads(line.strip().splitlines()[-1])
+            print(tag, json.dumps(runs[tag]), flush=True)
+        res["file_to_records"] = runs
+        # the drop-in benchmark beside the reference's own, same host
+        c1 = Path(args.shm) / f"pcppx_cfg1_{os.getpid()}.pcap"
+        b1 = synth.config(1)
+        write_pcap(c1, b1)
+        res["benchmark_config1"] = bench_pair(c1, (10, 510), b1.n)
+        print("config1", json.dumps(res["benchmark_config1"]), flush=True)
+        c1.unlink()
+        from conftest import GOLDEN, load_golden
+
+        ex, _ = load_golden(GOLDEN / "capture_example.npz")
+        exf = Path(args.shm) / f"pcppx_example_{os.getpid()}.pcap"
+        write_pcap(exf, ex)
+        res["benchmark_example_pcap"] = bench_pair(exf, (10, 210), ex.n)
+        print("example.pcap", json.dumps(res["benchmark_example_pcap"]), flush=True)
+        exf.unlink()
+        res["benchmark_imix_10M"] = bench_pair(big, (1, 3), args.packets)
+        print("imix", json.dumps(res["benchmark_imix_10M"]), flush=True)
+    finally:
+        big.unlink(missing_ok=True)
+    line = json.dumps(res, indent=1)
+    if args.out:
+        Path(args.out).write_text(line + "\n")
+    print(line)
+
+
+if __name__ == "__main__":
+    main()
