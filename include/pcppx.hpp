@@ -36,8 +36,11 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "pcppx.h"
@@ -116,6 +119,35 @@ private:
 };
 inline const IPv4Address IPv4Address::Zero{};
 
+/* An allocator whose resize() leaves new elements uninitialised: batch buffers are sized for the largest batch and
+ * then filled by the reader / the engine, so zero-filling them first (256 MiB of packet buffer per read) would cost
+ * more than the read itself. */
+template <class T>
+struct DefaultInitAllocator : std::allocator<T>
+{
+	template <class U>
+	struct rebind
+	{
+		using other = DefaultInitAllocator<U>;
+	};
+	DefaultInitAllocator() = default;
+	template <class U>
+	DefaultInitAllocator(const DefaultInitAllocator<U>&) noexcept
+	{}
+	template <class U>
+	void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value)
+	{
+		::new (static_cast<void*>(p)) U;
+	}
+	template <class U, class... A>
+	void construct(U* p, A&&... a)
+	{
+		::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+	}
+};
+template <class T>
+using buffer = std::vector<T, DefaultInitAllocator<T>>;
+
 /* PacketParseOptions (Packet++/header/Packet.h:17-37) plus the engine's record options */
 struct PacketParseOptions
 {
@@ -147,11 +179,11 @@ struct PacketParseOptions
  * Plays the role of pcpp::RawPacketVector (Packet++/header/RawPacket.h) for the batch prepass. */
 struct RawPacketVector
 {
-	std::vector<uint8_t> data;
-	std::vector<uint64_t> offsets;
-	std::vector<uint32_t> caplens;
-	std::vector<uint64_t> timestampsNs;
-	std::vector<uint32_t> frameLens; /* RawPacket::getFrameLength (original wire length) */
+	buffer<uint8_t> data;
+	buffer<uint64_t> offsets;
+	buffer<uint32_t> caplens;
+	buffer<uint64_t> timestampsNs;
+	buffer<uint32_t> frameLens; /* RawPacket::getFrameLength (original wire length) */
 	uint16_t linkType = 1; /* LINKTYPE_ETHERNET */
 
 	size_t size() const { return caplens.size(); }
@@ -451,8 +483,8 @@ private:
 	uint8_t m_MaxLayers;
 
 public:
-	std::vector<pcppx_summary> summaries;
-	std::vector<pcppx_layer> layers;
+	buffer<pcppx_summary> summaries; /* filled by the engine (or the host parser) for every packet */
+	buffer<pcppx_layer> layers;       /* entries past a packet's chain are unspecified, as in pcppx.h */
 };
 
 /* PCPPX_LAYOUT_PACKED entries (include/pcppx.h) -> the FIXED layout: packet i's chain starts at its tile's base

@@ -44,8 +44,11 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "pcppx.h"
 
@@ -108,6 +111,26 @@ uint64_t int_pow(uint64_t x, uint32_t y)
 	return r;
 }
 
+// Parallel record walk of large pcap regions (pcppx_pcap_map_batch). The chain of record starts is sequential by
+// nature -- each header's caplen gives the next position, one dependent memory access per packet (~0.1 us on a
+// capture the caches do not hold) -- so a region is cut into kParThreads segments, each thread walks its segment
+// from a re-synchronised start (the first position from which kSyncChain records in a row pass readNextPacket's
+// checks), and the merge accepts a segment's chain only from a record start the chain before it actually lands on;
+// a segment whose chain it does not land on is walked again from that start. The walk is deterministic, so the
+// result is exactly the sequential walk's (a false start only costs the re-walk).
+constexpr size_t kParRegion = 256ull << 20;  // bytes per parallel round
+constexpr size_t kParMin = 16ull << 20;      // fewer bytes left: walk sequentially
+constexpr unsigned kParThreads = 16;
+constexpr size_t kSyncScan = 1u << 16;  // bytes a segment searches for a plausible record start
+constexpr int kSyncChain = 4;
+
+struct Chain
+{
+	std::vector<size_t> starts;  // record starts below the segment's end
+	size_t end = 0;              // the first record start at or past it, or where the stream ends
+	bool stop = false;           // the stream ends at `end` (an invalid record)
+};
+
 struct Packet
 {
 	const uint8_t* bytes;
@@ -134,6 +157,10 @@ struct pcppx_pcap
 
 	// pcap record at pos (readNextPacket). false = the stream ends here.
 	bool next_pcap(Packet& pk) const
+	{
+		return pcap_at(pos, pk);
+	}
+	bool pcap_at(size_t pos, Packet& pk) const
 	{
 		if (size - pos < 16)
 			return false;
@@ -273,6 +300,90 @@ struct pcppx_pcap
 	bool next(Packet& pk)
 	{
 		return ng ? next_pcapng(pk) : next_pcap(pk);
+	}
+
+	// the sequential chain from p (a record start or a guess) up to hi
+	void walk(size_t p, size_t hi, Chain& c) const
+	{
+		Packet pk;
+		while (p < hi)
+		{
+			if (!pcap_at(p, pk))
+			{
+				c.end = p;
+				c.stop = true;
+				return;
+			}
+			c.starts.push_back(p);
+			p = pk.next_pos;
+		}
+		c.end = p;
+	}
+
+	bool plausible(size_t p) const
+	{
+		Packet pk;
+		for (int k = 0; k < kSyncChain; ++k)
+		{
+			if (!pcap_at(p, pk))
+				return false;
+			p = pk.next_pos;
+			if (p >= size)
+				return true;
+		}
+		return true;
+	}
+
+	// every record start in [pos, region_end) (and *end, *stop as Chain's), as the sequential walk finds them
+	void parallel_starts(size_t region_end, std::vector<size_t>& out, size_t* end, bool* stop) const
+	{
+		constexpr unsigned T = kParThreads;
+		size_t lo[T + 1];
+		for (unsigned t = 0; t <= T; ++t)
+			lo[t] = pos + (region_end - pos) / T * t;
+		lo[T] = region_end;
+		std::vector<Chain> seg(T);
+		std::vector<std::thread> th;
+		for (unsigned t = 0; t < T; ++t)
+			th.emplace_back([&, t] {
+				size_t s0 = lo[t];
+				if (t > 0)
+				{
+					const size_t lim = std::min(lo[t + 1], lo[t] + kSyncScan);
+					while (s0 < lim && !plausible(s0))
+						++s0;
+					if (s0 >= lim)
+					{
+						seg[t].end = lo[t];  // no start found: the merge walks this segment
+						return;
+					}
+				}
+				walk(s0, lo[t + 1], seg[t]);
+			});
+		for (auto& x : th)
+			x.join();
+		out = std::move(seg[0].starts);
+		*end = seg[0].end;
+		*stop = seg[0].stop;
+		for (unsigned t = 1; t < T && !*stop; ++t)
+		{
+			const std::vector<size_t>& c = seg[t].starts;
+			auto it = std::lower_bound(c.begin(), c.end(), *end);
+			if (it != c.end() && *it == *end)
+			{
+				out.insert(out.end(), it, c.end());  // the true chain lands on this segment's chain: one chain from here
+				*end = seg[t].end;
+				*stop = seg[t].stop;
+			}
+			else
+			{
+				Chain redo;
+				walk(*end, lo[t + 1], redo);
+				out.insert(out.end(), redo.starts.begin(), redo.starts.end());
+				*end = redo.end;
+				*stop = redo.stop;
+			}
+		}
 	}
 };
 
@@ -418,6 +529,42 @@ extern "C"
 		*data = r->map;
 		*data_len = r->size;
 		uint32_t n = 0;
+		// large pcap regions: the parallel walk (identical records), then the fields of each record in parallel
+		while (!r->ng && !r->done && n < max_packets && r->size - r->pos >= kParMin)
+		{
+			const size_t region_end = r->pos + std::min(r->size - r->pos, kParRegion);
+			std::vector<size_t> starts;
+			size_t end = 0;
+			bool stop = false;
+			r->parallel_starts(region_end, starts, &end, &stop);
+			const size_t k = std::min(starts.size(), (size_t)(max_packets - n));
+			std::vector<std::thread> th;
+			for (unsigned t = 0; t < kParThreads; ++t)
+				th.emplace_back([&, t] {
+					for (size_t i = k * t / kParThreads; i < k * (t + 1) / kParThreads; ++i)
+					{
+						Packet pk;
+						(void)r->pcap_at(starts[i], pk);  // a record of the chain: valid
+						offsets[n + i] = (uint64_t)(pk.bytes - r->map);
+						caplens[n + i] = pk.keep;
+						if (frame_lens)
+							frame_lens[n + i] = pk.frame_len;
+						if (timestamps_ns)
+							timestamps_ns[n + i] = pk.ts_ns;
+					}
+				});
+			for (auto& x : th)
+				x.join();
+			n += (uint32_t)k;
+			if (k < starts.size())
+			{
+				r->pos = starts[k];  // the batch is full: the next one starts at this record
+				break;
+			}
+			r->pos = end;
+			if (stop)
+				r->done = true;
+		}
 		while (!r->done && n < max_packets)
 		{
 			Packet pk;

@@ -254,3 +254,48 @@ def test_sanitizers(tmp_path):
     r = subprocess.run([str(exe), "200"] + files, capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.startswith(f"files={len(files)} ")
+
+
+def _big_pcap(tmp_path, name, n, seed, zero_payload=False, snaplen=262144, corrupt_at=None, cut_tail=False):
+    """A pcap large enough for the parallel record walk (>= 16 MiB), as bytes on disk."""
+    import struct
+
+    from pcapplusplus_amd import synth
+    from pcapplusplus_amd.pcap import write_pcap
+
+    b = synth.imix(n, seed)
+    if zero_payload:  # runs of zero bytes parse as chains of empty records: the false-start hazard
+        d = b.data.copy()
+        for i in range(0, b.n, 3):
+            o, c = int(b.offsets[i]), int(b.caplens[i])
+            d[o + 54:o + c] = 0
+        b = type(b)(d, b.offsets, b.caplens, b.linktype)
+    f = tmp_path / name
+    write_pcap(f, b, snaplen=snaplen)
+    raw = bytearray(f.read_bytes())
+    if corrupt_at is not None:  # an invalid record header: the stream ends there (readNextPacket, :799-886)
+        pos = 24 + 16 * corrupt_at + int(b.caplens[:corrupt_at].sum())
+        raw[pos + 8:pos + 12] = struct.pack("<I", 0x7FFFFFFF)
+    if cut_tail:
+        del raw[-37:]
+    f.write_bytes(bytes(raw))
+    return f
+
+
+@pytest.mark.parametrize("case", ["clean", "zeros", "corrupt", "snaplen", "cut"])
+def test_parallel_walk_equals_sequential(tmp_path, case):
+    """pcppx_pcap_map_batch walks large pcap regions in parallel (re-synchronised segments merged where the chains
+    meet): the same records as the sequential copying reader, on a 60-MiB capture -- clean, with runs of zero bytes
+    that look like empty records, with an invalid record mid-file (the stream ends there), with a snapshot length
+    below the packet sizes, and with the last record cut short."""
+    kw = {"clean": {}, "zeros": {"zero_payload": True}, "corrupt": {"corrupt_at": 123_457},
+          "snaplen": {"snaplen": 400}, "cut": {"cut_tail": True}}[case]
+    f = _big_pcap(tmp_path, f"{case}.pcap", 180_000, 11, **kw)
+    seq = native_read_all(f, max_packets=70_000, data_cap=1 << 30)
+    par = native_map_all(f, max_packets=70_000)
+    assert len(par["caplens"]) == len(seq["caplens"]) > 100_000 or case == "corrupt"
+    for key in ("caplens", "frame_lens", "ts_ns", "linktypes"):
+        assert np.array_equal(par[key], seq[key]), key
+    assert par["packets"] == seq["packets"]
+    if case == "corrupt":
+        assert len(par["caplens"]) == 123_457
