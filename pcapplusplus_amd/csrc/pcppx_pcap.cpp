@@ -482,6 +482,59 @@ extern "C"
 			return PCPPX_E_INVAL;
 		uint32_t n = 0;
 		uint64_t used = 0;
+		// large pcap regions: the parallel walk (identical records), then the fields and the copies in parallel
+		while (!r->ng && !r->done && n < max_packets && r->size - r->pos >= kParMin)
+		{
+			const size_t region_end = r->pos + std::min(r->size - r->pos, kParRegion);
+			std::vector<size_t> starts;
+			size_t end = 0;
+			bool stop = false;
+			r->parallel_starts(region_end, starts, &end, &stop);
+			// the records that fit: at most max_packets, and their bytes within data_cap (as the sequential loop below)
+			size_t k = 0;
+			std::vector<uint64_t> dst;
+			dst.reserve(std::min(starts.size(), (size_t)(max_packets - n)));
+			while (k < starts.size() && n + k < max_packets)
+			{
+				Packet pk;
+				(void)r->pcap_at(starts[k], pk);
+				if (used + pk.keep > data_cap)
+					break;
+				dst.push_back(used);
+				used += pk.keep;
+				++k;
+			}
+			if (k == 0 && n == 0 && !starts.empty())
+				return PCPPX_E_NOMEM;  // a single record does not fit the caller's buffer
+			std::vector<std::thread> th;
+			for (unsigned t = 0; t < kParThreads; ++t)
+				th.emplace_back([&, t] {
+					for (size_t i = k * t / kParThreads; i < k * (t + 1) / kParThreads; ++i)
+					{
+						Packet pk;
+						(void)r->pcap_at(starts[i], pk);
+						if (pk.keep)
+							std::memcpy(data + dst[i], pk.bytes, pk.keep);
+						offsets[n + i] = dst[i];
+						caplens[n + i] = pk.keep;
+						if (frame_lens)
+							frame_lens[n + i] = pk.frame_len == 0xFFFFFFFFu ? pk.keep : pk.frame_len;
+						if (timestamps_ns)
+							timestamps_ns[n + i] = pk.ts_ns;
+					}
+				});
+			for (auto& x : th)
+				x.join();
+			n += (uint32_t)k;
+			if (k < starts.size())
+			{
+				r->pos = starts[k];
+				break;
+			}
+			r->pos = end;
+			if (stop)
+				r->done = true;
+		}
 		while (!r->done && n < max_packets)
 		{
 			Packet pk;
@@ -548,7 +601,7 @@ extern "C"
 						offsets[n + i] = (uint64_t)(pk.bytes - r->map);
 						caplens[n + i] = pk.keep;
 						if (frame_lens)
-							frame_lens[n + i] = pk.frame_len;
+							frame_lens[n + i] = pk.frame_len == 0xFFFFFFFFu ? pk.keep : pk.frame_len;
 						if (timestamps_ns)
 							timestamps_ns[n + i] = pk.ts_ns;
 					}

@@ -288,11 +288,24 @@ def test_parallel_walk_equals_sequential(tmp_path, case):
     meet): the same records as the sequential copying reader, on a 60-MiB capture -- clean, with runs of zero bytes
     that look like empty records, with an invalid record mid-file (the stream ends there), with a snapshot length
     below the packet sizes, and with the last record cut short."""
+    import oracle
+
+    if not oracle.ref_available():
+        pytest.skip("the reference reader (oracle/_ref) is the sequential oracle here")
     kw = {"clean": {}, "zeros": {"zero_payload": True}, "corrupt": {"corrupt_at": 123_457},
           "snaplen": {"snaplen": 400}, "cut": {"cut_tail": True}}[case]
     f = _big_pcap(tmp_path, f"{case}.pcap", 180_000, 11, **kw)
-    seq = native_read_all(f, max_packets=70_000, data_cap=1 << 30)
+    want = oracle.ref_read_capture(f)  # PcapFileReaderDevice::getNextPacket, one packet at a time
+    cl = want["caplens"].astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(cl)])
+    seq = {k: want[k] for k in ("caplens", "frame_lens", "ts_ns", "linktypes")}
+    seq["packets"] = [want["data"][starts[i]:starts[i + 1]].tobytes() for i in range(len(cl))]
     par = native_map_all(f, max_packets=70_000)
+    # the copying reader takes the parallel walk too: batches cut by the byte limit as well as the count
+    cp = native_read_all(f, max_packets=50_000, data_cap=9_000_000)
+    for key in ("caplens", "frame_lens", "ts_ns", "linktypes"):
+        assert np.array_equal(cp[key], seq[key]), key
+    assert cp["packets"] == seq["packets"]
     assert len(par["caplens"]) == len(seq["caplens"]) > 100_000 or case == "corrupt"
     for key in ("caplens", "frame_lens", "ts_ns", "linktypes"):
         assert np.array_equal(par[key], seq[key]), key
