@@ -1951,11 +1951,13 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // whole window (false: tools/ab variant 50). Realign: a deep stack that ends past the window is re-gathered from a
 // dword-aligned start (mis <= 3 instead of <= 15) so that it fits (false: tools/ab variant 51).
 // LateGeneric: packets off the fast path are walked after the span stream ((4b)); tools/ab variant 53.
+// EarlyB (tools/ab variant 54/55): the second stream window is issued with the first, before the header gather.
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
-          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false>
+          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false,
+          bool EarlyB = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -2012,6 +2014,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	};
 	if (stream)
 		load(va, 0);
+	if (EarlyB && stream)  // tools/ab: both stream windows in flight during the gather and the parse
+		load(vb, 1);
 
 	// ---- (2) header gather into LDS: 8 lanes per packet, one 16-B chunk each (8 packets per wave-instruction) ----
 	Pkt p;
@@ -2302,7 +2306,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			};
 			// straight-line body (windows padded to an even count; loads past the span are clamped) so
 			// the compiler's vmcnt accounting sees one fixed issue order: one window always in flight
-			load(vb, 1);
+			if (!EarlyB)
+				load(vb, 1);
 			for (uint32_t wi = 0; wi < nwin; wi += 2)
 			{
 				process(va, wi);
@@ -3130,7 +3135,11 @@ constexpr int kParseWaves = 5, kParseSWin = 128;
 // walk's HBM peeks past the window); 1.5% faster than 112 B on config 3 in two interleaved A/Bs, and a two-round
 // 96 + 16 B gather is slower (profiles/r02_ab_windows96.txt)
 constexpr int kParseChunks = 6;
-#define PCPPX_PARSE_KERNEL parse_tile_kernel<kParseWaves, kParseSWin, kParseChunks, true>
+// round 3: both stream windows are issued before the header gather (EarlyB; same 96 VGPRs): 0.8-0.9% on config 3 in
+// interleaved A/Bs, fixed and packed layouts (profiles/r03_ab_earlyB_*.txt)
+#define PCPPX_PARSE_KERNEL                                                                                             \
+	parse_tile_kernel<kParseWaves, kParseSWin, kParseChunks, true, false, true, kParseChunks, false, true, false, false,  \
+	                  false, true, true, false, true>
 // parse-only launches (no checksums): no span stream; a 144-B window reached in two gather rounds (96 B for every
 // packet, the rest only for the deep stacks the first window cannot hold): 99.7% of config 5's deep stacks take the
 // fast path; 16 waves/CU of LDS (144 B: 0.88 ms on config 5, 160 B: 1.00 ms at 14 waves/CU, 112 B: 1.17 ms with

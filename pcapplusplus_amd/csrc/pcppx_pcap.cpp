@@ -119,8 +119,13 @@ uint64_t int_pow(uint64_t x, uint32_t y)
 // a segment whose chain it does not land on is walked again from that start. The walk is deterministic, so the
 // result is exactly the sequential walk's (a false start only costs the re-walk).
 constexpr size_t kParRegion = 256ull << 20;  // bytes per parallel round
-constexpr size_t kParMin = 16ull << 20;      // fewer bytes left: walk sequentially
-constexpr unsigned kParThreads = 16;
+constexpr size_t kParMin = 4ull << 20;       // fewer bytes left: walk sequentially
+constexpr unsigned kParThreads = 16;         // at most; one per MiB of the region at least
+unsigned par_threads(size_t bytes)
+{
+	const size_t t = bytes >> 20;
+	return t < 2 ? 2u : (t > kParThreads ? kParThreads : (unsigned)t);
+}
 constexpr size_t kSyncScan = 1u << 16;  // bytes a segment searches for a plausible record start
 constexpr int kSyncChain = 4;
 
@@ -337,8 +342,8 @@ struct pcppx_pcap
 	// every record start in [pos, region_end) (and *end, *stop as Chain's), as the sequential walk finds them
 	void parallel_starts(size_t region_end, std::vector<size_t>& out, size_t* end, bool* stop) const
 	{
-		constexpr unsigned T = kParThreads;
-		size_t lo[T + 1];
+		const unsigned T = par_threads(region_end - pos);
+		std::vector<size_t> lo(T + 1);
 		for (unsigned t = 0; t <= T; ++t)
 			lo[t] = pos + (region_end - pos) / T * t;
 		lo[T] = region_end;
@@ -506,10 +511,11 @@ extern "C"
 			}
 			if (k == 0 && n == 0 && !starts.empty())
 				return PCPPX_E_NOMEM;  // a single record does not fit the caller's buffer
+			const unsigned T = par_threads(region_end - r->pos);
 			std::vector<std::thread> th;
-			for (unsigned t = 0; t < kParThreads; ++t)
+			for (unsigned t = 0; t < T; ++t)
 				th.emplace_back([&, t] {
-					for (size_t i = k * t / kParThreads; i < k * (t + 1) / kParThreads; ++i)
+					for (size_t i = k * t / T; i < k * (t + 1) / T; ++i)
 					{
 						Packet pk;
 						(void)r->pcap_at(starts[i], pk);
@@ -591,10 +597,11 @@ extern "C"
 			bool stop = false;
 			r->parallel_starts(region_end, starts, &end, &stop);
 			const size_t k = std::min(starts.size(), (size_t)(max_packets - n));
+			const unsigned T = par_threads(region_end - r->pos);
 			std::vector<std::thread> th;
-			for (unsigned t = 0; t < kParThreads; ++t)
+			for (unsigned t = 0; t < T; ++t)
 				th.emplace_back([&, t] {
-					for (size_t i = k * t / kParThreads; i < k * (t + 1) / kParThreads; ++i)
+					for (size_t i = k * t / T; i < k * (t + 1) / T; ++i)
 					{
 						Packet pk;
 						(void)r->pcap_at(starts[i], pk);  // a record of the chain: valid

@@ -138,7 +138,7 @@ def test_gpu_edge_descriptors(engine):
     assert g[0]["flags"][4] == abi.F_OVERSIZE and g[0]["flags"][5] == abi.F_BAD_DESC
 
 
-@pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 200_000), (3, 200_000), (4, 200_000), (5, 200_000)])
+@pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 1_000_000), (3, 200_000), (4, 200_000), (5, 200_000)])
 def test_gpu_synthetic_configs(engine, cfg, n):
     b = synth.config(cfg, n)
     for opts in (abi.make_opts(), abi.make_opts(0, 8, False, 8)):
