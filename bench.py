@@ -264,7 +264,7 @@ def main() -> None:
     if rec_kind == "tuples" and ml:
         sys.exit("bench.py: --records tuples writes no layer records (use --max-layers 0)")
     opts = abi.make_opts(0, 8, want_csum, ml, abi.WINDOW_DEEP if args.window == "deep" else abi.WINDOW_DEFAULT,
-                         abi.LAYOUT_PACKED if layout == "packed" else abi.LAYOUT_FIXED)
+                         {"fixed": abi.LAYOUT_FIXED, "packed": abi.LAYOUT_PACKED}[layout])
     n = batch.n
     eng = Engine(local)
     data, offsets, caplens = to_device(batch, dev)
@@ -347,7 +347,7 @@ def main() -> None:
     chain_entries = int(torch.clamp(nl16, max=ml).sum().item()) if ml else 0
     per_pkt = (32 if summary is not None else 0) + (48 if tuples is not None else 0) + \
         (4 if flow_keys is not None else 0)
-    write_bytes = n * per_pkt + 8 * (chain_entries if layout == "packed" else n * ml)
+    write_bytes = n * per_pkt + {"fixed": 8 * n * ml, "packed": 8 * chain_entries}[layout]
     achieved = read_bytes / (kern_ms * 1e-3) / 1e9
 
     # sanity: every packet parses cleanly (synthetic data has no L7 triggers)
@@ -364,9 +364,17 @@ def main() -> None:
     if proto_stats is not None:  # collectStats over every launch (warmup + timed): the histogram of one pass
         launches = args.warmup + args.steps
         tot = proto_stats.cpu().numpy()
+        consistent = bool((tot % launches == 0).all() and int(tot[0]) // launches == n)
+        if world > 1:
+            # every rank's PacketStats summed, as FilterTraffic sums its per-core stats at exit
+            # (Examples/DpdkExample-FilterTraffic/main.cpp:279-287); after the timed region
+            tt = torch.tensor(np.concatenate([tot, [1 if consistent else 0]]).astype(np.int64), device=tdev)
+            dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+            tot, consistent = tt[:-1].cpu().numpy(), int(tt[-1]) == world
         stats_line = {f: int(tot[k]) // launches for k, f in enumerate(abi.PROTO_STATS_FIELDS)}
-        stats_line["launches"] = launches
-        stats_line["consistent"] = bool((tot % launches == 0).all() and stats_line["packet_count"] == n)
+        stats_line["launches_per_rank"] = launches
+        stats_line["ranks_merged"] = world
+        stats_line["consistent"] = consistent and stats_line["packet_count"] == n * world
     del ext_sum
 
     traffic, traffic_note = None, "not requested"

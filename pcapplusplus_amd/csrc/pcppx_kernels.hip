@@ -1952,12 +1952,17 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // dword-aligned start (mis <= 3 instead of <= 15) so that it fits (false: tools/ab variant 51).
 // LateGeneric: packets off the fast path are walked after the span stream ((4b)); tools/ab variant 53.
 // EarlyB (tools/ab variant 54/55): the second stream window is issued with the first, before the header gather.
+// StreamFirst: the span stream runs before the header gather and the parse. Its prefix picks need no parse result:
+// each lane takes the running prefix at its packet's first and last whole chunk and the sum of its partial last chunk;
+// after the parse the L4 whole-chunk sum is that difference less the packet's leading chunks before the L4 start
+// (LDS window), whenever the L4 layer runs to the packet's end (else whole chunks from HBM, as for sparse tiles). The
+// header gather then reads lines the stream has just brought into L2, and no stream register is live in the parse.
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
           bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false,
-          bool EarlyB = false>
+          bool EarlyB = false, bool StreamFirst = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -2014,8 +2019,58 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	};
 	if (stream)
 		load(va, 0);
-	if (EarlyB && stream)  // tools/ab: both stream windows in flight during the gather and the parse
+	if ((EarlyB || StreamFirst) && stream)  // both stream windows in flight during the gather and the parse
 		load(vb, 1);
+
+	// ---- (1b) StreamFirst: the whole span stream now, picking per packet the prefix before its first whole chunk (p0),
+	// before its last partial chunk (p1), and that partial chunk's sum (tsum) ----
+	const uintptr_t sf_a = (uintptr_t)pkt_addr, sf_e = sf_a + cap;
+	const uintptr_t sf_cs = (sf_a + 15) & ~(uintptr_t)15, sf_ce = sf_e & ~(uintptr_t)15;
+	uint32_t sf_p0 = 0, sf_p1 = 0, sf_tsum = 0;
+	if (StreamFirst && stream)
+	{
+		const bool whole = live && sf_cs <= sf_ce;
+		const int32_t t0 = whole ? (int32_t)((sf_cs - smin) >> 4) - 1 : -2;
+		const int32_t t1 = whole ? (int32_t)((sf_ce - smin) >> 4) - 1 : -2;
+		const int32_t te = (whole && sf_ce < sf_e) ? (int32_t)((sf_ce - smin) >> 4) : -2;
+		uint32_t carry = 0;
+		const uint32_t nwin = (nchunks + SWin - 1) / SWin;
+		auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
+#pragma unroll
+			for (int k = 0; k < SWin / 64; ++k)
+			{
+				const int32_t g = (int32_t)(win * SWin + 64 * k);
+				const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+				const uint32_t x = wave_incl_scan(h);
+				const uint32_t pre = carry + x;
+				const bool in0 = t0 >= g && t0 < g + 64, in1 = t1 >= g && t1 < g + 64;
+				if (__ballot(in0 || in1))
+				{
+					const uint32_t q0 = __shfl(pre, (t0 - g) & 63, 64);
+					const uint32_t q1 = __shfl(pre, (t1 - g) & 63, 64);
+					sf_p0 = in0 ? q0 : sf_p0;
+					sf_p1 = in1 ? q1 : sf_p1;
+				}
+				const bool ine = te >= g && te < g + 64;
+				if (__ballot(ine))
+				{
+					const int src = (te - g) & 63;
+					const uint4 d = make_uint4(__shfl(v[k].x, src, 64), __shfl(v[k].y, src, 64), __shfl(v[k].z, src, 64),
+					                           __shfl(v[k].w, src, 64));
+					if (ine)
+						sf_tsum = chunk_sum(d, sf_ce, sf_ce, sf_e);
+				}
+				carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+			}
+		};
+		for (uint32_t wi = 0; wi < nwin; wi += 2)
+		{
+			process(va, wi);
+			load(va, wi + 2);
+			process(vb, wi + 1);
+			load(vb, wi + 3);
+		}
+	}
 
 	// ---- (2) header gather into LDS: 8 lanes per packet, one 16-B chunk each (8 packets per wave-instruction) ----
 	Pkt p;
@@ -2260,6 +2315,24 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				l4c = l4_checksum_from(w, r, fw, ph, &l4s);
 				w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
 			}
+		}
+		else if (StreamFirst)
+		{
+			// the prefixes were picked before the parse: whole chunks [f0, f1) = [cs, ce) less [cs, f0) when the L4 layer
+			// ends at the packet's end (then f1 = ce and the partial tail is the captured one); anything else (a trailer
+			// or IP padding after the L4 layer, an L4 start in the last partial chunk, a sparse tile) from HBM
+			const bool combine = stream && need && ae == sf_e && f0 >= sf_cs && f0 <= f1;
+			if (combine)
+			{
+				uint32_t lead = 0;  // the packet's whole chunks before the L4 start: in the header window
+				for (uintptr_t c = sf_cs; c < f0; c += 16)
+					lead += edge_sum(p, c, c + 16);
+				fsum = sf_p1 - sf_p0 - lead;
+				tsum = sf_tsum;
+				tail_done = true;
+			}
+			else if (full)
+				fsum = full_chunks_sum(f0, f1);
 		}
 		else if (stream)
 		{

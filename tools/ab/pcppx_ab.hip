@@ -185,6 +185,9 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 53: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // checksum instance, late generic walk
 	case 54: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // early second window
 	case 55: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // early second window, 4 waves
+	case 56: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // stream first
+	case 57: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, false, false, true, 6, false, true, false, false, false, true, true, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // stream first, cached loads
+	case 58: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // stream first, 6 waves
 	case 51: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, false>), grid, dim3(kTile), 0, stream, prm); break;  // tight second round, no realign
 	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;

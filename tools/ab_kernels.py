@@ -35,6 +35,9 @@ cases = {
     "tile/packed": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 0),
     "tile/packed-earlyB": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 54),
     "tile/packed-skipgen": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 52),
+    "tile/packed-sf": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 56),
+    "tile/packed-sf-cached": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 57),
+    "tile/packed-sf-w6": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 58),
     "tile/late-generic": (abi.make_opts(0, 8, True, 8), 53),
     "tile/chaintails": (abi.make_opts(0, 8, True, 8), 12),
     "tile/ring": (abi.make_opts(0, 8, True, 8), 40),
@@ -61,6 +64,7 @@ cases = {
 _ml = int(__import__("os").environ.get("AB_ML", "8"))
 cases.update({
     "po/product": (abi.make_opts(0, 8, False, _ml), 0),
+    "po/packed": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 0),
     "po/w7": (abi.make_opts(0, 8, False, _ml), 20),
     "po/w10": (abi.make_opts(0, 8, False, _ml), 21),
     "po/w10r6": (abi.make_opts(0, 8, False, _ml), 22),
