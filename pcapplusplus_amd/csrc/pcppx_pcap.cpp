@@ -121,6 +121,28 @@ uint64_t int_pow(uint64_t x, uint32_t y)
 constexpr size_t kParRegion = 256ull << 20;  // bytes per parallel round
 constexpr size_t kParMin = 4ull << 20;       // fewer bytes left: walk sequentially
 constexpr unsigned kParThreads = 16;         // at most; one per MiB of the region at least
+// fn(t) for t in [0, T): on new threads where they can be started, the rest on the calling thread (a thread that
+// cannot be created never fails the read)
+template <class F>
+void run_parallel(unsigned T, const F& fn)
+{
+	std::vector<std::thread> th;
+	unsigned started = 1;
+	try
+	{
+		for (; started < T; ++started)
+			th.emplace_back(fn, started);
+	}
+	catch (...)
+	{
+	}
+	fn(0u);
+	for (unsigned t = started; t < T; ++t)
+		fn(t);
+	for (auto& x : th)
+		x.join();
+}
+
 unsigned par_threads(size_t bytes)
 {
 	const size_t t = bytes >> 20;
@@ -348,9 +370,7 @@ struct pcppx_pcap
 			lo[t] = pos + (region_end - pos) / T * t;
 		lo[T] = region_end;
 		std::vector<Chain> seg(T);
-		std::vector<std::thread> th;
-		for (unsigned t = 0; t < T; ++t)
-			th.emplace_back([&, t] {
+		run_parallel(T, [&](unsigned t) {
 				size_t s0 = lo[t];
 				if (t > 0)
 				{
@@ -365,8 +385,6 @@ struct pcppx_pcap
 				}
 				walk(s0, lo[t + 1], seg[t]);
 			});
-		for (auto& x : th)
-			x.join();
 		out = std::move(seg[0].starts);
 		*end = seg[0].end;
 		*stop = seg[0].stop;
@@ -512,9 +530,7 @@ extern "C"
 			if (k == 0 && n == 0 && !starts.empty())
 				return PCPPX_E_NOMEM;  // a single record does not fit the caller's buffer
 			const unsigned T = par_threads(region_end - r->pos);
-			std::vector<std::thread> th;
-			for (unsigned t = 0; t < T; ++t)
-				th.emplace_back([&, t] {
+			run_parallel(T, [&](unsigned t) {
 					for (size_t i = k * t / T; i < k * (t + 1) / T; ++i)
 					{
 						Packet pk;
@@ -529,8 +545,6 @@ extern "C"
 							timestamps_ns[n + i] = pk.ts_ns;
 					}
 				});
-			for (auto& x : th)
-				x.join();
 			n += (uint32_t)k;
 			if (k < starts.size())
 			{
@@ -598,9 +612,7 @@ extern "C"
 			r->parallel_starts(region_end, starts, &end, &stop);
 			const size_t k = std::min(starts.size(), (size_t)(max_packets - n));
 			const unsigned T = par_threads(region_end - r->pos);
-			std::vector<std::thread> th;
-			for (unsigned t = 0; t < T; ++t)
-				th.emplace_back([&, t] {
+			run_parallel(T, [&](unsigned t) {
 					for (size_t i = k * t / T; i < k * (t + 1) / T; ++i)
 					{
 						Packet pk;
@@ -613,8 +625,6 @@ extern "C"
 							timestamps_ns[n + i] = pk.ts_ns;
 					}
 				});
-			for (auto& x : th)
-				x.join();
 			n += (uint32_t)k;
 			if (k < starts.size())
 			{
