@@ -53,9 +53,11 @@ def r01_lib(so: Path = R01_SO) -> C.CDLL:
 
 
 def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers, stream: int,
-                 variant: int) -> None:
+                 variant: int, tuples=None) -> None:
     b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
-    rec = abi.Records(abi.ptr(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None)
+    rec = abi.Records(abi.ptr(summary) if summary is not None else None,
+                      abi.ptr(layers) if (layers is not None and opts.max_layers) else None, None,
+                      abi.ptr(tuples) if tuples is not None else None)
     if variant in (R01, PREV):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
         abi.check(r01_lib(R01_SO if variant == R01 else PREV_SO).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
                   "pcppx_r01_parse_device")

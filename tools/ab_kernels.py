@@ -35,6 +35,8 @@ cases = {
     "tile/packed": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 0),
     "tile/packed-earlyB": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 54),
     "tile/packed-skipgen": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 52),
+    "tile/packed-win3": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 65),
+    "tile/packed-win3x1k": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 66),
     "tile/packed-sf": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 56),
     "tile/packed-sf-cached": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 57),
     "tile/packed-sf-w6": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 58),
@@ -79,6 +81,13 @@ cases.update({
     "po/chaintails": (abi.make_opts(0, 8, False, _ml), 26),
     "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
     "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),
+    "po/c6": (abi.make_opts(0, 8, False, _ml), 60),
+    "po/c6w6": (abi.make_opts(0, 8, False, _ml), 61),
+    "po/c5w6": (abi.make_opts(0, 8, False, _ml), 63),
+    "po/persist": (abi.make_opts(0, 8, False, _ml), 70),
+    "po/persist-packed": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 70),
+    "po/persist-c6": (abi.make_opts(0, 8, False, _ml), 71),
+    "po/persist-half": (abi.make_opts(0, 8, False, _ml), 72),
     "po/gather-only": (abi.make_opts(0, 8, False, _ml), 29),
     "po/skip-generic": (abi.make_opts(0, 8, False, _ml), 44),
 })
