@@ -55,8 +55,11 @@ def parse_args():
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py; default profiles/traffic_cfg<N>.json); "
                          "used only if it was measured on this kernel source, config, size and record options")
     ap.add_argument("--no-traffic", action="store_true", help="do not report PMC traffic (the PMC passes themselves)")
-    ap.add_argument("--window", choices=("default", "deep"), default="default",
-                    help="checksum launches' header window (pcppx_opts.window): deep = two-round 144 B for deep stacks")
+    ap.add_argument("--window", choices=("auto", "default", "deep", "short"), default="auto",
+                    help="the header window the parse gathers (pcppx_opts.window; records identical): deep = two-round "
+                         "144 B for checksum launches over deep stacks, short = one 96-B round for parse-only launches over "
+                         "plain stacks (auto: " + ", ".join(f"config {c} {v}" for c, v in sorted(CONFIG_WINDOW.items())) +
+                         ", else default)")
     ap.add_argument("--layout", choices=("auto", "fixed", "packed"), default="auto",
                     help="layer-record layout (pcppx_opts.layout): fixed = max_layers entries per packet; packed = only the "
                          "chain's entries, dense per 64-packet tile (the same entries; auto: " + ", ".join(
@@ -73,6 +76,8 @@ def parse_args():
 CONFIG_PACKETS = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000_000}
 CONFIG_MAX_LAYERS = {2: 0, 3: 8, 4: 0, 5: 12}
 CONFIG_LAYOUT = {3: "packed", 5: "packed"}  # configs with layer records
+# plain Eth / VLAN / IP / L4 stacks (configs 2 and 4): the one-round parse-only window (PCPPX_WINDOW_SHORT)
+CONFIG_WINDOW = {2: "short", 4: "short"}
 KERNEL_SRC = ROOT / "pcapplusplus_amd" / "csrc" / "pcppx_kernels.hip"
 
 
@@ -84,7 +89,7 @@ def kernel_sha() -> str:
 
 
 def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool, layout: str = "fixed",
-                 records: str = "summary") -> tuple[int | None, str]:
+                 records: str = "summary", window: str = "default") -> tuple[int | None, str]:
     """(HBM bytes per parse launch, note) from a PMC traffic file, only if it matches this run exactly."""
     if not path.exists():
         return None, f"no PMC measurement ({path.name})"
@@ -93,8 +98,9 @@ def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool, layout: str 
     except (ValueError, OSError) as e:
         return None, f"unreadable {path.name}: {e}"
     want = {"config": cfg, "packets": n, "max_layers": ml, "checksums": csum, "layout": layout, "records": records,
+            "window": window,
             "kernel_sha": kernel_sha()}
-    got = {k: tj.get(k, {"layout": "fixed", "records": "summary"}.get(k)) for k in want}
+    got = {k: tj.get(k, {"layout": "fixed", "records": "summary", "window": "default"}.get(k)) for k in want}
     if got != want:
         return None, f"stale {path.name}: measured {got}, this run {want}"
     return int(tj["hbm_bytes_per_launch"]), f"{path.name} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
@@ -263,7 +269,9 @@ def main() -> None:
     rec_kind = args.records if args.records != "auto" else ("tuples" if cfg == 2 else "summary")
     if rec_kind == "tuples" and ml:
         sys.exit("bench.py: --records tuples writes no layer records (use --max-layers 0)")
-    opts = abi.make_opts(0, 8, want_csum, ml, abi.WINDOW_DEEP if args.window == "deep" else abi.WINDOW_DEFAULT,
+    window = args.window if args.window != "auto" else CONFIG_WINDOW.get(cfg, "default")
+    opts = abi.make_opts(0, 8, want_csum, ml, {"default": abi.WINDOW_DEFAULT, "deep": abi.WINDOW_DEEP,
+                                               "short": abi.WINDOW_SHORT}[window],
                          {"fixed": abi.LAYOUT_FIXED, "packed": abi.LAYOUT_PACKED}[layout])
     n = batch.n
     eng = Engine(local)
@@ -380,7 +388,7 @@ def main() -> None:
     traffic, traffic_note = None, "not requested"
     if not args.no_traffic:
         tp = Path(args.traffic) if args.traffic else ROOT / "profiles" / f"traffic_cfg{cfg}.json"
-        traffic, traffic_note = load_traffic(tp, cfg, n, ml, want_csum, layout, rec_kind)
+        traffic, traffic_note = load_traffic(tp, cfg, n, ml, want_csum, layout, rec_kind, window)
 
     e2e = None
     if not args.no_e2e and rank == 0 and world == 1:
@@ -463,7 +471,7 @@ def main() -> None:
                 "packets_per_gpu": n,
                 "wire_bytes_per_gpu": wire,
                 "checksums": want_csum,
-                "window": args.window,
+                "window": window,
                 "max_layers": ml,
                 "layout": layout,
                 "records": rec_kind,

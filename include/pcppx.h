@@ -124,15 +124,20 @@ typedef struct pcppx_opts {
 	uint8_t parse_until_osi;     /* pcpp::OsiModelLayer; 8 = OsiModelLayerUnknown */
 	uint8_t want_checksums;      /* compute IPv4 / L4 checksums */
 	uint8_t max_layers;          /* 0 = do not write layers; else layers stride per packet (1..16) */
-	uint8_t window;              /* PCPPX_WINDOW_*: the header window of checksum launches (records are identical
-	                                either way; parse-only launches always gather a two-round deep window) */
+	uint8_t window;              /* PCPPX_WINDOW_*: the header window the parse gathers per packet (a speed choice for
+	                                the caller's traffic: the records are identical whichever window runs) */
 	uint8_t layout;              /* PCPPX_LAYOUT_*: how pcppx_records.layers is laid out */
 	uint8_t reserved[3];
 } pcppx_opts;
-#define PCPPX_WINDOW_DEFAULT 0 /* 96-B header window, 5 waves/SIMD: the fastest for Eth / VLAN / IP / L4 traffic */
-#define PCPPX_WINDOW_DEEP 1    /* + a second gather round up to 144 B for stacks deeper than the first window
-                                  (QinQ, MPLS, GRE, IPv6 extensions): those packets stay on the fast path instead of
-                                  the generic walk; 4 waves/SIMD */
+#define PCPPX_WINDOW_DEFAULT 0 /* checksum launches: one 96-B window, 5 waves/SIMD (the fastest for Eth / VLAN / IP /
+                                  L4 traffic); parse-only launches: 96 B plus a second gather round up to 144 B for the
+                                  stacks the first window cannot hold (QinQ, MPLS, GRE, IPv6 extensions) */
+#define PCPPX_WINDOW_DEEP 1    /* checksum launches too gather the two-round 144-B window: deep stacks stay on the
+                                  fast path instead of the generic walk; 4 waves/SIMD. Parse-only: as DEFAULT */
+#define PCPPX_WINDOW_SHORT 2   /* parse-only launches: one 96-B gather round and no second one (7 KiB of LDS per wave
+                                  instead of 10: more waves per CU) -- faster on plain Eth / VLAN / IP / L4 traffic
+                                  (IMIX 7%, 64-B packets 16%), about 2x slower on deep encapsulation, whose stacks past
+                                  96 B take the generic walk. Checksum launches: as DEFAULT */
 
 /* pcppx_records.layers layouts (pcppx_opts.layout). Both hold the same pcppx_layer entries, bit for bit:
  *   FIXED:  packet i's layer k is layers[i * max_layers + k], k < min(n_layers, max_layers); entries past

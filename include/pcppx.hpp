@@ -155,7 +155,9 @@ struct PacketParseOptions
 	OsiModelLayer parseUntilLayer = OsiModelLayerUnknown;
 	bool computeChecksums = true; /* IPv4 header + TCP/UDP checksum verification */
 	uint8_t maxLayers = PCPPX_MAX_LAYERS;
-	bool deepWindow = false; /* PCPPX_WINDOW_DEEP: two-round 144-B header window for checksum launches over deep stacks */
+	bool deepWindow = false;  /* PCPPX_WINDOW_DEEP: two-round 144-B header window for checksum launches over deep stacks */
+	bool shortWindow = false; /* PCPPX_WINDOW_SHORT: one 96-B round for parse-only launches over plain stacks (ignored
+	                             when deepWindow is set) */
 
 	PacketParseOptions() = default;
 	PacketParseOptions(ProtocolTypeFamily until, OsiModelLayer layer = OsiModelLayerUnknown)
@@ -170,7 +172,7 @@ struct PacketParseOptions
 		o.parse_until_osi = parseUntilLayer;
 		o.want_checksums = computeChecksums ? 1 : 0;
 		o.max_layers = maxLayers;
-		o.window = deepWindow ? PCPPX_WINDOW_DEEP : PCPPX_WINDOW_DEFAULT;
+		o.window = deepWindow ? PCPPX_WINDOW_DEEP : (shortWindow ? PCPPX_WINDOW_SHORT : PCPPX_WINDOW_DEFAULT);
 		return o;
 	}
 };

@@ -18,7 +18,7 @@ ENGINE_SO = PKG_DIR / "libpcppx.so"
 ABI_VERSION = 5
 MAX_LAYERS = 16
 MAX_CAPLEN = 65535
-WINDOW_DEFAULT, WINDOW_DEEP = 0, 1  # pcppx_opts.window (PCPPX_WINDOW_*)
+WINDOW_DEFAULT, WINDOW_DEEP, WINDOW_SHORT = 0, 1, 2  # pcppx_opts.window (PCPPX_WINDOW_*)
 LAYOUT_FIXED, LAYOUT_PACKED = 0, 1  # pcppx_opts.layout (PCPPX_LAYOUT_*)
 PACKED_MAX_LAYERS = 12
 TILE = 64  # packets per tile of the PACKED layout
@@ -152,12 +152,13 @@ def ipv4_to_int(dotted: str) -> int:
 def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checksums: bool = True,
               max_layers: int = MAX_LAYERS, window: int = 0, layout: int = LAYOUT_FIXED) -> Opts:
     """pcpp::PacketParseOptions defaults (Packet++/header/Packet.h:17-37) + output selection; window:
-    WINDOW_DEFAULT / WINDOW_DEEP (the checksum launch's header window, records identical); layout: LAYOUT_FIXED /
+    WINDOW_DEFAULT / WINDOW_DEEP / WINDOW_SHORT (the header window the parse gathers: a speed choice, records
+    identical; DEEP: two rounds for checksum launches, SHORT: one 96-B round for parse-only launches); layout: LAYOUT_FIXED /
     LAYOUT_PACKED (the layer entries, bit for bit the same; unpack_layers)."""
     if not 0 <= max_layers <= MAX_LAYERS:
         raise ValueError(f"max_layers must be in [0, {MAX_LAYERS}]")
-    if window not in (WINDOW_DEFAULT, WINDOW_DEEP):
-        raise ValueError("window must be WINDOW_DEFAULT or WINDOW_DEEP")
+    if window not in (WINDOW_DEFAULT, WINDOW_DEEP, WINDOW_SHORT):
+        raise ValueError("window must be WINDOW_DEFAULT, WINDOW_DEEP or WINDOW_SHORT")
     if layout not in (LAYOUT_FIXED, LAYOUT_PACKED) or (layout == LAYOUT_PACKED and max_layers > PACKED_MAX_LAYERS):
         raise ValueError(f"layout must be LAYOUT_FIXED, or LAYOUT_PACKED with max_layers <= {PACKED_MAX_LAYERS}")
     o = Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, window)

@@ -183,7 +183,7 @@ bool ok(hipError_t e)
 
 int valid_opts(const pcppx_opts* o)
 {
-	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->window > PCPPX_WINDOW_DEEP ||
+	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->window > PCPPX_WINDOW_SHORT ||
 	    o->layout > PCPPX_LAYOUT_PACKED || (o->layout == PCPPX_LAYOUT_PACKED && o->max_layers > PCPPX_PACKED_MAX_LAYERS))
 		return PCPPX_E_INVAL;
 	return PCPPX_OK;

@@ -1957,14 +1957,12 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // after the parse the L4 whole-chunk sum is that difference less the packet's leading chunks before the L4 start
 // (LDS window), whenever the L4 layer runs to the packet's end (else whole chunks from HBM, as for sparse tiles). The
 // header gather then reads lines the stream has just brought into L2, and no stream register is live in the parse.
-// Win3: the span stream keeps a third window in flight once the parse is done (issued after it, so the parse's register
-// peak does not grow): 3 x SWin chunks per wave during the stream instead of 2.
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
           bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false,
-          bool EarlyB = false, bool StreamFirst = false, bool Win3 = false, bool Persist = false>
+          bool EarlyB = false, bool StreamFirst = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1984,141 +1982,372 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	const bool want_csum = Csum && prm.want_csum;  // uniform
 
 	const uint32_t lane = threadIdx.x;
-	// Persist: a persistent grid; each wave walks tiles blockIdx.x, + gridDim.x, ... and keeps the NEXT tile's descriptors
-	// and first-round header window in flight (registers) while it parses the current one: the two dependent HBM round
-	// trips of a tile (descriptors -> header gather) leave the wave's critical path
-	static_assert(!Persist || !Csum, "Persist: parse-only instances");
-	// the lane index as the loop sees it: made opaque at every iteration, so that the compiler does not hoist lane-derived
-	// addresses of the whole body out of the loop (they would stay live across it: 220 VGPRs instead of ~110)
-	uint32_t ln = lane;
-	constexpr int kPF = Persist ? Chunks1 : 1;  // first-round 16-B pieces per lane: 64 packets x Chunks1 / 64 lanes
-	uint4 pf[kPF];
-	uint32_t pf_mask = 0;
-	uint64_t cur_off = 0, nx_off = 0;
-	uint32_t cur_cap = 0, nx_cap = 0;
-	const uint32_t ntiles = (uint32_t)(((uint64_t)prm.n + kTile - 1) / kTile);
-	auto ld_desc = [&](uint64_t t, uint64_t& o, uint32_t& c) {
-		const uint64_t j = t * kTile + ln;
-		const bool ok = j < prm.n;
-		o = ok ? prm.offsets[j] : 0;
-		c = ok ? prm.caplens[j] : 0;
-	};
-	// a packet's first-round gather range (the body's p.a0 / p.nch rules)
-	auto first_round = [&](uint64_t t, uint64_t o, uint32_t c, uint64_t& a0, uint32_t& nch) {
-		bool e = true;
-		const bool in_ = t * kTile + ln < prm.n;
-		const bool lv = in_ && !(in_ ? desc_flags(o, c, prm.data_len, &e) : 1u) && !e;
-		const uintptr_t g = (uintptr_t)(prm.data + (lv ? o : 0));
-		a0 = g & ~(uintptr_t)15;
-		const uint32_t nd = ((uint32_t)(g - a0) + c + 15) >> 4;
-		nch = lv ? (nd < (uint32_t)Chunks1 ? nd : (uint32_t)Chunks1) : 0u;
-	};
-	// issue the first-round pieces of the tile whose ranges are in m_a0 / m_nch: piece k * 64 + lane is chunk
-	// (piece % Chunks1) of packet (piece / Chunks1), so consecutive lanes read consecutive chunks
-	auto issue_pf = [&]() {
-		pf_mask = 0;
+	const uint32_t i = blockIdx.x * kTile + lane;
+	const bool in = i < prm.n;
+	const uint64_t off = in ? prm.offsets[i] : 0;
+	const uint32_t cap = in ? prm.caplens[i] : 0;
+	bool empty = true;
+	const uint32_t bad = in ? desc_flags(off, cap, prm.data_len, &empty) : 0;
+	const bool live = in && !bad && !empty;
+
+	// ---- tile span for the L4 checksum stream: whole packets, known before the parse, so the first
+	// stream window is issued now and lands while the headers are gathered and parsed ----
+	const uint64_t pkt_addr = (uint64_t)(uintptr_t)prm.data + off;
+	// wave reductions are uniform: moved to SGPRs so the window loop is a scalar loop
+	const uint64_t smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
+	const uint64_t emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
+	const uint64_t wire = uniform_u64(wave_sum_u64(live ? cap : 0));
+	const bool stream = want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
+	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
+	uint4 va[SWin / 64], vb[SWin / 64];
+	auto load = [&](uint4 (&v)[SWin / 64], uint32_t win) {
 #pragma unroll
-		for (int k = 0; k < kPF; ++k)
+		for (int k = 0; k < SWin / 64; ++k)
 		{
-			const uint32_t pc = (uint32_t)k * kTile + ln, q = pc / (uint32_t)Chunks1, sub = pc - q * (uint32_t)Chunks1;
-			if (sub < m_nch[q])
+			// clamped, not masked: lanes past the span re-read its last chunk (same line, no extra
+			// traffic); their values lie after every prefix target, so they are inert
+			const uint32_t c = win * SWin + 64 * k + lane;
+			const uintptr_t a = smin + 16ull * (c < nchunks ? c : nchunks - 1);
+			if (NT)
 			{
-				pf[k] = ld16(m_a0[q] + 16 * sub);
-				pf_mask |= 1u << k;
+				const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<gptr16>(a));
+				v[k] = make_uint4(t.x, t.y, t.z, t.w);
 			}
+			else
+				v[k] = ld16(a);
 		}
 	};
-	auto put_pf = [&]() {
+	if (stream)
+		load(va, 0);
+	if ((EarlyB || StreamFirst) && stream)  // both stream windows in flight during the gather and the parse
+		load(vb, 1);
+
+	// ---- (1b) StreamFirst: the whole span stream now, picking per packet the prefix before its first whole chunk (p0),
+	// before its last partial chunk (p1), and that partial chunk's sum (tsum) ----
+	const uintptr_t sf_a = (uintptr_t)pkt_addr, sf_e = sf_a + cap;
+	const uintptr_t sf_cs = (sf_a + 15) & ~(uintptr_t)15, sf_ce = sf_e & ~(uintptr_t)15;
+	uint32_t sf_p0 = 0, sf_p1 = 0, sf_tsum = 0;
+	if (StreamFirst && stream)
+	{
+		const bool whole = live && sf_cs <= sf_ce;
+		const int32_t t0 = whole ? (int32_t)((sf_cs - smin) >> 4) - 1 : -2;
+		const int32_t t1 = whole ? (int32_t)((sf_ce - smin) >> 4) - 1 : -2;
+		const int32_t te = (whole && sf_ce < sf_e) ? (int32_t)((sf_ce - smin) >> 4) : -2;
+		uint32_t carry = 0;
+		const uint32_t nwin = (nchunks + SWin - 1) / SWin;
+		auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
 #pragma unroll
-		for (int k = 0; k < kPF; ++k)
-		{
-			const uint32_t pc = (uint32_t)k * kTile + ln, q = pc / (uint32_t)Chunks1, sub = pc - q * (uint32_t)Chunks1;
-			if ((pf_mask >> k) & 1u)
-			{
-				lptr32w slot = (lptr32w)(stage) + q * kTSlotDw + 4 * sub;
-				slot[0] = pf[k].x;
-				slot[1] = pf[k].y;
-				slot[2] = pf[k].z;
-				slot[3] = pf[k].w;
-			}
-		}
-	};
-	if constexpr (Persist)
-	{
-		ld_desc(blockIdx.x, cur_off, cur_cap);
-		ld_desc((uint64_t)blockIdx.x + gridDim.x, nx_off, nx_cap);
-		uint64_t a0;
-		uint32_t nch;
-		first_round(blockIdx.x, cur_off, cur_cap, a0, nch);
-		m_a0[ln] = a0;
-		m_nch[ln] = nch;
-		__syncthreads();
-		issue_pf();
-	}
-
-	for (uint32_t tile = blockIdx.x;; tile += gridDim.x)
-	{
-	if (Persist && tile >= ntiles)
-		break;
-	if constexpr (Persist)
-		asm volatile("" : "+v"(ln));
-	{
-	const uint32_t lane = ln;
-		const uint32_t i = tile * kTile + lane;
-		const bool in = i < prm.n;
-		const uint64_t off = Persist ? cur_off : (in ? prm.offsets[i] : 0);
-		const uint32_t cap = Persist ? cur_cap : (in ? prm.caplens[i] : 0);
-		bool empty = true;
-		const uint32_t bad = in ? desc_flags(off, cap, prm.data_len, &empty) : 0;
-		const bool live = in && !bad && !empty;
-
-		// ---- tile span for the L4 checksum stream: whole packets, known before the parse, so the first
-		// stream window is issued now and lands while the headers are gathered and parsed ----
-		const uint64_t pkt_addr = (uint64_t)(uintptr_t)prm.data + off;
-		// wave reductions are uniform: moved to SGPRs so the window loop is a scalar loop
-		const uint64_t smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
-		const uint64_t emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
-		const uint64_t wire = uniform_u64(wave_sum_u64(live ? cap : 0));
-		const bool stream = want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
-		const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
-		uint4 va[SWin / 64], vb[SWin / 64];
-		auto load = [&](uint4 (&v)[SWin / 64], uint32_t win) {
-	#pragma unroll
 			for (int k = 0; k < SWin / 64; ++k)
 			{
-				// clamped, not masked: lanes past the span re-read its last chunk (same line, no extra
-				// traffic); their values lie after every prefix target, so they are inert
-				const uint32_t c = win * SWin + 64 * k + lane;
-				const uintptr_t a = smin + 16ull * (c < nchunks ? c : nchunks - 1);
-				if (NT)
+				const int32_t g = (int32_t)(win * SWin + 64 * k);
+				const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+				const uint32_t x = wave_incl_scan(h);
+				const uint32_t pre = carry + x;
+				const bool in0 = t0 >= g && t0 < g + 64, in1 = t1 >= g && t1 < g + 64;
+				if (__ballot(in0 || in1))
 				{
-					const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<gptr16>(a));
-					v[k] = make_uint4(t.x, t.y, t.z, t.w);
+					const uint32_t q0 = __shfl(pre, (t0 - g) & 63, 64);
+					const uint32_t q1 = __shfl(pre, (t1 - g) & 63, 64);
+					sf_p0 = in0 ? q0 : sf_p0;
+					sf_p1 = in1 ? q1 : sf_p1;
 				}
-				else
-					v[k] = ld16(a);
+				const bool ine = te >= g && te < g + 64;
+				if (__ballot(ine))
+				{
+					const int src = (te - g) & 63;
+					const uint4 d = make_uint4(__shfl(v[k].x, src, 64), __shfl(v[k].y, src, 64), __shfl(v[k].z, src, 64),
+					                           __shfl(v[k].w, src, 64));
+					if (ine)
+						sf_tsum = chunk_sum(d, sf_ce, sf_ce, sf_e);
+				}
+				carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 			}
 		};
-		if (stream)
-			load(va, 0);
-		if ((EarlyB || StreamFirst) && stream)  // both stream windows in flight during the gather and the parse
-			load(vb, 1);
-
-		// ---- (1b) StreamFirst: the whole span stream now, picking per packet the prefix before its first whole chunk (p0),
-		// before its last partial chunk (p1), and that partial chunk's sum (tsum) ----
-		const uintptr_t sf_a = (uintptr_t)pkt_addr, sf_e = sf_a + cap;
-		const uintptr_t sf_cs = (sf_a + 15) & ~(uintptr_t)15, sf_ce = sf_e & ~(uintptr_t)15;
-		uint32_t sf_p0 = 0, sf_p1 = 0, sf_tsum = 0;
-		if (StreamFirst && stream)
+		for (uint32_t wi = 0; wi < nwin; wi += 2)
 		{
-			const bool whole = live && sf_cs <= sf_ce;
-			const int32_t t0 = whole ? (int32_t)((sf_cs - smin) >> 4) - 1 : -2;
-			const int32_t t1 = whole ? (int32_t)((sf_ce - smin) >> 4) - 1 : -2;
-			const int32_t te = (whole && sf_ce < sf_e) ? (int32_t)((sf_ce - smin) >> 4) : -2;
-			uint32_t carry = 0;
+			process(va, wi);
+			load(va, wi + 2);
+			process(vb, wi + 1);
+			load(vb, wi + 3);
+		}
+	}
+
+	// ---- (2) header gather into LDS: 8 lanes per packet, one 16-B chunk each (8 packets per wave-instruction) ----
+	Pkt p;
+	p.g = (gptr8)(prm.data + (live ? off : 0));
+	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
+	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+	const uint32_t need = (p.mis + cap + 15) >> 4;  // chunks holding the whole packet
+	p.nch = (live && !StreamOnly) ? (need < (uint32_t)Chunks1 ? need : (uint32_t)Chunks1) : 0;
+	m_a0[lane] = p.a0;
+	m_nch[lane] = p.nch;
+	auto gather = [&]() {  // chunks [lo, hi) of every packet of the tile (m_nch)
+#pragma unroll
+		for (int r = 0; r < (Chunks + 7) / 8; ++r)
+		{
+			const uint32_t sub = (lane & 7) + 8 * r, grp = lane >> 3;
+			uint4 v[8];
+#pragma unroll
+			for (int j = 0; j < 8; ++j)
+			{
+				const uint32_t q = 8 * j + grp, rg = m_nch[q];
+				if (sub >= (rg >> 8) && sub < (rg & 0xFF))
+					v[j] = ld16(m_a0[q] + 16 * sub);
+			}
+#pragma unroll
+			for (int j = 0; j < 8; ++j)
+			{
+				const uint32_t q = 8 * j + grp, rg = m_nch[q];
+				if (sub >= (rg >> 8) && sub < (rg & 0xFF))
+				{
+					lptr32w slot = (lptr32w)(stage) + q * kTSlotDw + 4 * sub;
+					slot[0] = v[j].x;
+					slot[1] = v[j].y;
+					slot[2] = v[j].z;
+					slot[3] = v[j].w;
+				}
+			}
+		}
+	};
+	__syncthreads();
+	gather();
+	__syncthreads();
+	p.s = reinterpret_cast<lptr8>((lptr32w)(stage) + lane * kTSlotDw);
+	auto set_lim = [&]() {
+		const uint32_t staged = 16 * p.nch - p.mis;
+		p.lim = (live && p.nch) ? (staged < cap ? staged : cap) : 0;
+	};
+	set_lim();
+	if (Chunks1 < Chunks)
+	{
+		// second round before any walk: the rest of the window for the stacks the first round cannot hold (an MPLS
+		// label, or an IP layer not followed directly by TCP / UDP: GRE, IPv6 extension headers, ...), from a
+		// pre-scan of the Ethernet / VLAN / IP fields of the first window
+		uint32_t et = swap16(lds_u32(p, 12)), o = 14;
+#pragma unroll
+		for (int t = 0; t < 2; ++t)
+		{
+			const bool vl = (et == 0x8100 || et == 0x88A8) && o + 8 <= p.lim;
+			const uint32_t e2 = swap16(lds_u32(p, vl ? o : 0) >> 16);
+			et = vl ? e2 : et;
+			o = vl ? o + 4 : o;
+		}
+		const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 8 <= p.lim ? o + 8 : 0);
+		const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
+		const bool deep = et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
+		uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
+		bool more = live && !StreamOnly && (deep || GatherOnly) && full > p.nch;
+		uint32_t from = p.nch;  // the second round gathers chunks [from, full)
+		if (TightR2 && !GatherOnly && __ballot(more))  // wave-uniform: waves without a deep stack skip the extent
+		{
+			// only as far as the fast path reads: the deep stack's header extent, when the first window names it
+			const uint32_t ext = deep_extent(p, et, o);
+			uint32_t xc = (p.mis + ext + 15) >> 4;
+			// a stack ending past the 16-B-aligned window (up to 15 B of it lie before the packet), or one whose end the
+			// first window does not show: this lane re-gathers its whole window from a dword-aligned start instead, so
+			// that the fast path still takes it
+			const bool past = ext != 0xFFFFu ? xc > (uint32_t)Chunks : (need > (uint32_t)Chunks && p.mis > 3);
+			// the re-gathered window holds only 16-B pieces that lie wholly inside the packet: a piece starting at a
+			// dword could otherwise run past the end of the batch buffer (the packet's tail stays readable from HBM)
+			const uint32_t mis4 = (uint32_t)((uintptr_t)p.g & 3), whole4 = (mis4 + cap) >> 4;
+			const bool realign = Realign && more && past && whole4 >= (uint32_t)Chunks;
+			if (realign)
+			{
+				p.a0 = (uintptr_t)p.g - mis4;
+				p.mis = mis4;
+				m_a0[lane] = p.a0;
+				full = (uint32_t)Chunks;
+				xc = (p.mis + ext + 15) >> 4;
+				from = 0;
+			}
+			full = xc < full ? xc : full;
+			more = more && full > from;
+		}
+		if (__ballot(more))  // wave-uniform
+		{
+			m_nch[lane] = more ? (full | (from << 8)) : 0u;
+			__syncthreads();
+			gather();
+			__syncthreads();
+			p.nch = more ? full : p.nch;
+			set_lim();
+		}
+	}
+	Fast f;
+	bool fast = live && !StreamOnly && !GatherOnly && fast_walk(p, cap, prm, f);
+
+	// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
+	const uint32_t ml = prm.max_layers;
+	const bool stage_layers = prm.layers != nullptr && ml != 0;
+	Walk w;
+	w.flags = bad;
+	w.n_layers = 0;
+	w.mask = 0;
+	w.v4 = w.v6 = -1;
+	w.l4i = -1;
+	w.l4o = w.l4dlen = 0;
+	w.is_tcp = false;
+	uint32_t h5 = 0, h5d = 0, h2 = 0, ipc = 0, ips = 0, l4c = 0, l4s = 0;
+	if (live && StreamOnly)
+	{
+		w.l4i = 0;
+		w.l4o = 14;
+		w.l4dlen = cap > 14 ? cap - 14 : 0;
+		w.is_tcp = true;
+		w.l4pp = 0;
+	}
+	else if (live && !GatherOnly)
+	{
+		if (fast)
+		{
+			fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
+			fast_l7(p, f, cap);
+			// a classified HTTP / SSL / DNS payload or a UDP tunnel (VXLAN, GTPv1: an unclassified L7 flag): the
+			// generic walk builds their layers
+			const uint32_t l7 = f.l7();
+			fast = !(l7 & kL7Built) && !((l7 & PCPPX_F_NEEDS_HOST_L7) && !(l7 & PCPPX_F_L7_KNOWN));
+		}
+		if (fast)
+		{
+			w = fast_to_walk(f, ml);
+			if (want_csum && w.v4 >= 0)
+			{
+				ipc = fast_ipv4_checksum(p, w, &ips);
+				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+			}
+		}
+		else if (!SkipGeneric && !LateGeneric)
+		{
+			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
+			w = walk_chain(p, cap, prm, lay_out);
+			hashes(p, w, h5, h5d, h2);
+			if (want_csum && w.v4 >= 0)
+			{
+				ipc = ipv4_checksum(p, w, &ips);
+				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+			}
+		}
+	}
+
+	// the TCP flags byte for the fused reassembly output (the LDS stage is reused by the layer rows below)
+	const uint32_t tcp_fl = (prm.reasm != nullptr && fast && f.simple() && f.tcp()) ? (uint32_t)p.s[p.mis + f.l4o() + 13] : 0u;
+
+	// ---- (4) L4 checksums over the tile span ----
+	if (want_csum)  // uniform
+	{
+		const bool need = live && w.l4i >= 0;
+		const uintptr_t as = (uintptr_t)p.g + w.l4o, ae = as + w.l4dlen;
+		const uintptr_t f0 = (as + 15) & ~(uintptr_t)15, f1 = ae & ~(uintptr_t)15;
+		const bool full = need && f0 < f1;
+		const bool tail = need && f0 <= f1 && f1 < ae;  // partial last chunk [f1, ae)
+		uint32_t fsum = 0, tsum = 0;
+		bool tail_done = false;
+		if constexpr (Ring)
+		{
+			// (a) header-window inputs, before the ring overwrites the stage
+			uint32_t head = 0, fw = 0, ph = 0;
+			uint4 tv = make_uint4(0, 0, 0, 0);
+			if (need)
+			{
+				head = f0 <= f1 ? edge_sum(p, as, f0) : edge_sum(p, as, ae);
+				l4_inputs(p, w, &fw, &ph);
+				if (tail)
+				{
+					if ((p.a0 & 15) == 0 && (uint32_t)((f1 - p.a0) >> 4) < p.nch)
+					{
+						tsum = edge_sum(p, f1, ae);
+						tail_done = true;
+					}
+					else
+						tv = ld16(f1);  // lands during the stream
+				}
+			}
+			__syncthreads();  // every lane is done with the header stage
+			if (stream)
+			{
+				// (b) the span stream: per 64-chunk group a halves-sum, a DPP inclusive scan and the running prefix
+				// P into ring[c mod 512]; after each 4 groups the lanes whose P(c0-1) / P(c1-1) fell in them read it
+				lptr32w ring = (lptr32w)(stage);
+				constexpr uint32_t kRing = 4 * SWin < 512 ? 512u : 4u * SWin;  // 4 stream windows of prefixes
+				static_assert(kRing <= (uint32_t)(kTile * kTSlotDw), "ring");
+				const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
+				const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
+				uint32_t p0 = 0, p1 = 0, carry = 0;
+				const uint32_t nwin = (nchunks + SWin - 1) / SWin;
+				auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
+#pragma unroll
+					for (int k = 0; k < SWin / 64; ++k)
+					{
+						const uint32_t g = win * SWin + 64 * k;
+						const uint32_t h = halves(v[k].x, halves(v[k].y)) + halves(v[k].z, halves(v[k].w));
+						const uint32_t x = wave_incl_scan(h);
+						ring[(g & (kRing - 1)) + lane] = carry + x;
+						carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+					}
+				};
+				load(vb, 1);
+				for (uint32_t wi = 0; wi < nwin; wi += 2)
+				{
+					process(va, wi);
+					load(va, wi + 2);
+					process(vb, wi + 1);
+					load(vb, wi + 3);
+					const int32_t lo = (int32_t)(wi * SWin), hi = lo + 2 * SWin;
+					const bool in0 = t0 >= lo && t0 < hi, in1 = t1 >= lo && t1 < hi;
+					const uint32_t r0 = ring[(uint32_t)(in0 ? t0 : 0) & (kRing - 1)];
+					const uint32_t r1 = ring[(uint32_t)(in1 ? t1 : 0) & (kRing - 1)];
+					p0 = in0 ? r0 : p0;
+					p1 = in1 ? r1 : p1;
+				}
+				if (full)
+					fsum = p1 - p0;
+			}
+			else if (full)
+				fsum = full_chunks_sum(f0, f1);
+			if (need)
+			{
+				if (tail && !tail_done)
+					tsum = chunk_sum(tv, f1, f1, ae);
+				uint32_t acc = mod65535(fsum) + head + (f0 <= f1 ? tsum : 0u);
+				uint32_t r = mod65535(acc);
+				if (as & 1)
+					r = (r * 256u) % 65535u;
+				l4c = l4_checksum_from(w, r, fw, ph, &l4s);
+				w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
+			}
+		}
+		else if (StreamFirst)
+		{
+			// the prefixes were picked before the parse: whole chunks [f0, f1) = [cs, ce) less [cs, f0) when the L4 layer
+			// ends at the packet's end (then f1 = ce and the partial tail is the captured one); anything else (a trailer
+			// or IP padding after the L4 layer, an L4 start in the last partial chunk, a sparse tile) from HBM
+			const bool combine = stream && need && ae == sf_e && f0 >= sf_cs && f0 <= f1;
+			if (combine)
+			{
+				uint32_t lead = 0;  // the packet's whole chunks before the L4 start: in the header window
+				for (uintptr_t c = sf_cs; c < f0; c += 16)
+					lead += edge_sum(p, c, c + 16);
+				fsum = sf_p1 - sf_p0 - lead;
+				tsum = sf_tsum;
+				tail_done = true;
+			}
+			else if (full)
+				fsum = full_chunks_sum(f0, f1);
+		}
+		else if (stream)
+		{
+			// Stream the tile span once, 4 x 1 KiB wave-loads per window, two register windows in
+			// flight. Per 64-chunk group: halves-sums -> DPP inclusive scan -> running prefix P; each
+			// lane picks P(c1-1) and P(c0-1) of its own whole-chunk L4 range and its partial tail chunk
+			// straight out of the owning lanes' registers (ds_bpermute), only in groups where some lane
+			// needs them.
+			const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
+			const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
+			const int32_t te = tail ? (int32_t)((f1 - smin) >> 4) : -2;      // tail chunk
+			uint32_t p0 = 0, p1 = 0, carry = 0;
 			const uint32_t nwin = (nchunks + SWin - 1) / SWin;
 			auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
-	#pragma unroll
+#pragma unroll
 				for (int k = 0; k < SWin / 64; ++k)
 				{
 					const int32_t g = (int32_t)(win * SWin + 64 * k);
@@ -2130,21 +2359,28 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 					{
 						const uint32_t q0 = __shfl(pre, (t0 - g) & 63, 64);
 						const uint32_t q1 = __shfl(pre, (t1 - g) & 63, 64);
-						sf_p0 = in0 ? q0 : sf_p0;
-						sf_p1 = in1 ? q1 : sf_p1;
+						p0 = in0 ? q0 : p0;
+						p1 = in1 ? q1 : p1;
 					}
 					const bool ine = te >= g && te < g + 64;
 					if (__ballot(ine))
 					{
 						const int src = (te - g) & 63;
-						const uint4 d = make_uint4(__shfl(v[k].x, src, 64), __shfl(v[k].y, src, 64), __shfl(v[k].z, src, 64),
-						                           __shfl(v[k].w, src, 64));
+						const uint4 d = make_uint4(__shfl(v[k].x, src, 64), __shfl(v[k].y, src, 64),
+						                           __shfl(v[k].z, src, 64), __shfl(v[k].w, src, 64));
 						if (ine)
-							sf_tsum = chunk_sum(d, sf_ce, sf_ce, sf_e);
+						{
+							tsum = chunk_sum(d, f1, f1, ae);
+							tail_done = true;
+						}
 					}
 					carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 				}
 			};
+			// straight-line body (windows padded to an even count; loads past the span are clamped) so
+			// the compiler's vmcnt accounting sees one fixed issue order: one window always in flight
+			if (!EarlyB)
+				load(vb, 1);
 			for (uint32_t wi = 0; wi < nwin; wi += 2)
 			{
 				process(va, wi);
@@ -2152,535 +2388,176 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				process(vb, wi + 1);
 				load(vb, wi + 3);
 			}
+			if (full)
+				fsum = p1 - p0;
 		}
-
-		// ---- (2) header gather into LDS: 8 lanes per packet, one 16-B chunk each (8 packets per wave-instruction) ----
-		Pkt p;
-		p.g = (gptr8)(prm.data + (live ? off : 0));
-		p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
-		p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
-		const uint32_t need = (p.mis + cap + 15) >> 4;  // chunks holding the whole packet
-		p.nch = (live && !StreamOnly) ? (need < (uint32_t)Chunks1 ? need : (uint32_t)Chunks1) : 0;
-		if (Persist)
-			__syncthreads();  // the previous tile is done with the stage and with m_a0 / m_nch
-		m_a0[lane] = p.a0;
-		m_nch[lane] = p.nch;
-		auto gather = [&]() {  // chunks [lo, hi) of every packet of the tile (m_nch)
-	#pragma unroll
-			for (int r = 0; r < (Chunks + 7) / 8; ++r)
-			{
-				const uint32_t sub = (lane & 7) + 8 * r, grp = lane >> 3;
-				uint4 v[8];
-	#pragma unroll
-				for (int j = 0; j < 8; ++j)
-				{
-					const uint32_t q = 8 * j + grp, rg = m_nch[q];
-					if (sub >= (rg >> 8) && sub < (rg & 0xFF))
-						v[j] = ld16(m_a0[q] + 16 * sub);
-				}
-	#pragma unroll
-				for (int j = 0; j < 8; ++j)
-				{
-					const uint32_t q = 8 * j + grp, rg = m_nch[q];
-					if (sub >= (rg >> 8) && sub < (rg & 0xFF))
-					{
-						lptr32w slot = (lptr32w)(stage) + q * kTSlotDw + 4 * sub;
-						slot[0] = v[j].x;
-						slot[1] = v[j].y;
-						slot[2] = v[j].z;
-						slot[3] = v[j].w;
-					}
-				}
-			}
-		};
-		if constexpr (Persist)
-			put_pf();  // this tile's first round, gathered while the previous tile was parsed
-		else
+		else if (full)
+			fsum = full_chunks_sum(f0, f1);
+		if (!Ring && need)
 		{
-			__syncthreads();
-			gather();
-		}
-		__syncthreads();
-		p.s = reinterpret_cast<lptr8>((lptr32w)(stage) + lane * kTSlotDw);
-		auto set_lim = [&]() {
-			const uint32_t staged = 16 * p.nch - p.mis;
-			p.lim = (live && p.nch) ? (staged < cap ? staged : cap) : 0;
-		};
-		set_lim();
-		if (Chunks1 < Chunks)
-		{
-			// second round before any walk: the rest of the window for the stacks the first round cannot hold (an MPLS
-			// label, or an IP layer not followed directly by TCP / UDP: GRE, IPv6 extension headers, ...), from a
-			// pre-scan of the Ethernet / VLAN / IP fields of the first window
-			uint32_t et = swap16(lds_u32(p, 12)), o = 14;
-	#pragma unroll
-			for (int t = 0; t < 2; ++t)
-			{
-				const bool vl = (et == 0x8100 || et == 0x88A8) && o + 8 <= p.lim;
-				const uint32_t e2 = swap16(lds_u32(p, vl ? o : 0) >> 16);
-				et = vl ? e2 : et;
-				o = vl ? o + 4 : o;
-			}
-			const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 8 <= p.lim ? o + 8 : 0);
-			const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
-			const bool deep = et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
-			uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
-			bool more = live && !StreamOnly && (deep || GatherOnly) && full > p.nch;
-			uint32_t from = p.nch;  // the second round gathers chunks [from, full)
-			if (TightR2 && !GatherOnly && __ballot(more))  // wave-uniform: waves without a deep stack skip the extent
-			{
-				// only as far as the fast path reads: the deep stack's header extent, when the first window names it
-				const uint32_t ext = deep_extent(p, et, o);
-				uint32_t xc = (p.mis + ext + 15) >> 4;
-				// a stack ending past the 16-B-aligned window (up to 15 B of it lie before the packet), or one whose end the
-				// first window does not show: this lane re-gathers its whole window from a dword-aligned start instead, so
-				// that the fast path still takes it
-				const bool past = ext != 0xFFFFu ? xc > (uint32_t)Chunks : (need > (uint32_t)Chunks && p.mis > 3);
-				// the re-gathered window holds only 16-B pieces that lie wholly inside the packet: a piece starting at a
-				// dword could otherwise run past the end of the batch buffer (the packet's tail stays readable from HBM)
-				const uint32_t mis4 = (uint32_t)((uintptr_t)p.g & 3), whole4 = (mis4 + cap) >> 4;
-				const bool realign = Realign && more && past && whole4 >= (uint32_t)Chunks;
-				if (realign)
-				{
-					p.a0 = (uintptr_t)p.g - mis4;
-					p.mis = mis4;
-					m_a0[lane] = p.a0;
-					full = (uint32_t)Chunks;
-					xc = (p.mis + ext + 15) >> 4;
-					from = 0;
-				}
-				full = xc < full ? xc : full;
-				more = more && full > from;
-			}
-			if (__ballot(more))  // wave-uniform
-			{
-				m_nch[lane] = more ? (full | (from << 8)) : 0u;
-				__syncthreads();
-				gather();
-				__syncthreads();
-				p.nch = more ? full : p.nch;
-				set_lim();
-			}
-		}
-		if constexpr (Persist)
-		{
-			// the next tile's first round (and the descriptors of the one after it) in flight during this tile's parse
-			uint64_t a0n;
-			uint32_t nchn;
-			first_round((uint64_t)tile + gridDim.x, nx_off, nx_cap, a0n, nchn);
-			__syncthreads();  // round 2 is done with m_a0 / m_nch
-			m_a0[lane] = a0n;
-			m_nch[lane] = nchn;
-			__syncthreads();
-			issue_pf();
-			cur_off = nx_off;
-			cur_cap = nx_cap;
-			ld_desc((uint64_t)tile + 2ull * gridDim.x, nx_off, nx_cap);
-		}
-		Fast f;
-		bool fast = live && !StreamOnly && !GatherOnly && fast_walk(p, cap, prm, f);
-
-		// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
-		const uint32_t ml = prm.max_layers;
-		const bool stage_layers = prm.layers != nullptr && ml != 0;
-		Walk w;
-		w.flags = bad;
-		w.n_layers = 0;
-		w.mask = 0;
-		w.v4 = w.v6 = -1;
-		w.l4i = -1;
-		w.l4o = w.l4dlen = 0;
-		w.is_tcp = false;
-		uint32_t h5 = 0, h5d = 0, h2 = 0, ipc = 0, ips = 0, l4c = 0, l4s = 0;
-		if (live && StreamOnly)
-		{
-			w.l4i = 0;
-			w.l4o = 14;
-			w.l4dlen = cap > 14 ? cap - 14 : 0;
-			w.is_tcp = true;
-			w.l4pp = 0;
-		}
-		else if (live && !GatherOnly)
-		{
-			if (fast)
-			{
-				fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
-				fast_l7(p, f, cap);
-				// a classified HTTP / SSL / DNS payload or a UDP tunnel (VXLAN, GTPv1: an unclassified L7 flag): the
-				// generic walk builds their layers
-				const uint32_t l7 = f.l7();
-				fast = !(l7 & kL7Built) && !((l7 & PCPPX_F_NEEDS_HOST_L7) && !(l7 & PCPPX_F_L7_KNOWN));
-			}
-			if (fast)
-			{
-				w = fast_to_walk(f, ml);
-				if (want_csum && w.v4 >= 0)
-				{
-					ipc = fast_ipv4_checksum(p, w, &ips);
-					w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
-				}
-			}
-			else if (!SkipGeneric && !LateGeneric)
-			{
-				uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
-				w = walk_chain(p, cap, prm, lay_out);
-				hashes(p, w, h5, h5d, h2);
-				if (want_csum && w.v4 >= 0)
-				{
-					ipc = ipv4_checksum(p, w, &ips);
-					w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
-				}
-			}
-		}
-
-		// the TCP flags byte for the fused reassembly output (the LDS stage is reused by the layer rows below)
-		const uint32_t tcp_fl = (prm.reasm != nullptr && fast && f.simple() && f.tcp()) ? (uint32_t)p.s[p.mis + f.l4o() + 13] : 0u;
-
-		// ---- (4) L4 checksums over the tile span ----
-		if (want_csum)  // uniform
-		{
-			const bool need = live && w.l4i >= 0;
-			const uintptr_t as = (uintptr_t)p.g + w.l4o, ae = as + w.l4dlen;
-			const uintptr_t f0 = (as + 15) & ~(uintptr_t)15, f1 = ae & ~(uintptr_t)15;
-			const bool full = need && f0 < f1;
-			const bool tail = need && f0 <= f1 && f1 < ae;  // partial last chunk [f1, ae)
-			uint32_t fsum = 0, tsum = 0;
-			bool tail_done = false;
-			if constexpr (Ring)
-			{
-				// (a) header-window inputs, before the ring overwrites the stage
-				uint32_t head = 0, fw = 0, ph = 0;
-				uint4 tv = make_uint4(0, 0, 0, 0);
-				if (need)
-				{
-					head = f0 <= f1 ? edge_sum(p, as, f0) : edge_sum(p, as, ae);
-					l4_inputs(p, w, &fw, &ph);
-					if (tail)
-					{
-						if ((p.a0 & 15) == 0 && (uint32_t)((f1 - p.a0) >> 4) < p.nch)
-						{
-							tsum = edge_sum(p, f1, ae);
-							tail_done = true;
-						}
-						else
-							tv = ld16(f1);  // lands during the stream
-					}
-				}
-				__syncthreads();  // every lane is done with the header stage
-				if (stream)
-				{
-					// (b) the span stream: per 64-chunk group a halves-sum, a DPP inclusive scan and the running prefix
-					// P into ring[c mod 512]; after each 4 groups the lanes whose P(c0-1) / P(c1-1) fell in them read it
-					lptr32w ring = (lptr32w)(stage);
-					constexpr uint32_t kRing = 4 * SWin < 512 ? 512u : 4u * SWin;  // 4 stream windows of prefixes
-					static_assert(kRing <= (uint32_t)(kTile * kTSlotDw), "ring");
-					const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
-					const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
-					uint32_t p0 = 0, p1 = 0, carry = 0;
-					const uint32_t nwin = (nchunks + SWin - 1) / SWin;
-					auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
-	#pragma unroll
-						for (int k = 0; k < SWin / 64; ++k)
-						{
-							const uint32_t g = win * SWin + 64 * k;
-							const uint32_t h = halves(v[k].x, halves(v[k].y)) + halves(v[k].z, halves(v[k].w));
-							const uint32_t x = wave_incl_scan(h);
-							ring[(g & (kRing - 1)) + lane] = carry + x;
-							carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-						}
-					};
-					load(vb, 1);
-					for (uint32_t wi = 0; wi < nwin; wi += 2)
-					{
-						process(va, wi);
-						load(va, wi + 2);
-						process(vb, wi + 1);
-						load(vb, wi + 3);
-						const int32_t lo = (int32_t)(wi * SWin), hi = lo + 2 * SWin;
-						const bool in0 = t0 >= lo && t0 < hi, in1 = t1 >= lo && t1 < hi;
-						const uint32_t r0 = ring[(uint32_t)(in0 ? t0 : 0) & (kRing - 1)];
-						const uint32_t r1 = ring[(uint32_t)(in1 ? t1 : 0) & (kRing - 1)];
-						p0 = in0 ? r0 : p0;
-						p1 = in1 ? r1 : p1;
-					}
-					if (full)
-						fsum = p1 - p0;
-				}
-				else if (full)
-					fsum = full_chunks_sum(f0, f1);
-				if (need)
-				{
-					if (tail && !tail_done)
-						tsum = chunk_sum(tv, f1, f1, ae);
-					uint32_t acc = mod65535(fsum) + head + (f0 <= f1 ? tsum : 0u);
-					uint32_t r = mod65535(acc);
-					if (as & 1)
-						r = (r * 256u) % 65535u;
-					l4c = l4_checksum_from(w, r, fw, ph, &l4s);
-					w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
-				}
-			}
-			else if (StreamFirst)
-			{
-				// the prefixes were picked before the parse: whole chunks [f0, f1) = [cs, ce) less [cs, f0) when the L4 layer
-				// ends at the packet's end (then f1 = ce and the partial tail is the captured one); anything else (a trailer
-				// or IP padding after the L4 layer, an L4 start in the last partial chunk, a sparse tile) from HBM
-				const bool combine = stream && need && ae == sf_e && f0 >= sf_cs && f0 <= f1;
-				if (combine)
-				{
-					uint32_t lead = 0;  // the packet's whole chunks before the L4 start: in the header window
-					for (uintptr_t c = sf_cs; c < f0; c += 16)
-						lead += edge_sum(p, c, c + 16);
-					fsum = sf_p1 - sf_p0 - lead;
-					tsum = sf_tsum;
-					tail_done = true;
-				}
-				else if (full)
-					fsum = full_chunks_sum(f0, f1);
-			}
-			else if (stream)
-			{
-				// Stream the tile span once, 4 x 1 KiB wave-loads per window, two register windows in
-				// flight. Per 64-chunk group: halves-sums -> DPP inclusive scan -> running prefix P; each
-				// lane picks P(c1-1) and P(c0-1) of its own whole-chunk L4 range and its partial tail chunk
-				// straight out of the owning lanes' registers (ds_bpermute), only in groups where some lane
-				// needs them.
-				const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
-				const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
-				const int32_t te = tail ? (int32_t)((f1 - smin) >> 4) : -2;      // tail chunk
-				uint32_t p0 = 0, p1 = 0, carry = 0;
-				const uint32_t nwin = (nchunks + SWin - 1) / SWin;
-				auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
-	#pragma unroll
-					for (int k = 0; k < SWin / 64; ++k)
-					{
-						const int32_t g = (int32_t)(win * SWin + 64 * k);
-						const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
-						const uint32_t x = wave_incl_scan(h);
-						const uint32_t pre = carry + x;
-						const bool in0 = t0 >= g && t0 < g + 64, in1 = t1 >= g && t1 < g + 64;
-						if (__ballot(in0 || in1))
-						{
-							const uint32_t q0 = __shfl(pre, (t0 - g) & 63, 64);
-							const uint32_t q1 = __shfl(pre, (t1 - g) & 63, 64);
-							p0 = in0 ? q0 : p0;
-							p1 = in1 ? q1 : p1;
-						}
-						const bool ine = te >= g && te < g + 64;
-						if (__ballot(ine))
-						{
-							const int src = (te - g) & 63;
-							const uint4 d = make_uint4(__shfl(v[k].x, src, 64), __shfl(v[k].y, src, 64),
-							                           __shfl(v[k].z, src, 64), __shfl(v[k].w, src, 64));
-							if (ine)
-							{
-								tsum = chunk_sum(d, f1, f1, ae);
-								tail_done = true;
-							}
-						}
-						carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-					}
-				};
-				// straight-line body (windows padded to an even count; loads past the span are clamped) so
-				// the compiler's vmcnt accounting sees one fixed issue order: one window always in flight
-				if (!EarlyB)
-					load(vb, 1);
-				if constexpr (Win3)
-				{
-					uint4 vc[SWin / 64];
-					load(vc, 2);
-					for (uint32_t wi = 0; wi < nwin; wi += 3)
-					{
-						process(va, wi);
-						load(va, wi + 3);
-						process(vb, wi + 1);
-						load(vb, wi + 4);
-						process(vc, wi + 2);
-						load(vc, wi + 5);
-					}
-				}
-				else
-					for (uint32_t wi = 0; wi < nwin; wi += 2)
-					{
-						process(va, wi);
-						load(va, wi + 2);
-						process(vb, wi + 1);
-						load(vb, wi + 3);
-					}
-				if (full)
-					fsum = p1 - p0;
-			}
-			else if (full)
-				fsum = full_chunks_sum(f0, f1);
-			if (!Ring && need)
-			{
-				uint32_t acc = mod65535(fsum);
-				if (f0 <= f1)
-					acc += edge_sum(p, as, f0) + (tail_done ? tsum : edge_sum(p, f1, ae));
-				else
-					acc += edge_sum(p, as, ae);
-				uint32_t r = mod65535(acc);
-				if (as & 1)
-					r = (r * 256u) % 65535u;
-				l4c = l4_checksum(p, w, r, &l4s);
-				w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
-			}
-		}
-
-		// ---- (4b) LateGeneric: the packets off the fast path are walked after the span stream (the LDS window is still
-		// intact), so the stream's registers and the generic walk's are never live together; their L4 sums come from the
-		// window and HBM (range_residue) instead of the stream's prefixes. Same records. ----
-		if (LateGeneric && live && !fast && !StreamOnly && !GatherOnly && !SkipGeneric)
-		{
-			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
-			w = walk_chain(p, cap, prm, lay_out);
-			hashes(p, w, h5, h5d, h2);
-			if (want_csum && w.v4 >= 0)
-			{
-				ipc = ipv4_checksum(p, w, &ips);
-				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
-			}
-			if (want_csum && w.l4i >= 0)
-			{
-				l4c = l4_checksum(p, w, range_residue(p, w.l4o, w.l4o + w.l4dlen), &l4s);
-				w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
-			}
-		}
-
-		if (in && NT && prm.summary != nullptr)
-		{
-			const uint32_t l4b = w.l4i >= 0 ? (uint32_t)w.l4i : 0xFFu;
-			u32x4 s0, s1;
-			s0.x = h5; s0.y = h5d; s0.z = h2; s0.w = w.flags | (MarkFast && fast ? 0x8000u : 0u) | (w.n_layers << 16) | (l4b << 24);
-			s1.x = (uint32_t)w.mask; s1.y = (uint32_t)(w.mask >> 32); s1.z = ipc | (ips << 16); s1.w = l4c | (l4s << 16);
-			u32x4* so = reinterpret_cast<u32x4*>(prm.summary + i);
-			__builtin_nontemporal_store(s0, so);
-			__builtin_nontemporal_store(s1, so + 1);
-		}
-		else if (in && prm.summary != nullptr)
-			write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
-		if (in && prm.flow_keys != nullptr)
-			__builtin_nontemporal_store(h5, prm.flow_keys + i);
-		if (in && prm.tuples != nullptr)  // the LDS window is still intact here (the rows below reuse it)
-			write_tuple(p, w, h5, prm.tuples + i);
-		if (prm.wave_stats != nullptr)  // uniform
-			wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + tile);
-
-		// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
-		// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
-		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-		typedef __attribute__((address_space(3))) u32x2* lptr64w;
-		// PCPPX_LAYOUT_PACKED: the tile's chains dense in LDS (entry excl + k of the lane's exclusive prefix), stored as one
-		// contiguous run of entries from the tile's base; needs kTile * PCPPX_PACKED_MAX_LAYERS entries of stage
-		constexpr bool kPackedOk = kTSlotDw >= 2 * PCPPX_PACKED_MAX_LAYERS;
-		if (kPackedOk && stage_layers && prm.packed)  // uniform
-		{
-			const uint32_t cnt = in ? (w.n_layers < ml ? w.n_layers : ml) : 0u;
-			const uint32_t incl = wave_incl_scan(cnt);
-			const uint32_t excl = incl - cnt;
-			const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-			u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)tile * kTile * ml;
-			__syncthreads();  // every lane is done with the header stage
-			lptr64w rows = (lptr64w)(stage);
-			if (fast)
-				fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) {
-					u32x2 e;
-					e.x = r.x;
-					e.y = r.y;
-					rows[excl + k] = e;
-				});
+			uint32_t acc = mod65535(fsum);
+			if (f0 <= f1)
+				acc += edge_sum(p, as, f0) + (tail_done ? tsum : edge_sum(p, f1, ae));
 			else
-				for (uint32_t k = 0; k < cnt; ++k)  // the generic walk wrote this lane's chain at its fixed-layout slot
-					rows[excl + k] = dst[lane * ml + k];
-			__syncthreads();
-			for (uint32_t r = lane; r < total; r += kTile)
-				__builtin_nontemporal_store(rows[r], &dst[r]);
-		}
-		else if (stage_layers && ml > kRowMl)  // uniform: deep records, each fast lane stores its own row
-		{
-			if (fast)
-			{
-				uint2* dst = reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml;
-				fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) { dst[k] = r; });
-			}
-		}
-		else if (stage_layers)  // uniform
-		{
-			__syncthreads();  // every lane is done with the header stage
-			m_nch[lane] = (fast || GatherOnly) ? (FillTails ? ml : w.n_layers) : 0u;  // records of the row to store
-			lptr64w rows = (lptr64w)(stage);
-			const uint32_t rs = ml + 1;  // padded row stride (records): breaks the power-of-two bank pattern
-			if (FillTails && (fast || GatherOnly))
-				for (uint32_t k = 0; k < ml; ++k)
-					rows[lane * rs + k] = u32x2{ 0u, 0u };
-			if (fast)
-				fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) {
-					u32x2 e;
-					e.x = r.x;
-					e.y = r.y;
-					rows[lane * rs + k] = e;
-				});
-			__syncthreads();
-			const uint32_t first = tile * kTile;
-			const uint32_t nrows = prm.n - first < (uint32_t)kTile ? prm.n - first : (uint32_t)kTile;
-			u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)first * ml;
-			// kTile / ml rows per pass, lane -> (row, record): consecutive lanes write consecutive records
-			const uint32_t per = kTile / ml, rr = lane / ml, kk = lane - rr * ml;
-			for (uint32_t r0 = 0; r0 < nrows; r0 += per)
-			{
-				const uint32_t r = r0 + rr;
-				if (rr < per && r < nrows && kk < m_nch[r])
-				{
-					if (NT)
-						__builtin_nontemporal_store(rows[r * rs + kk], &dst[r * ml + kk]);
-					else
-						dst[r * ml + kk] = rows[r * rs + kk];
-				}
-			}
-		}
-
-		// ---- (6) fused reassembly front ends (same records as reasm_kernel): plain fast-path packets straight from
-		// their parse (IPv4 not a fragment, IPv6 without extensions, the TCP flags byte read before the LDS reuse), every
-		// other packet from its layer records ----
-		if (prm.reasm != nullptr)  // uniform pointer
-		{
-			__syncthreads();  // the fast-path rows of (5) were stored by other lanes
-			__threadfence_block();
-		}
-		if (prm.reasm != nullptr && in)
-		{
-			uint4 r;
-			if (fast && f.simple())
-			{
-				const uint32_t nl = w.n_layers, ipk = 1 + f.nv(), l4k = 2 + f.nv();
-				const bool unfinished = (w.flags & PCPPX_F_DEPTH_OVERFLOW) || ((w.flags & PCPPX_F_NEEDS_HOST_L7) && !f.tcp());
-				const bool v4r = !f.v6a() && ipk < nl, v6r = f.v6a() && ipk < nl, tcpr = f.tcp() && l4k < nl;
-				const uint32_t ipst = v4r ? PCPPX_IPR_NON_FRAGMENT
-				                          : (unfinished ? PCPPX_IPR_HOST
-				                                        : (v6r ? (PCPPX_IPR_F_IPV6 | PCPPX_IPR_NON_FRAGMENT) : PCPPX_IPR_NON_IP));
-				uint32_t ts, pay = 0;
-				if (unfinished)
-					ts = PCPPX_TCPR_HOST;
-				else if (!v4r && !v6r)
-					ts = PCPPX_TCPR_NON_IP;
-				else if (!tcpr)
-					ts = PCPPX_TCPR_NON_TCP;
-				else
-				{
-					const uint32_t fl = tcp_fl;
-					pay = f.l4dlen() - f.l4hdr();
-					ts = ((pay == 0 && (fl & 7) == 0) ? PCPPX_TCPR_NO_DATA : PCPPX_TCPR_DATA) |
-					     ((fl & 1) ? PCPPX_TCPR_F_FIN : 0) | ((fl & 2) ? PCPPX_TCPR_F_SYN : 0) | ((fl & 4) ? PCPPX_TCPR_F_RST : 0);
-				}
-				r = make_uint4(0, 0, (ipst << 16) | (ts << 24), pay);
-			}
-			else
-				r = reasm_one(w.flags, w.n_layers, prm.layers + (size_t)i * ml, ml, prm.data + off);
-			reinterpret_cast<uint4*>(prm.reasm)[i] = r;
+				acc += edge_sum(p, as, ae);
+			uint32_t r = mod65535(acc);
+			if (as & 1)
+				r = (r * 256u) % 65535u;
+			l4c = l4_checksum(p, w, r, &l4s);
+			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
 		}
 	}
-	if (!Persist)
-		break;
+
+	// ---- (4b) LateGeneric: the packets off the fast path are walked after the span stream (the LDS window is still
+	// intact), so the stream's registers and the generic walk's are never live together; their L4 sums come from the
+	// window and HBM (range_residue) instead of the stream's prefixes. Same records. ----
+	if (LateGeneric && live && !fast && !StreamOnly && !GatherOnly && !SkipGeneric)
+	{
+		uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
+		w = walk_chain(p, cap, prm, lay_out);
+		hashes(p, w, h5, h5d, h2);
+		if (want_csum && w.v4 >= 0)
+		{
+			ipc = ipv4_checksum(p, w, &ips);
+			w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
+		}
+		if (want_csum && w.l4i >= 0)
+		{
+			l4c = l4_checksum(p, w, range_residue(p, w.l4o, w.l4o + w.l4dlen), &l4s);
+			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
+		}
+	}
+
+	if (in && NT && prm.summary != nullptr)
+	{
+		const uint32_t l4b = w.l4i >= 0 ? (uint32_t)w.l4i : 0xFFu;
+		u32x4 s0, s1;
+		s0.x = h5; s0.y = h5d; s0.z = h2; s0.w = w.flags | (MarkFast && fast ? 0x8000u : 0u) | (w.n_layers << 16) | (l4b << 24);
+		s1.x = (uint32_t)w.mask; s1.y = (uint32_t)(w.mask >> 32); s1.z = ipc | (ips << 16); s1.w = l4c | (l4s << 16);
+		u32x4* so = reinterpret_cast<u32x4*>(prm.summary + i);
+		__builtin_nontemporal_store(s0, so);
+		__builtin_nontemporal_store(s1, so + 1);
+	}
+	else if (in && prm.summary != nullptr)
+		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
+	if (in && prm.flow_keys != nullptr)
+		__builtin_nontemporal_store(h5, prm.flow_keys + i);
+	if (in && prm.tuples != nullptr)  // the LDS window is still intact here (the rows below reuse it)
+		write_tuple(p, w, h5, prm.tuples + i);
+	if (prm.wave_stats != nullptr)  // uniform
+		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + blockIdx.x);
+
+	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
+	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
+	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+	typedef __attribute__((address_space(3))) u32x2* lptr64w;
+	// PCPPX_LAYOUT_PACKED: the tile's chains dense in LDS (entry excl + k of the lane's exclusive prefix), stored as one
+	// contiguous run of entries from the tile's base; needs kTile * PCPPX_PACKED_MAX_LAYERS entries of stage
+	constexpr bool kPackedOk = kTSlotDw >= 2 * PCPPX_PACKED_MAX_LAYERS;
+	if (kPackedOk && stage_layers && prm.packed)  // uniform
+	{
+		const uint32_t cnt = in ? (w.n_layers < ml ? w.n_layers : ml) : 0u;
+		const uint32_t incl = wave_incl_scan(cnt);
+		const uint32_t excl = incl - cnt;
+		const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)blockIdx.x * kTile * ml;
+		__syncthreads();  // every lane is done with the header stage
+		lptr64w rows = (lptr64w)(stage);
+		if (fast)
+			fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) {
+				u32x2 e;
+				e.x = r.x;
+				e.y = r.y;
+				rows[excl + k] = e;
+			});
+		else
+			for (uint32_t k = 0; k < cnt; ++k)  // the generic walk wrote this lane's chain at its fixed-layout slot
+				rows[excl + k] = dst[lane * ml + k];
+		__syncthreads();
+		for (uint32_t r = lane; r < total; r += kTile)
+			__builtin_nontemporal_store(rows[r], &dst[r]);
+	}
+	else if (stage_layers && ml > kRowMl)  // uniform: deep records, each fast lane stores its own row
+	{
+		if (fast)
+		{
+			uint2* dst = reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml;
+			fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) { dst[k] = r; });
+		}
+	}
+	else if (stage_layers)  // uniform
+	{
+		__syncthreads();  // every lane is done with the header stage
+		m_nch[lane] = (fast || GatherOnly) ? (FillTails ? ml : w.n_layers) : 0u;  // records of the row to store
+		lptr64w rows = (lptr64w)(stage);
+		const uint32_t rs = ml + 1;  // padded row stride (records): breaks the power-of-two bank pattern
+		if (FillTails && (fast || GatherOnly))
+			for (uint32_t k = 0; k < ml; ++k)
+				rows[lane * rs + k] = u32x2{ 0u, 0u };
+		if (fast)
+			fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) {
+				u32x2 e;
+				e.x = r.x;
+				e.y = r.y;
+				rows[lane * rs + k] = e;
+			});
+		__syncthreads();
+		const uint32_t first = blockIdx.x * kTile;
+		const uint32_t nrows = prm.n - first < (uint32_t)kTile ? prm.n - first : (uint32_t)kTile;
+		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)first * ml;
+		// kTile / ml rows per pass, lane -> (row, record): consecutive lanes write consecutive records
+		const uint32_t per = kTile / ml, rr = lane / ml, kk = lane - rr * ml;
+		for (uint32_t r0 = 0; r0 < nrows; r0 += per)
+		{
+			const uint32_t r = r0 + rr;
+			if (rr < per && r < nrows && kk < m_nch[r])
+			{
+				if (NT)
+					__builtin_nontemporal_store(rows[r * rs + kk], &dst[r * ml + kk]);
+				else
+					dst[r * ml + kk] = rows[r * rs + kk];
+			}
+		}
+	}
+
+	// ---- (6) fused reassembly front ends (same records as reasm_kernel): plain fast-path packets straight from
+	// their parse (IPv4 not a fragment, IPv6 without extensions, the TCP flags byte read before the LDS reuse), every
+	// other packet from its layer records ----
+	if (prm.reasm != nullptr)  // uniform pointer
+	{
+		__syncthreads();  // the fast-path rows of (5) were stored by other lanes
+		__threadfence_block();
+	}
+	if (prm.reasm != nullptr && in)
+	{
+		uint4 r;
+		if (fast && f.simple())
+		{
+			const uint32_t nl = w.n_layers, ipk = 1 + f.nv(), l4k = 2 + f.nv();
+			const bool unfinished = (w.flags & PCPPX_F_DEPTH_OVERFLOW) || ((w.flags & PCPPX_F_NEEDS_HOST_L7) && !f.tcp());
+			const bool v4r = !f.v6a() && ipk < nl, v6r = f.v6a() && ipk < nl, tcpr = f.tcp() && l4k < nl;
+			const uint32_t ipst = v4r ? PCPPX_IPR_NON_FRAGMENT
+			                          : (unfinished ? PCPPX_IPR_HOST
+			                                        : (v6r ? (PCPPX_IPR_F_IPV6 | PCPPX_IPR_NON_FRAGMENT) : PCPPX_IPR_NON_IP));
+			uint32_t ts, pay = 0;
+			if (unfinished)
+				ts = PCPPX_TCPR_HOST;
+			else if (!v4r && !v6r)
+				ts = PCPPX_TCPR_NON_IP;
+			else if (!tcpr)
+				ts = PCPPX_TCPR_NON_TCP;
+			else
+			{
+				const uint32_t fl = tcp_fl;
+				pay = f.l4dlen() - f.l4hdr();
+				ts = ((pay == 0 && (fl & 7) == 0) ? PCPPX_TCPR_NO_DATA : PCPPX_TCPR_DATA) |
+				     ((fl & 1) ? PCPPX_TCPR_F_FIN : 0) | ((fl & 2) ? PCPPX_TCPR_F_SYN : 0) | ((fl & 4) ? PCPPX_TCPR_F_RST : 0);
+			}
+			r = make_uint4(0, 0, (ipst << 16) | (ts << 24), pay);
+		}
+		else
+			r = reasm_one(w.flags, w.n_layers, prm.layers + (size_t)i * ml, ml, prm.data + off);
+		reinterpret_cast<uint4*>(prm.reasm)[i] = r;
 	}
 }
 
@@ -3345,6 +3222,10 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 // checksum launches with opts.window = PCPPX_WINDOW_DEEP: the parse-only instance's two-round 144-B window (tight second
 // round, dword-aligned re-gather) with the span stream; LDS 10 KiB, 4 waves/SIMD
 #define PCPPX_PARSE_DEEP_KERNEL parse_tile_kernel<4, kParseSWin, kParseOnlyChunks, true, false, true, kParseOnlyChunks1>
+// parse-only launches with opts.window = PCPPX_WINDOW_SHORT: one 96-B round, LDS 7 KiB (22 waves/CU, 5 waves/SIMD of
+// registers): config 4 0.464 -> 0.432 ms, config 2 43.2 -> 36.3 us, config 5 0.75 -> 1.61 ms (tools/ab variant 60,
+// profiles/r03_ab_windows_persist.txt)
+#define PCPPX_PARSE_SHORT_KERNEL parse_tile_kernel<1, 64, kParseChunks, true, false, false, kParseChunks>
 
 // the flow-table shape: 1024-thread blocks, 8192 LDS slots, 4096-packet batches with the next batch prefetched,
 // 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)
@@ -3383,6 +3264,8 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	else if (o->want_checksums)
 		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else if (o->window == PCPPX_WINDOW_SHORT)
+		hipLaunchKernelGGL(PCPPX_PARSE_SHORT_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	else
 		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel", stream);
@@ -3400,6 +3283,8 @@ int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records*
 		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	else if (o->want_checksums)
 		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else if (o->window == PCPPX_WINDOW_SHORT)
+		hipLaunchKernelGGL(PCPPX_PARSE_SHORT_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	else
 		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	return check_launch("parse_tile_kernel(reasm)", stream);

@@ -60,7 +60,7 @@ def test_engine_rejects_bad_arguments_without_gpu():
     lib.pcppx_default_opts(C.byref(o))
     assert (o.parse_until_family, o.parse_until_osi, o.want_checksums, o.max_layers) == (0, 8, 1, 16)
     assert lib.pcppx_strerror(abi.E_INVAL) == b"invalid argument"
-    o.window = 2  # PCPPX_WINDOW_DEFAULT / PCPPX_WINDOW_DEEP only
+    o.window = 3  # PCPPX_WINDOW_DEFAULT / DEEP / SHORT only
     b = abi.Batch(1, 1, 1, 1, 1, 1, 0)
     r = abi.Records(1, 1)
     assert lib.pcppx_parse_batch_device(C.c_void_p(1), C.byref(b), C.byref(o), C.byref(r), None) == abi.E_INVAL

@@ -206,3 +206,57 @@ def test_gpu_packed_layout_golden(engine):
             g = _device(engine, batch, po, tuples=False, stats=False)
             os_, ol = oracle.oracle_parse(batch, opts)
             oracle.compare_exact(g["summary"], g["layers"], os_, ol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,ml,layout", [(2, 0, abi.LAYOUT_FIXED), (4, 0, abi.LAYOUT_FIXED), (4, 8, abi.LAYOUT_PACKED),
+                                           (3, 8, abi.LAYOUT_FIXED), (5, 12, abi.LAYOUT_PACKED)])
+def test_gpu_short_window(engine, cfg, ml, layout):
+    """opts.window = PCPPX_WINDOW_SHORT (parse-only launches gather one 96-B round and no second one; stacks past it take
+    the generic walk): summary, layers, tuples and collectStats identical to the default two-round window's and to the
+    restatement's on configs 2-5 with checksums off (config 5's deep stacks run the generic walk), config 2 at its full
+    1M through the bench's own output (tuples alone), a gapped batch, the host path, crafted stacks and every golden set
+    under its option variants (checksum launches run their DEFAULT window under SHORT)."""
+    from mutate import as_batch, crafted, crafted_l7
+
+    from pcapplusplus_amd.engine import parse_on_device
+
+    n = 1_000_000 if cfg == 2 else 100_000
+    b = synth.config(cfg, n)
+    short = abi.make_opts(0, 8, False, ml, abi.WINDOW_SHORT, layout)
+    gs = _device(engine, b, short, summary=cfg != 2, stats=cfg != 2)
+    if cfg == 2:  # bench config 2's launch: the 5-tuple extract alone
+        _, _, ot = oracle.oracle_parse_tuples(b, short, threads=8)
+        assert gs["tuples"].tobytes() == ot.tobytes()
+        return
+    gd = _device(engine, b, abi.make_opts(0, 8, False, ml, layout=layout))
+
+    def lay(g):  # max_layers 0 writes no layers
+        return g.get("layers", np.zeros((len(g["summary"]), 0), dtype=abi.LAYER_DTYPE))
+
+    oracle.compare_exact(gs["summary"], lay(gs), gd["summary"], lay(gd))
+    assert gs["tuples"].tobytes() == gd["tuples"].tobytes() and gs["proto_stats"] == gd["proto_stats"]
+    sub = as_batch([b.packet(i) for i in range(0, n, 11)], gaps=True, seed=cfg)
+    g = _device(engine, sub, short)
+    os_, ol, ot = oracle.oracle_parse_tuples(sub, short, threads=8)
+    assert g["tuples"].tobytes() == ot.tobytes()
+    oracle.compare_exact(g["summary"], lay(g), os_, ol)
+    if layout == abi.LAYOUT_FIXED and ml:
+        h = engine.parse_host(b, short)  # the host path's chunked launches pick the same instance
+        oracle.compare_exact(h[0], h[1], gs["summary"], gs["layers"])
+    if cfg != 4 or ml:
+        return
+    cb = as_batch(crafted() + crafted_l7(), gaps=True, seed=29)
+    for csum in (False, True):
+        o = abi.make_opts(0, 8, csum, 16, abi.WINDOW_SHORT)
+        s, lay = parse_on_device(engine, cb, o)
+        os_, ol = oracle.oracle_parse(cb, o)
+        oracle.compare_exact(s, lay, os_, ol)
+    for path in golden_files():
+        batch, variants = load_golden(path)
+        for v, (opts, rsum, rlay) in variants.items():
+            o = abi.make_opts(opts.parse_until_family, opts.parse_until_osi, bool(opts.want_checksums), opts.max_layers,
+                              abi.WINDOW_SHORT)
+            s, lay = parse_on_device(engine, batch, o)
+            os_, ol = oracle.oracle_parse(batch, o)
+            oracle.compare_exact(s, lay, os_, ol)

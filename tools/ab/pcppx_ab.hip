@@ -150,16 +150,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	hipStream_t stream = static_cast<hipStream_t>(hip_stream);
 	const Params prm = make_params(b, o, r, nullptr);
 	const dim3 grid((b->n + kTile - 1) / kTile);
-	// a persistent launch: every resident wave slot once (occupancy x CUs / div), at most one block per tile
-	auto persist = [&](auto kern, int div) {
-		int dev = 0, cus = 0, per = 0;
-		(void)hipGetDevice(&dev);
-		(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-		(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kTile, 0);
-		uint32_t g = (uint32_t)(per * cus / div);
-		g = g < 1 ? 1 : (g > grid.x ? grid.x : g);
-		hipLaunchKernelGGL(kern, dim3(g), dim3(kTile), 0, stream, prm);
-	};
 	switch (variant)
 	{
 	case 1:
@@ -204,13 +194,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 62: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window
 	case 63: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 6 waves
 	case 64: hipLaunchKernelGGL((parse_tile_kernel<8, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 8 waves
-	case 65: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // product + third stream window
-	case 66: hipLaunchKernelGGL((parse_tile_kernel<5, 64, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // 3 x 1-KiB windows
-	// persistent parse-only instances: next tile's descriptors + first-round window prefetched during the parse
-	case 70: persist(parse_tile_kernel<4, 64, 9, true, false, false, 6, false, true, false, false, false, true, true, false, false, false, false, true>, 1); break;
-	case 71: persist(parse_tile_kernel<4, 64, 6, true, false, false, 6, false, true, false, false, false, true, true, false, false, false, false, true>, 1); break;
-	case 72: persist(parse_tile_kernel<4, 64, 9, true, false, false, 6, false, true, false, false, false, true, true, false, false, false, false, true>, 2); break;
-	case 73: persist(parse_tile_kernel<4, 64, 5, true, false, false, 5, false, true, false, false, false, true, true, false, false, false, false, true>, 1); break;
 	case 51: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, false>), grid, dim3(kTile), 0, stream, prm); break;  // tight second round, no realign
 	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;

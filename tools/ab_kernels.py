@@ -35,8 +35,6 @@ cases = {
     "tile/packed": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 0),
     "tile/packed-earlyB": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 54),
     "tile/packed-skipgen": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 52),
-    "tile/packed-win3": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 65),
-    "tile/packed-win3x1k": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 66),
     "tile/packed-sf": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 56),
     "tile/packed-sf-cached": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 57),
     "tile/packed-sf-w6": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 58),
@@ -84,10 +82,6 @@ cases.update({
     "po/c6": (abi.make_opts(0, 8, False, _ml), 60),
     "po/c6w6": (abi.make_opts(0, 8, False, _ml), 61),
     "po/c5w6": (abi.make_opts(0, 8, False, _ml), 63),
-    "po/persist": (abi.make_opts(0, 8, False, _ml), 70),
-    "po/persist-packed": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 70),
-    "po/persist-c6": (abi.make_opts(0, 8, False, _ml), 71),
-    "po/persist-half": (abi.make_opts(0, 8, False, _ml), 72),
     "po/gather-only": (abi.make_opts(0, 8, False, _ml), 29),
     "po/skip-generic": (abi.make_opts(0, 8, False, _ml), 44),
 })
