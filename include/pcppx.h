@@ -238,7 +238,7 @@ PCPPX_API int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, c
 
 /* Per-flow counters keyed by hash5Tuple (Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:99-125).
  * Device pointers: summary[n] from a previous parse, caplens[n]. The table is open-addressed with
- * `capacity` slots (power of two), split into min(256, max(1, capacity / 4096)) equal regions by the key's hash (a
+ * `capacity` slots (power of two), split into min(512, max(1, capacity / 4096)) equal regions by the key's hash (a
  * flow lives in its region; every region has at least 4096 slots, or is the whole table); keys[i]==0 marks an
  * empty slot — flow key 0 (non-5-tuple packets, PacketUtils.cpp:141-148) is counted in stats[0] (packets) /
  * stats[1] (bytes) instead, and packets whose region had no free slot in stats[2]. Counts accumulate across

@@ -2616,7 +2616,7 @@ constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 // record queue (one global atomic per partition per batch reserves the space); flow_merge_kernel then gives every
 // partition to one block, which folds its queue in LDS and updates its own table region with plain loads and stores.
 // A full queue falls back to atomics on the region.
-constexpr uint32_t kFlowMaxParts = 256;  // flow-table partitions (merge blocks) at most
+constexpr uint32_t kFlowMaxParts = 1024;  // flow-table partitions (merge blocks) at most
 struct FlowPart
 {
 	uint4* recs;       // P queues of rec_cap records {key, 0, packed lo, packed hi}
@@ -3233,12 +3233,14 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 // the partitioned flush (product): the same aggregation, then per-partition queues and one merge block per partition
 #define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true>
 #define PCPPX_FLOW_PART_DENSE_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true>
-#define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<kFlowMergeThreads, 8192, 2>
+// merge: 512-thread blocks with a 4096-slot LDS table (48 KiB: 3 blocks per CU) over 512 partitions -- count + merge
+// 0.194 -> 0.181 ms on config 4 against 1024 threads / 8192 slots / 256 partitions (profiles/r03_ab_flow_merge.txt)
+#define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<kFlowMergeThreads, 4096, 2>
 constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 4096, kFlowBlocks = 256;
 constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed LDS/HBM counters hold
-constexpr uint32_t kFlowPartLog2 = 8;            // flow-table partitions (merge blocks); at most kFlowMaxParts
-constexpr uint32_t kFlowMinRegionLog2 = 12;      // slots per partition at least (capacity 2^20+ -> 256 partitions)
-constexpr uint32_t kFlowMergeThreads = 1024;
+constexpr uint32_t kFlowPartLog2 = 9;            // flow-table partitions (merge blocks); at most kFlowMaxParts
+constexpr uint32_t kFlowMinRegionLog2 = 12;      // slots per partition at least (capacity 2^21+ -> 512 partitions)
+constexpr uint32_t kFlowMergeThreads = 512;
 
 }  // namespace
 

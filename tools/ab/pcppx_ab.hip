@@ -230,7 +230,9 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	auto* pk = reinterpret_cast<unsigned long long*>(packets);
 	auto* by = reinterpret_cast<unsigned long long*>(bytes);
 	auto* st = reinterpret_cast<unsigned long long*>(stats);
-	const uint32_t l = log2u(capacity), lp = l < kFlowPartLog2 ? l : kFlowPartLog2;
+	// shapes 4-7: the product count kernel with 512 / 1024 partitions (regions) and smaller merge blocks
+	const uint32_t want = shape == 4 || shape == 5 ? 9u : (shape == 7 ? 10u : kFlowPartLog2);
+	const uint32_t l = log2u(capacity), lp = l < want ? l : want;
 	const FlowPart fp{ static_cast<uint4*>(queues), rec_cap, fill, lp, l - lp };
 	auto go = [&](auto kern, uint32_t threads, uint32_t batch, uint32_t blocks) {
 		const uint32_t batches = (n + batch - 1) / batch;
@@ -247,7 +249,12 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	int rc = check_launch("pcppx_ab_flow_part", stream);
 	if (rc != PCPPX_OK)
 		return rc;
-	hipLaunchKernelGGL(PCPPX_FLOW_MERGE_KERNEL, dim3(1u << lp), dim3(kFlowMergeThreads), 0, stream, fp, keys, pk, by, st);
+	if (shape == 4)
+		hipLaunchKernelGGL((flow_merge_kernel<1024, 4096, 1>), dim3(1u << lp), dim3(1024), 0, stream, fp, keys, pk, by, st);
+	else if (shape >= 5 && shape <= 7)
+		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
+	else
+		hipLaunchKernelGGL(PCPPX_FLOW_MERGE_KERNEL, dim3(1u << lp), dim3(kFlowMergeThreads), 0, stream, fp, keys, pk, by, st);
 	return check_launch("flow_merge_kernel", stream);
 }
 
