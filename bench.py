@@ -64,9 +64,10 @@ def parse_args():
                     help="layer-record layout (pcppx_opts.layout): fixed = max_layers entries per packet; packed = only the "
                          "chain's entries, dense per 64-packet tile (the same entries; auto: " + ", ".join(
                              f"config {c} {v}" for c, v in sorted(CONFIG_LAYOUT.items())) + ")")
-    ap.add_argument("--records", choices=("auto", "summary", "tuples"), default="auto",
-                    help="per-packet record: the 32-B summary, or the 48-B 5-tuple extract (pcppx_tuple) alone "
-                         "(auto: tuples for config 2's 5-tuple extract, else summary)")
+    ap.add_argument("--records", choices=("auto", "summary", "tuples", "keys"), default="auto",
+                    help="per-packet record: the 32-B summary, the 48-B 5-tuple extract (pcppx_tuple) alone, or (config "
+                         "4) only what the flow table reads: the dense hash5 column + collectStats, no summary (auto: "
+                         "tuples for config 2's 5-tuple extract, keys for config 4's flow table, else summary)")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: a multi-rank rehearsal on fewer GPUs than ranks (ranks share cards round-robin); "
                          "the timed numbers of such a run are not a scaling measurement")
@@ -266,9 +267,11 @@ def main() -> None:
     gen_s = time.time() - t0
     want_csum = args.checksums == "on" or (args.checksums == "auto" and cfg == 3)
     layout = args.layout if args.layout != "auto" else CONFIG_LAYOUT.get(cfg, "fixed")
-    rec_kind = args.records if args.records != "auto" else ("tuples" if cfg == 2 else "summary")
-    if rec_kind == "tuples" and ml:
-        sys.exit("bench.py: --records tuples writes no layer records (use --max-layers 0)")
+    rec_kind = args.records if args.records != "auto" else {2: "tuples", 4: "keys"}.get(cfg, "summary")
+    if rec_kind in ("tuples", "keys") and ml:
+        sys.exit(f"bench.py: --records {rec_kind} writes no layer records (use --max-layers 0)")
+    if rec_kind == "keys" and cfg != 4:
+        sys.exit("bench.py: --records keys is config 4's flow-table launch")
     window = args.window if args.window != "auto" else CONFIG_WINDOW.get(cfg, "default")
     opts = abi.make_opts(0, 8, want_csum, ml, {"default": abi.WINDOW_DEFAULT, "deep": abi.WINDOW_DEEP,
                                                "short": abi.WINDOW_SHORT}[window],
@@ -368,6 +371,8 @@ def main() -> None:
                        "hash5_equal_summary": bool(torch.equal(tv[:, 10], s[:, 0]))}
     else:
         tuple_check = None
+    # the flow table's keys: the timed launches' dense hash5 column equals the full parse's summary hash5
+    keys_equal = bool(torch.equal(flow_keys, s[:, 0])) if flow_keys is not None else None
     stats_line = None
     if proto_stats is not None:  # collectStats over every launch (warmup + timed): the histogram of one pass
         launches = args.warmup + args.steps
@@ -503,6 +508,8 @@ def main() -> None:
             line["e2e_host_to_host"] = e2e
         if flow_check is not None:
             line["config"]["flow_table"] = flow_check
+        if keys_equal is not None:
+            line["config"]["flow_keys_equal_hash5"] = keys_equal
         if stats_line is not None:
             line["config"]["collect_stats"] = stats_line
         if tuple_check is not None:

@@ -192,7 +192,8 @@ typedef struct pcppx_tuple {
 
 /* Output arrays (same memory space as the batch for the _device call, host for the _host call). */
 typedef struct pcppx_records {
-	pcppx_summary* summary; /* n entries; may be NULL on the device path when tuples is set and layout is FIXED */
+	pcppx_summary* summary; /* n entries; may be NULL on the device path when max_layers is 0 and one of tuples /
+	                           flow_keys / proto_stats is set (e.g. a flow table's launch: dense keys + collectStats) */
 	pcppx_layer* layers;    /* n * max_layers entries in pcppx_opts.layout, or NULL when max_layers == 0 */
 	uint32_t* flow_keys;    /* optional (NULL): n entries, flow_keys[i] = summary[i].hash5 -- the dense column
 	                           FilterTraffic's flow table is keyed by (pcppx_flow_count_keys_device reads 8 B per

@@ -189,13 +189,16 @@ int valid_opts(const pcppx_opts* o)
 	return PCPPX_OK;
 }
 
-// the device path's record arguments: layers when max_layers > 0; a summary unless only the 5-tuples are wanted
-// (a PACKED layout is decoded through the summary's n_layers)
+// the device path's record arguments: layers when max_layers > 0; a summary unless the caller wants only the
+// summary-free outputs -- the 5-tuple extract, the dense flow-key column and / or the collectStats counters (a
+// FilterTraffic-style consumer reads nothing else) -- with no layers (a PACKED layout is decoded through the summary's
+// n_layers)
 bool valid_device_records(const pcppx_opts* o, const pcppx_records* r)
 {
 	if (o->max_layers != 0 && r->layers == nullptr)
 		return false;
-	if (r->summary == nullptr && (r->tuples == nullptr || o->max_layers != 0))
+	if (r->summary == nullptr &&
+	    (o->max_layers != 0 || (r->tuples == nullptr && r->flow_keys == nullptr && r->proto_stats == nullptr)))
 		return false;
 	return true;
 }

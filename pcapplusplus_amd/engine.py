@@ -61,9 +61,9 @@ class Engine:
     def parse_device(self, data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers=None,
                      stream: int | None = None, flow_keys=None, tuples=None, proto_stats=None) -> None:
         """Queue a parse of device tensors on `stream` (a hipStream_t handle, e.g.
-        torch.cuda.current_stream().cuda_stream). summary: uint8 tensor of n*32 bytes (or None with tuples and no
-        layers); layers: n*max_layers*8; tuples: n*48 bytes (5-tuple extracts); proto_stats: 16 x int64,
-        accumulated (collectStats)."""
+        torch.cuda.current_stream().cuda_stream). summary: uint8 tensor of n*32 bytes (or None with no layers when
+        tuples / flow_keys / proto_stats is given); layers: n*max_layers*8; flow_keys: n int32 (hash5); tuples: n*48
+        bytes (5-tuple extracts); proto_stats: 16 x int64, accumulated (collectStats)."""
         b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
         opt = lambda t: abi.ptr(t) if t is not None else None  # noqa: E731
         rec = abi.Records(opt(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None,
@@ -257,9 +257,9 @@ def records_from_device(summary_t, layers_t, n: int, max_layers: int):
 
 
 def parse_on_device_ex(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = None, device: str = "cuda:0",
-                       summary: bool = True, tuples: bool = False, proto_stats: bool = False):
+                       summary: bool = True, tuples: bool = False, proto_stats: bool = False, flow_keys: bool = False):
     """parse_on_device with the optional outputs: {"summary", "layers" (FIXED [n, max_layers], decoded when the
-    layout is PACKED), "packed" (the raw PACKED entries), "tuples", "proto_stats" (dict)}."""
+    layout is PACKED), "packed" (the raw PACKED entries), "tuples", "proto_stats" (dict), "flow_keys" (u32 hash5)}."""
     import torch
 
     opts = opts or abi.make_opts()
@@ -269,8 +269,9 @@ def parse_on_device_ex(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = 
     lay = torch.zeros(max(n * opts.max_layers, 1) * 8, dtype=torch.uint8, device=device)
     tp = torch.zeros(max(n, 1) * 48, dtype=torch.uint8, device=device) if tuples else None
     ps = torch.zeros(abi.PROTO_STATS, dtype=torch.int64, device=device) if proto_stats else None
+    fk = torch.zeros(max(n, 1), dtype=torch.int32, device=device) if flow_keys else None
     eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, st, lay if opts.max_layers else None,
-                     torch.cuda.current_stream(device).cuda_stream, tuples=tp, proto_stats=ps)
+                     torch.cuda.current_stream(device).cuda_stream, flow_keys=fk, tuples=tp, proto_stats=ps)
     torch.cuda.synchronize(device)
     out = {}
     if st is not None:
@@ -284,6 +285,8 @@ def parse_on_device_ex(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = 
             out["layers"] = raw.reshape(n, opts.max_layers)
     if tp is not None:
         out["tuples"] = tp.cpu().numpy().view(abi.TUPLE_DTYPE)[:n]
+    if fk is not None:
+        out["flow_keys"] = fk.cpu().numpy().view(np.uint32)[:n]
     if ps is not None:
         v = ps.cpu().numpy()
         out["proto_stats"] = {f: int(v[k]) for k, f in enumerate(abi.PROTO_STATS_FIELDS)}

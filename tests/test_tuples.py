@@ -260,3 +260,25 @@ def test_gpu_short_window(engine, cfg, ml, layout):
             s, lay = parse_on_device(engine, batch, o)
             os_, ol = oracle.oracle_parse(batch, o)
             oracle.compare_exact(s, lay, os_, ol)
+
+
+@pytest.mark.gpu
+def test_gpu_summary_free_flow_launch(engine):
+    """A flow table's launch (bench config 4): no summary, only the dense hash5 column and the collectStats counters
+    (pcppx_records.summary = NULL) -- the keys equal the summary's hash5 of a full launch and the restatement's, the
+    counters equal the full launch's, under the default and the SHORT window."""
+    b = synth.config(4, 200_000)
+    full = _device(engine, b, abi.make_opts(0, 8, False, 0), tuples=False, stats=True)
+    for w in (abi.WINDOW_DEFAULT, abi.WINDOW_SHORT):
+        g = _device(engine, b, abi.make_opts(0, 8, False, 0, w), summary=False, tuples=False, stats=True)
+        assert "summary" not in g
+        from pcapplusplus_amd.engine import parse_on_device_ex
+        k = parse_on_device_ex(engine, b, abi.make_opts(0, 8, False, 0, w), summary=False, proto_stats=True,
+                               flow_keys=True)
+        assert (k["flow_keys"] == full["summary"]["hash5"]).all()
+        assert k["proto_stats"] == full["proto_stats"] == g["proto_stats"]
+    idx = np.arange(0, b.n, 17)
+    from mutate import as_batch
+    sub = as_batch([b.packet(int(i)) for i in idx])
+    os_, _ = oracle.oracle_parse(sub, abi.make_opts(0, 8, False, 0))
+    assert (k["flow_keys"][idx] == os_["hash5"]).all()

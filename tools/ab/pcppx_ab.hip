@@ -113,6 +113,40 @@ __global__ __launch_bounds__(kTile) void diag_tile_read(const uint8_t* data, uin
 		out[blockIdx.x] = acc;
 }
 
+// variant 7: the tile-shaped read of variant 3 plus the parse's record stores -- each wave also writes w_per_wave bytes of
+// non-temporal 16-B stores (config 3: 65.6 B of records per 333-B packet, 0.195 of the bytes read): the traffic floor of
+// the checksum kernel's read + write mix without its header gather and parse
+__global__ __launch_bounds__(kTile) void diag_tile_rw(const uint8_t* data, uint64_t len, uint32_t per_wave,
+                                                       uint8_t* wout, uint32_t w_per_wave, uint32_t* out)
+{
+	const uint64_t base = (uint64_t)blockIdx.x * per_wave;
+	uint32_t acc = 0;
+	for (uint32_t c = threadIdx.x; 16ull * c < per_wave; c += 4 * kTile)
+	{
+		uint4 v[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+		{
+			const uint64_t a = base + 16ull * (c + k * kTile);
+			v[k] = a + 16 <= len ? ld16((uintptr_t)data + a) : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+	}
+	acc = wave_incl_scan(acc);
+	typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+	u32x4* w = reinterpret_cast<u32x4*>(wout + (uint64_t)blockIdx.x * w_per_wave);
+	for (uint32_t c = threadIdx.x; 16 * c < w_per_wave; c += kTile)
+	{
+		u32x4 x;
+		x.x = acc + c; x.y = acc; x.z = c; x.w = blockIdx.x;
+		__builtin_nontemporal_store(x, w + c);
+	}
+	if (threadIdx.x == 63)
+		out[blockIdx.x] = acc;
+}
+
 __global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, uint64_t len, uint32_t* out)
 {
 	const uint64_t nch = len / 16;
@@ -168,6 +202,17 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 		}
 		else
 			hipLaunchKernelGGL(diag_grid_read, dim3(256 * 8), dim3(kBlock), 0, stream, b->data, b->data_len, out);
+		break;
+	}
+	case 7:
+	{
+		// writes over the layer-record buffer (n * max_layers * 8 B must hold 0.2 x the batch bytes)
+		const uint32_t per_wave = 21 * 1024, w_per_wave = 4192;  // 64 packets x 65.5 B
+		const uint32_t blocks = (uint32_t)((b->data_len + per_wave - 1) / per_wave);
+		if ((uint64_t)blocks * w_per_wave > (uint64_t)b->n * o->max_layers * 8)
+			return PCPPX_E_INVAL;
+		hipLaunchKernelGGL(diag_tile_rw, dim3(blocks), dim3(kTile), 0, stream, b->data, b->data_len, per_wave,
+		                   reinterpret_cast<uint8_t*>(r->layers), w_per_wave, reinterpret_cast<uint32_t*>(r->summary));
 		break;
 	}
 	case 5: hipLaunchKernelGGL((parse_tile_kernel<5, 256>), grid, dim3(kTile), 0, stream, prm); break;

@@ -59,6 +59,7 @@ cases = {
     "tile/stream-only": (abi.make_opts(0, 8, True, 0), 2),
     "diag/tile-read": (abi.make_opts(0, 8, True, 0), 3),
     "diag/grid-read": (abi.make_opts(0, 8, True, 0), 4),
+    "diag/tile-rw": (abi.make_opts(0, 8, True, 16), 7),
 }
 # parse-only instances (checksums off): LDS window chunks / first-round chunks; records per packet AB_ML
 _ml = int(__import__("os").environ.get("AB_ML", "8"))
@@ -95,7 +96,7 @@ want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
     first = next(iter(cases.values()))[0]
     if o.max_layers != first.max_layers or o.want_checksums != want_csum_ref or o.layout != first.layout or \
-            v in (2, 3, 4, 29, 44, 52, -2):  # diagnostics with wrong records; -2: L7 records of an older contract
+            v in (2, 3, 4, 7, 29, 44, 52, -2):  # diagnostics with wrong records; -2: L7 records of an older contract
         continue
     summ.zero_()
     lay.zero_()
