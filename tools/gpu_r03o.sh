@@ -9,3 +9,5 @@ tools/bench_all.sh r03o 4 > gpurun_out/r03o_bench_all.log 2>&1 || { tail -20 gpu
 python3 -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print(d['value'], d['ms_per_step'], c['kernel_ms'], c['records'], c['window'], d['roofline']['frac'], d['roofline']['traffic'], c.get('flow_keys_equal_hash5'), c['flow_table']['exact'], c['collect_stats']['consistent'])" gpurun_out/r03o_bench_cfg4.json
 AB_CASES=tile/packed,diag/tile-read,diag/tile-rw timeout -k 10 400 python -u tools/ab_kernels.py 10000000 15 3 > gpurun_out/r03o_ab_floor.log 2>&1 || { tail -20 gpurun_out/r03o_ab_floor.log; exit 4; }
 grep -E "median" gpurun_out/r03o_ab_floor.log
+AB_SHAPES=0,5,8 timeout -k 10 400 python -u tools/ab_flow_part.py 15 > gpurun_out/r03o_ab_flow.log 2>&1 || { tail -20 gpurun_out/r03o_ab_flow.log; exit 5; }
+grep -v amdgpu.ids gpurun_out/r03o_ab_flow.log
