@@ -2617,15 +2617,13 @@ constexpr uint32_t log2u(uint32_t v) { return v <= 1 ? 0 : 1 + log2u(v >> 1); }
 // partition to one block, which folds its queue in LDS and updates its own table region with plain loads and stores.
 // A full queue falls back to atomics on the region.
 constexpr uint32_t kFlowMaxParts = 1024;  // flow-table partitions (merge blocks) at most
-constexpr uint32_t kFlowMaxSegs = 256;    // count blocks with block-local queue segments (kLocalQ) at most
 struct FlowPart
 {
-	uint4* recs;       // P queues of rec_cap records {key, 0, packed lo, packed hi} (kLocalQ: P x nseg segments)
-	uint32_t rec_cap;  // records per queue (kLocalQ: per segment)
-	uint32_t* fill;    // P queue lengths (kLocalQ: P x nseg segment lengths), zero before the launch
+	uint4* recs;       // P queues of rec_cap records {key, 0, packed lo, packed hi}
+	uint32_t rec_cap;
+	uint32_t* fill;    // P queue lengths (zero before the launch)
 	uint32_t log2p;    // partitions
 	uint32_t log2r;    // slots per region
-	uint32_t nseg;     // kLocalQ: count blocks (one queue segment per partition each)
 };
 
 __device__ __forceinline__ uint32_t flow_part(uint32_t key, uint32_t log2p)
@@ -2657,10 +2655,8 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 }
 
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
-// kLocalQ (with kPart): each count block appends to its own segment of every partition's queue at a block-local running
-// length (LDS), so a batch's flush needs no global reservation atomic; the lengths are stored once at the end.
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false, bool kLocalQ = false>
+          bool kPart = false, bool kDense = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -2682,11 +2678,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	}
 	if (kPart)
 		for (uint32_t j = t; j < kFlowMaxParts; j += kFB)
-		{
 			s_bin[j] = 0;
-			if (kLocalQ)
-				s_base[j] = 0;
-		}
 	__syncthreads();
 	// kPrefetch: the next batch's keys and lengths are loaded into registers before this batch's flush,
 	// so their latency overlaps the flush's HBM reads and atomics
@@ -2767,35 +2759,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				fseen[u] = fk[u] ? atomicAdd(&s_bin[fs[u]], 1u) : 0u;
 			}
 			__syncthreads();
-			if constexpr (kLocalQ)
-			{
-				// this block's segment of each partition queue, at its running length
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; ++u)
-				{
-					const uint32_t j = u * kFB + t;
-					const uint32_t key = fk[u];
-					if (key == 0)
-						continue;
-					const uint32_t pos = s_base[fs[u]] + fseen[u];
-					const unsigned long long c = s_cnt[j];
-					if (pos < fpart.rec_cap)
-						fpart.recs[((size_t)fs[u] * fpart.nseg + blockIdx.x) * fpart.rec_cap + pos] =
-							make_uint4(key, 0u, (uint32_t)c, (uint32_t)(c >> 32));
-					else if (!flow_region_add_atomic(keys, packets, bytes, fpart, key, c >> 40, c & ((1ull << 40) - 1)))
-						lost += c >> 40;
-					s_key[j] = 0;
-					s_cnt[j] = 0;
-				}
-				__syncthreads();
-				for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
-				{
-					s_base[b] += s_bin[b];
-					s_bin[b] = 0;
-				}
-				__syncthreads();
-				continue;
-			}
 			for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
 			{
 				const uint32_t c = s_bin[b];
@@ -2861,9 +2824,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		}
 		__syncthreads();
 	}
-	if constexpr (kPart && kLocalQ)  // the segment lengths (records past rec_cap went to the region atomically)
-		for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
-			fpart.fill[(size_t)b * fpart.nseg + blockIdx.x] = s_base[b] < fpart.rec_cap ? s_base[b] : fpart.rec_cap;
 	z_pk = wave_sum_u64(z_pk);
 	z_by = wave_sum_u64(z_by);
 	lost = wave_sum_u64(lost);
@@ -2898,50 +2858,17 @@ __global__ __launch_bounds__(kBlock) void flow_unpack_kernel(unsigned long long*
 // thread per round; flushed whenever more than half full), then adds each distinct key's counts into its own table
 // region -- which no other block touches, so the counts take plain loads and stores (a CAS only claims a new key's
 // slot against the block's other threads). Resets the queue length for the next launch.
-// kLocalQ: the partition's queue is nseg block segments; a flat record index maps to (segment, position) through the
-// segments' prefix lengths in LDS (a binary search)
-template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT, bool kLocalQ = false>
+template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT>
 __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* keys, unsigned long long* packets,
                                                          unsigned long long* bytes, unsigned long long* stats)
 {
 	__shared__ uint32_t s_key[kMLds];
 	__shared__ unsigned long long s_cnt[kMLds];
 	__shared__ uint32_t s_used;
-	__shared__ uint32_t s_seg[kLocalQ ? kFlowMaxSegs + 1 : 1];  // segment prefix lengths
 	static_assert(kMB * kPerT <= kMLds / 4 && (kMLds & (kMLds - 1)) == 0, "merge table");
-	static_assert(!kLocalQ || kMB >= kFlowMaxSegs / 4, "merge: one wave scans the segment lengths");
 	const uint32_t t = threadIdx.x, p = blockIdx.x;
-	uint32_t cnt = 0;
-	if constexpr (kLocalQ)
-	{
-		if (t < 64)
-		{
-			// lane l holds segments 4l..4l+3 (nseg <= 256)
-			uint32_t c[4], sum = 0;
-#pragma unroll
-			for (int k = 0; k < 4; ++k)
-			{
-				const uint32_t sg = 4 * t + k;
-				c[k] = sg < fp.nseg ? fp.fill[(size_t)p * fp.nseg + sg] : 0u;
-				sum += c[k];
-			}
-			const uint32_t incl = wave_incl_scan(sum);
-			uint32_t run = incl - sum;
-#pragma unroll
-			for (int k = 0; k < 4; ++k)
-			{
-				s_seg[4 * t + k] = run;
-				run += c[k];
-			}
-			if (t == 63)
-				s_seg[kFlowMaxSegs] = incl;
-		}
-		__syncthreads();
-		cnt = s_seg[kFlowMaxSegs];
-	}
-	else
-		cnt = fp.fill[p] < fp.rec_cap ? fp.fill[p] : fp.rec_cap;
-	const uint4* q = fp.recs + (size_t)p * fp.rec_cap * (kLocalQ ? fp.nseg : 1u);
+	const uint32_t cnt = fp.fill[p] < fp.rec_cap ? fp.fill[p] : fp.rec_cap;
+	const uint4* q = fp.recs + (size_t)p * fp.rec_cap;
 	const uint32_t rbase = p << fp.log2r, rm = (1u << fp.log2r) - 1u;
 	for (uint32_t j = t; j < kMLds; j += kMB)
 	{
@@ -2959,22 +2886,7 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 		for (uint32_t k = 0; k < kPerT; ++k)
 		{
 			const uint32_t idx = base + k * kMB + t;
-			if constexpr (kLocalQ)
-			{
-				// the last segment whose prefix is <= idx
-				uint32_t lo = 0, hi = kFlowMaxSegs - 1;
-				while (lo < hi)
-				{
-					const uint32_t mid = (lo + hi + 1) >> 1;
-					if (s_seg[mid] <= idx)
-						lo = mid;
-					else
-						hi = mid - 1;
-				}
-				nxt[k] = idx < cnt ? q[(size_t)lo * fp.rec_cap + (idx - s_seg[lo])] : make_uint4(0, 0, 0, 0);
-			}
-			else
-				nxt[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
+			nxt[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
 		}
 	};
 	fetch(0);
@@ -3058,10 +2970,7 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 	lost = wave_sum_u64(lost);
 	if ((t & 63) == 0 && lost)
 		atomicAdd(&stats[2], lost);
-	if (kLocalQ)
-		for (uint32_t sg = t; sg < fp.nseg; sg += kMB)
-			fp.fill[(size_t)p * fp.nseg + sg] = 0;
-	else if (t == 0)
+	if (t == 0)
 		fp.fill[p] = 0;
 }
 

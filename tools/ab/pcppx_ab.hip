@@ -278,9 +278,7 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	// shapes 4-7: the product count kernel with 512 / 1024 partitions (regions) and smaller merge blocks
 	const uint32_t want = shape == 6 ? 8u : (shape == 7 ? 10u : 9u);  // partitions (log2): tools/ab_flow_part.py PARTS
 	const uint32_t l = log2u(capacity), lp = l < want ? l : want;
-	const uint32_t nseg_batches = (n + 4095) / 4096;
-	// shape 8: block-local queue segments (kLocalQ), 256 count blocks, rec_cap records per segment
-	const FlowPart fp{ static_cast<uint4*>(queues), rec_cap, fill, lp, l - lp, nseg_batches < 256 ? nseg_batches : 256u };
+	const FlowPart fp{ static_cast<uint4*>(queues), rec_cap, fill, lp, l - lp };
 	auto go = [&](auto kern, uint32_t threads, uint32_t batch, uint32_t blocks) {
 		const uint32_t batches = (n + batch - 1) / batch;
 		hipLaunchKernelGGL(kern, dim3(batches < blocks ? batches : blocks), dim3(threads), 0, stream, nullptr, caplens, n,
@@ -291,15 +289,12 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 1: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true, true, true>, 512, 2048, 768); break;
 	case 2: go(flow_count_kernel<256, 2048, 1024, kFlowHot, true, true, true>, 256, 1024, 1536); break;
 	case 3: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 512); break;
-	case 8: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, true>, 1024, 4096, 256); break;
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);
 	if (rc != PCPPX_OK)
 		return rc;
-	if (shape == 8)
-		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, true>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
-	else if (shape == 4)
+	if (shape == 4)
 		hipLaunchKernelGGL((flow_merge_kernel<1024, 4096, 1>), dim3(1u << lp), dim3(1024), 0, stream, fp, keys, pk, by, st);
 	else if (shape >= 5 && shape <= 7)
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
