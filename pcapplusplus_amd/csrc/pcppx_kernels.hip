@@ -2571,13 +2571,25 @@ __global__ __launch_bounds__(kBlock) void proto_stats_reduce_kernel(const uint4*
 #pragma unroll
 	for (int k = 0; k < kC; ++k)
 		a[k] = 0;
-	for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < nw; j += gridDim.x * kBlock)
+	// 8 independent record loads in flight per thread (128 blocks cover 262k waves = 16.7M packets in one round trip)
+	constexpr uint32_t kU = 8;
+	for (uint32_t b0 = blockIdx.x * kBlock * kU; b0 < nw; b0 += gridDim.x * kBlock * kU)
 	{
-		const uint4 v = part[j];
-		const uint32_t w[3] = { v.x, v.y, v.z };
+		uint4 v[kU];
 #pragma unroll
-		for (int k = 0; k < kC; ++k)
-			a[k] += (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+		for (uint32_t u = 0; u < kU; ++u)
+		{
+			const uint32_t j = b0 + u * kBlock + threadIdx.x;
+			v[u] = j < nw ? part[j] : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < kU; ++u)
+		{
+			const uint32_t w[3] = { v[u].x, v[u].y, v[u].z };
+#pragma unroll
+			for (int k = 0; k < kC; ++k)
+				a[k] += (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+		}
 	}
 	__shared__ unsigned long long s_part[kBlock / 64][kC];
 	const uint32_t wv = threadIdx.x >> 6;
@@ -3302,7 +3314,7 @@ int launch_proto_stats_reduce(const void* wave_stats, uint32_t n, uint64_t* out,
 	if (n == 0)
 		return PCPPX_OK;
 	const uint32_t nw = parse_waves(n);
-	const uint32_t blocks = (nw + kBlock - 1) / kBlock;
+	const uint32_t blocks = (nw + 8 * kBlock - 1) / (8 * kBlock);
 	hipLaunchKernelGGL(proto_stats_reduce_kernel, dim3(blocks < 128 ? blocks : 128), dim3(kBlock), 0, stream,
 	                   static_cast<const uint4*>(wave_stats), nw, reinterpret_cast<unsigned long long*>(out));
 	return check_launch("proto_stats_reduce_kernel", stream);
