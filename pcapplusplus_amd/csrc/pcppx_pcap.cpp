@@ -121,6 +121,7 @@ uint64_t int_pow(uint64_t x, uint32_t y)
 constexpr size_t kParRegion = 256ull << 20;  // bytes per parallel round
 constexpr size_t kParMin = 4ull << 20;       // fewer bytes left: walk sequentially
 constexpr unsigned kParThreads = 16;         // at most; one per MiB of the region at least
+constexpr unsigned kParChains = 4;           // interleaved chains (segments) per thread
 // fn(t) for t in [0, T): on new threads where they can be started, the rest on the calling thread (a thread that
 // cannot be created never fails the read)
 template <class F>
@@ -177,6 +178,11 @@ struct pcppx_pcap
 	uint32_t snaplen = 0;
 	uint32_t linktype = 0;  // pcap: the file's; pcapng: of the last batch returned (before it: of the first packet)
 	bool done = false;
+	// the record starts of the last parallel walk not yet handed out (a batch that ends inside a walked region leaves
+	// the rest here for the next batch instead of walking it again)
+	std::vector<size_t> pend;
+	size_t pend_i = 0, pend_end = 0;
+	bool pend_stop = false, pend_ok = false;
 	// pcapng: the file-wide interface list of light_pcapng_file_info
 	uint32_t n_if = 0;
 	uint16_t if_link[kMaxInterfaces];
@@ -329,6 +335,36 @@ struct pcppx_pcap
 		return ng ? next_pcapng(pk) : next_pcap(pk);
 	}
 
+	// a parallel walk of the next region when no walked starts are pending
+	bool parallel_ready() const
+	{
+		return !ng && !done && (pend_ok || size - pos >= kParMin);
+	}
+	void fill_pending()
+	{
+		if (pend_ok)
+			return;
+		const size_t region_end = pos + std::min(size - pos, kParRegion);
+		parallel_starts(region_end, pend, &pend_end, &pend_stop);
+		pend_i = 0;
+		pend_ok = true;
+	}
+	// k pending starts handed out; true when starts are left (the batch is full: it ends before the next one)
+	bool consume(size_t k)
+	{
+		pend_i += k;
+		if (pend_i < pend.size())
+		{
+			pos = pend[pend_i];
+			return true;
+		}
+		pos = pend_end;
+		pend_ok = false;
+		if (pend_stop)
+			done = true;
+		return false;
+	}
+
 	// the sequential chain from p (a record start or a guess) up to hi
 	void walk(size_t p, size_t hi, Chain& c) const
 	{
@@ -361,52 +397,112 @@ struct pcppx_pcap
 		return true;
 	}
 
-	// every record start in [pos, region_end) (and *end, *stop as Chain's), as the sequential walk finds them
+	// every record start in [pos, region_end) (and *end, *stop as Chain's), as the sequential walk finds them.
+	// The region is cut into kParChains segments per thread, and each thread advances its segments' chains in lockstep:
+	// a chain is one dependent header read per record (the next position comes from this header's caplen), so the
+	// interleaved chains keep kParChains of those reads in flight per core instead of one.
 	void parallel_starts(size_t region_end, std::vector<size_t>& out, size_t* end, bool* stop) const
 	{
-		const unsigned T = par_threads(region_end - pos);
-		std::vector<size_t> lo(T + 1);
-		for (unsigned t = 0; t <= T; ++t)
-			lo[t] = pos + (region_end - pos) / T * t;
-		lo[T] = region_end;
-		std::vector<Chain> seg(T);
+		const unsigned T = par_threads(region_end - pos), S = T * kParChains;
+		std::vector<size_t> lo(S + 1);
+		for (unsigned t = 0; t <= S; ++t)
+			lo[t] = pos + (region_end - pos) / S * t;
+		lo[S] = region_end;
+		std::vector<Chain> seg(S);
 		run_parallel(T, [&](unsigned t) {
-				size_t s0 = lo[t];
-				if (t > 0)
+				struct Cur
 				{
-					const size_t lim = std::min(lo[t + 1], lo[t] + kSyncScan);
-					while (s0 < lim && !plausible(s0))
-						++s0;
-					if (s0 >= lim)
+					size_t p, hi;
+					bool on;
+				};
+				Cur w[kParChains];
+				for (unsigned k = 0; k < kParChains; ++k)
+				{
+					const unsigned g = t * kParChains + k;
+					size_t s0 = lo[g];
+					w[k] = Cur{ s0, lo[g + 1], true };
+					if (g > 0)
 					{
-						seg[t].end = lo[t];  // no start found: the merge walks this segment
-						return;
+						const size_t lim = std::min(lo[g + 1], lo[g] + kSyncScan);
+						while (s0 < lim && !plausible(s0))
+							++s0;
+						if (s0 >= lim)
+						{
+							seg[g].end = lo[g];  // no start found: the merge walks this segment
+							w[k].on = false;
+							continue;
+						}
+						w[k].p = s0;
+					}
+					if (w[k].p >= w[k].hi)
+					{
+						seg[g].end = w[k].p;
+						w[k].on = false;
 					}
 				}
-				walk(s0, lo[t + 1], seg[t]);
+				for (unsigned live = kParChains; live;)
+				{
+					live = 0;
+					for (unsigned k = 0; k < kParChains; ++k)
+					{
+						if (!w[k].on)
+							continue;
+						Chain& c = seg[t * kParChains + k];
+						Packet pk{};
+						if (!pcap_at(w[k].p, pk))
+						{
+							c.end = w[k].p;  // walk()'s rules: the stream ends here
+							c.stop = true;
+							w[k].on = false;
+							continue;
+						}
+						c.starts.push_back(w[k].p);
+						w[k].p = pk.next_pos;
+						if (w[k].p >= w[k].hi)
+						{
+							c.end = w[k].p;
+							w[k].on = false;
+							continue;
+						}
+						++live;
+					}
+				}
 			});
-		out = std::move(seg[0].starts);
+		// the accepted part of every segment, in order (a segment whose chain the true chain does not land on is walked
+		// again from the true position), then one parallel copy into `out`
+		std::vector<std::pair<const std::vector<size_t>*, size_t>> take;
+		take.reserve(S);
+		std::vector<Chain> redo(S);
+		take.emplace_back(&seg[0].starts, 0);
 		*end = seg[0].end;
 		*stop = seg[0].stop;
-		for (unsigned t = 1; t < T && !*stop; ++t)
+		for (unsigned t = 1; t < S && !*stop; ++t)
 		{
 			const std::vector<size_t>& c = seg[t].starts;
 			auto it = std::lower_bound(c.begin(), c.end(), *end);
 			if (it != c.end() && *it == *end)
 			{
-				out.insert(out.end(), it, c.end());  // the true chain lands on this segment's chain: one chain from here
+				take.emplace_back(&c, (size_t)(it - c.begin()));  // the true chain lands on this segment's chain
 				*end = seg[t].end;
 				*stop = seg[t].stop;
 			}
 			else
 			{
-				Chain redo;
-				walk(*end, lo[t + 1], redo);
-				out.insert(out.end(), redo.starts.begin(), redo.starts.end());
-				*end = redo.end;
-				*stop = redo.stop;
+				walk(*end, lo[t + 1], redo[t]);
+				take.emplace_back(&redo[t].starts, 0);
+				*end = redo[t].end;
+				*stop = redo[t].stop;
 			}
 		}
+		std::vector<size_t> at(take.size() + 1, 0);
+		for (size_t j = 0; j < take.size(); ++j)
+			at[j + 1] = at[j] + (take[j].first->size() - take[j].second);
+		out.resize(at.back());
+		run_parallel(T, [&](unsigned t) {
+				for (size_t j = t; j < take.size(); j += T)
+					std::copy(take[j].first->begin() + (ptrdiff_t)take[j].second, take[j].first->end(),
+					          out.begin() + (ptrdiff_t)at[j]);
+			});
 	}
 };
 
@@ -506,20 +602,18 @@ extern "C"
 		uint32_t n = 0;
 		uint64_t used = 0;
 		// large pcap regions: the parallel walk (identical records), then the fields and the copies in parallel
-		while (!r->ng && !r->done && n < max_packets && r->size - r->pos >= kParMin)
+		while (n < max_packets && r->parallel_ready())
 		{
-			const size_t region_end = r->pos + std::min(r->size - r->pos, kParRegion);
-			std::vector<size_t> starts;
-			size_t end = 0;
-			bool stop = false;
-			r->parallel_starts(region_end, starts, &end, &stop);
+			r->fill_pending();
+			const size_t* starts = r->pend.data() + r->pend_i;
+			const size_t avail = r->pend.size() - r->pend_i;
 			// the records that fit: at most max_packets, and their bytes within data_cap (as the sequential loop below)
 			size_t k = 0;
 			std::vector<uint64_t> dst;
-			dst.reserve(std::min(starts.size(), (size_t)(max_packets - n)));
-			while (k < starts.size() && n + k < max_packets)
+			dst.reserve(std::min(avail, (size_t)(max_packets - n)));
+			while (k < avail && n + k < max_packets)
 			{
-				Packet pk;
+				Packet pk{};
 				(void)r->pcap_at(starts[k], pk);
 				if (used + pk.keep > data_cap)
 					break;
@@ -527,13 +621,13 @@ extern "C"
 				used += pk.keep;
 				++k;
 			}
-			if (k == 0 && n == 0 && !starts.empty())
+			if (k == 0 && n == 0 && avail)
 				return PCPPX_E_NOMEM;  // a single record does not fit the caller's buffer
-			const unsigned T = par_threads(region_end - r->pos);
+			const unsigned T = par_threads(k * 512);
 			run_parallel(T, [&](unsigned t) {
 					for (size_t i = k * t / T; i < k * (t + 1) / T; ++i)
 					{
-						Packet pk;
+						Packet pk{};
 						(void)r->pcap_at(starts[i], pk);
 						if (pk.keep)
 							std::memcpy(data + dst[i], pk.bytes, pk.keep);
@@ -546,14 +640,8 @@ extern "C"
 					}
 				});
 			n += (uint32_t)k;
-			if (k < starts.size())
-			{
-				r->pos = starts[k];
+			if (r->consume(k))
 				break;
-			}
-			r->pos = end;
-			if (stop)
-				r->done = true;
 		}
 		while (!r->done && n < max_packets)
 		{
@@ -603,19 +691,16 @@ extern "C"
 		*data_len = r->size;
 		uint32_t n = 0;
 		// large pcap regions: the parallel walk (identical records), then the fields of each record in parallel
-		while (!r->ng && !r->done && n < max_packets && r->size - r->pos >= kParMin)
+		while (n < max_packets && r->parallel_ready())
 		{
-			const size_t region_end = r->pos + std::min(r->size - r->pos, kParRegion);
-			std::vector<size_t> starts;
-			size_t end = 0;
-			bool stop = false;
-			r->parallel_starts(region_end, starts, &end, &stop);
-			const size_t k = std::min(starts.size(), (size_t)(max_packets - n));
-			const unsigned T = par_threads(region_end - r->pos);
+			r->fill_pending();
+			const size_t* starts = r->pend.data() + r->pend_i;
+			const size_t k = std::min(r->pend.size() - r->pend_i, (size_t)(max_packets - n));
+			const unsigned T = par_threads(k * 512);
 			run_parallel(T, [&](unsigned t) {
 					for (size_t i = k * t / T; i < k * (t + 1) / T; ++i)
 					{
-						Packet pk;
+						Packet pk{};
 						(void)r->pcap_at(starts[i], pk);  // a record of the chain: valid
 						offsets[n + i] = (uint64_t)(pk.bytes - r->map);
 						caplens[n + i] = pk.keep;
@@ -626,14 +711,8 @@ extern "C"
 					}
 				});
 			n += (uint32_t)k;
-			if (k < starts.size())
-			{
-				r->pos = starts[k];  // the batch is full: the next one starts at this record
-				break;
-			}
-			r->pos = end;
-			if (stop)
-				r->done = true;
+			if (r->consume(k))
+				break;  // the batch is full: the next one starts at the first pending record
 		}
 		while (!r->done && n < max_packets)
 		{
