@@ -381,6 +381,21 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
     if shorter.any():
         i = int(np.nonzero(shorter)[0][0])
         raise AssertionError(f"flagged packet #{i} has more layers than the reference")
+    # NEEDS_HOST_L7 packets whose whole reference chain is visible and holds no IPv4 / IPv6 / TCP / UDP layer past the
+    # engine's prefix: hash5Tuple / hash2Tuple (first IP, last TCP else UDP: PacketUtils.cpp:139-245), the port layer
+    # and both checksums come from layers the engine built, so they are exact as well
+    l7only = flagged & ((eng_sum["flags"] & (abi.F_NEEDS_HOST & ~abi.F_NEEDS_HOST_L7)) == 0)
+    past = (idx >= eng_sum["n_layers"][:, None]) & (idx < ref_sum["n_layers"][:, None]) & \
+        np.isin(ref_lay["proto"], (2, 3, 4, 5))
+    l7exact = l7only & (ref_sum["n_layers"] < ml) & ~past.any(axis=1)
+    for f in ("hash5", "hash5_dir", "hash2", "l4_layer", "ip_csum_calc", "ip_csum_stored", "l4_csum_calc",
+              "l4_csum_stored"):
+        bad = np.nonzero(l7exact & (eng_sum[f] != ref_sum[f]))[0]
+        if len(bad):
+            i = int(bad[0])
+            raise AssertionError(f"field {f} differs on {len(bad)} NEEDS_HOST_L7 packets; first #{i}: "
+                                 f"engine={eng_sum[i]} ref={ref_sum[i]} layers engine={eng_lay[i]} ref={ref_lay[i]}")
+    stats["l7_flagged_exact_5tuple"] = int(l7exact.sum())
     return stats
 
 
