@@ -1957,16 +1957,12 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // after the parse the L4 whole-chunk sum is that difference less the packet's leading chunks before the L4 start
 // (LDS window), whenever the L4 layer runs to the packet's end (else whole chunks from HBM, as for sparse tiles). The
 // header gather then reads lines the stream has just brought into L2, and no stream register is live in the parse.
-// SkipGathered: the span stream does not load again the 16-B chunks the header gather already staged (a bitmap of the
-// gathered chunks in LDS; windows past the two issued before the gather): a packet's L4 sum adds its own skipped
-// chunks back from its LDS window. Only for tiles of ascending, non-overlapping packets, where another packet's window
-// reaches into a packet's whole-chunk L4 range nowhere (only its partial first / last chunk).
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
           bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false,
-          bool EarlyB = false, bool StreamFirst = false, bool SkipGathered = false>
+          bool EarlyB = false, bool StreamFirst = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1974,8 +1970,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	__shared__ uint32_t stage[kTile * kTSlotDw];
 	__shared__ uint64_t m_a0[kTile];
 	__shared__ uint32_t m_nch[kTile];  // gather range of each packet: chunks [bits 8-15, bits 0-7)
-	constexpr uint32_t kSkipWords = 256;  // SkipGathered: gathered-chunk bitmap of spans up to 8192 chunks (128 KiB)
-	__shared__ uint32_t skipmap[SkipGathered ? kSkipWords : 1];
 	// layer rows staged in LDS up to this max_layers (a row = ml + 1 padded 8-B records); beyond, direct stores
 	constexpr uint32_t kRowMl = (uint32_t)kTSlotDw / 2 - 1 < kRowMaxMl ? (uint32_t)kTSlotDw / 2 - 1 : kRowMaxMl;
 	static_assert(kTile * (kRowMl + 1) * 2 <= kTile * kTSlotDw, "stage too small for layer rows");
@@ -2006,8 +2000,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	const bool stream = want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
 	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
 	uint4 va[SWin / 64], vb[SWin / 64];
-	bool skip_on = false;  // uniform: SkipGathered's bitmap is set for this tile
-	uint64_t skip_bits = 0;  // SkipGathered: bit 2*win + k = this lane's chunk of window win, load k, is skipped
 	auto load = [&](uint4 (&v)[SWin / 64], uint32_t win) {
 #pragma unroll
 		for (int k = 0; k < SWin / 64; ++k)
@@ -2015,11 +2007,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// clamped, not masked: lanes past the span re-read its last chunk (same line, no extra
 			// traffic); their values lie after every prefix target, so they are inert
 			const uint32_t c = win * SWin + 64 * k + lane;
-			// SkipGathered: a chunk the header gather staged is not loaded again -- the lane reads the span's first
-			// chunk instead (a line already in L2; no branch, so the window's loads stay one straight-line group) and
-			// its value is dropped in the stream
-			const bool sk = SkipGathered && ((skip_bits >> (2 * win + k)) & 1u);
-			const uintptr_t a = sk ? smin : smin + 16ull * (c < nchunks ? c : nchunks - 1);
+			const uintptr_t a = smin + 16ull * (c < nchunks ? c : nchunks - 1);
 			if (NT)
 			{
 				const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<gptr16>(a));
@@ -2125,47 +2113,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	gather();
 	__syncthreads();
 	p.s = reinterpret_cast<lptr8>((lptr32w)(stage) + lane * kTSlotDw);
-	if constexpr (SkipGathered)
-	{
-		// the gathered chunks of the span, when every packet of the tile is live and they lie in ascending,
-		// non-overlapping order (a packed or gapped batch) and the span is long enough for windows past the early two
-		const uint64_t nxt = __shfl_down(pkt_addr, 1, 64);
-		const bool nxt_in = __shfl_down(in ? 1 : 0, 1, 64) != 0;
-		const bool order_ok = !in || lane == 63 || !nxt_in || pkt_addr + cap <= nxt;
-		static_assert(SWin == 128 || !SkipGathered, "SkipGathered: two loads per window, 32 windows in 64 bits");
-		skip_on = stream && nchunks > 2u * SWin && nchunks <= 32u * 2 * 64 && __ballot(!order_ok) == 0 &&
-		          __ballot(in && !live) == 0;
-		if (skip_on)  // uniform
-		{
-			for (uint32_t w = lane; w < (nchunks + 31) / 32; w += kTile)
-				skipmap[w] = 0;
-			__syncthreads();
-			if (live && p.nch)
-			{
-				const uint32_t c0 = (uint32_t)((p.a0 - smin) >> 4), c1 = c0 + p.nch;  // p.nch <= Chunks < 32
-				const uint32_t w0 = c0 >> 5, w1 = (c1 - 1) >> 5;
-				const uint32_t lo = c0 & 31, hi = (c1 - 1) & 31;
-				if (w0 == w1)
-					atomicOr(&skipmap[w0], (uint32_t)((((uint64_t)1 << (hi - lo + 1)) - 1) << lo));
-				else
-				{
-					atomicOr(&skipmap[w0], ~0u << lo);
-					atomicOr(&skipmap[w1], (uint32_t)(((uint64_t)1 << (hi + 1)) - 1));
-				}
-			}
-			__syncthreads();
-			// this lane's skipped loads, windows 2 and up, into a register mask (no LDS read in the stream loop)
-			const uint32_t nwin = (nchunks + SWin - 1) / SWin;
-			for (uint32_t wi = 2; wi < nwin; ++wi)
-#pragma unroll
-				for (int k = 0; k < SWin / 64; ++k)
-				{
-					const uint32_t c = wi * SWin + 64 * k + lane;
-					if (c < nchunks && ((skipmap[c >> 5] >> (c & 31)) & 1u))
-						skip_bits |= 1ull << (2 * wi + k);
-				}
-		}
-	}
 	auto set_lim = [&]() {
 		const uint32_t staged = 16 * p.nch - p.mis;
 		p.lim = (live && p.nch) ? (staged < cap ? staged : cap) : 0;
@@ -2396,10 +2343,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// needs them.
 			const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
 			const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
-			// tail chunk (not from the stream when SkipGathered skipped it: then from the LDS window / HBM below)
-			const bool te_skip = SkipGathered && skip_on && tail && (uint32_t)((f1 - smin) >> 4) >= 2u * SWin &&
-			                     ((skipmap[(uint32_t)((f1 - smin) >> 4) >> 5] >> (((f1 - smin) >> 4) & 31)) & 1u);
-			const int32_t te = (tail && !te_skip) ? (int32_t)((f1 - smin) >> 4) : -2;
+			const int32_t te = tail ? (int32_t)((f1 - smin) >> 4) : -2;      // tail chunk
 			uint32_t p0 = 0, p1 = 0, carry = 0;
 			const uint32_t nwin = (nchunks + SWin - 1) / SWin;
 			auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
@@ -2407,9 +2351,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				for (int k = 0; k < SWin / 64; ++k)
 				{
 					const int32_t g = (int32_t)(win * SWin + 64 * k);
-					uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
-					if (SkipGathered)
-						h = ((skip_bits >> (2 * win + k)) & 1u) ? 0u : h;  // a skipped chunk counts 0 here
+					const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
 					const uint32_t x = wave_incl_scan(h);
 					const uint32_t pre = carry + x;
 					const bool in0 = t0 >= g && t0 < g + 64, in1 = t1 >= g && t1 < g + 64;
@@ -2448,21 +2390,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			}
 			if (full)
 				fsum = p1 - p0;
-			if (SkipGathered && skip_on && full)
-			{
-				// this packet's own skipped chunks in [f0, f1): the only skipped ones there (ascending tiles), read
-				// back from its LDS window
-				const uint32_t c0 = (uint32_t)((p.a0 - smin) >> 4);
-				const uint32_t f0c = (uint32_t)((f0 - smin) >> 4), f1c = (uint32_t)((f1 - smin) >> 4);
-				uint32_t lo = f0c > c0 ? f0c : c0;
-				lo = lo > 2u * SWin ? lo : 2u * SWin;
-				const uint32_t hi = f1c < c0 + p.nch ? f1c : c0 + p.nch;
-				for (uint32_t c = lo; c < hi; ++c)
-				{
-					lptr32 wv = reinterpret_cast<lptr32>(p.s) + (c - c0) * 4;
-					fsum += halves(wv[0]) + halves(wv[1]) + halves(wv[2]) + halves(wv[3]);
-				}
-			}
 		}
 		else if (full)
 			fsum = full_chunks_sum(f0, f1);

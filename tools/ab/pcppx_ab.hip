@@ -239,7 +239,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 62: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window
 	case 63: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 6 waves
 	case 64: hipLaunchKernelGGL((parse_tile_kernel<8, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 8 waves
-	case 67: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // product + skip the gathered chunks in the stream
 	case 51: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, false>), grid, dim3(kTile), 0, stream, prm); break;  // tight second round, no realign
 	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;

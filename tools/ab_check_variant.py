@@ -2,7 +2,7 @@
 config-3 batch -- gapped (every start alignment, HBM edge chunks), deep stacks with checksums, crafted and L7 stacks,
 config-3 batches with gaps of zero bytes, every golden set -- records equal byte for byte (summary and layers).
 
-  AB_VARIANT=67 python tools/ab_check_variant.py
+  AB_VARIANT=<n> python tools/ab_check_variant.py   (variant 67, SkipGathered, lives in commit history: profiles/r03_ab_skip_gathered.txt)
 """
 import os
 import sys

@@ -35,8 +35,6 @@ cases = {
     "tile/packed": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 0),
     "tile/packed-earlyB": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 54),
     "tile/packed-skipgen": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 52),
-    "tile/packed-skipg": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 67),
-    "tile/fixed-skipg": (abi.make_opts(0, 8, True, 8), 67),
     "tile/packed-sf": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 56),
     "tile/packed-sf-cached": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 57),
     "tile/packed-sf-w6": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 58),
