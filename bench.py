@@ -43,8 +43,8 @@ def parse_args():
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU (default: the config's size)")
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 4, 5))
     ap.add_argument("--max-layers", type=int, default=None,
-                    help="layer records per packet (default: 8 for config 3, 12 for config 5, 0 (summary only) for the "
-                         "configs whose consumer reads only the summary: 2's 5-tuple extract, 4's flow table)")
+                    help="layer records per packet (default: 8 for config 3, 12 for config 5, 0 for the configs whose "
+                         "consumer reads no layers: 2's 5-tuple extract, 4's flow table)")
     ap.add_argument("--checksums", choices=("auto", "on", "off"), default="auto",
                     help="IPv4/L4 checksum verify (auto: on for config 3 only)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="packets in the CPU-baseline sample")

@@ -239,6 +239,8 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 62: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window
 	case 63: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 6 waves
 	case 64: hipLaunchKernelGGL((parse_tile_kernel<8, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 8 waves
+	case 68: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // parse-only, cached record stores
+	case 69: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 6, false, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // SHORT, cached record stores
 	case 51: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, false>), grid, dim3(kTile), 0, stream, prm); break;  // tight second round, no realign
 	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;

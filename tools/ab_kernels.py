@@ -81,6 +81,8 @@ cases.update({
     "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
     "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),
     "po/c6": (abi.make_opts(0, 8, False, _ml), 60),
+    "po/packed-cached": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 68),
+    "po/c6-cached": (abi.make_opts(0, 8, False, _ml), 69),
     "po/c6w6": (abi.make_opts(0, 8, False, _ml), 61),
     "po/c5w6": (abi.make_opts(0, 8, False, _ml), 63),
     "po/gather-only": (abi.make_opts(0, 8, False, _ml), 29),
