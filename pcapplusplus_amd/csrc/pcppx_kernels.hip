@@ -1957,15 +1957,12 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 // after the parse the L4 whole-chunk sum is that difference less the packet's leading chunks before the L4 start
 // (LDS window), whenever the L4 layer runs to the packet's end (else whole chunks from HBM, as for sparse tiles). The
 // header gather then reads lines the stream has just brought into L2, and no stream register is live in the parse.
-// XcdTiles: blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8); with XcdTiles the blocks of one
-// XCD take one contiguous eighth of the tiles, so neighbouring tiles (their shared boundary lines, a packet's header
-// lines next to the previous tile's tail) meet in one XCD's L2.
 // GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
 // record stores (zero rows), no parse: the memory time of the parse-only access pattern.
 template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
           bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
           bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false,
-          bool EarlyB = false, bool StreamFirst = false, bool XcdTiles = false>
+          bool EarlyB = false, bool StreamFirst = false>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1985,17 +1982,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	const bool want_csum = Csum && prm.want_csum;  // uniform
 
 	const uint32_t lane = threadIdx.x;
-	uint32_t tile = blockIdx.x;
-	if constexpr (XcdTiles)
-	{
-		// XCD x runs blocks x, x + 8, ...: ceil((G - x) / 8) of them; its k-th one takes tile prefix(x) + k
-		const uint32_t G = gridDim.x, x = blockIdx.x & 7;
-		uint32_t pre = 0;
-		for (uint32_t y = 0; y < x; ++y)
-			pre += (G - y + 7) >> 3;
-		tile = pre + (blockIdx.x >> 3);
-	}
-	const uint32_t i = tile * kTile + lane;
+	const uint32_t i = blockIdx.x * kTile + lane;
 	const bool in = i < prm.n;
 	const uint64_t off = in ? prm.offsets[i] : 0;
 	const uint32_t cap = in ? prm.caplens[i] : 0;
@@ -2458,7 +2445,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	if (in && prm.tuples != nullptr)  // the LDS window is still intact here (the rows below reuse it)
 		write_tuple(p, w, h5, prm.tuples + i);
 	if (prm.wave_stats != nullptr)  // uniform
-		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + tile);
+		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + blockIdx.x);
 
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
 	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
@@ -2473,7 +2460,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		const uint32_t incl = wave_incl_scan(cnt);
 		const uint32_t excl = incl - cnt;
 		const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)tile * kTile * ml;
+		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)blockIdx.x * kTile * ml;
 		__syncthreads();  // every lane is done with the header stage
 		lptr64w rows = (lptr64w)(stage);
 		if (fast)
@@ -2515,7 +2502,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				rows[lane * rs + k] = e;
 			});
 		__syncthreads();
-		const uint32_t first = tile * kTile;
+		const uint32_t first = blockIdx.x * kTile;
 		const uint32_t nrows = prm.n - first < (uint32_t)kTile ? prm.n - first : (uint32_t)kTile;
 		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)first * ml;
 		// kTile / ml rows per pass, lane -> (row, record): consecutive lanes write consecutive records

@@ -241,9 +241,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 64: hipLaunchKernelGGL((parse_tile_kernel<8, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 8 waves
 	case 68: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // parse-only, cached record stores
 	case 69: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 6, false, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // SHORT, cached record stores
-	case 75: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // product + XCD-contiguous tiles
-	case 76: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 6, true, false, false, 6, false, true, false, false, false, true, true, false, false, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // SHORT + XCD-contiguous tiles
-	case 77: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, true, false, false, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // parse-only + XCD-contiguous tiles
 	case 51: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, false>), grid, dim3(kTile), 0, stream, prm); break;  // tight second round, no realign
 	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
 	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;

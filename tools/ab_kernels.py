@@ -35,7 +35,6 @@ cases = {
     "tile/packed": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 0),
     "tile/packed-earlyB": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 54),
     "tile/packed-skipgen": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 52),
-    "tile/packed-xcd": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 75),
     "tile/packed-sf": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 56),
     "tile/packed-sf-cached": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 57),
     "tile/packed-sf-w6": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 58),
@@ -82,8 +81,6 @@ cases.update({
     "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
     "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),
     "po/c6": (abi.make_opts(0, 8, False, _ml), 60),
-    "po/c6-xcd": (abi.make_opts(0, 8, False, _ml), 76),
-    "po/packed-xcd": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 77),
     "po/packed-cached": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 68),
     "po/c6-cached": (abi.make_opts(0, 8, False, _ml), 69),
     "po/c6w6": (abi.make_opts(0, 8, False, _ml), 61),
