@@ -11,6 +11,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 sys.path.insert(0, str(ROOT))
@@ -75,3 +77,28 @@ def test_real_launcher_starts_n_ranks(tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "ranks 2 2 --config 4" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [2, 4, 5])
+def test_bench_small_run_checks_its_records(cfg):
+    """bench.py end to end on the GPU at a small size for the configs whose launch differs from the default one: config 2
+    (5-tuple extract alone, SHORT window), config 4 (dense keys + collectStats without a summary, SHORT window, the flow
+    table) and config 5 (two-round window, PACKED rows) -- one JSON line whose own checks hold."""
+    import json
+
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", str(cfg), "--packets", "200000", "--steps",
+                        "3", "--warmup", "1", "--no-cpu-baseline", "--no-e2e", "--no-traffic"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    c = line["config"]
+    assert line["n_gpus"] == 1 and line["value"] > 0 and c["flagged_packets"] == 0
+    if cfg == 2:
+        assert c["records"] == "tuples" and c["window"] == "short"
+        assert c["tuples"] == {"with_5tuple": 200000, "hash5_equal_summary": True}
+    if cfg == 4:
+        assert c["records"] == "keys" and c["window"] == "short" and c["flow_keys_equal_hash5"]
+        assert c["flow_table"]["exact"] and c["flow_table"]["conserved"] and c["collect_stats"]["consistent"]
+    if cfg == 5:
+        assert c["records"] == "summary" and c["layout"] == "packed" and c["window"] == "default"
