@@ -1,46 +1,42 @@
 /**
  * PcapPlusPlus benchmark application on the GPU parse engine
  * ==========================================================
- * The reference application (Examples/PcapPlusPlus-benchmark/benchmark.cpp:60-109), with one change: instead of
- * reading one RawPacket and building one Packet at a time, the reader fills a batch (getNextPackets, the reference's
- * IFileReaderDevice batch read) and the engine parses the whole batch on the GPU (the batch prepass); the next
- * batch is read by a reader thread meanwhile. The per-packet handler then runs over Packet views with
- * pcpp::Packet's names, as before.
+ * The reference application (Examples/PcapPlusPlus-benchmark/benchmark.cpp:60-109) over the engine's facade
+ * (include/pcppx.hpp) instead of Packet++ / Pcap++: `namespace pcpp = pcppx`, and the packet loop is the reference's
+ * token for token -- reader.getNextPacket(rawPacket) hands out packets of pages the reader has already parsed on the
+ * GPU (the batch prepass runs inside the library, ahead of the loop), and Packet(&rawPacket, pcpp::TCP) binds to
+ * that packet's records.
  *
- *   benchmark <input-file> packet <repetitions> [--host-parser <lib.so>] [--dump]
+ *   benchmark <input-file> <dns|packet> <repetitions> [--host-parser <lib.so>] [--dump]
  *
- * Output: "<packets per run> <average ms per run>", as the reference. The reference's dns mode iterates DnsLayer's
- * queries and answers, an L7 dissector outside the engine: it is refused. Packets the engine leaves to the host
- * (an L7 layer it does not dissect) are completed by the caller's own Packet++ parse when --host-parser names a
- * library exporting `pcppx_host_parse` (include/pcppx.h, pcppx_host_parse_fn). --dump also prints every
- * packet's layer list and hash5Tuple (used by the tests to compare with the reference).
+ * Output: "<packets per run> <average ms per run>", as the reference. Two engine-side options, taken off the command
+ * line before the reference's argument check: --host-parser names a library exporting `pcppx_host_parse`
+ * (include/pcppx.h, pcppx_host_parse_fn): the caller's own Packet++ parse, which completes the packets the engine
+ * leaves to the host (an L7 layer it does not dissect); --dump prints every packet's layer list and hash5Tuple in the
+ * first run (the tests compare them with the reference). The dns mode iterates DnsLayer's queries and answers, an L7
+ * dissector the engine does not build: it is refused.
  */
 #include <dlfcn.h>
 
-#include <chrono>
 #include <cinttypes>
 #include <cstdio>
-#include <future>
 #include <iostream>
-#include <numeric>
+#include <chrono>
 #include <string>
 #include <vector>
+#include <numeric>
 
 #include "pcppx.hpp"
 
-using namespace pcppx;
+namespace pcpp = pcppx;
+using namespace pcpp;
 
 size_t count = 0;
 
-bool handle_packet(Packet& packet)
-{
-	(void)packet;
-	count++;
-	return true;
-}
-
 namespace
 {
+bool dumpPackets = false;
+
 // --dump: "<index> <n_layers> <proto>:<offset>:<hdr_len>:<data_len> ... h5=<hash5Tuple> h5d=<dir> h2=<hash2Tuple>"
 void dump(size_t index, const Packet& packet)
 {
@@ -64,91 +60,95 @@ pcppx_host_parse_fn loadHostParser(const std::string& path)
 		throw Error(PCPPX_E_INVAL, path + " does not export pcppx_host_parse");
 	return fn;
 }
+
+// take the engine-side options off argv; false on a malformed one
+bool engineOptions(int& argc, char* argv[])
+{
+	int out = 1;
+	for (int k = 1; k < argc; ++k)
+	{
+		const std::string a = argv[k];
+		if (a == "--dump")
+			dumpPackets = true;
+		else if (a == "--host-parser")
+		{
+			if (k + 1 >= argc)
+				return false;
+			setHostParser(loadHostParser(argv[++k]));
+		}
+		else
+			argv[out++] = argv[k];
+	}
+	argc = out;
+	return true;
+}
 }  // namespace
+
+bool handle_packet(Packet& packet)
+{
+	if (dumpPackets)
+		dump(count, packet);
+	count++;
+	return true;
+}
 
 int main(int argc, char* argv[])
 {
-	if (argc < 4)
-	{
-		std::cout << "Usage: " << *argv << " <input-file> packet <repetitions> [--host-parser <lib.so>] [--dump]\n";
-		return 1;
-	}
-	std::string input_type(argv[2]);
-	if (input_type != "packet")
-	{
-		// dns mode walks DnsLayer's queries and answers (benchmark.cpp:30-52): an L7 dissector, left to Packet++
-		std::cerr << "only packet mode runs on the engine: dns mode iterates DnsLayer resources (L7)\n";
-		return 1;
-	}
-	int total_runs = std::stoi(argv[3]);
-	std::string hostParser;
-	bool dumpPackets = false;
-	for (int k = 4; k < argc; ++k)
-	{
-		const std::string a = argv[k];
-		if (a == "--host-parser" && k + 1 < argc)
-			hostParser = argv[++k];
-		else if (a == "--dump")
-			dumpPackets = true;
-		else
-		{
-			std::cout << "Usage: " << *argv << " <input-file> packet <repetitions> [--host-parser <lib.so>] [--dump]\n";
-			return 1;
-		}
-	}
-	size_t total_packets = 0;
-	std::vector<std::chrono::high_resolution_clock::duration> durations;
 	try
 	{
-		Engine engine(0);
-		if (!hostParser.empty())
-			engine.setHostParser(loadHostParser(hostParser));
-		RawPacketVector bufs[2];  // batch k is parsed while batch k+1 is read (a reader thread; distinct buffers)
+		if (!engineOptions(argc, argv))
+		{
+			std::cout << "Usage: " << *argv << " <input-file> <dns|packet> <repetitions> [--host-parser <lib.so>] [--dump]\n";
+			return 1;
+		}
+		if (argc != 4)
+		{
+			std::cout << "Usage: " << *argv << " <input-file> <dns|packet> <repetitions>\n";
+			return 1;
+		}
+		std::string input_type(argv[2]);
+		if (input_type == "dns")
+		{
+			// dns mode walks DnsLayer's queries and answers (benchmark.cpp:30-52): an L7 dissector, left to Packet++
+			std::cerr << "only packet mode runs on the engine: dns mode iterates DnsLayer resources (L7)\n";
+			return 1;
+		}
+		int total_runs = std::stoi(argv[3]);
+		size_t total_packets = 0;
+		std::vector<std::chrono::high_resolution_clock::duration> durations;
 		for (int i = 0; i < total_runs; ++i)
 		{
 			count = 0;
-			size_t index = 0;
 			PcapFileReaderDevice reader(argv[1]);
 			reader.open();
 			std::chrono::high_resolution_clock::time_point start;
 			{
 				start = std::chrono::high_resolution_clock::now();
-				PacketParseOptions options(TCP);  // Packet(&rawPacket, pcpp::TCP)
-				options.computeChecksums = false;
-				int cur = 0;
-				auto next = std::async(std::launch::async, [&] { return reader.getNextPackets(bufs[0], 1 << 20); });
-				while (next.get() > 0)
+				RawPacket rawPacket;
+				while (reader.getNextPacket(rawPacket))
 				{
-					next = std::async(std::launch::async,
-					                  [&, k = cur ^ 1] { return reader.getNextPackets(bufs[k], 1 << 20); });
-					ParsedBatch parsed = engine.parse(bufs[cur], options);  // the batch prepass
-					for (Packet packet : parsed)
-					{
-						handle_packet(packet);
-						if (dumpPackets && i == 0)
-							dump(index, packet);
-						++index;
-					}
-					cur ^= 1;
+					Packet packet(&rawPacket, pcpp::TCP);
+					handle_packet(packet);
 				}
 			}
 			auto end = std::chrono::high_resolution_clock::now();
 			durations.push_back(end - start);
 			total_packets += count;
 			reader.close();
+			dumpPackets = false;
 		}
+		auto total_time =
+		    std::accumulate(durations.begin(), durations.end(), std::chrono::high_resolution_clock::duration(0));
+
+		using std::chrono::duration_cast;
+		using std::chrono::milliseconds;
+		auto total_time_in_ms = duration_cast<milliseconds>(total_time).count();
+		std::cout << (total_packets / total_runs) << " " << (total_time_in_ms / durations.size()) << std::endl;
 	}
 	catch (const Error& e)
 	{
 		std::cerr << e.what() << "\n";
 		return 2;
 	}
-	auto total_time =
-	    std::accumulate(durations.begin(), durations.end(), std::chrono::high_resolution_clock::duration(0));
-
-	using std::chrono::duration_cast;
-	using std::chrono::milliseconds;
-	auto total_time_in_ms = duration_cast<milliseconds>(total_time).count();
-	std::cout << (total_packets / total_runs) << " " << (total_time_in_ms / durations.size()) << std::endl;
 	return 0;
 }

@@ -2,12 +2,12 @@
  * DpdkExample-FilterTraffic's worker on the GPU parse engine
  * ==========================================================
  * The reference worker (Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:45-162, PacketStats Common.h:57-142,
- * PacketMatchingEngine.h:43-107, the stats table main.cpp:244-264) with a pcap file in place of the DPDK RX queues
- * and one change: each received burst is parsed by the engine in one batch (the batch prepass), and the per-packet
- * loop - collectStats, hash5Tuple, the flow table, isMatched, the pcap writer - runs as before over Packet views
- * with pcpp::Packet's names. Packets the engine leaves to the host are completed by the caller's own Packet++
- * parse (--host-parser <lib.so> exporting pcppx_host_parse), so every counter, HTTP/DNS/TLS included, is the
- * reference's.
+ * PacketMatchingEngine.h:43-107, the stats table main.cpp:244-264) over the engine's facade (`namespace pcpp =
+ * pcppx`), with a capture file in place of the DPDK RX queues: receivePackets fills each burst of RawPackets from
+ * pages the reader has already parsed on the GPU (the batch prepass runs inside the library), and the burst loop --
+ * `pcpp::Packet parsedPacket(packetArr[i])`, collectStats, hash5Tuple, the flow table, isMatched, the pcap writer --
+ * is the reference's. Packets the engine leaves to the host are completed by the caller's own Packet++ parse
+ * (--host-parser <lib.so> exporting pcppx_host_parse), so every counter, HTTP/DNS/TLS included, is the reference's.
  *
  * --device-worker runs the whole worker on the GPU instead (pcppx_filter_batch_host: flow table, matching and
  * statistics in HBM); its HTTP/DNS/TLS counters cover the packets the device settles ("left to host" counts the
@@ -15,6 +15,7 @@
  *
  *   filter_traffic -f in.pcap [-o out.pcap] [-s SRC_IP] [-d DST_IP] [-S SRC_PORT] [-D DST_PORT] [-P TCP|UDP]
  *                  [-b BURST] [--host-parser <lib.so>] [--device-worker]
+ * BURST: packets per receivePackets call (MAX_RECEIVE_BURST, 64) or, with --device-worker, per device batch (1M).
  */
 #include <dlfcn.h>
 
@@ -28,6 +29,8 @@
 #include <vector>
 
 #include "pcppx.hpp"
+
+namespace pcpp = pcppx;
 
 namespace
 {
@@ -137,50 +140,6 @@ private:
 	bool m_MatchSrcIp, m_MatchDstIp, m_MatchSrcPort, m_MatchDstPort, m_MatchProtocol;
 };
 
-/* PcapFileWriterDevice (Pcap++/header/PcapFileDevice.h): classic pcap, microsecond timestamps */
-class PcapFileWriterDevice
-{
-public:
-	PcapFileWriterDevice(const std::string& path, uint32_t linkType) : m_Path(path), m_LinkType(linkType) {}
-	~PcapFileWriterDevice()
-	{
-		if (m_F)
-			std::fclose(m_F);
-	}
-	bool open()
-	{
-		m_F = std::fopen(m_Path.c_str(), "wb");
-		if (m_F == nullptr)
-			return false;
-		const uint32_t hdr[6] = { 0xa1b2c3d4u, 2u | (4u << 16), 0, 0, 262144, m_LinkType };
-		return std::fwrite(hdr, 4, 6, m_F) == 6;
-	}
-	/* PcapFileWriterDevice::writePacket (Pcap++/src/PcapFileDevice.cpp:1026-1039): a file holds one link type, a
-	 * packet of another is refused (a pcapng input can switch link types between interfaces) */
-	bool writePacket(const pcppx::RawPacketVector& b, size_t i)
-	{
-		if (b.linkType != m_LinkType)
-		{
-			if (m_Dropped++ == 0)
-				std::cerr << "Cannot write a packet with a different link type\n";
-			return false;
-		}
-		const uint64_t ts = b.timestampsNs[i];
-		const uint32_t h[4] = { (uint32_t)(ts / 1000000000ull), (uint32_t)(ts % 1000000000ull / 1000ull), b.caplens[i],
-			                    b.caplens[i] };
-		std::fwrite(h, 4, 4, m_F);
-		std::fwrite(b.packetData(i), 1, b.caplens[i], m_F);
-		return true;
-	}
-	uint64_t droppedPackets() const { return m_Dropped; }
-
-private:
-	std::string m_Path;
-	uint32_t m_LinkType;
-	uint64_t m_Dropped = 0;
-	FILE* m_F = nullptr;
-};
-
 /* the worker (AppWorkerThread.h:45-162): the input file replaces the DPDK RX queues */
 class AppWorkerThread
 {
@@ -190,19 +149,24 @@ public:
 	{}
 	PacketStats& getStats() { return m_Stats; }
 
-	bool run(pcppx::PcapFileReaderDevice& reader, PcapFileWriterDevice* pcapWriter)
+	/* AppWorkerThread::run (AppWorkerThread.h:45-162): the capture is the RX queue (receivePackets fills a burst
+	 * of RawPackets from pages the reader has already parsed on the GPU), and the burst loop is the reference's */
+	bool run(pcppx::PcapFileReaderDevice* dev, pcpp::PcapFileWriterDevice* pcapWriter)
 	{
-		pcppx::RawPacketVector packetArr;
-		pcppx::PacketParseOptions options;  // pcpp::Packet parsedPacket(rawPacket): full parse
-		options.computeChecksums = false;
-		// receive a burst (was dev->receivePackets(packetArr, MAX_RECEIVE_BURST, rxQueue), AppWorkerThread.h:85)
-		while (reader.getNextPackets(packetArr, (int)m_Burst) > 0)
+		std::vector<pcpp::RawPacket*> packetArr(m_Burst, nullptr);
+
+		// main loop, runs until the capture ends
+		while (!m_Stop)
 		{
-			pcppx::ParsedBatch parsed = m_Engine.parse(packetArr, options);  // the batch prepass
-			for (size_t i = 0; i < parsed.size(); i++)
+			// receive packets from the capture (was dev->receivePackets(packetArr, MAX_RECEIVE_BURST, rxQueue))
+			uint16_t packetsReceived = dev->receivePackets(packetArr.data(), (uint16_t)m_Burst, 0);
+			if (packetsReceived == 0)
+				break;
+
+			for (int i = 0; i < packetsReceived; i++)
 			{
 				// parse packet
-				pcppx::Packet parsedPacket = parsed[i];
+				pcpp::Packet parsedPacket(packetArr[i]);
 
 				// collect packet statistics
 				m_Stats.collectStats(parsedPacket);
@@ -211,12 +175,14 @@ public:
 
 				// hash the packet by 5-tuple and look in the flow table to see whether this packet belongs to an
 				// existing or new flow
-				uint32_t hash = pcppx::hash5Tuple(&parsedPacket);
+				uint32_t hash = pcpp::hash5Tuple(&parsedPacket);
 				auto iter3 = m_FlowTable.find(hash);
 
 				// if packet belongs to an already existing flow
 				if (iter3 != m_FlowTable.end() && iter3->second)
+				{
 					packetMatched = true;
+				}
 				else  // packet belongs to a new flow
 				{
 					packetMatched = m_PacketMatchingEngine.isMatched(parsedPacket);
@@ -226,10 +192,14 @@ public:
 						m_FlowTable[hash] = true;
 
 						// collect stats
-						if (parsedPacket.isPacketOfType(pcppx::TCP))
+						if (parsedPacket.isPacketOfType(pcpp::TCP))
+						{
 							m_Stats.matchedTcpFlows++;
-						else if (parsedPacket.isPacketOfType(pcppx::UDP))
+						}
+						else if (parsedPacket.isPacketOfType(pcpp::UDP))
+						{
 							m_Stats.matchedUdpFlows++;
+						}
 					}
 				}
 
@@ -237,16 +207,26 @@ public:
 				{
 					// save packet to file if needed
 					if (pcapWriter != nullptr)
-						pcapWriter->writePacket(packetArr, i);
+					{
+						pcapWriter->writePacket(*packetArr[i]);
+					}
+
 					m_Stats.matchedPackets++;
 				}
 			}
+		}
+
+		// free packet array
+		for (size_t i = 0; i < packetArr.size(); i++)
+		{
+			if (packetArr[i] != nullptr)
+				delete packetArr[i];
 		}
 		return true;
 	}
 
 	/* the whole worker on the GPU: flow table, matching and statistics in HBM (pcppx_filter_batch_host) */
-	bool runOnDevice(pcppx::PcapFileReaderDevice& reader, PcapFileWriterDevice* pcapWriter)
+	bool runOnDevice(pcppx::PcapFileReaderDevice& reader, pcpp::PcapFileWriterDevice* pcapWriter)
 	{
 		pcppx::RawPacketVector packetArr;
 		std::vector<uint8_t> matched;
@@ -259,7 +239,15 @@ public:
 			if (pcapWriter != nullptr)
 				for (size_t i = 0; i < packetArr.size(); ++i)
 					if (matched[i])
-						pcapWriter->writePacket(packetArr, i);
+					{
+						const uint64_t ts = packetArr.timestampsNs[i];
+						pcpp::RawPacket raw(packetArr.packetData(i), (int)packetArr.caplens[i],
+						                    timespec{ (time_t)(ts / 1000000000ull), (long)(ts % 1000000000ull) }, false,
+						                    packetArr.linkType);
+						(void)raw.setRawData(packetArr.packetData(i), (int)packetArr.caplens[i], false,
+						                     raw.getPacketTimeStamp(), packetArr.linkType, (int)packetArr.frameLens[i]);
+						pcapWriter->writePacket(raw);
+					}
 		}
 		m_Stats.packetCount = s.packet_count;
 		m_Stats.ethCount = s.eth_count;
@@ -282,6 +270,7 @@ private:
 	pcppx::Engine& m_Engine;
 	const PacketMatchingEngine& m_PacketMatchingEngine;
 	size_t m_Burst;
+	bool m_Stop = false;
 	PacketStats m_Stats;
 	std::unordered_map<uint32_t, bool> m_FlowTable;
 };
@@ -343,7 +332,7 @@ int main(int argc, char* argv[])
 {
 	std::string in, out, sip, dip, hostParser;
 	uint16_t sport = 0, dport = 0;
-	size_t burst = 1u << 20;
+	size_t burst = 0;  // 0: 64 per receivePackets call, 1M per device-worker batch
 	bool deviceWorker = false;
 	pcppx::ProtocolType proto = pcppx::UnknownProtocol;
 	for (int k = 1; k < argc; ++k)
@@ -384,7 +373,7 @@ int main(int argc, char* argv[])
 			return 1;
 		}
 	}
-	if (in.empty() || burst == 0)
+	if (in.empty() || burst > (deviceWorker ? (size_t)UINT32_MAX : (size_t)UINT16_MAX))
 	{
 		usage(argv[0]);
 		return 1;
@@ -396,30 +385,34 @@ int main(int argc, char* argv[])
 		                                          sport, dport, proto);
 		pcppx::Engine engine(0);
 		if (!hostParser.empty())
-			engine.setHostParser(loadHostParser(hostParser));
+		{
+			const pcppx_host_parse_fn fn = loadHostParser(hostParser);
+			pcppx::setHostParser(fn);  // the per-packet worker's Packets
+			engine.setHostParser(fn);
+		}
 		pcppx::PcapFileReaderDevice reader(in);
 		if (!reader.open())
 		{
 			std::cerr << "cannot open " << in << "\n";
 			return 1;
 		}
-		std::unique_ptr<PcapFileWriterDevice> pcapWriter;
+		std::unique_ptr<pcpp::PcapFileWriterDevice> pcapWriter;
 		if (!out.empty())
 		{
-			pcapWriter = std::make_unique<PcapFileWriterDevice>(out, reader.getLinkLayerType());
+			pcapWriter = std::make_unique<pcpp::PcapFileWriterDevice>(out, reader.getLinkLayerType());
 			if (!pcapWriter->open())
 			{
 				std::cerr << "Couldn't open pcap writer device\n";
 				return 1;
 			}
 		}
-		AppWorkerThread worker(engine, matchingEngine, burst);
+		AppWorkerThread worker(engine, matchingEngine, burst ? burst : (deviceWorker ? 1u << 20 : 64));
 		if (deviceWorker)
 			worker.runOnDevice(reader, pcapWriter.get());
 		else
-			worker.run(reader, pcapWriter.get());
-		if (pcapWriter && pcapWriter->droppedPackets())
-			std::cerr << pcapWriter->droppedPackets() << " matched packets not written: link type differs from the "
+			worker.run(&reader, pcapWriter.get());
+		if (pcapWriter && pcapWriter->packetsNotWritten())
+			std::cerr << pcapWriter->packetsNotWritten() << " matched packets not written: link type differs from the "
 			          << "output file's\n";
 		pcapWriter.reset();
 		printStats(worker.getStats(), deviceWorker ? "GPU worker" : "Worker");

@@ -1,44 +1,56 @@
 /* pcppx.hpp — the Packet++-shaped C++ facade over the engine's C ABI (pcppx.h). Header-only, no HIP types, no
  * Packet++ dependency.
  *
- * A reference caller writes, per packet (Examples/PcapPlusPlus-benchmark/benchmark.cpp:89-95,
- * Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:85-139):
+ * A reference caller's per-packet loop compiles against it unchanged (namespace aside:
+ * Examples/PcapPlusPlus-benchmark/benchmark.cpp:89-95, Examples/DpdkExample-FilterTraffic/AppWorkerThread.h:85-139):
  *
- *   pcpp::RawPacket rawPacket;
- *   while (reader.getNextPacket(rawPacket)) {
- *       pcpp::Packet packet(&rawPacket, pcpp::TCP);              // Packet++/src/Packet.cpp:202-209
- *       if (packet.isPacketOfType(pcpp::TCP)) flows[pcpp::hash5Tuple(&packet)]++;
+ *   pcppx::PcapFileReaderDevice reader(path);          // Pcap++/header/PcapFileDevice.h
+ *   reader.open();
+ *   pcppx::RawPacket rawPacket;
+ *   while (reader.getNextPacket(rawPacket)) {           // Pcap++/src/PcapFileDevice.cpp:770-792
+ *       pcppx::Packet packet(&rawPacket, pcppx::TCP);   // Packet++/src/Packet.cpp:198-232
+ *       if (packet.isPacketOfType(pcppx::TCP)) flows[pcppx::hash5Tuple(&packet)]++;
  *   }
  *
- * With the engine the only change is a batch prepass: the reader fills a RawPacketVector, one call parses the
- * whole batch on the GPU, and the per-packet loop runs unchanged over pcppx::Packet views with the same names
- * (isPacketOfType, getLayerOfType<IPv4Layer/TcpLayer/UdpLayer>, getFirstLayer, hash5Tuple(&packet), ...):
+ * How the per-packet entry points reach the GPU (the batch prepass moved inside the library):
+ *  - the reader memory-maps the capture; a mapper thread indexes the records of the next pages (up to 1M packets
+ *    each, pcppx_pcap_map_batch: no per-packet copy) ahead of the caller;
+ *  - a parser thread parses each page on the GPU (pcppx_parse_batch_host: staged to HBM, parsed, records DMA'd into
+ *    page-locked memory) while the caller walks the page before it;
+ *  - getNextPacket(rawPacket) points rawPacket at the packet's bytes in the map and at its page (no copy; the
+ *    RawPacket keeps the page, and with it the map, alive);
+ *  - Packet(&rawPacket, parseUntil...) binds to that packet's records. The reader learns the parse-until options
+ *    from the first Packet built on a page and parses the next pages with them; a Packet with other options than
+ *    its page was parsed with re-parses that page on the GPU for those options (kept beside the first), so every
+ *    chain is exactly the one Packet::parsePacket builds for the options given (Packet.cpp:66-196);
+ *  - a RawPacket that did not come from a reader (the caller's own bytes) is parsed as a one-packet batch.
+ * Packets the engine leaves to the host (PCPPX_F_NEEDS_HOST: an L7 dissector, an out-of-scope L2/L3 layer) carry an
+ * exact layer prefix; with a host parser registered (pcppx::setHostParser: the caller's own Packet++ parse of one
+ * packet) they are completed before the caller sees them. libpcppx.so never links Packet++.
  *
- *   pcppx::Engine engine(0);
- *   engine.setHostParser(myPacketPlusPlusParse);                  // optional, see below
- *   pcppx::RawPacketVector batch;
- *   while (reader.getNextPackets(batch, 1 << 20) > 0) {
- *       pcppx::ParsedBatch parsed = engine.parse(batch, pcppx::PacketParseOptions(pcppx::TCP));
- *       for (pcppx::Packet packet : parsed)
- *           if (packet.isPacketOfType(pcppx::TCP)) flows[pcppx::hash5Tuple(&packet)]++;
- *   }
- *
- * Packets the engine leaves to the host (PCPPX_F_NEEDS_HOST: an L7 dissector, an out-of-scope L2/L3 layer) carry
- * an exact layer prefix. A caller that registers a host parser (pcppx_host_parse_fn: its own Packet++ parse of one
- * packet) gets them completed inside Engine::parse, so every Packet view answers as
- * pcpp::Packet would; without one, needsHost() reports them. libpcppx.so never links Packet++.
+ * The batch API remains for callers that want it: RawPacketVector + Engine::parse -> ParsedBatch of Packet views.
  *
  * Errors are reported as pcppx::Error (a std::runtime_error carrying the PCPPX_E_* code).
  */
 #ifndef PCPPX_HPP
 #define PCPPX_HPP
 
+#include <sys/time.h>
+
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <ctime>
+#include <deque>
+#include <fstream>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -47,7 +59,7 @@
 
 namespace pcppx
 {
-/* ProtocolType / ProtocolTypeFamily / OsiModelLayer values of Packet++/header/ProtocolType.h:42-284 */
+/* ProtocolType / ProtocolTypeFamily / OsiModelLayer values of Packet++/header/ProtocolType.h:33-284 */
 using ProtocolType = uint8_t;
 using ProtocolTypeFamily = uint32_t;
 constexpr ProtocolType UnknownProtocol = 0, Ethernet = 1, IPv4 = 2, IPv6 = 3, TCP = 4, UDP = 5, HTTPRequest = 6,
@@ -66,7 +78,13 @@ enum OsiModelLayer : uint8_t
 	OsiModelLayerUnknown = 8
 };
 
-/* facade-level summary flag: the records were filled by the caller's host parser (Engine::setHostParser) */
+/* pcpp::LinkLayerType values the engine parses (Packet++/header/RawPacket.h:24-178) */
+using LinkLayerType = uint16_t;
+constexpr LinkLayerType LINKTYPE_NULL = 0, LINKTYPE_ETHERNET = 1, LINKTYPE_DLT_RAW1 = 12, LINKTYPE_DLT_RAW2 = 14,
+                        LINKTYPE_RAW = 101, LINKTYPE_LINUX_SLL = 113, LINKTYPE_IPV4 = 228, LINKTYPE_IPV6 = 229,
+                        LINKTYPE_LINUX_SLL2 = 276, LINKTYPE_INVALID = 0xFFFF;
+
+/* facade-level summary flag: the records were filled by the caller's host parser (setHostParser) */
 constexpr uint16_t F_HOST_PARSED = 0x4000;
 
 class Error : public std::runtime_error
@@ -177,8 +195,555 @@ struct PacketParseOptions
 	}
 };
 
+/* ---- process-wide settings of the per-packet entry points ---- */
+namespace detail
+{
+inline int& defaultDevice()
+{
+	static int d = 0;
+	return d;
+}
+inline std::atomic<pcppx_host_parse_fn>& hostParser()
+{
+	static std::atomic<pcppx_host_parse_fn> f{ nullptr };
+	return f;
+}
+}  // namespace detail
+
+/* The GPU the per-packet entry points (readers, Packet(RawPacket*)) use; set before the first one runs. */
+inline void setDefaultDevice(int device)
+{
+	detail::defaultDevice() = device;
+}
+/* The caller's own Packet++ parse of one packet (pcppx_host_parse_fn): completes the packets the
+ * engine flags PCPPX_F_NEEDS_HOST before a Packet is built on them. nullptr = leave them flagged. */
+inline void setHostParser(pcppx_host_parse_fn fn)
+{
+	detail::hostParser().store(fn);
+}
+
+namespace detail
+{
+/* Page-locked blocks for record pages, reused across pages and readers (pinning memory is slow). Blocks go back to
+ * the pool when a page is released; at most kKeep bytes stay cached. The pool is never destroyed: the process may
+ * outlive the HIP runtime's teardown at exit. */
+class PinnedPool
+{
+public:
+	static PinnedPool& instance()
+	{
+		static PinnedPool* p = new PinnedPool();
+		return *p;
+	}
+	void* take(size_t bytes, size_t* got)
+	{
+		bytes = (bytes + kGrain - 1) & ~(kGrain - 1);
+		{
+			std::lock_guard<std::mutex> g(m_Mu);
+			auto it = m_Free.lower_bound(bytes);
+			if (it != m_Free.end() && it->first <= 2 * bytes)
+			{
+				void* p = it->second;
+				*got = it->first;
+				m_Cached -= it->first;
+				m_Free.erase(it);
+				return p;
+			}
+		}
+		void* p = pcppx_host_alloc(bytes);
+		if (p == nullptr)
+			throw Error(PCPPX_E_NOMEM, "pcppx_host_alloc");
+		*got = bytes;
+		return p;
+	}
+	void give(void* p, size_t bytes)
+	{
+		if (p == nullptr)
+			return;
+		{
+			std::lock_guard<std::mutex> g(m_Mu);
+			if (m_Cached + bytes <= kKeep)
+			{
+				m_Free.emplace(bytes, p);
+				m_Cached += bytes;
+				return;
+			}
+		}
+		pcppx_host_free(p);
+	}
+
+private:
+	static constexpr size_t kGrain = 1u << 20;
+	static constexpr size_t kKeep = 2ull << 30;
+	std::mutex m_Mu;
+	std::multimap<size_t, void*> m_Free;
+	size_t m_Cached = 0;
+};
+
+/* The context the per-packet entry points parse on: one per process (device defaultDevice()), its calls serialised
+ * (a pcppx context is used by one thread at a time; every entry point selects its device itself). Never destroyed,
+ * like the pool. */
+class Service
+{
+public:
+	static Service& instance()
+	{
+		static Service* s = new Service(defaultDevice());
+		return *s;
+	}
+	void parse(const pcppx_batch& b, const pcppx_opts& o, pcppx_records& r)
+	{
+		std::lock_guard<std::mutex> g(m_Mu);
+		check(pcppx_parse_batch_host(m_Ctx, &b, &o, &r), "pcppx_parse_batch_host");
+	}
+
+private:
+	explicit Service(int device) { check(pcppx_open(device, &m_Ctx), "pcppx_open"); }
+	std::mutex m_Mu;
+	pcppx_ctx* m_Ctx = nullptr;
+};
+
+/* Complete the packets the engine left to the host with fn (records at stride maxLayers); returns how many. */
+inline size_t completeOnHost(pcppx_host_parse_fn fn, const uint8_t* data, const uint64_t* offsets,
+                             const uint32_t* caplens, uint32_t n, uint16_t linkType, const pcppx_opts& o,
+                             pcppx_summary* sum, pcppx_layer* lay)
+{
+	if (fn == nullptr || o.max_layers == 0)
+		return 0;
+	size_t done = 0;
+	for (uint32_t i = 0; i < n; ++i)
+	{
+		pcppx_summary& s = sum[i];
+		if (!(s.flags & PCPPX_F_NEEDS_HOST) || (s.flags & PCPPX_F_BAD_DESC))
+			continue;
+		check(fn(data + offsets[i], caplens[i], linkType, &o, &s, lay + (size_t)i * o.max_layers), "host parser");
+		s.flags = (uint16_t)(s.flags | F_HOST_PARSED);
+		++done;
+	}
+	return done;
+}
+
+/* Packet::parsePacket's options (Packet.cpp:66-196): what a page's records were parsed for */
+struct ParseKey
+{
+	ProtocolTypeFamily family = UnknownProtocol;
+	uint8_t osi = OsiModelLayerUnknown;
+	bool operator==(const ParseKey& o) const { return family == o.family && osi == o.osi; }
+	/* the reader's parse: every layer record (PCPPX_MAX_LAYERS, FIXED) and the checksums */
+	pcppx_opts opts() const
+	{
+		pcppx_opts o;
+		pcppx_default_opts(&o);
+		o.parse_until_family = family;
+		o.parse_until_osi = osi;
+		return o;
+	}
+};
+
+/* one page's records for one ParseKey, in page-locked memory: summary[n] then layers[n][PCPPX_MAX_LAYERS] */
+struct Records
+{
+	ParseKey key;
+	pcppx_summary* sum = nullptr;
+	pcppx_layer* lay = nullptr;
+	Records(ParseKey k, uint32_t n) : key(k)
+	{
+		m_Block = PinnedPool::instance().take((size_t)n * (sizeof(pcppx_summary) + PCPPX_MAX_LAYERS * sizeof(pcppx_layer)),
+		                                      &m_Bytes);
+		sum = static_cast<pcppx_summary*>(m_Block);
+		lay = reinterpret_cast<pcppx_layer*>(sum + n);
+	}
+	~Records() { PinnedPool::instance().give(m_Block, m_Bytes); }
+	Records(const Records&) = delete;
+	Records& operator=(const Records&) = delete;
+
+private:
+	void* m_Block = nullptr;
+	size_t m_Bytes = 0;
+};
+
+/* records of one packet parsed on its own (a RawPacket that did not come from a reader) */
+struct OwnedRecords
+{
+	pcppx_summary sum{};
+	pcppx_layer lay[PCPPX_MAX_LAYERS]{};
+};
+
+/* the capture map: closed when the reader and every page of it are gone */
+struct MapHandle
+{
+	pcppx_pcap* reader = nullptr;
+	~MapHandle() { pcppx_pcap_close(reader); }
+};
+
+class ReaderCore;
+
+/* A run of consecutive packets of one capture and one link type, pointing into the map, with its GPU records. */
+struct Page
+{
+	std::shared_ptr<MapHandle> map;  // keeps the bytes valid
+	std::weak_ptr<ReaderCore> core;  // the reader, to learn the parse options from the caller's Packets
+	const uint8_t* base = nullptr;
+	uint64_t dataLen = 0;
+	uint16_t linkType = LINKTYPE_ETHERNET;
+	uint32_t n = 0;
+	buffer<uint64_t> offsets, tsNs;
+	buffer<uint32_t> caplens, frameLens;
+
+	/* records for the reader's options, published once (acquire / release); 0 mapped, 1 parsing, 2 parsed */
+	std::atomic<const Records*> primary{ nullptr };
+	std::atomic<int> state{ 0 };
+	int error = PCPPX_OK;
+	std::mutex mu;
+	std::condition_variable cv;
+	std::unique_ptr<Records> primaryOwned;
+	std::vector<std::unique_ptr<Records>> extra;  // records for other options (a Packet that asked for them)
+
+	std::unique_ptr<Records> parseRecords(ParseKey k) const
+	{
+		auto r = std::make_unique<Records>(k, n);
+		const pcppx_opts o = k.opts();
+		const pcppx_batch b{ base, offsets.data(), caplens.data(), dataLen, n, linkType, 0 };
+		pcppx_records rec{ r->sum, r->lay, nullptr, nullptr, nullptr };
+		Service::instance().parse(b, o, rec);
+		completeOnHost(hostParser().load(), base, offsets.data(), caplens.data(), n, linkType, o, r->sum, r->lay);
+		return r;
+	}
+	/* parse for k unless another thread has started: false if it has */
+	bool tryParse(ParseKey k)
+	{
+		int idle = 0;
+		if (!state.compare_exchange_strong(idle, 1))
+			return false;
+		std::unique_ptr<Records> r;
+		int err = PCPPX_OK;
+		try
+		{
+			r = parseRecords(k);
+		}
+		catch (const Error& e)
+		{
+			err = e.code();
+		}
+		catch (const std::bad_alloc&)
+		{
+			err = PCPPX_E_NOMEM;
+		}
+		{
+			std::lock_guard<std::mutex> g(mu);
+			primaryOwned = std::move(r);
+			error = err;
+			primary.store(primaryOwned.get(), std::memory_order_release);
+			state.store(2);
+		}
+		cv.notify_all();
+		return true;
+	}
+	/* the records for k (Packet's slow path: the page not parsed yet, or parsed for other options) */
+	const Records* recordsFor(ParseKey k);
+};
+
+/* The reader's pipeline: a mapper thread indexes pages ahead of the caller, a parser thread parses them on the GPU
+ * once the caller's parse options are known. */
+class ReaderCore : public std::enable_shared_from_this<ReaderCore>
+{
+public:
+	static constexpr size_t kAhead = 2;              // pages mapped ahead of the caller's
+	static constexpr uint32_t kFirstPage = 1u << 14;  // packets: small first pages (the caller starts sooner),
+	static constexpr uint32_t kMaxPage = 1u << 20;    // then x4 per page up to this
+
+	explicit ReaderCore(pcppx_pcap* r) : m_Map(std::make_shared<MapHandle>()) { m_Map->reader = r; }
+	~ReaderCore() { stop(); }
+	ReaderCore(const ReaderCore&) = delete;
+	ReaderCore& operator=(const ReaderCore&) = delete;
+
+	void start()
+	{
+		m_Mapper = std::thread([this] { mapLoop(); });
+		m_Parser = std::thread([this] { parseLoop(); });
+	}
+	void stop()
+	{
+		{
+			std::lock_guard<std::mutex> g(m_Mu);
+			m_Stop = true;
+		}
+		m_Cv.notify_all();
+		if (m_Mapper.joinable())
+			m_Mapper.join();
+		if (m_Parser.joinable())
+			m_Parser.join();
+		std::lock_guard<std::mutex> g(m_Mu);
+		m_Pages.clear();
+		m_ToParse.clear();
+	}
+	/* the next page in capture order; nullptr at the end of the capture (or after a read error: error()) */
+	std::shared_ptr<Page> nextPage()
+	{
+		std::unique_lock<std::mutex> g(m_Mu);
+		m_Cv.wait(g, [&] { return !m_Pages.empty() || m_Eof || m_Stop; });
+		if (m_Pages.empty())
+			return nullptr;
+		std::shared_ptr<Page> p = std::move(m_Pages.front());
+		m_Pages.pop_front();
+		g.unlock();
+		m_Cv.notify_all();
+		return p;
+	}
+	/* the caller built a Packet with these options: parse the following pages for them */
+	void learn(ParseKey k)
+	{
+		{
+			std::lock_guard<std::mutex> g(m_Mu);
+			if (m_KeyKnown && m_Key == k)
+				return;
+			m_Key = k;
+			m_KeyKnown = true;
+		}
+		m_Cv.notify_all();
+	}
+	int error() const
+	{
+		std::lock_guard<std::mutex> g(m_Mu);
+		return m_Error;
+	}
+
+private:
+	void mapLoop()
+	{
+		uint32_t size = kFirstPage;
+		for (;;)
+		{
+			{
+				std::unique_lock<std::mutex> g(m_Mu);
+				m_Cv.wait(g, [&] { return m_Stop || m_Pages.size() < kAhead; });
+				if (m_Stop)
+					return;
+			}
+			auto pg = std::make_shared<Page>();
+			int rc = PCPPX_OK;
+			uint32_t n = 0;
+			try
+			{
+				pg->map = m_Map;
+				pg->core = weak_from_this();
+				pg->offsets.resize(size);
+				pg->tsNs.resize(size);
+				pg->caplens.resize(size);
+				pg->frameLens.resize(size);
+				rc = pcppx_pcap_map_batch(m_Map->reader, &pg->base, &pg->dataLen, pg->offsets.data(), pg->caplens.data(),
+				                          pg->frameLens.data(), pg->tsNs.data(), size, &n);
+			}
+			catch (const std::bad_alloc&)
+			{
+				rc = PCPPX_E_NOMEM;
+			}
+			std::lock_guard<std::mutex> g(m_Mu);
+			if (rc != PCPPX_OK || n == 0)
+			{
+				m_Error = rc;
+				m_Eof = true;
+				m_Cv.notify_all();
+				return;
+			}
+			pg->n = n;
+			pg->linkType = (uint16_t)pcppx_pcap_linktype(m_Map->reader);
+			m_Pages.push_back(pg);
+			m_ToParse.push_back(pg);
+			m_Cv.notify_all();
+			size = size < kMaxPage / 4 ? size * 4 : kMaxPage;
+		}
+	}
+	void parseLoop()
+	{
+		for (;;)
+		{
+			std::shared_ptr<Page> pg;
+			ParseKey k;
+			{
+				std::unique_lock<std::mutex> g(m_Mu);
+				m_Cv.wait(g, [&] { return m_Stop || (m_KeyKnown && !m_ToParse.empty()); });
+				if (m_Stop)
+					return;
+				pg = m_ToParse.front().lock();  // expired: the caller is done with the page
+				m_ToParse.pop_front();
+				k = m_Key;
+			}
+			if (pg)
+				(void)pg->tryParse(k);
+		}
+	}
+
+	std::shared_ptr<MapHandle> m_Map;
+	mutable std::mutex m_Mu;
+	std::condition_variable m_Cv;
+	std::deque<std::shared_ptr<Page>> m_Pages;   // mapped, not yet handed to the caller
+	std::deque<std::weak_ptr<Page>> m_ToParse;   // mapped, not yet parsed (in capture order)
+	bool m_Eof = false, m_Stop = false, m_KeyKnown = false;
+	ParseKey m_Key;
+	int m_Error = PCPPX_OK;
+	std::thread m_Mapper, m_Parser;
+};
+
+inline const Records* Page::recordsFor(ParseKey k)
+{
+	const Records* r = primary.load(std::memory_order_acquire);
+	if (r != nullptr && r->key == k)
+		return r;
+	if (auto c = core.lock())
+		c->learn(k);  // the next pages are parsed for k
+	if (state.load() != 2 && !tryParse(k))
+	{
+		std::unique_lock<std::mutex> g(mu);
+		cv.wait(g, [&] { return state.load() == 2; });
+	}
+	std::lock_guard<std::mutex> g(mu);
+	if (error != PCPPX_OK)
+		throw Error(error, "parse of a capture page");
+	r = primary.load(std::memory_order_acquire);
+	if (r != nullptr && r->key == k)
+		return r;
+	// parsed for other options: parse the page again for these, kept beside the first records
+	for (const auto& e : extra)
+		if (e->key == k)
+			return e.get();
+	extra.push_back(parseRecords(k));
+	return extra.back().get();
+}
+}  // namespace detail
+
+/* pcpp::RawPacket (Packet++/header/RawPacket.h:288-566): a packet's bytes, lengths, timestamp and link type.
+ * A RawPacket filled by PcapFileReaderDevice::getNextPacket refers to the packet's bytes in the reader's memory map
+ * and to the page of GPU records they were parsed into; it keeps both alive (no copy is made). One made from the
+ * caller's bytes (the constructors / setRawData) owns them when takeOwnership is set, as in the reference. The
+ * bytes are read-only (packet crafting is outside the engine). */
+class RawPacket
+{
+public:
+	RawPacket() = default;
+	RawPacket(const uint8_t* pRawData, int rawDataLen, timeval timestamp, bool takeOwnership,
+	          LinkLayerType layerType = LINKTYPE_ETHERNET)
+	{
+		setRawData(pRawData, rawDataLen, takeOwnership, timestamp, layerType);
+	}
+	RawPacket(const uint8_t* pRawData, int rawDataLen, timespec timestamp, bool takeOwnership,
+	          LinkLayerType layerType = LINKTYPE_ETHERNET)
+	{
+		setRawData(pRawData, rawDataLen, takeOwnership, timestamp, layerType);
+	}
+	virtual ~RawPacket() { release(); }
+	/* copies share a reader page (its bytes are immutable); the caller's own bytes are copied (RawPacket.cpp) */
+	RawPacket(const RawPacket& other) { copyFrom(other); }
+	RawPacket& operator=(const RawPacket& other)
+	{
+		if (this != &other)
+		{
+			release();
+			copyFrom(other);
+		}
+		return *this;
+	}
+	virtual RawPacket* clone() const { return new RawPacket(*this); }
+
+	bool setRawData(const uint8_t* pRawData, int rawDataLen, bool takeOwnership, timeval timestamp,
+	                LinkLayerType layerType = LINKTYPE_ETHERNET, int frameLength = -1)
+	{
+		return setRawData(pRawData, rawDataLen, takeOwnership,
+		                  timespec{ timestamp.tv_sec, (long)timestamp.tv_usec * 1000 }, layerType, frameLength);
+	}
+	bool setRawData(const uint8_t* pRawData, int rawDataLen, bool takeOwnership, timespec timestamp,
+	                LinkLayerType layerType = LINKTYPE_ETHERNET, int frameLength = -1)
+	{
+		release();
+		m_RawData = pRawData;
+		m_RawDataLen = rawDataLen;
+		m_FrameLength = frameLength == -1 ? rawDataLen : frameLength;
+		m_TsNs = (uint64_t)timestamp.tv_sec * 1000000000ull + (uint64_t)timestamp.tv_nsec;
+		m_OwnsRawData = takeOwnership;
+		m_LinkLayerType = layerType;
+		m_RawPacketSet = true;
+		return true;
+	}
+
+	const uint8_t* getRawData() const { return m_RawData; }
+	int getRawDataLen() const { return m_RawDataLen; }
+	int getFrameLength() const { return m_FrameLength; }
+	LinkLayerType getLinkLayerType() const { return m_LinkLayerType; }
+	timespec getPacketTimeStamp() const
+	{
+		return timespec{ (time_t)(m_TsNs / 1000000000ull), (long)(m_TsNs % 1000000000ull) };
+	}
+	bool isPacketSet() const { return m_RawPacketSet; }
+	virtual void clear() { release(); }
+
+private:
+	friend class PcapFileReaderDevice;
+	friend class Packet;
+
+	void release()
+	{
+		if (m_OwnsRawData)
+			delete[] m_RawData;
+		m_RawData = nullptr;
+		m_RawDataLen = m_FrameLength = 0;
+		m_TsNs = 0;
+		m_OwnsRawData = m_RawPacketSet = false;
+		m_Page.reset();
+		m_Index = 0;
+	}
+	void copyFrom(const RawPacket& o)
+	{
+		m_RawDataLen = o.m_RawDataLen;
+		m_FrameLength = o.m_FrameLength;
+		m_TsNs = o.m_TsNs;
+		m_LinkLayerType = o.m_LinkLayerType;
+		m_RawPacketSet = o.m_RawPacketSet;
+		m_Page = o.m_Page;
+		m_Index = o.m_Index;
+		if (o.m_Page != nullptr || o.m_RawData == nullptr)
+		{
+			m_RawData = o.m_RawData;
+			m_OwnsRawData = false;
+			return;
+		}
+		uint8_t* copy = new uint8_t[o.m_RawDataLen > 0 ? o.m_RawDataLen : 1];
+		std::memcpy(copy, o.m_RawData, o.m_RawDataLen > 0 ? (size_t)o.m_RawDataLen : 0);
+		m_RawData = copy;
+		m_OwnsRawData = true;
+	}
+	/* getNextPacket's per-packet step: point at packet i of a page (the page pointer changes once per page) */
+	void setFromPage(const std::shared_ptr<detail::Page>& pg, uint32_t i)
+	{
+		if (m_OwnsRawData)
+		{
+			delete[] m_RawData;
+			m_OwnsRawData = false;
+		}
+		if (m_Page.get() != pg.get())
+			m_Page = pg;
+		const detail::Page& p = *pg;
+		m_Index = i;
+		m_RawData = p.base + p.offsets[i];
+		m_RawDataLen = (int)p.caplens[i];
+		m_FrameLength = (int)p.frameLens[i];
+		m_TsNs = p.tsNs[i];
+		m_LinkLayerType = p.linkType;
+		m_RawPacketSet = true;
+	}
+
+	const uint8_t* m_RawData = nullptr;
+	int m_RawDataLen = 0;
+	int m_FrameLength = 0;
+	uint64_t m_TsNs = 0;
+	bool m_OwnsRawData = false;
+	bool m_RawPacketSet = false;
+	LinkLayerType m_LinkLayerType = LINKTYPE_ETHERNET;
+	std::shared_ptr<detail::Page> m_Page;  // set when the packet came from a reader
+	uint32_t m_Index = 0;
+};
+
 /* A batch of raw packets back to back in one buffer: packet i = data[offsets[i], offsets[i] + caplens[i]).
- * Plays the role of pcpp::RawPacketVector (Packet++/header/RawPacket.h) for the batch prepass. */
+ * The batch prepass's container (the role of pcpp::RawPacketVector, Packet++/header/RawPacket.h) for Engine::parse. */
 struct RawPacketVector
 {
 	buffer<uint8_t> data;
@@ -186,7 +751,7 @@ struct RawPacketVector
 	buffer<uint32_t> caplens;
 	buffer<uint64_t> timestampsNs;
 	buffer<uint32_t> frameLens; /* RawPacket::getFrameLength (original wire length) */
-	uint16_t linkType = 1; /* LINKTYPE_ETHERNET */
+	uint16_t linkType = LINKTYPE_ETHERNET;
 
 	size_t size() const { return caplens.size(); }
 	void clear()
@@ -198,12 +763,12 @@ struct RawPacketVector
 		frameLens.clear();
 	}
 	/* RawPacket::setRawData-style append (Packet++/header/RawPacket.h) */
-	void add(const uint8_t* bytes, uint32_t len, uint64_t tsNs = 0)
+	void add(const uint8_t* bytes, uint32_t len, uint64_t tsNs = 0, uint32_t frameLen = 0)
 	{
 		offsets.push_back(data.size());
 		caplens.push_back(len);
 		timestampsNs.push_back(tsNs);
-		frameLens.push_back(len);
+		frameLens.push_back(frameLen ? frameLen : len);
 		data.insert(data.end(), bytes, bytes + len);
 	}
 	const uint8_t* packetData(size_t i) const { return data.data() + offsets[i]; }
@@ -215,9 +780,9 @@ struct RawPacketVector
 };
 using RawBatch = RawPacketVector;
 
-/* PcapFileReaderDevice / PcapNgFileReaderDevice (Pcap++/header/PcapFileDevice.h): open / getNextPackets / close.
- * The format (pcap or pcapng) comes from the file's first bytes; a batch holds one link type (pcapng
- * interfaces may differ), given by getLinkLayerType() after the batch is read. */
+/* PcapFileReaderDevice / PcapNgFileReaderDevice (Pcap++/header/PcapFileDevice.h): the format (pcap or pcapng) comes
+ * from the file's first bytes (IFileReaderDevice::createReader, PcapFileDevice.cpp:546-583). open() starts the
+ * page pipeline (see the top of this file); close() stops it (RawPackets already read stay valid). */
 class PcapFileReaderDevice
 {
 public:
@@ -226,48 +791,188 @@ public:
 	PcapFileReaderDevice(const PcapFileReaderDevice&) = delete;
 	PcapFileReaderDevice& operator=(const PcapFileReaderDevice&) = delete;
 
-	bool open() { return m_Reader != nullptr || pcppx_pcap_open(m_FileName.c_str(), &m_Reader) == PCPPX_OK; }
-	bool isOpened() const { return m_Reader != nullptr; }
+	/* PcapFileReaderDevice::open (PcapFileDevice.cpp:707-768): false when already open or the file is not a
+	 * readable pcap / pcapng capture */
+	bool open()
+	{
+		if (m_Core != nullptr)
+			return false;  // "File already opened"
+		pcppx_pcap* r = nullptr;
+		if (pcppx_pcap_open(m_FileName.c_str(), &r) != PCPPX_OK)
+			return false;
+		m_OpenLinkType = (LinkLayerType)pcppx_pcap_linktype(r);
+		m_Core = std::make_shared<detail::ReaderCore>(r);
+		m_Core->start();
+		return true;
+	}
+	bool isOpened() const { return m_Core != nullptr; }
 	void close()
 	{
-		pcppx_pcap_close(m_Reader);
-		m_Reader = nullptr;
+		if (m_Core != nullptr)
+			m_Core->stop();
+		m_Core.reset();
+		m_Cur.reset();
+		m_Pos = 0;
 	}
-	uint32_t getLinkLayerType() const { return pcppx_pcap_linktype(m_Reader); }
+	/* the link type of the packets being read (before the first packet: of the first packet) */
+	LinkLayerType getLinkLayerType() const { return m_Cur ? m_Cur->linkType : m_OpenLinkType; }
+	const std::string& getFileName() const { return m_FileName; }
 
-	/* IFileReaderDevice::getNextPackets(RawPacketVector&, int numOfPacketsToRead) (PcapFileDevice.cpp:604-624):
-	 * replaces `batch` with the next packets (at most numOfPacketsToRead, -1 = as many as maxBytes holds); returns
-	 * the count, 0 at end of file. */
+	/* IFileReaderDevice::getNextPacket (PcapFileDevice.cpp:770-792): false at the end of the capture, on a read
+	 * error, or when the reader is not open */
+	bool getNextPacket(RawPacket& rawPacket)
+	{
+		if (m_Cur == nullptr || m_Pos >= m_Cur->n)
+		{
+			if (!advance())
+				return false;
+		}
+		rawPacket.setFromPage(m_Cur, m_Pos++);
+		return true;
+	}
+
+	/* DpdkDevice::receivePackets(MBufRawPacket**, ...) (Pcap++/src/DpdkDevice.cpp:922-990) with the capture as the
+	 * RX queue: fills rawPacketsArr[0..k) (allocating a RawPacket where an entry is null) and returns k, 0 at the end */
+	uint16_t receivePackets(RawPacket** rawPacketsArr, uint16_t rawPacketArrLength, uint16_t rxQueueId = 0)
+	{
+		(void)rxQueueId;
+		if (rawPacketsArr == nullptr)
+			return 0;
+		uint16_t k = 0;
+		for (; k < rawPacketArrLength; ++k)
+		{
+			if (rawPacketsArr[k] == nullptr)
+				rawPacketsArr[k] = new RawPacket();
+			if (!getNextPacket(*rawPacketsArr[k]))
+				break;
+		}
+		return k;
+	}
+
+	/* IFileReaderDevice::getNextPackets(RawPacketVector&, int numOfPacketsToRead) (PcapFileDevice.cpp:604-624), into
+	 * the batch container: replaces `batch` with the next packets (at most numOfPacketsToRead, -1 = as many as
+	 * maxBytes holds; one link type per batch); returns the count, 0 at the end of the capture. */
 	int getNextPackets(RawPacketVector& batch, int numOfPacketsToRead = -1, uint64_t maxBytes = 256ull << 20)
 	{
-		if (!open())
-			throw Error(PCPPX_E_INVAL, "PcapFileReaderDevice::open(" + m_FileName + ")");
-		const uint32_t maxPackets = numOfPacketsToRead > 0 ? (uint32_t)numOfPacketsToRead : (uint32_t)(maxBytes / 16);
-		batch.data.resize(maxBytes);
-		batch.offsets.resize(maxPackets);
-		batch.caplens.resize(maxPackets);
-		batch.timestampsNs.resize(maxPackets);
-		batch.frameLens.resize(maxPackets);
-		uint32_t n = 0;
-		uint64_t used = 0;
-		check(pcppx_pcap_read_batch_ex(m_Reader, batch.data.data(), maxBytes, batch.offsets.data(), batch.caplens.data(),
-		                               batch.frameLens.data(), batch.timestampsNs.data(), maxPackets, &n, &used),
-		      "pcppx_pcap_read_batch_ex");
-		batch.data.resize(used);
-		batch.offsets.resize(n);
-		batch.caplens.resize(n);
-		batch.timestampsNs.resize(n);
-		batch.frameLens.resize(n);
-		batch.linkType = (uint16_t)getLinkLayerType();
-		return (int)n;
+		batch.clear();
+		int n = 0;
+		while (numOfPacketsToRead < 0 || n < numOfPacketsToRead)
+		{
+			if (m_Cur == nullptr || m_Pos >= m_Cur->n)
+			{
+				if (!advance())
+					break;
+				if (n > 0 && m_Cur->linkType != batch.linkType)
+					break;  // the next batch starts with this page
+			}
+			const uint32_t cap = m_Cur->caplens[m_Pos];
+			if (n > 0 && batch.data.size() + cap > maxBytes)
+				break;
+			if (n == 0)
+			{
+				batch.linkType = m_Cur->linkType;
+				if (numOfPacketsToRead > 0)
+				{
+					batch.offsets.reserve((size_t)numOfPacketsToRead);
+					batch.caplens.reserve((size_t)numOfPacketsToRead);
+					batch.timestampsNs.reserve((size_t)numOfPacketsToRead);
+					batch.frameLens.reserve((size_t)numOfPacketsToRead);
+				}
+			}
+			batch.add(m_Cur->base + m_Cur->offsets[m_Pos], cap, m_Cur->tsNs[m_Pos], m_Cur->frameLens[m_Pos]);
+			++m_Pos;
+			++n;
+		}
+		return n;
 	}
 
 private:
+	bool advance()
+	{
+		if (m_Core == nullptr)
+			return false;
+		m_Cur.reset();
+		m_Pos = 0;
+		m_Cur = m_Core->nextPage();
+		return m_Cur != nullptr;
+	}
+
 	std::string m_FileName;
-	pcppx_pcap* m_Reader = nullptr;
+	std::shared_ptr<detail::ReaderCore> m_Core;
+	std::shared_ptr<detail::Page> m_Cur;
+	uint32_t m_Pos = 0;
+	LinkLayerType m_OpenLinkType = LINKTYPE_ETHERNET;
 };
 using PcapNgFileReaderDevice = PcapFileReaderDevice;
 using IFileReaderDevice = PcapFileReaderDevice;
+
+/* PcapFileWriterDevice (Pcap++/src/PcapFileDevice.cpp:892-1119): classic pcap, micro- or nanosecond timestamps; a
+ * packet of another link type than the file's is refused and counted (writePacket :1026-1039). */
+class PcapFileWriterDevice
+{
+public:
+	explicit PcapFileWriterDevice(const std::string& fileName, LinkLayerType linkLayerType = LINKTYPE_ETHERNET,
+	                              bool nanosecondsPrecision = false)
+	    : m_FileName(fileName),
+	      m_LinkType(linkLayerType == LINKTYPE_DLT_RAW1 || linkLayerType == LINKTYPE_DLT_RAW2 ? LINKTYPE_RAW
+	                                                                                          : linkLayerType),
+	      m_Nano(nanosecondsPrecision)
+	{}
+	~PcapFileWriterDevice() { close(); }
+	PcapFileWriterDevice(const PcapFileWriterDevice&) = delete;
+	PcapFileWriterDevice& operator=(const PcapFileWriterDevice&) = delete;
+
+	bool open()
+	{
+		if (m_File.is_open())
+			return false;
+		m_File.open(m_FileName, std::ios::binary | std::ios::out);
+		if (!m_File.is_open())
+			return false;
+		const uint32_t hdr[6] = { m_Nano ? 0xa1b23c4du : 0xa1b2c3d4u, 2u | (4u << 16), 0, 0, 262144, m_LinkType };
+		return (bool)m_File.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
+	}
+	bool writePacket(const RawPacket& packet)
+	{
+		if (!m_File.is_open())
+			return false;
+		if (packet.getLinkLayerType() != m_LinkType)
+		{
+			++m_NotWritten;  // "Cannot write a packet with a different link type"
+			return false;
+		}
+		const timespec ts = packet.getPacketTimeStamp();
+		const uint32_t h[4] = { (uint32_t)ts.tv_sec, (uint32_t)(m_Nano ? ts.tv_nsec : ts.tv_nsec / 1000),
+			                    (uint32_t)packet.getRawDataLen(), (uint32_t)packet.getFrameLength() };
+		if (!m_File.write(reinterpret_cast<const char*>(h), sizeof(h)) ||
+		    !m_File.write(reinterpret_cast<const char*>(packet.getRawData()), packet.getRawDataLen()))
+		{
+			++m_NotWritten;
+			return false;
+		}
+		++m_Written;
+		return true;
+	}
+	void flush()
+	{
+		if (m_File.is_open())
+			m_File.flush();
+	}
+	void close()
+	{
+		if (m_File.is_open())
+			m_File.close();
+	}
+	uint64_t packetsWritten() const { return m_Written; }
+	uint64_t packetsNotWritten() const { return m_NotWritten; }
+
+private:
+	std::string m_FileName;
+	uint32_t m_LinkType;
+	bool m_Nano;
+	std::ofstream m_File;
+	uint64_t m_Written = 0, m_NotWritten = 0;
+};
 
 /* One layer of a parsed packet: Layer::getProtocol / getOsiModelLayer / getData / getHeaderLen / getDataLen /
  * getLayerPayloadSize / isMemberOfProtocolFamily (Packet++/header/Layer.h) */
@@ -361,10 +1066,37 @@ private:
 	bool m_Ok = false;
 };
 
-/* A parsed packet: the pcpp::Packet (Packet++/header/Packet.h) queries of the two callers */
+/* A parsed packet: the pcpp::Packet (Packet++/header/Packet.h) queries of the two callers. Built from a RawPacket
+ * (the reference's constructors) or as a view into a ParsedBatch. Like the reference's Packet it reads the
+ * RawPacket's bytes and must not outlive the RawPacket's current contents. */
 class Packet
 {
 public:
+	/* Packet::Packet(RawPacket*, bool freeRawPacket, ProtocolType / ProtocolTypeFamily parseUntil, OsiModelLayer)
+	 * and the short forms (Packet.h:94-134, Packet.cpp:198-234) */
+	explicit Packet(RawPacket* rawPacket, bool freeRawPacket = false, ProtocolType parseUntil = UnknownProtocol,
+	                OsiModelLayer parseUntilLayer = OsiModelLayerUnknown)
+	{
+		bind(rawPacket, freeRawPacket, parseUntil, parseUntilLayer);
+	}
+	explicit Packet(RawPacket* rawPacket, bool freeRawPacket, ProtocolTypeFamily parseUntil,
+	                OsiModelLayer parseUntilLayer = OsiModelLayerUnknown)
+	{
+		bind(rawPacket, freeRawPacket, parseUntil, parseUntilLayer);
+	}
+	explicit Packet(RawPacket* rawPacket, ProtocolType parseUntil)
+	{
+		bind(rawPacket, false, parseUntil, OsiModelLayerUnknown);
+	}
+	explicit Packet(RawPacket* rawPacket, ProtocolTypeFamily parseUntilFamily)
+	{
+		bind(rawPacket, false, parseUntilFamily, OsiModelLayerUnknown);
+	}
+	explicit Packet(RawPacket* rawPacket, OsiModelLayer parseUntilLayer)
+	{
+		bind(rawPacket, false, UnknownProtocol, parseUntilLayer);
+	}
+	/* a view into records the caller holds (ParsedBatch) */
 	Packet(const pcppx_summary* s, const pcppx_layer* layers, uint8_t maxLayers, const uint8_t* raw, uint32_t caplen)
 	    : m_Sum(s), m_Layers(layers), m_MaxLayers(maxLayers), m_Raw(raw), m_Caplen(caplen)
 	{}
@@ -412,7 +1144,7 @@ public:
 
 	/* engine flags: the host must finish the packet (an L7 or an out-of-scope L2/L3 layer) and no host parser did */
 	bool needsHost() const { return (m_Sum->flags & PCPPX_F_NEEDS_HOST) != 0; }
-	/* the records come from the caller's host parser (Engine::setHostParser) */
+	/* the records come from the caller's host parser (setHostParser / Engine::setHostParser) */
 	bool wasHostParsed() const { return (m_Sum->flags & F_HOST_PARSED) != 0; }
 	bool hasTrailer() const { return (m_Sum->flags & PCPPX_F_TRAILER) != 0; }
 	/* IPv4Layer::computeCalculateFields checksum vs the stored one (IPv4Layer.cpp:410-412) */
@@ -426,11 +1158,53 @@ public:
 	const pcppx_summary& summary() const { return *m_Sum; }
 
 private:
-	const pcppx_summary* m_Sum;
-	const pcppx_layer* m_Layers;
-	uint8_t m_MaxLayers;
-	const uint8_t* m_Raw;
-	uint32_t m_Caplen;
+	static const pcppx_summary* emptySummary()
+	{
+		static const pcppx_summary s{ 0, 0, 0, 0, 0, 0xFF, 0, 0, 0, 0, 0 };
+		return &s;
+	}
+	void bind(RawPacket* raw, bool freeRawPacket, ProtocolTypeFamily parseUntil, OsiModelLayer parseUntilLayer)
+	{
+		m_Sum = emptySummary();
+		m_MaxLayers = PCPPX_MAX_LAYERS;
+		if (raw == nullptr)
+			return;  // Packet::setRawPacket: no RawPacket, no layers (Packet.cpp:60-61)
+		if (freeRawPacket)
+			m_OwnedRaw.reset(raw);
+		m_Raw = raw->m_RawData;
+		m_Caplen = raw->m_RawDataLen > 0 ? (uint32_t)raw->m_RawDataLen : 0;
+		const detail::ParseKey k{ parseUntil, parseUntilLayer };
+		if (detail::Page* p = raw->m_Page.get())
+		{
+			const detail::Records* r = p->primary.load(std::memory_order_acquire);
+			if (r == nullptr || !(r->key == k))
+				r = p->recordsFor(k);
+			m_Sum = r->sum + raw->m_Index;
+			m_Layers = r->lay + (size_t)raw->m_Index * PCPPX_MAX_LAYERS;
+			return;
+		}
+		if (m_Raw == nullptr)
+			return;  // no data: createFirstLayer builds nothing (Packet.cpp:88-94)
+		// the caller's own bytes: a one-packet batch
+		m_Own = std::make_shared<detail::OwnedRecords>();
+		const pcppx_opts o = k.opts();
+		const uint64_t off = 0;
+		const pcppx_batch b{ m_Raw, &off, &m_Caplen, m_Caplen, 1, raw->m_LinkLayerType, 0 };
+		pcppx_records rec{ &m_Own->sum, m_Own->lay, nullptr, nullptr, nullptr };
+		detail::Service::instance().parse(b, o, rec);
+		detail::completeOnHost(detail::hostParser().load(), m_Raw, &off, &m_Caplen, 1, raw->m_LinkLayerType, o,
+		                       &m_Own->sum, m_Own->lay);
+		m_Sum = &m_Own->sum;
+		m_Layers = m_Own->lay;
+	}
+
+	const pcppx_summary* m_Sum = nullptr;
+	const pcppx_layer* m_Layers = nullptr;
+	uint8_t m_MaxLayers = 0;
+	const uint8_t* m_Raw = nullptr;
+	uint32_t m_Caplen = 0;
+	std::shared_ptr<detail::OwnedRecords> m_Own;  // a RawPacket that did not come from a reader
+	std::shared_ptr<RawPacket> m_OwnedRaw;        // freeRawPacket
 };
 using ParsedPacket = Packet;
 using ParsedLayer = Layer;
@@ -524,7 +1298,7 @@ struct MatchSpec
 	}
 };
 
-/* One GPU worker: a pcppx context. */
+/* One GPU worker for the batch API: a pcppx context. */
 class Engine
 {
 public:
@@ -550,19 +1324,9 @@ public:
 		const pcppx_opts o = options.toC();
 		pcppx_records r{ out.summaries.data(), options.maxLayers ? out.layers.data() : nullptr, nullptr, nullptr, nullptr };
 		check(pcppx_parse_batch_host(m_Ctx, &b, &o, &r), "pcppx_parse_batch_host");
-		out.hostParsed = 0;
-		if (m_HostParser == nullptr || options.maxLayers == 0)
-			return;
-		for (size_t i = 0; i < batch.size(); ++i)
-		{
-			pcppx_summary& s = out.summaries[i];
-			if (!(s.flags & PCPPX_F_NEEDS_HOST) || (s.flags & PCPPX_F_BAD_DESC))
-				continue;
-			pcppx_layer* lay = out.layers.data() + i * (size_t)options.maxLayers;
-			check(m_HostParser(batch.packetData(i), batch.caplens[i], batch.linkType, &o, &s, lay), "host parser");
-			s.flags = (uint16_t)(s.flags | F_HOST_PARSED);
-			++out.hostParsed;
-		}
+		out.hostParsed = detail::completeOnHost(m_HostParser, batch.data.data(), batch.offsets.data(),
+		                                        batch.caplens.data(), (uint32_t)batch.size(), batch.linkType, o,
+		                                        out.summaries.data(), out.layers.data());
 	}
 
 	/* FilterTraffic's whole worker on the device (AppWorkerThread.h:85-139): matched[i] = 1 for packets to send on;

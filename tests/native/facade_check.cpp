@@ -1,0 +1,202 @@
+/* facade_check — test driver for the per-packet entry points of include/pcppx.hpp (tests/test_facade.py).
+ *
+ *   facade_check read <packet|burst:N|batch:N> <outdir> <capture>...
+ *       reads every capture through PcapFileReaderDevice::getNextPacket, receivePackets (bursts of N) or
+ *       getNextPackets (batches of N) and writes <outdir>/<k>.bin: per packet u32 caplen, u32 frame length,
+ *       u64 timestamp (ns), u32 link type, then the bytes; a file holding "NOOPEN" when open() fails.  (CPU only.)
+ *   facade_check parse <capture> <outfile> <plan>
+ *       reads the capture with getNextPacket and builds, per packet, the Packets the plan names (a comma-separated
+ *       list of variants, applied to packet i in turn: full | tcp | ip | osi3 | osi4 | own | copy | free);
+ *       writes per packet and variant the pcppx_summary (32 B) and the PCPPX_MAX_LAYERS layer records the Packet
+ *       holds (zero past its chain).  (GPU.)
+ *   env PCPPX_CHECK_HOST_PARSER=<lib.so>: register that library's pcppx_host_parse with setHostParser.
+ */
+#include <dlfcn.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pcppx.hpp"
+
+namespace
+{
+void put(std::FILE* f, const void* p, size_t n)
+{
+	if (n && std::fwrite(p, 1, n, f) != n)
+	{
+		std::perror("fwrite");
+		std::exit(3);
+	}
+}
+
+void putRaw(std::FILE* f, const pcppx::RawPacket& r)
+{
+	const uint32_t cap = (uint32_t)r.getRawDataLen(), flen = (uint32_t)r.getFrameLength(), lt = r.getLinkLayerType();
+	const timespec ts = r.getPacketTimeStamp();
+	const uint64_t tns = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+	put(f, &cap, 4);
+	put(f, &flen, 4);
+	put(f, &tns, 8);
+	put(f, &lt, 4);
+	put(f, r.getRawData(), cap);
+}
+
+int readMode(const std::string& mode, const std::string& outdir, int nfiles, char** files)
+{
+	for (int k = 0; k < nfiles; ++k)
+	{
+		const std::string out = outdir + "/" + std::to_string(k) + ".bin";
+		std::FILE* f = std::fopen(out.c_str(), "wb");
+		if (f == nullptr)
+			return 2;
+		pcppx::PcapFileReaderDevice reader(files[k]);
+		if (!reader.open())
+		{
+			put(f, "NOOPEN", 6);
+			std::fclose(f);
+			continue;
+		}
+		if (mode == "packet")
+		{
+			pcppx::RawPacket raw;
+			while (reader.getNextPacket(raw))
+				putRaw(f, raw);
+		}
+		else if (mode.rfind("burst:", 0) == 0)
+		{
+			const int n = std::atoi(mode.c_str() + 6);
+			std::vector<pcppx::RawPacket*> arr((size_t)n, nullptr);
+			for (;;)
+			{
+				const uint16_t got = reader.receivePackets(arr.data(), (uint16_t)n, 0);
+				if (got == 0)
+					break;
+				for (uint16_t i = 0; i < got; ++i)
+					putRaw(f, *arr[i]);
+			}
+			for (auto* p : arr)
+				delete p;
+		}
+		else if (mode.rfind("batch:", 0) == 0)
+		{
+			const int n = std::atoi(mode.c_str() + 6);
+			pcppx::RawPacketVector b;
+			while (reader.getNextPackets(b, n) > 0)
+				for (size_t i = 0; i < b.size(); ++i)
+				{
+					const uint64_t t = b.timestampsNs[i];
+					pcppx::RawPacket raw;
+					raw.setRawData(b.packetData(i), (int)b.caplens[i], false,
+					               timespec{ (time_t)(t / 1000000000ull), (long)(t % 1000000000ull) }, b.linkType,
+					               (int)b.frameLens[i]);
+					putRaw(f, raw);
+				}
+		}
+		else
+			return 1;
+		reader.close();
+		std::fclose(f);
+	}
+	return 0;
+}
+
+void putPacket(std::FILE* f, const pcppx::Packet& p)
+{
+	put(f, &p.summary(), sizeof(pcppx_summary));
+	pcppx_layer lay[PCPPX_MAX_LAYERS];
+	std::memset(lay, 0, sizeof(lay));
+	for (size_t k = 0; k < p.getRecordedLayerCount() && k < PCPPX_MAX_LAYERS; ++k)
+	{
+		const pcppx::Layer l = p.getLayer(k);
+		lay[k] = pcppx_layer{ l.getProtocol(), (uint8_t)l.getOsiModelLayer(), l.getOffset(), (uint16_t)l.getHeaderLen(),
+			                  (uint16_t)l.getDataLen() };
+	}
+	put(f, lay, sizeof(lay));
+}
+
+int parseMode(const char* capture, const char* outfile, const std::string& plan)
+{
+	std::vector<std::string> variants;
+	for (size_t a = 0; a <= plan.size();)
+	{
+		size_t b = plan.find(',', a);
+		if (b == std::string::npos)
+			b = plan.size();
+		variants.push_back(plan.substr(a, b - a));
+		a = b + 1;
+	}
+	std::FILE* f = std::fopen(outfile, "wb");
+	if (f == nullptr)
+		return 2;
+	pcppx::PcapFileReaderDevice reader(capture);
+	if (!reader.open())
+		return 4;
+	pcppx::RawPacket raw;
+	size_t i = 0;
+	while (reader.getNextPacket(raw))
+	{
+		const std::string& v = variants[i % variants.size()];
+		if (v == "full")
+			putPacket(f, pcppx::Packet(&raw));
+		else if (v == "tcp")
+			putPacket(f, pcppx::Packet(&raw, pcppx::TCP));
+		else if (v == "ip")
+			putPacket(f, pcppx::Packet(&raw, pcppx::IP));
+		else if (v == "osi3")
+			putPacket(f, pcppx::Packet(&raw, pcppx::OsiModelNetworkLayer));
+		else if (v == "osi4")
+			putPacket(f, pcppx::Packet(&raw, false, pcppx::UnknownProtocol, pcppx::OsiModelTransportLayer));
+		else if (v == "own")  // the caller's own bytes: a one-packet batch
+		{
+			pcppx::RawPacket mine(raw.getRawData(), raw.getRawDataLen(), timespec{ 0, 0 }, false, raw.getLinkLayerType());
+			putPacket(f, pcppx::Packet(&mine));
+		}
+		else if (v == "copy")  // a copy shares the page
+		{
+			pcppx::RawPacket c(raw);
+			putPacket(f, pcppx::Packet(&c, pcppx::TCP));
+		}
+		else if (v == "free")  // freeRawPacket: the Packet deletes a heap copy of the caller's bytes
+		{
+			uint8_t* bytes = new uint8_t[raw.getRawDataLen() > 0 ? raw.getRawDataLen() : 1];
+			std::memcpy(bytes, raw.getRawData(), (size_t)raw.getRawDataLen());
+			auto* heap = new pcppx::RawPacket(bytes, raw.getRawDataLen(), timespec{ 0, 0 }, true, raw.getLinkLayerType());
+			putPacket(f, pcppx::Packet(heap, true));
+		}
+		else
+			return 1;
+		++i;
+	}
+	std::fclose(f);
+	return 0;
+}
+}  // namespace
+
+int main(int argc, char** argv)
+{
+	try
+	{
+		if (const char* lib = std::getenv("PCPPX_CHECK_HOST_PARSER"))
+		{
+			void* h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+			auto fn = h ? reinterpret_cast<pcppx_host_parse_fn>(dlsym(h, "pcppx_host_parse")) : nullptr;
+			if (fn == nullptr)
+				return 5;
+			pcppx::setHostParser(fn);
+		}
+		if (argc >= 4 && std::string(argv[1]) == "read")
+			return readMode(argv[2], argv[3], argc - 4, argv + 4);
+		if (argc == 5 && std::string(argv[1]) == "parse")
+			return parseMode(argv[2], argv[3], argv[4]);
+	}
+	catch (const pcppx::Error& e)
+	{
+		std::fprintf(stderr, "%s\n", e.what());
+		return 6;
+	}
+	std::fprintf(stderr, "usage: facade_check read <mode> <outdir> <capture>... | parse <capture> <out> <plan>\n");
+	return 1;
+}

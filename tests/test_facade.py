@@ -1,0 +1,241 @@
+"""The facade's per-packet entry points (include/pcppx.hpp): PcapFileReaderDevice::getNextPacket / receivePackets /
+getNextPackets over the prefetching zero-copy page pipeline, and Packet(RawPacket*, ...) bound to GPU records.
+
+CPU: the reader hands out exactly what the reference's PcapFileReaderDevice / PcapNgFileReaderDevice return from
+getNextPacket (tests/golden/ingest/expected.npz: caplen, frame length, timestamp, link type and bytes of every packet
+of 3,155 captures) in all three read modes; and the drop-in benchmark's packet loop is the reference's token for
+token (Examples/PcapPlusPlus-benchmark/benchmark.cpp:89-95).
+
+GPU: every Packet built from a reader's RawPacket -- Packet(&raw), Packet(&raw, TCP), Packet(&raw, IP),
+Packet(&raw, OsiModelNetworkLayer), the 4-argument form, the options mixed packet by packet (pages re-parsed for
+options other than the reader learnt), copies of a RawPacket, the caller's own bytes (one-packet batches) and
+freeRawPacket -- equals the C restatement's records for the same options bit for bit; with the reference
+registered as host parser, every packet equals the reference Packet++ (layers, hashes)."""
+from __future__ import annotations
+
+import re
+import struct
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import ingest_cases as ic
+import oracle
+from conftest import GOLDEN, ROOT, load_golden
+from pcapplusplus_amd import abi, synth
+from pcapplusplus_amd.pcap import from_packets, write_pcap
+
+BIN = ROOT / "examples" / "bin"
+CHECK = BIN / "facade_check"
+GOLD = GOLDEN / "ingest"
+REF = Path("/root/reference")
+
+
+@pytest.fixture(scope="module")
+def built():
+    r = subprocess.run(["make", "-s", "-C", str(ROOT / "examples")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return CHECK
+
+
+def _read_dump(path: Path):
+    raw = path.read_bytes()
+    if raw == b"NOOPEN":
+        return None
+    out = {"packets": [], "caplens": [], "frame_lens": [], "ts_ns": [], "linktypes": []}
+    pos = 0
+    while pos < len(raw):
+        cap, flen, ts, lt = struct.unpack_from("<IIQI", raw, pos)
+        pos += 20
+        out["packets"].append(raw[pos:pos + cap])
+        pos += cap
+        out["caplens"].append(cap)
+        out["frame_lens"].append(flen)
+        out["ts_ns"].append(ts)
+        out["linktypes"].append(lt)
+    for k, t in (("caplens", np.uint32), ("frame_lens", np.uint32), ("ts_ns", np.uint64), ("linktypes", np.uint32)):
+        out[k] = np.array(out[k], t)
+    return out
+
+
+@pytest.mark.parametrize("mode", ["packet", "burst:64", "batch:333"])
+def test_reader_entry_points_equal_reference(built, tmp_path, mode):
+    """getNextPacket(RawPacket&) / receivePackets(RawPacket**, 64) / getNextPackets(RawPacketVector&, 333) over every
+    fixture, crafted case and mutation of the ingest golden set: the reference readers' packets, field for field."""
+    from test_ingest import _case_bytes, _golden
+
+    g, starts = _golden()
+    data = _case_bytes(g)
+    names, files = [], []
+    for k, name in enumerate(g["names"]):
+        b = data[str(name)]
+        if b is None:
+            continue
+        f = tmp_path / f"c{k}"
+        f.write_bytes(b)
+        names.append(k)
+        files.append(str(f))
+    out = tmp_path / "out"
+    out.mkdir()
+    for lo in range(0, len(files), 400):  # argv length
+        r = subprocess.run([str(built), "read", mode, str(out), *files[lo:lo + 400]], capture_output=True, text=True,
+                           timeout=600)
+        assert r.returncode == 0, r.stderr
+        for j in range(lo, min(lo + 400, len(files))):
+            (out / f"{j - lo}.bin").rename(out / f"r{j}.bin")
+    checked = 0
+    for j, k in enumerate(names):
+        got = _read_dump(out / f"r{j}.bin")
+        assert (got is not None) == bool(g["opened"][k]), f"{g['names'][k]}: open"
+        if got is None:
+            continue
+        s, e = starts[k], starts[k + 1]
+        assert len(got["caplens"]) == e - s, f"{g['names'][k]}: packet count {len(got['caplens'])} vs {e - s}"
+        for key in ("caplens", "frame_lens", "ts_ns", "linktypes"):
+            assert np.array_equal(got[key], g[key][s:e]), f"{g['names'][k]}: {key}"
+        assert np.array_equal(ic.digest(got["packets"]), g["digests"][s:e]), f"{g['names'][k]}: packet bytes"
+        checked += 1
+    assert checked > 2500
+
+
+def test_reader_pages_span_a_large_capture(built, tmp_path):
+    """A capture larger than the first pages (16k, then 64k, 256k packets): getNextPacket crosses page boundaries
+    with nothing lost or repeated, and stops cleanly at the end."""
+    b = synth.config(3, 90_000)
+    f = tmp_path / "in.pcap"
+    write_pcap(f, b)
+    out = tmp_path / "o"
+    out.mkdir()
+    r = subprocess.run([str(built), "read", "packet", str(out), str(f)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = _read_dump(out / "0.bin")
+    assert np.array_equal(got["caplens"], b.caplens.astype(np.uint32))
+    assert ic.digest(got["packets"]).tolist() == ic.digest([b.packet(i) for i in range(b.n)]).tolist()
+
+
+def test_benchmark_packet_loop_is_the_references():
+    """examples/benchmark.cpp's packet branch is Examples/PcapPlusPlus-benchmark/benchmark.cpp:89-95 token for token
+    (read from the reference where it is present; the namespace alias `pcpp = pcppx` aside)."""
+    ref = REF / "Examples" / "PcapPlusPlus-benchmark" / "benchmark.cpp"
+    if not ref.exists():
+        pytest.skip("/root/reference absent")
+    tok = lambda s: re.findall(r"[A-Za-z_][A-Za-z_0-9]*|::|->|[^\s\w]", s)  # noqa: E731
+    want = tok("".join(ref.read_text().splitlines(keepends=True)[88:95]))
+    ours = tok((ROOT / "examples" / "benchmark.cpp").read_text())
+    assert want[:4] == ["start", "=", "std", "::"] and "getNextPacket" in want and "TCP" in want
+    assert any(ours[i:i + len(want)] == want for i in range(len(ours))), "packet loop differs from the reference's"
+    # FilterTraffic's burst loop body: `pcpp::Packet parsedPacket(packetArr[i]);` and the flow-table lines
+    ft = tok((ROOT / "examples" / "filter_traffic.cpp").read_text())
+    for line in ("pcpp::Packet parsedPacket(packetArr[i]);", "uint32_t hash = pcpp::hash5Tuple(&parsedPacket);",
+                 "m_Stats.collectStats(parsedPacket);", "pcapWriter->writePacket(*packetArr[i]);"):
+        w = tok(line)
+        assert any(ft[i:i + len(w)] == w for i in range(len(ft))), line
+
+
+# ---- GPU: Packet(RawPacket*, ...) records ----
+
+VARIANTS = {  # facade_check plan name -> (parse_until_family, parse_until_osi)
+    "full": (0, 8), "tcp": (4, 8), "ip": (0x203, 8), "osi3": (0, 3), "osi4": (0, 4), "own": (0, 8), "copy": (4, 8),
+    "free": (0, 8),
+}
+REC = np.dtype([("sum", abi.SUMMARY_DTYPE), ("lay", abi.LAYER_DTYPE, (abi.MAX_LAYERS,))])
+
+
+def _run_plan(built, tmp_path, batch, plan, host_parser=False):
+    f, o = tmp_path / "in.pcap", tmp_path / "rec.bin"
+    write_pcap(f, batch)
+    env = None
+    if host_parser:
+        import os
+
+        env = dict(os.environ, PCPPX_CHECK_HOST_PARSER=str(oracle.REF_SO))
+    r = subprocess.run([str(built), "parse", str(f), str(o), plan], capture_output=True, text=True, timeout=600,
+                       env=env)
+    assert r.returncode == 0, r.stderr
+    rec = np.frombuffer(o.read_bytes(), REC)
+    assert len(rec) == batch.n
+    return rec
+
+
+def _expected(batch, plan, reference=False):
+    """per packet the records of the variant the plan applies to it: from the restatement (or the reference)"""
+    names = plan.split(",")
+    want_sum = np.zeros(batch.n, abi.SUMMARY_DTYPE)
+    want_lay = np.zeros((batch.n, abi.MAX_LAYERS), abi.LAYER_DTYPE)
+    for v in set(names):
+        fam, osi = VARIANTS[v]
+        opts = abi.make_opts(fam, osi, True, abi.MAX_LAYERS)
+        s, lay = oracle.ref_parse(batch, opts) if reference else oracle.oracle_parse(batch, opts, threads=8)
+        idx = np.array([i for i in range(batch.n) if names[i % len(names)] == v], np.int64)
+        want_sum[idx] = s[idx]
+        want_lay[idx] = lay[idx]
+    return want_sum, want_lay
+
+
+def _captures():
+    b, _ = load_golden(GOLDEN / "capture_example.npz")
+    out = [("example.pcap", b)]
+    for gname in ("pcap_lt1.npz", "pcap_lt113.npz", "pcap_lt276.npz", "pcap_lt0.npz", "dat_ethernet.npz"):
+        gb, _ = load_golden(GOLDEN / gname)
+        out.append((gname, gb))
+    out.append(("synth_cfg5_40k", synth.config(5, 40_000)))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plan", ["full", "tcp", "osi3", "full,tcp,ip,osi3,osi4", "copy,free,tcp"])
+def test_gpu_packet_from_reader_equals_restatement(built, tmp_path, plan):
+    """Every Packet a reader's RawPacket builds equals the restatement's records for its options, bit for bit
+    (flagged packets: their exact prefix, as the device writes it); mixed plans force page re-parses."""
+    for name, b in _captures():
+        rec = _run_plan(built, tmp_path, b, plan)
+        ws, wl = _expected(b, plan)
+        try:
+            oracle.compare_exact(rec["sum"], rec["lay"], ws, wl)
+        except AssertionError as e:
+            raise AssertionError(f"{name}: {e}") from None
+
+
+@pytest.mark.gpu
+def test_gpu_packet_from_own_bytes(built, tmp_path):
+    """A RawPacket over the caller's own bytes (not from a reader) is parsed as a one-packet batch: the same records."""
+    b, _ = load_golden(GOLDEN / "capture_example.npz")
+    b = b.slice(0, 1500)
+    rec = _run_plan(built, tmp_path, b, "own,full")
+    ws, wl = _expected(b, "own,full")
+    oracle.compare_exact(rec["sum"], rec["lay"], ws, wl)
+
+
+@pytest.mark.gpu
+def test_gpu_packet_large_capture_pages(built, tmp_path):
+    """350k IMIX packets (pages of 16k, 64k, 256k packets, parsed ahead by the pipeline) under Packet(&raw, TCP):
+    every record equal to the restatement's."""
+    b = synth.config(3, 350_000)
+    rec = _run_plan(built, tmp_path, b, "tcp")
+    ws, wl = _expected(b, "tcp")
+    oracle.compare_exact(rec["sum"], rec["lay"], ws, wl)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plan", ["full", "tcp", "full,tcp,osi3"])
+def test_gpu_packet_host_parser_equals_reference(built, tmp_path, plan):
+    """With the reference registered as host parser (setHostParser), every Packet -- flagged ones completed on the
+    host -- equals the reference Packet++'s chain and hashes for its options."""
+    if not oracle.ref_available():
+        pytest.skip("reference library not built")
+    for name, b in _captures()[:-1]:
+        rec = _run_plan(built, tmp_path, b, plan, host_parser=True)
+        ws, wl = _expected(b, plan, reference=True)
+        s = rec["sum"]
+        nl = np.minimum(ws["n_layers"], abi.MAX_LAYERS)
+        for f in ("hash5", "hash5_dir", "hash2"):
+            bad = np.nonzero(s[f] != ws[f])[0]
+            assert len(bad) == 0, f"{name}: {f} differs on {len(bad)}; first {bad[:3]}"
+        bad = np.nonzero(s["n_layers"] != nl)[0]
+        assert len(bad) == 0, f"{name}: n_layers differs on {len(bad)}; first {bad[:3]}"
+        valid = np.arange(abi.MAX_LAYERS)[None, :] < nl[:, None]
+        for f in ("proto", "offset", "hdr_len", "data_len"):
+            bad = np.nonzero(((rec["lay"][f] != wl[f]) & valid).any(axis=1))[0]
+            assert len(bad) == 0, f"{name}: layers.{f} differs on {len(bad)}; first {bad[:3]}"

@@ -1,0 +1,78 @@
+#!/bin/bash
+# The one GPU-box recipe (repo root on the box): each argument is a step, run in order, each under its own time limit;
+# the first failing step ends the call.
+#   tools/gpu_run.sh <tag> <step>...
+# steps:
+#   tests[:<pytest paths/-k ...>]  the -m gpu suite (default: all of tests/)  -> gpurun_out/<tag>_gpu_tests.log
+#   smoke                          __graft_entry__.smoke()                      -> <tag>_smoke.log
+#   e2e                            tools/e2e_file.py (file -> records, drop-in benchmark vs reference)  -> <tag>_e2e_file.json
+#   bench:<cfgs>                   bench.py line per config (comma list; "3s64" etc. = config 3 at one packet size)
+#   prof:<cfgs>                    the bench line under rocprofv3 --kernel-trace, plus the timed-launch-only summary
+#                                  (tools/timed_stats.py) -> <tag>_prof_cfg<c>/, <tag>_kernel_stats_cfg<c>.csv
+#   traffic:<cfgs>                 PMC FETCH/WRITE passes -> <tag>_traffic_cfg<c>.json (tools/measure_traffic.sh)
+#   sq:<cfg>                       SQ issue counters (tools/sq_counters.sh)
+#   cmd:<shell command>            anything else, under a 600 s limit
+set -o pipefail
+TAG=$1
+shift
+OUT=gpurun_out
+ROOT=$(pwd)
+mkdir -p "$OUT"
+cfgargs() {  # "3s512" -> --config 3 --sizes 512
+  case "$1" in
+    *s*) echo "--config ${1%%s*} --sizes ${1#*s}" ;;
+    *) echo "--config $1" ;;
+  esac
+}
+tr() { [ -f "$ROOT/$OUT/${TAG}_traffic_cfg$1.json" ] && echo "--traffic $ROOT/$OUT/${TAG}_traffic_cfg$1.json"; }
+for step in "$@"; do
+  name=${step%%:*}
+  arg=${step#*:}
+  [ "$arg" = "$step" ] && arg=""
+  echo "== $step"
+  case "$name" in
+    tests)
+      sel=${arg:-tests}
+      timeout -k 10 1100 python -u -m pytest $sel -m gpu -x -v --timeout 400 --timeout-method thread \
+        > "$OUT/${TAG}_gpu_tests.log" 2>&1 || { tail -40 "$OUT/${TAG}_gpu_tests.log"; exit 1; }
+      tail -2 "$OUT/${TAG}_gpu_tests.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/${TAG}_smoke.log" 2>&1 \
+        || { tail -20 "$OUT/${TAG}_smoke.log"; exit 2; }
+      cat "$OUT/${TAG}_smoke.log" ;;
+    e2e)
+      timeout -k 10 1000 python -u tools/e2e_file.py --out "$OUT/${TAG}_e2e_file.json" $arg > "$OUT/${TAG}_e2e.log" 2>&1 \
+        || { tail -20 "$OUT/${TAG}_e2e.log"; exit 3; }
+      grep -E "^map|^copy|^config1|^example|^imix|^filter" "$OUT/${TAG}_e2e.log" | cut -c1-500 ;;
+    bench)
+      for c in ${arg//,/ }; do
+        timeout -k 10 400 python -u bench.py $(cfgargs "$c") $(tr "$c") > "$OUT/${TAG}_bench_cfg$c.json" \
+          2> "$OUT/${TAG}_bench_cfg$c.err" || { tail -20 "$OUT/${TAG}_bench_cfg$c.err"; exit 4; }
+        echo "cfg $c: $(head -c 400 "$OUT/${TAG}_bench_cfg$c.json")"
+      done ;;
+    prof)
+      for c in ${arg//,/ }; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/${TAG}_prof_cfg$c" \
+          -o bench --output-format csv -- python3 "$ROOT/bench.py" $(cfgargs "$c") --steps 20 --warmup 5 --no-e2e $(tr "$c") \
+          > "$ROOT/$OUT/${TAG}_prof_bench_cfg$c.json" 2> "$ROOT/$OUT/${TAG}_prof_cfg$c.err") \
+          || { tail -20 "$OUT/${TAG}_prof_cfg$c.err"; exit 5; }
+        python3 tools/timed_stats.py "$OUT/${TAG}_prof_cfg$c" "$OUT/${TAG}_prof_bench_cfg$c.json" \
+          > "$OUT/${TAG}_kernel_stats_cfg$c.csv" || exit 5
+        echo "cfg $c: $(head -c 400 "$OUT/${TAG}_prof_bench_cfg$c.json")"
+        cat "$OUT/${TAG}_kernel_stats_cfg$c.csv"
+      done ;;
+    traffic)
+      for c in ${arg//,/ }; do
+        tools/measure_traffic.sh "$TAG" "$c" > "$OUT/${TAG}_traffic_cfg$c.log" 2>&1 \
+          || { tail -20 "$OUT/${TAG}_traffic_cfg$c.log"; exit 6; }
+        grep -E '"config"|hbm_bytes|write_bytes' "$OUT/${TAG}_traffic_cfg$c.json"
+      done ;;
+    sq)
+      tools/sq_counters.sh "$TAG" "$arg" || exit 7 ;;
+    cmd)
+      timeout -k 10 600 bash -c "$arg" || exit 8 ;;
+    *)
+      echo "unknown step $step"; exit 9 ;;
+  esac
+done
+echo "gpu_run $TAG ok"
