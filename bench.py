@@ -42,6 +42,10 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU (default: the config's size)")
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 4, 5))
+    ap.add_argument("--sizes", choices=("imix", "64", "512", "1500"), default="imix",
+                    help="config 3's packet sizes: the 64/512/1500-B IMIX at 7:4:1 (the headline), or one size only (the "
+                         "north star's per-size batches: same VLAN / IPv4 / IPv6 / TCP / UDP mix and checksum verify; "
+                         f"packets per GPU {SIZED_PACKETS})")
     ap.add_argument("--max-layers", type=int, default=None,
                     help="layer records per packet (default: 8 for config 3, 12 for config 5, 0 for the configs whose "
                          "consumer reads no layers: 2's 5-tuple extract, 4's flow table)")
@@ -75,6 +79,7 @@ def parse_args():
 
 
 CONFIG_PACKETS = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000_000}
+SIZED_PACKETS = {64: 10_000_000, 512: 10_000_000, 1500: 5_000_000}  # config 3 at one size: 0.6 / 5.1 / 7.5 GB per GPU
 CONFIG_MAX_LAYERS = {2: 0, 3: 8, 4: 0, 5: 12}
 CONFIG_LAYOUT = {3: "packed", 5: "packed"}  # configs with layer records
 # plain Eth / VLAN / IP / L4 stacks (configs 2 and 4): the one-round parse-only window (PCPPX_WINDOW_SHORT)
@@ -90,7 +95,7 @@ def kernel_sha() -> str:
 
 
 def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool, layout: str = "fixed",
-                 records: str = "summary", window: str = "default") -> tuple[int | None, str]:
+                 records: str = "summary", window: str = "default", sizes: str = "imix") -> tuple[int | None, str]:
     """(HBM bytes per parse launch, note) from a PMC traffic file, only if it matches this run exactly."""
     if not path.exists():
         return None, f"no PMC measurement ({path.name})"
@@ -99,9 +104,10 @@ def load_traffic(path: Path, cfg: int, n: int, ml: int, csum: bool, layout: str 
     except (ValueError, OSError) as e:
         return None, f"unreadable {path.name}: {e}"
     want = {"config": cfg, "packets": n, "max_layers": ml, "checksums": csum, "layout": layout, "records": records,
-            "window": window,
+            "window": window, "sizes": sizes,
             "kernel_sha": kernel_sha()}
-    got = {k: tj.get(k, {"layout": "fixed", "records": "summary", "window": "default"}.get(k)) for k in want}
+    got = {k: tj.get(k, {"layout": "fixed", "records": "summary", "window": "default", "sizes": "imix"}.get(k))
+           for k in want}
     if got != want:
         return None, f"stale {path.name}: measured {got}, this run {want}"
     return int(tj["hbm_bytes_per_launch"]), f"{path.name} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
@@ -252,12 +258,15 @@ def main() -> None:
 
     # ---- synthetic shard for this rank (per-GPU work fixed: weak scaling) ----
     cfg = args.config
-    npk = args.packets or CONFIG_PACKETS[cfg]
+    if args.sizes != "imix" and cfg != 3:
+        sys.exit("bench.py: --sizes selects config 3's packet size")
+    sized = int(args.sizes) if args.sizes != "imix" else None
+    npk = args.packets or (SIZED_PACKETS[sized] if sized else CONFIG_PACKETS[cfg])
     ml = args.max_layers if args.max_layers is not None else CONFIG_MAX_LAYERS[cfg]
     t0 = time.time()
     seed = shard.shard_seed(cfg, rank)
     if cfg == 3:
-        batch = synth.imix(npk, seed)
+        batch = synth.imix(npk, seed, sizes=(sized,), weights=(1,)) if sized else synth.imix(npk, seed)
     elif cfg == 4:
         batch = synth.imix(npk, seed, flows=1_000_000, corrupt_frac=0.0)
     elif cfg == 5:
@@ -392,8 +401,9 @@ def main() -> None:
 
     traffic, traffic_note = None, "not requested"
     if not args.no_traffic:
-        tp = Path(args.traffic) if args.traffic else ROOT / "profiles" / f"traffic_cfg{cfg}.json"
-        traffic, traffic_note = load_traffic(tp, cfg, n, ml, want_csum, layout, rec_kind, window)
+        tag = f"{cfg}s{sized}" if sized else f"{cfg}"
+        tp = Path(args.traffic) if args.traffic else ROOT / "profiles" / f"traffic_cfg{tag}.json"
+        traffic, traffic_note = load_traffic(tp, cfg, n, ml, want_csum, layout, rec_kind, window, args.sizes)
 
     e2e = None
     if not args.no_e2e and rank == 0 and world == 1:
@@ -472,7 +482,9 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"{n} packets/GPU, " + WORKLOADS[cfg],
+                "workload": f"{n} packets/GPU, " + (WORKLOADS[cfg] if not sized else WORKLOADS[cfg].replace(
+                    "IMIX 64/512/1500 B 7:4:1", f"{sized} B packets only (IMIX mix of stacks)")),
+                "sizes": args.sizes,
                 "packets_per_gpu": n,
                 "wire_bytes_per_gpu": wire,
                 "checksums": want_csum,

@@ -107,7 +107,9 @@ int main(int argc, char* argv[])
 		o.want_checksums = csum ? 1 : 0;
 		o.max_layers = layers;
 		Pinned sum(batchN * sizeof(pcppx_summary)), lay((size_t)batchN * (layers ? layers : 1) * sizeof(pcppx_layer));
-		pcppx_records rec{ sum.as<pcppx_summary>(), layers ? lay.as<pcppx_layer>() : nullptr, nullptr, nullptr, nullptr };
+		pcppx_records rec{};
+		rec.summary = sum.as<pcppx_summary>();
+		rec.layers = layers ? lay.as<pcppx_layer>() : nullptr;
 		double best = 1e30, best_read = 0;
 		uint64_t packets = 0, wire = 0, digest = 0;
 		for (int r = 0; r < reps; ++r)

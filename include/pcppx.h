@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PCPPX_ABI_VERSION 5
+#define PCPPX_ABI_VERSION 6
 /* the library is built with hidden visibility: exactly the functions declared here are exported */
 #define PCPPX_API __attribute__((visibility("default")))
 #define PCPPX_MAX_LAYERS 16     /* fixed depth cap; deeper chains set PCPPX_F_DEPTH_OVERFLOW */
@@ -146,8 +146,10 @@ typedef struct pcppx_opts {
  *           64t .. 64t+63) start at layers[64 * t * max_layers], and packet i's entries follow those of the packets
  *           before it in its tile: layers[64 * t * max_layers + sum_{64t <= j < i} min(n_layers_j, max_layers) + k].
  *           The buffer is sized as for FIXED (n * max_layers entries); the summary is required (its n_layers
- *           decode the positions: pcppx_unpack_layers, include/pcppx.hpp). The write traffic is the chain, not
- *           max_layers rows per packet. max_layers <= PCPPX_PACKED_MAX_LAYERS. Device path only. */
+ *           decode the positions: pcppx_unpack_layers below, pcppx::unpackLayers in include/pcppx.hpp). The write
+ *           traffic is the chain, not max_layers rows per packet. max_layers <= PCPPX_PACKED_MAX_LAYERS. Device parse
+ *           only; the consumers of a parse's records (pcppx_filter_device, pcppx_reasm_device) read FIXED records and
+ *           refuse PACKED ones (pcppx_records.layout). */
 #define PCPPX_LAYOUT_FIXED 0
 #define PCPPX_LAYOUT_PACKED 1
 #define PCPPX_PACKED_MAX_LAYERS 12
@@ -201,6 +203,10 @@ typedef struct pcppx_records {
 	pcppx_tuple* tuples;    /* optional (NULL): n 5-tuple extracts. Device path only */
 	uint64_t* proto_stats;  /* optional (NULL): PCPPX_PROTO_STATS counters, accumulated (collectStats). Device path
 	                           only; calls that set it on one context are ordered (they share its scratch) */
+	uint8_t layout;         /* PCPPX_LAYOUT_* of `layers`: written by the parse calls (= opts->layout); read by
+	                           pcppx_filter_device / pcppx_reasm_device, which refuse PCPPX_LAYOUT_PACKED records.
+	                           Zero-initialised records are FIXED. */
+	uint8_t reserved[7];
 } pcppx_records;
 
 /* The caller's own host parse of ONE packet — its Packet++ (`pcpp::Packet packet(&raw, parseUntil...)`) turned
@@ -384,6 +390,11 @@ PCPPX_API int pcppx_pcap_map_batch(pcppx_pcap* reader, const uint8_t** data, uin
                                    uint32_t* caplens, uint32_t* frame_lens, uint64_t* timestamps_ns, uint32_t max_packets,
                                    uint32_t* n_out);
 PCPPX_API void pcppx_pcap_close(pcppx_pcap* reader);
+
+/* PCPPX_LAYOUT_PACKED layer entries (host memory, from a device parse) -> the FIXED layout: fixed[i * max_layers + k]
+ * for k < min(summary[i].n_layers, max_layers), zero past each chain. max_layers <= PCPPX_PACKED_MAX_LAYERS. */
+PCPPX_API int pcppx_unpack_layers(const pcppx_summary* summary, const pcppx_layer* packed, uint64_t n,
+                                  uint32_t max_layers, pcppx_layer* fixed);
 PCPPX_API void* pcppx_host_alloc(size_t bytes); /* page-locked host memory (hipHostMalloc) */
 PCPPX_API void pcppx_host_free(void* p);
 

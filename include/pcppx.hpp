@@ -404,7 +404,9 @@ struct Page
 		auto r = std::make_unique<Records>(k, n);
 		const pcppx_opts o = k.opts();
 		const pcppx_batch b{ base, offsets.data(), caplens.data(), dataLen, n, linkType, 0 };
-		pcppx_records rec{ r->sum, r->lay, nullptr, nullptr, nullptr };
+		pcppx_records rec{};
+		rec.summary = r->sum;
+		rec.layers = r->lay;
 		Service::instance().parse(b, o, rec);
 		completeOnHost(hostParser().load(), base, offsets.data(), caplens.data(), n, linkType, o, r->sum, r->lay);
 		return r;
@@ -1190,7 +1192,9 @@ private:
 		const pcppx_opts o = k.opts();
 		const uint64_t off = 0;
 		const pcppx_batch b{ m_Raw, &off, &m_Caplen, m_Caplen, 1, raw->m_LinkLayerType, 0 };
-		pcppx_records rec{ &m_Own->sum, m_Own->lay, nullptr, nullptr, nullptr };
+		pcppx_records rec{};
+		rec.summary = &m_Own->sum;
+		rec.layers = m_Own->lay;
 		detail::Service::instance().parse(b, o, rec);
 		detail::completeOnHost(detail::hostParser().load(), m_Raw, &off, &m_Caplen, 1, raw->m_LinkLayerType, o,
 		                       &m_Own->sum, m_Own->lay);
@@ -1322,7 +1326,9 @@ public:
 	{
 		const pcppx_batch b = batch.toC();
 		const pcppx_opts o = options.toC();
-		pcppx_records r{ out.summaries.data(), options.maxLayers ? out.layers.data() : nullptr, nullptr, nullptr, nullptr };
+		pcppx_records r{};
+		r.summary = out.summaries.data();
+		r.layers = options.maxLayers ? out.layers.data() : nullptr;
 		check(pcppx_parse_batch_host(m_Ctx, &b, &o, &r), "pcppx_parse_batch_host");
 		out.hostParsed = detail::completeOnHost(m_HostParser, batch.data.data(), batch.offsets.data(),
 		                                        batch.caplens.data(), (uint32_t)batch.size(), batch.linkType, o,

@@ -15,7 +15,7 @@ PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 ENGINE_SO = PKG_DIR / "libpcppx.so"
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_LAYERS = 16
 MAX_CAPLEN = 65535
 WINDOW_DEFAULT, WINDOW_DEEP, WINDOW_SHORT = 0, 1, 2  # pcppx_opts.window (PCPPX_WINDOW_*)
@@ -121,7 +121,7 @@ class Opts(C.Structure):
 
 class Records(C.Structure):
     _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p), ("flow_keys", C.c_void_p), ("tuples", C.c_void_p),
-                ("proto_stats", C.c_void_p)]
+                ("proto_stats", C.c_void_p), ("layout", C.c_uint8), ("reserved", C.c_uint8 * 7)]
 
 
 class MatchSpec(C.Structure):
@@ -243,6 +243,8 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_host_alloc.restype = P
     lib.pcppx_host_free.argtypes = [P]
     lib.pcppx_host_free.restype = None
+    lib.pcppx_unpack_layers.argtypes = [P, P, C.c_uint64, C.c_uint32, P]
+    lib.pcppx_unpack_layers.restype = C.c_int
     for name in ("pcppx_device_count", "pcppx_open", "pcppx_sync", "pcppx_parse_batch_device",
                  "pcppx_parse_batch_host", "pcppx_flow_count_device"):
         getattr(lib, name).restype = C.c_int
@@ -257,6 +259,7 @@ EXPORTED_SYMBOLS = (
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
     "pcppx_flow_count_device", "pcppx_flow_count_keys_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_parse_batch_device_reasm", "pcppx_pcap_open", "pcppx_pcap_linktype",
     "pcppx_pcap_read_batch", "pcppx_pcap_read_batch_ex", "pcppx_pcap_map_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
+    "pcppx_unpack_layers",
 )
 
 

@@ -708,6 +708,7 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
+		r->layout = o->layout;
 		return device_parse(c, b, o, r, nullptr, static_cast<hipStream_t>(hip_stream));
 	}
 
@@ -723,6 +724,7 @@ extern "C"
 		// device-path-only outputs
 		if (r->tuples != nullptr || r->proto_stats != nullptr || o->layout != PCPPX_LAYOUT_FIXED)
 			return PCPPX_E_INVAL;
+		r->layout = PCPPX_LAYOUT_FIXED;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
 		int rc = init_host_path(c);
@@ -745,7 +747,8 @@ extern "C"
 		if (b->n == 0)
 			return PCPPX_OK;
 		if (b->data == nullptr || b->offsets == nullptr || r->summary == nullptr || r->layers == nullptr ||
-		    flow_keys == nullptr || flow_first == nullptr || matched == nullptr || stats == nullptr)
+		    flow_keys == nullptr || flow_first == nullptr || matched == nullptr || stats == nullptr ||
+		    r->layout != PCPPX_LAYOUT_FIXED)
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
@@ -766,6 +769,7 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
+		r->layout = PCPPX_LAYOUT_FIXED;
 		return device_parse(c, b, o, r, info, static_cast<hipStream_t>(hip_stream));
 	}
 
@@ -777,7 +781,7 @@ extern "C"
 		if (b->n == 0)
 			return PCPPX_OK;
 		if (b->data == nullptr || b->offsets == nullptr || r->summary == nullptr || r->layers == nullptr ||
-		    info == nullptr)
+		    info == nullptr || r->layout != PCPPX_LAYOUT_FIXED)
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
@@ -908,5 +912,26 @@ extern "C"
 	{
 		if (p)
 			(void)hipHostFree(p);
+	}
+
+	int pcppx_unpack_layers(const pcppx_summary* summary, const pcppx_layer* packed, uint64_t n, uint32_t max_layers,
+	                        pcppx_layer* fixed)
+	{
+		if (n == 0)
+			return PCPPX_OK;
+		if (summary == nullptr || packed == nullptr || fixed == nullptr || max_layers == 0 ||
+		    max_layers > PCPPX_PACKED_MAX_LAYERS)
+			return PCPPX_E_INVAL;
+		uint64_t pos = 0;
+		for (uint64_t i = 0; i < n; ++i)
+		{
+			if (i % 64 == 0)
+				pos = i * max_layers;  // tile t's run starts at entry 64 * t * max_layers
+			const uint32_t cnt = summary[i].n_layers < max_layers ? summary[i].n_layers : max_layers;
+			for (uint32_t k = 0; k < max_layers; ++k)
+				fixed[i * max_layers + k] = k < cnt ? packed[pos + k] : pcppx_layer{};
+			pos += cnt;
+		}
+		return PCPPX_OK;
 	}
 }

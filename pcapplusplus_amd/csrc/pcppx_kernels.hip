@@ -1791,8 +1791,6 @@ __global__ __launch_bounds__(kBlock) void reasm_kernel(ReasmParams rp)
 // partial edge chunks. The ones'-complement sum only needs the byte-order fix-up for an odd L4
 // start at the very end (a multiply by 256 mod 65535).
 constexpr int kTile = 64;
-// header window per packet: 7 x 16 B = 112 B (160 B measured slower even for deep stacks: occupancy)
-constexpr int kTStageChunks = 7;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 {
@@ -1929,40 +1927,37 @@ __device__ __forceinline__ uint32_t deep_extent(const Pkt& p, uint32_t et, uint3
 
 constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_layers; beyond, direct stores
 
-// MinWaves: __launch_bounds__ minimum waves per SIMD (1 = compiler's choice). LDS is 8 KiB per block
-// with 7-chunk windows (stage 7424 B + 768 B of per-lane state): 20 blocks = 5 waves/SIMD fit a CU's
-// 160 KiB. SWin: stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers).
-// Chunks: 16-B header chunks a packet's LDS window holds.
-// NT: non-temporal span-stream loads and record stores (read-once / write-once data; A/B variant 11)
-// Csum: the instance computes checksums when the launch asks (false: a parse-only instance, no span stream).
-// Chunks1 < Chunks: a two-round gather: first min(packet, Chunks1) chunks for every packet, then up to Chunks for
-// the packets the fast path could not take from the first window (deep stacks), which then retry it.
-// MarkFast (tools only): flags bit 0x8000 set on the packets the fast path took. FillTails: the staged layer rows
-// are zero-filled past n_layers and stored whole: full-line stores, 3.5% faster on config 3 than storing only the
-// chain's records (profiles/r02_ab_tails.txt).
-// Ring: the span stream writes every chunk's running prefix into a ring in the (by then free) header stage, and each
-// packet lane reads its two prefixes from it once per 4 stream groups, instead of pulling them (and its partial tail
-// chunk) from the owning lanes by ds_bpermute in every group; the header-window inputs of the L4 sum (edge chunks,
-// checksum field, pseudo header) are taken before the ring overwrites the stage, a tail chunk past the window by a
-// global load issued before the stream.
-// SkipGeneric (tools only, a diagnostic: wrong records): packets off the fast path are not walked -- the time the
-// generic walk costs the waves that hold such a packet.
-// TightR2: the second gather round reads only up to the deep stack's header extent (deep_extent) instead of the
-// whole window (false: tools/ab variant 50). Realign: a deep stack that ends past the window is re-gathered from a
-// dword-aligned start (mis <= 3 instead of <= 15) so that it fits (false: tools/ab variant 51).
-// LateGeneric: packets off the fast path are walked after the span stream ((4b)); tools/ab variant 53.
-// EarlyB (tools/ab variant 54/55): the second stream window is issued with the first, before the header gather.
-// StreamFirst: the span stream runs before the header gather and the parse. Its prefix picks need no parse result:
-// each lane takes the running prefix at its packet's first and last whole chunk and the sum of its partial last chunk;
-// after the parse the L4 whole-chunk sum is that difference less the packet's leading chunks before the L4 start
-// (LDS window), whenever the L4 layer runs to the packet's end (else whole chunks from HBM, as for sparse tiles). The
-// header gather then reads lines the stream has just brought into L2, and no stream register is live in the parse.
-// GatherOnly (tools only, a diagnostic): descriptors, both gather rounds (the second for every packet) and the
-// record stores (zero rows), no parse: the memory time of the parse-only access pattern.
-template <int MinWaves, int SWin, int Chunks = kTStageChunks, bool NT = false, bool StreamOnly = false,
-          bool Csum = true, int Chunks1 = Chunks, bool MarkFast = false, bool FillTails = true, bool GatherOnly = false,
-          bool Ring = false, bool SkipGeneric = false, bool TightR2 = true, bool Realign = true, bool LateGeneric = false,
-          bool EarlyB = false, bool StreamFirst = false>
+// The shape switches of one parse_tile_kernel instance. The product instances use ParseShape<> (below: only the
+// checksum instance of PCPPX_WINDOW_DEEP differs, in EarlyB); the diagnostics exist for tools/ab/libpcppx_ab.so only.
+//   NT: non-temporal span-stream loads and record stores (read-once / write-once data; profiles/r01_ab_nontemporal.txt)
+//   FillTails: the staged FIXED layer rows are zero-filled past n_layers and stored whole: full-line stores, 3.5% faster
+//     on config 3 than storing only the chain's records (profiles/r02_ab_tails.txt)
+//   TightR2: the second gather round reads only up to the deep stack's header extent (deep_extent) instead of the whole
+//     window (profiles/r02_ab_tight_r2.txt)
+//   Realign: a deep stack that ends past the window is re-gathered from a dword-aligned start (mis <= 3 instead of <= 15)
+//     so that it fits (profiles/r02_ab_realign.txt)
+//   EarlyB: the second span-stream window is issued with the first, before the header gather (0.8-0.9% on config 3,
+//     profiles/r03_ab_earlyB_*.txt)
+//   diagnostics (wrong or marked records; static_assert'ed out of libpcppx.so): StreamOnly (no header gather / parse;
+//     L4 range = [14, caplen)), MarkFast (flags bit 0x8000 on the packets the fast path took), GatherOnly (descriptors,
+//     both gather rounds for every packet and the record stores, no parse: the memory time of the access pattern),
+//     SkipGeneric (packets off the fast path are not walked: the time the generic walk costs)
+template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
+          bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false>
+struct ParseShape
+{
+	static constexpr bool NT = kNT, FillTails = kFillTails, TightR2 = kTightR2, Realign = kRealign, EarlyB = kEarlyB;
+	static constexpr bool StreamOnly = kStreamOnly, MarkFast = kMarkFast, GatherOnly = kGatherOnly,
+	                      SkipGeneric = kSkipGeneric;
+};
+
+// One wave = one 64-packet tile. MinWaves: __launch_bounds__ minimum waves per SIMD (1 = the compiler's choice).
+// SWin: span-stream window in 16-B chunks (SWin/64 wave-loads in flight per buffer, two buffers). Chunks: 16-B header
+// chunks a packet's LDS window holds (the stage: 64 slots of 4 * Chunks + 1 dwords). Csum: the instance computes
+// checksums when the launch asks (false: a parse-only instance, no span stream). Chunks1 < Chunks: a two-round
+// gather: first min(packet, Chunks1) chunks for every packet, then up to Chunks for the packets the fast path could not
+// take from the first window (deep stacks).
+template <int MinWaves, int SWin, int Chunks, bool Csum, int Chunks1, class S = ParseShape<>>
 __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 {
 	constexpr int kTSlotDw = 4 * Chunks + 1;  // + 1 pad dword against bank conflicts
@@ -1974,11 +1969,16 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	constexpr uint32_t kRowMl = (uint32_t)kTSlotDw / 2 - 1 < kRowMaxMl ? (uint32_t)kTSlotDw / 2 - 1 : kRowMaxMl;
 	static_assert(kTile * (kRowMl + 1) * 2 <= kTile * kTSlotDw, "stage too small for layer rows");
 	static_assert(Chunks1 <= Chunks && Chunks < 256, "gather rounds");
+	// PCPPX_LAYOUT_PACKED stages a tile's chains (kTile * PCPPX_PACKED_MAX_LAYERS entries) in the stage
+	constexpr bool kPackedOk = kTSlotDw >= 2 * PCPPX_PACKED_MAX_LAYERS;
 #ifndef PCPPX_TOOLS_AB
 	// the diagnostic switches write wrong or marked records: only tools/ab/libpcppx_ab.so (built with PCPPX_TOOLS_AB)
-	// may instantiate them, never libpcppx.so
-	static_assert(!MarkFast && !GatherOnly && !SkipGeneric && !StreamOnly, "tools-only parse_tile_kernel switch");
+	// may instantiate them, never libpcppx.so; and every product instance can stage a PACKED run
+	static_assert(!S::MarkFast && !S::GatherOnly && !S::SkipGeneric && !S::StreamOnly, "tools-only parse_tile_kernel switch");
+	static_assert(kPackedOk, "a product instance must stage PCPPX_LAYOUT_PACKED rows");
 #endif
+	constexpr bool NT = S::NT, StreamOnly = S::StreamOnly, MarkFast = S::MarkFast, FillTails = S::FillTails,
+	               GatherOnly = S::GatherOnly, SkipGeneric = S::SkipGeneric, TightR2 = S::TightR2, Realign = S::Realign;
 	const bool want_csum = Csum && prm.want_csum;  // uniform
 
 	const uint32_t lane = threadIdx.x;
@@ -2019,58 +2019,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	};
 	if (stream)
 		load(va, 0);
-	if ((EarlyB || StreamFirst) && stream)  // both stream windows in flight during the gather and the parse
+	if (S::EarlyB && stream)  // both stream windows in flight during the gather and the parse
 		load(vb, 1);
-
-	// ---- (1b) StreamFirst: the whole span stream now, picking per packet the prefix before its first whole chunk (p0),
-	// before its last partial chunk (p1), and that partial chunk's sum (tsum) ----
-	const uintptr_t sf_a = (uintptr_t)pkt_addr, sf_e = sf_a + cap;
-	const uintptr_t sf_cs = (sf_a + 15) & ~(uintptr_t)15, sf_ce = sf_e & ~(uintptr_t)15;
-	uint32_t sf_p0 = 0, sf_p1 = 0, sf_tsum = 0;
-	if (StreamFirst && stream)
-	{
-		const bool whole = live && sf_cs <= sf_ce;
-		const int32_t t0 = whole ? (int32_t)((sf_cs - smin) >> 4) - 1 : -2;
-		const int32_t t1 = whole ? (int32_t)((sf_ce - smin) >> 4) - 1 : -2;
-		const int32_t te = (whole && sf_ce < sf_e) ? (int32_t)((sf_ce - smin) >> 4) : -2;
-		uint32_t carry = 0;
-		const uint32_t nwin = (nchunks + SWin - 1) / SWin;
-		auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
-#pragma unroll
-			for (int k = 0; k < SWin / 64; ++k)
-			{
-				const int32_t g = (int32_t)(win * SWin + 64 * k);
-				const uint32_t h = halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
-				const uint32_t x = wave_incl_scan(h);
-				const uint32_t pre = carry + x;
-				const bool in0 = t0 >= g && t0 < g + 64, in1 = t1 >= g && t1 < g + 64;
-				if (__ballot(in0 || in1))
-				{
-					const uint32_t q0 = __shfl(pre, (t0 - g) & 63, 64);
-					const uint32_t q1 = __shfl(pre, (t1 - g) & 63, 64);
-					sf_p0 = in0 ? q0 : sf_p0;
-					sf_p1 = in1 ? q1 : sf_p1;
-				}
-				const bool ine = te >= g && te < g + 64;
-				if (__ballot(ine))
-				{
-					const int src = (te - g) & 63;
-					const uint4 d = make_uint4(__shfl(v[k].x, src, 64), __shfl(v[k].y, src, 64), __shfl(v[k].z, src, 64),
-					                           __shfl(v[k].w, src, 64));
-					if (ine)
-						sf_tsum = chunk_sum(d, sf_ce, sf_ce, sf_e);
-				}
-				carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-			}
-		};
-		for (uint32_t wi = 0; wi < nwin; wi += 2)
-		{
-			process(va, wi);
-			load(va, wi + 2);
-			process(vb, wi + 1);
-			load(vb, wi + 3);
-		}
-	}
 
 	// ---- (2) header gather into LDS: 8 lanes per packet, one 16-B chunk each (8 packets per wave-instruction) ----
 	Pkt p;
@@ -2216,7 +2166,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
 			}
 		}
-		else if (!SkipGeneric && !LateGeneric)
+		else if (!SkipGeneric)
 		{
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 			w = walk_chain(p, cap, prm, lay_out);
@@ -2242,99 +2192,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		const bool tail = need && f0 <= f1 && f1 < ae;  // partial last chunk [f1, ae)
 		uint32_t fsum = 0, tsum = 0;
 		bool tail_done = false;
-		if constexpr (Ring)
-		{
-			// (a) header-window inputs, before the ring overwrites the stage
-			uint32_t head = 0, fw = 0, ph = 0;
-			uint4 tv = make_uint4(0, 0, 0, 0);
-			if (need)
-			{
-				head = f0 <= f1 ? edge_sum(p, as, f0) : edge_sum(p, as, ae);
-				l4_inputs(p, w, &fw, &ph);
-				if (tail)
-				{
-					if ((p.a0 & 15) == 0 && (uint32_t)((f1 - p.a0) >> 4) < p.nch)
-					{
-						tsum = edge_sum(p, f1, ae);
-						tail_done = true;
-					}
-					else
-						tv = ld16(f1);  // lands during the stream
-				}
-			}
-			__syncthreads();  // every lane is done with the header stage
-			if (stream)
-			{
-				// (b) the span stream: per 64-chunk group a halves-sum, a DPP inclusive scan and the running prefix
-				// P into ring[c mod 512]; after each 4 groups the lanes whose P(c0-1) / P(c1-1) fell in them read it
-				lptr32w ring = (lptr32w)(stage);
-				constexpr uint32_t kRing = 4 * SWin < 512 ? 512u : 4u * SWin;  // 4 stream windows of prefixes
-				static_assert(kRing <= (uint32_t)(kTile * kTSlotDw), "ring");
-				const int32_t t0 = full ? (int32_t)((f0 - smin) >> 4) - 1 : -2;  // P(c0-1); -1 -> 0
-				const int32_t t1 = full ? (int32_t)((f1 - smin) >> 4) - 1 : -2;  // P(c1-1)
-				uint32_t p0 = 0, p1 = 0, carry = 0;
-				const uint32_t nwin = (nchunks + SWin - 1) / SWin;
-				auto process = [&](uint4 (&v)[SWin / 64], uint32_t win) {
-#pragma unroll
-					for (int k = 0; k < SWin / 64; ++k)
-					{
-						const uint32_t g = win * SWin + 64 * k;
-						const uint32_t h = halves(v[k].x, halves(v[k].y)) + halves(v[k].z, halves(v[k].w));
-						const uint32_t x = wave_incl_scan(h);
-						ring[(g & (kRing - 1)) + lane] = carry + x;
-						carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-					}
-				};
-				load(vb, 1);
-				for (uint32_t wi = 0; wi < nwin; wi += 2)
-				{
-					process(va, wi);
-					load(va, wi + 2);
-					process(vb, wi + 1);
-					load(vb, wi + 3);
-					const int32_t lo = (int32_t)(wi * SWin), hi = lo + 2 * SWin;
-					const bool in0 = t0 >= lo && t0 < hi, in1 = t1 >= lo && t1 < hi;
-					const uint32_t r0 = ring[(uint32_t)(in0 ? t0 : 0) & (kRing - 1)];
-					const uint32_t r1 = ring[(uint32_t)(in1 ? t1 : 0) & (kRing - 1)];
-					p0 = in0 ? r0 : p0;
-					p1 = in1 ? r1 : p1;
-				}
-				if (full)
-					fsum = p1 - p0;
-			}
-			else if (full)
-				fsum = full_chunks_sum(f0, f1);
-			if (need)
-			{
-				if (tail && !tail_done)
-					tsum = chunk_sum(tv, f1, f1, ae);
-				uint32_t acc = mod65535(fsum) + head + (f0 <= f1 ? tsum : 0u);
-				uint32_t r = mod65535(acc);
-				if (as & 1)
-					r = (r * 256u) % 65535u;
-				l4c = l4_checksum_from(w, r, fw, ph, &l4s);
-				w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
-			}
-		}
-		else if (StreamFirst)
-		{
-			// the prefixes were picked before the parse: whole chunks [f0, f1) = [cs, ce) less [cs, f0) when the L4 layer
-			// ends at the packet's end (then f1 = ce and the partial tail is the captured one); anything else (a trailer
-			// or IP padding after the L4 layer, an L4 start in the last partial chunk, a sparse tile) from HBM
-			const bool combine = stream && need && ae == sf_e && f0 >= sf_cs && f0 <= f1;
-			if (combine)
-			{
-				uint32_t lead = 0;  // the packet's whole chunks before the L4 start: in the header window
-				for (uintptr_t c = sf_cs; c < f0; c += 16)
-					lead += edge_sum(p, c, c + 16);
-				fsum = sf_p1 - sf_p0 - lead;
-				tsum = sf_tsum;
-				tail_done = true;
-			}
-			else if (full)
-				fsum = full_chunks_sum(f0, f1);
-		}
-		else if (stream)
+		if (stream)
 		{
 			// Stream the tile span once, 4 x 1 KiB wave-loads per window, two register windows in
 			// flight. Per 64-chunk group: halves-sums -> DPP inclusive scan -> running prefix P; each
@@ -2379,7 +2237,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			};
 			// straight-line body (windows padded to an even count; loads past the span are clamped) so
 			// the compiler's vmcnt accounting sees one fixed issue order: one window always in flight
-			if (!EarlyB)
+			if (!S::EarlyB)
 				load(vb, 1);
 			for (uint32_t wi = 0; wi < nwin; wi += 2)
 			{
@@ -2393,7 +2251,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 		else if (full)
 			fsum = full_chunks_sum(f0, f1);
-		if (!Ring && need)
+		if (need)
 		{
 			uint32_t acc = mod65535(fsum);
 			if (f0 <= f1)
@@ -2404,26 +2262,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			if (as & 1)
 				r = (r * 256u) % 65535u;
 			l4c = l4_checksum(p, w, r, &l4s);
-			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
-		}
-	}
-
-	// ---- (4b) LateGeneric: the packets off the fast path are walked after the span stream (the LDS window is still
-	// intact), so the stream's registers and the generic walk's are never live together; their L4 sums come from the
-	// window and HBM (range_residue) instead of the stream's prefixes. Same records. ----
-	if (LateGeneric && live && !fast && !StreamOnly && !GatherOnly && !SkipGeneric)
-	{
-		uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
-		w = walk_chain(p, cap, prm, lay_out);
-		hashes(p, w, h5, h5d, h2);
-		if (want_csum && w.v4 >= 0)
-		{
-			ipc = ipv4_checksum(p, w, &ips);
-			w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
-		}
-		if (want_csum && w.l4i >= 0)
-		{
-			l4c = l4_checksum(p, w, range_residue(p, w.l4o, w.l4o + w.l4dlen), &l4s);
 			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
 		}
 	}
@@ -2452,8 +2290,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 	typedef __attribute__((address_space(3))) u32x2* lptr64w;
 	// PCPPX_LAYOUT_PACKED: the tile's chains dense in LDS (entry excl + k of the lane's exclusive prefix), stored as one
-	// contiguous run of entries from the tile's base; needs kTile * PCPPX_PACKED_MAX_LAYERS entries of stage
-	constexpr bool kPackedOk = kTSlotDw >= 2 * PCPPX_PACKED_MAX_LAYERS;
+	// contiguous run of entries from the tile's base (an instance that cannot stage it is refused by the launch)
 	if (kPackedOk && stage_layers && prm.packed)  // uniform
 	{
 		const uint32_t cnt = in ? (w.n_layers < ml ? w.n_layers : ml) : 0u;
@@ -3222,22 +3059,22 @@ constexpr int kParseWaves = 5, kParseSWin = 128;
 constexpr int kParseChunks = 6;
 // round 3: both stream windows are issued before the header gather (EarlyB; same 96 VGPRs): 0.8-0.9% on config 3 in
 // interleaved A/Bs, fixed and packed layouts (profiles/r03_ab_earlyB_*.txt)
-#define PCPPX_PARSE_KERNEL                                                                                             \
-	parse_tile_kernel<kParseWaves, kParseSWin, kParseChunks, true, false, true, kParseChunks, false, true, false, false,  \
-	                  false, true, true, false, true>
+#define PCPPX_PARSE_KERNEL parse_tile_kernel<kParseWaves, kParseSWin, kParseChunks, true, kParseChunks>
 // parse-only launches (no checksums): no span stream; a 144-B window reached in two gather rounds (96 B for every
 // packet, the rest only for the deep stacks the first window cannot hold): 99.7% of config 5's deep stacks take the
 // fast path; 16 waves/CU of LDS (144 B: 0.88 ms on config 5, 160 B: 1.00 ms at 14 waves/CU, 112 B: 1.17 ms with
 // 22% of the packets on the generic walk; gpurun_out r02l_ab_cfg5 -> profiles/r02_ab_parse_only.txt)
 constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
-#define PCPPX_PARSE_ONLY_KERNEL parse_tile_kernel<1, 64, kParseOnlyChunks, true, false, false, kParseOnlyChunks1>
+#define PCPPX_PARSE_ONLY_KERNEL parse_tile_kernel<1, 64, kParseOnlyChunks, false, kParseOnlyChunks1>
 // checksum launches with opts.window = PCPPX_WINDOW_DEEP: the parse-only instance's two-round 144-B window (tight second
-// round, dword-aligned re-gather) with the span stream; LDS 10 KiB, 4 waves/SIMD
-#define PCPPX_PARSE_DEEP_KERNEL parse_tile_kernel<4, kParseSWin, kParseOnlyChunks, true, false, true, kParseOnlyChunks1>
+// round, dword-aligned re-gather) with the span stream; LDS 10 KiB, 4 waves/SIMD; the second stream window is issued
+// after the parse (EarlyB off: this instance's register budget)
+#define PCPPX_PARSE_DEEP_KERNEL                                                                                        \
+	parse_tile_kernel<4, kParseSWin, kParseOnlyChunks, true, kParseOnlyChunks1, ParseShape<true, true, true, true, false>>
 // parse-only launches with opts.window = PCPPX_WINDOW_SHORT: one 96-B round, LDS 7 KiB (22 waves/CU, 5 waves/SIMD of
 // registers): config 4 0.464 -> 0.432 ms, config 2 43.2 -> 36.3 us, config 5 0.75 -> 1.61 ms (tools/ab variant 60,
 // profiles/r03_ab_windows_persist.txt)
-#define PCPPX_PARSE_SHORT_KERNEL parse_tile_kernel<1, 64, kParseChunks, true, false, false, kParseChunks>
+#define PCPPX_PARSE_SHORT_KERNEL parse_tile_kernel<1, 64, kParseChunks, false, kParseChunks>
 
 // the flow-table shape: 1024-thread blocks, 8192 LDS slots, 4096-packet batches with the next batch prefetched,
 // 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)

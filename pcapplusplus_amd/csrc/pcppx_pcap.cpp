@@ -183,6 +183,8 @@ struct pcppx_pcap
 	std::vector<size_t> pend;
 	size_t pend_i = 0, pend_end = 0;
 	bool pend_stop = false, pend_ok = false;
+	// an allocation of the parallel walk failed: the reader goes on with the sequential walk (same records)
+	bool par_off = false;
 	// pcapng: the file-wide interface list of light_pcapng_file_info
 	uint32_t n_if = 0;
 	uint16_t if_link[kMaxInterfaces];
@@ -338,7 +340,7 @@ struct pcppx_pcap
 	// a parallel walk of the next region when no walked starts are pending
 	bool parallel_ready() const
 	{
-		return !ng && !done && (pend_ok || size - pos >= kParMin);
+		return !ng && !done && !par_off && (pend_ok || size - pos >= kParMin);
 	}
 	void fill_pending()
 	{
@@ -601,8 +603,11 @@ extern "C"
 			return PCPPX_E_INVAL;
 		uint32_t n = 0;
 		uint64_t used = 0;
-		// large pcap regions: the parallel walk (identical records), then the fields and the copies in parallel
+		// large pcap regions: the parallel walk (identical records), then the fields and the copies in parallel. Its
+		// scratch (record starts, segment chains) can be tens of MB: when an allocation fails the reader state is as
+		// before the failed step (pos at the next record, n the packets already placed) and the sequential walk goes on.
 		while (n < max_packets && r->parallel_ready())
+		try
 		{
 			r->fill_pending();
 			const size_t* starts = r->pend.data() + r->pend_i;
@@ -642,6 +647,10 @@ extern "C"
 			n += (uint32_t)k;
 			if (r->consume(k))
 				break;
+		}
+		catch (const std::bad_alloc&)
+		{
+			r->par_off = true;
 		}
 		while (!r->done && n < max_packets)
 		{
@@ -690,8 +699,10 @@ extern "C"
 		*data = r->map;
 		*data_len = r->size;
 		uint32_t n = 0;
-		// large pcap regions: the parallel walk (identical records), then the fields of each record in parallel
+		// large pcap regions: the parallel walk (identical records), then the fields of each record in parallel (an
+		// allocation failure falls back to the sequential walk, as in pcppx_pcap_read_batch_ex)
 		while (n < max_packets && r->parallel_ready())
+		try
 		{
 			r->fill_pending();
 			const size_t* starts = r->pend.data() + r->pend_i;
@@ -713,6 +724,10 @@ extern "C"
 			n += (uint32_t)k;
 			if (r->consume(k))
 				break;  // the batch is full: the next one starts at the first pending record
+		}
+		catch (const std::bad_alloc&)
+		{
+			r->par_off = true;
 		}
 		while (!r->done && n < max_packets)
 		{

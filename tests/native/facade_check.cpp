@@ -6,7 +6,7 @@
  *       u64 timestamp (ns), u32 link type, then the bytes; a file holding "NOOPEN" when open() fails.  (CPU only.)
  *   facade_check parse <capture> <outfile> <plan>
  *       reads the capture with getNextPacket and builds, per packet, the Packets the plan names (a comma-separated
- *       list of variants, applied to packet i in turn: full | tcp | ip | osi3 | osi4 | own | copy | free);
+ *       list of variants, applied to packet i in turn: full | tcp | ip | osi2 | osi3 | osi4 | own | copy | free);
  *       writes per packet and variant the pcppx_summary (32 B) and the PCPPX_MAX_LAYERS layer records the Packet
  *       holds (zero past its chain).  (GPU.)
  *   env PCPPX_CHECK_HOST_PARSER=<lib.so>: register that library's pcppx_host_parse with setHostParser.
@@ -147,6 +147,8 @@ int parseMode(const char* capture, const char* outfile, const std::string& plan)
 			putPacket(f, pcppx::Packet(&raw, pcppx::IP));
 		else if (v == "osi3")
 			putPacket(f, pcppx::Packet(&raw, pcppx::OsiModelNetworkLayer));
+		else if (v == "osi2")
+			putPacket(f, pcppx::Packet(&raw, pcppx::OsiModelDataLinkLayer));
 		else if (v == "osi4")
 			putPacket(f, pcppx::Packet(&raw, false, pcppx::UnknownProtocol, pcppx::OsiModelTransportLayer));
 		else if (v == "own")  // the caller's own bytes: a one-packet batch

@@ -101,3 +101,63 @@ def test_struct_layout_matches_header():
         dt = abi.SUMMARY_DTYPE if t == "pcppx_summary" else abi.LAYER_DTYPE
         assert dt.fields[f][1] == int(off), name
         assert dt.fields[f][0].itemsize == int(size), name
+
+
+def test_records_struct_matches_header():
+    """pcppx_records (ABI 6: + layout) is laid out as the ctypes mirror."""
+    src = r"""
+    #include <stdio.h>
+    #include <stddef.h>
+    #include "pcppx.h"
+    int main(void) { printf("%zu %zu %zu\n", sizeof(pcppx_records), offsetof(pcppx_records, layout),
+                            offsetof(pcppx_records, proto_stats)); return 0; }
+    """
+    with tempfile.TemporaryDirectory() as d:
+        c = Path(d) / "r.c"
+        c.write_text(src)
+        exe = Path(d) / "r"
+        subprocess.run(["gcc", "-I", str(HEADER.parent), str(c), "-o", str(exe)], check=True)
+        size, off_layout, off_ps = (int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                                    text=True).stdout.split())
+    assert size == C.sizeof(abi.Records)
+    assert off_layout == abi.Records.layout.offset and off_ps == abi.Records.proto_stats.offset
+
+
+def test_unpack_layers_export_equals_the_mirrors():
+    """pcppx_unpack_layers (the C decoder of PCPPX_LAYOUT_PACKED) equals abi.unpack_layers on ragged chains, a
+    partial last tile and chains longer than max_layers."""
+    import numpy as np
+
+    lib = abi.load_engine()
+    rng = np.random.default_rng(7)
+    for n, ml in ((1, 1), (63, 4), (64, 12), (200, 8), (1000, 12)):
+        s = np.zeros(n, abi.SUMMARY_DTYPE)
+        s["n_layers"] = rng.integers(0, 16, n)
+        packed = np.zeros(max(n * ml, 1), abi.LAYER_DTYPE)
+        packed["offset"] = rng.integers(0, 65535, len(packed))
+        packed["proto"] = rng.integers(1, 40, len(packed))
+        fixed = np.ones(n * ml, abi.LAYER_DTYPE)
+        assert lib.pcppx_unpack_layers(s.ctypes.data, packed.ctypes.data, n, ml, fixed.ctypes.data) == 0
+        want = abi.unpack_layers(s, packed, ml)
+        got = fixed.reshape(n, ml)
+        valid = np.arange(ml)[None, :] < np.minimum(s["n_layers"], ml)[:, None]
+        for f in abi.LAYER_DTYPE.names:
+            assert (got[f][valid] == want[f][valid]).all(), (n, ml, f)
+            assert (got[f][~valid] == 0).all(), (n, ml, f)
+    assert lib.pcppx_unpack_layers(None, None, 5, 4, None) == abi.E_INVAL
+    assert lib.pcppx_unpack_layers(s.ctypes.data, packed.ctypes.data, n, abi.PACKED_MAX_LAYERS + 1,
+                                   fixed.ctypes.data) == abi.E_INVAL
+
+
+def test_consumers_refuse_packed_records_without_gpu():
+    """pcppx_filter_device / pcppx_reasm_device read FIXED records: PACKED ones (records.layout, written by the parse)
+    are refused with PCPPX_E_INVAL before any device work."""
+    lib = abi.load_engine()
+    b = abi.Batch(1, 1, 1, 1, 1, 1, 0)
+    r = abi.Records(1, 1)
+    r.layout = abi.LAYOUT_PACKED
+    spec = abi.MatchSpec()
+    ctx = C.c_void_p(1)  # never dereferenced: the argument checks fail first
+    assert lib.pcppx_reasm_device(ctx, C.byref(b), C.byref(r), 8, C.c_void_p(1), None) == abi.E_INVAL
+    assert lib.pcppx_filter_device(ctx, C.byref(b), C.byref(r), 8, C.byref(spec), 0, C.c_void_p(1), C.c_void_p(1),
+                                   1024, C.c_void_p(1), C.c_void_p(1), None) == abi.E_INVAL

@@ -137,7 +137,8 @@ def test_benchmark_packet_loop_is_the_references():
 # ---- GPU: Packet(RawPacket*, ...) records ----
 
 VARIANTS = {  # facade_check plan name -> (parse_until_family, parse_until_osi)
-    "full": (0, 8), "tcp": (4, 8), "ip": (0x203, 8), "osi3": (0, 3), "osi4": (0, 4), "own": (0, 8), "copy": (4, 8),
+    "full": (0, 8), "tcp": (4, 8), "ip": (0x203, 8), "osi2": (0, 2), "osi3": (0, 3), "osi4": (0, 4), "own": (0, 8),
+    "copy": (4, 8),
     "free": (0, 8),
 }
 REC = np.dtype([("sum", abi.SUMMARY_DTYPE), ("lay", abi.LAYER_DTYPE, (abi.MAX_LAYERS,))])
@@ -239,3 +240,58 @@ def test_gpu_packet_host_parser_equals_reference(built, tmp_path, plan):
         for f in ("proto", "offset", "hdr_len", "data_len"):
             bad = np.nonzero(((rec["lay"][f] != wl[f]) & valid).any(axis=1))[0]
             assert len(bad) == 0, f"{name}: layers.{f} differs on {len(bad)}; first {bad[:3]}"
+
+
+GOLDEN_PLAN = {"full": "full", "until_tcp": "tcp", "until_ip": "ip", "until_osi3": "osi3", "until_osi2": "osi2"}
+CSUM_FLAGS = abi.F_IP_CSUM | abi.F_IP_CSUM_OK | abi.F_L4_CSUM | abi.F_L4_CSUM_OK
+
+
+@pytest.mark.gpu
+def test_gpu_host_completion_every_golden_record(built, tmp_path):
+    """Every golden set under every parse-option variant, read through the facade (getNextPacket + Packet(&raw, ...))
+    with the reference registered as host parser: every record -- the packets the engine finishes itself and the
+    flagged ones the host parser completes (their hashes, port layer, protocol mask and checksums included) -- equals
+    the reference Packet++'s golden record, field for field (flags: the reference's, plus F_HOST_PARSED on the
+    completed ones)."""
+    if not oracle.ref_available():
+        pytest.skip("reference library not built")
+    from conftest import golden_files
+
+    checked = completed = 0
+    for path in golden_files():
+        b, variants = load_golden(path)
+        for v, (opts, rs, rl) in variants.items():
+            if v not in GOLDEN_PLAN:
+                continue
+            rec = _run_plan(built, tmp_path, b, GOLDEN_PLAN[v], host_parser=True)
+            s, lay = rec["sum"], rec["lay"]
+            ml = int(opts.max_layers)
+            host = (s["flags"] & F_HOST) != 0
+            csum = bool(opts.want_checksums)
+            nl = np.minimum(s["n_layers"], ml)
+            where = f"{path.name}/{v}"
+            assert (nl == rs["n_layers"]).all(), f"{where}: n_layers {np.nonzero(nl != rs['n_layers'])[0][:5]}"
+            fields = ["hash5", "hash5_dir", "hash2", "l4_layer", "proto_mask"]
+            if csum:
+                fields += ["ip_csum_calc", "ip_csum_stored", "l4_csum_calc", "l4_csum_stored"]
+            for f in fields:
+                bad = np.nonzero(s[f] != rs[f])[0]
+                assert len(bad) == 0, f"{where}: {f} differs on {len(bad)} packets, first #{bad[0]} " \
+                                      f"(host-completed: {bool(host[bad[0]])})"
+            keep = ~np.uint16(F_HOST | (0 if csum else CSUM_FLAGS))
+            fl = s["flags"] & keep
+            if ml < abi.MAX_LAYERS:  # the reference record's depth cap is the variant's
+                fl = (fl & ~np.uint16(abi.F_DEPTH_OVERFLOW)) | np.where(s["n_layers"] > ml, abi.F_DEPTH_OVERFLOW, 0)
+            bad = np.nonzero(fl != (rs["flags"] & keep))[0]
+            assert len(bad) == 0, f"{where}: flags differ on {len(bad)} packets, first #{bad[0]}: {s[bad[0]]} vs {rs[bad[0]]}"
+            assert not (s["flags"] & abi.F_NEEDS_HOST).any(), f"{where}: a packet left uncompleted"
+            valid = np.arange(ml)[None, :] < nl[:, None]
+            for f in ("proto", "osi", "offset", "hdr_len", "data_len"):
+                bad = np.nonzero(((lay[:, :ml][f] != rl[f]) & valid).any(axis=1))[0]
+                assert len(bad) == 0, f"{where}: layers.{f} differs on {len(bad)} packets, first #{bad[0]}"
+            checked += b.n
+            completed += int(host.sum())
+    assert checked > 100_000 and completed > 1000, (checked, completed)
+
+
+F_HOST = 0x4000  # pcppx::F_HOST_PARSED (include/pcppx.hpp)

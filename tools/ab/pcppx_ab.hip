@@ -171,9 +171,11 @@ __global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, ui
 using namespace pcppx;
 
 /* variant: 1 lane kernel; 2 stream-only diagnostic (no header gather / parse; L4 range = [14, caplen));
- * 3 / 4 tile-shaped / grid-stride read of the batch bytes (results written over summary[]);
- * 5 tile 5 waves + 4 KiB windows; 6 compiler occupancy + 2 KiB; 8 compiler occupancy + 4 KiB;
- * 11 cached loads and stores; anything else: the product kernel. Records equal the product's for 1, 5, 6, 8, 11. */
+ * 3 / 4 tile-shaped / grid-stride read of the batch bytes (results written over summary[]); 7 tile-shaped read + the
+ * parse's record stores; 29 gather-only diagnostic; 30 / 31 the checksum / parse-only instance marking fast-path
+ * packets (flags bit 0x8000); 44 / 52 skip-generic diagnostics; 70 the DEEP checksum instance with the early second
+ * stream window; anything else: the product kernel. Records equal the product's for 1, 70 (30 / 31 up to the mark).
+ * The shape variants measured in rounds 1-3 are in git history (profiles/r0*_ab_*.txt hold their results). */
 PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, void* hip_stream,
                                        int variant)
 {
@@ -189,7 +191,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 1:
 		hipLaunchKernelGGL(parse_lane_kernel, dim3((b->n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, prm);
 		break;
-	case 2: hipLaunchKernelGGL((parse_tile_kernel<5, 128, kTStageChunks, true, true>), grid, dim3(kTile), 0, stream, prm); break;
 	case 3:
 	case 4:
 	{
@@ -215,52 +216,16 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 		                   reinterpret_cast<uint8_t*>(r->layers), w_per_wave, reinterpret_cast<uint32_t*>(r->summary));
 		break;
 	}
-	case 5: hipLaunchKernelGGL((parse_tile_kernel<5, 256>), grid, dim3(kTile), 0, stream, prm); break;
-	case 6: hipLaunchKernelGGL((parse_tile_kernel<1, 128>), grid, dim3(kTile), 0, stream, prm); break;
-	case 8: hipLaunchKernelGGL((parse_tile_kernel<1, 256>), grid, dim3(kTile), 0, stream, prm); break;
-	case 11: hipLaunchKernelGGL((parse_tile_kernel<5, 128>), grid, dim3(kTile), 0, stream, prm); break;
-	case 12: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 7, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // chain records only
-	// parse-only instances (checksums off in opts): window chunks / first-round chunks
-	case 20: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, false, 7>), grid, dim3(kTile), 0, stream, prm); break;
-	case 21: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 10>), grid, dim3(kTile), 0, stream, prm); break;
-	case 22: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	case 23: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	case 50: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // whole-window second round
-	case 52: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // checksum instance, skip-generic diagnostic
-	case 53: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // checksum instance, late generic walk
-	case 54: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // early second window
-	case 55: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // early second window, 4 waves
-	case 56: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // stream first
-	case 57: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, false, false, true, 6, false, true, false, false, false, true, true, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // stream first, cached loads
-	case 58: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, false, true, 6, false, true, false, false, false, true, true, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // stream first, 6 waves
-	// small-packet parse-only instances (config 2): one gather round, fewer LDS bytes per wave -> more waves per CU
-	case 60: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 6, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96-B window
-	case 61: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 6, true, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96-B window, 6 waves
-	case 62: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window
-	case 63: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 6 waves
-	case 64: hipLaunchKernelGGL((parse_tile_kernel<8, 64, 5, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;  // 80-B window, 8 waves
-	case 68: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // parse-only, cached record stores
-	case 69: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 6, false, false, false, 6>), grid, dim3(kTile), 0, stream, prm); break;  // SHORT, cached record stores
-	case 51: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, false, true, false>), grid, dim3(kTile), 0, stream, prm); break;  // tight second round, no realign
-	case 24: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
-	case 25: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 7, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
-	case 26: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, false>), grid, dim3(kTile), 0, stream, prm); break;  // chain records only
-	case 27: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 5>), grid, dim3(kTile), 0, stream, prm); break;
-	case 40: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 7, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // prefix ring
-	case 41: hipLaunchKernelGGL((parse_tile_kernel<5, 256, 7, true, false, true, 7, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // ring, 4-KiB windows
-	case 42: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, false, true, 6, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // ring, 96-B windows, 6 waves
-	case 43: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, false, true, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // ring, 96-B windows
-	case 45: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96-B windows
-	case 46: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, false, true, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96-B windows, 6 waves
-	case 47: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 7, true, false, true, 6>), grid, dim3(kTile), 0, stream, prm); break;  // 96 + 16 B two-round
-	case 48: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 6, true>), grid, dim3(kTile), 0, stream, prm); break;  // 1-KiB windows, 6 waves
-	case 49: hipLaunchKernelGGL((parse_tile_kernel<5, 64, 6, true>), grid, dim3(kTile), 0, stream, prm); break;   // 1-KiB windows
-	case 44: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, false, false, true>), grid, dim3(kTile), 0, stream, prm); break;  // skip-generic diagnostic
-	case 29: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, false, true, true>), grid, dim3(kTile), 0, stream, prm); break;  // gather-only diagnostic
-	case 28: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 5, false, false>), grid, dim3(kTile), 0, stream, prm); break;
-	// the product shapes with flags bit 0x8000 marking the packets the fast path took (records otherwise equal)
-	case 30: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, false, true, 6, true>), grid, dim3(kTile), 0, stream, prm); break;
-	case 31: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, true, false, false, 6, true>), grid, dim3(kTile), 0, stream, prm); break;
+	// diagnostics over the product shapes (ParseShape<NT, FillTails, TightR2, Realign, EarlyB, StreamOnly, MarkFast,
+	// GatherOnly, SkipGeneric>): stream only, gather only, fast-path marks, skip the generic walk
+	case 2: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, true>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 29: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 30: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 31: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 44: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 52: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
+	// the PCPPX_WINDOW_DEEP checksum instance with the early second stream window (the product's runs it late)
+	case 70: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 9, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	default: return launch_parse(b, o, r, stream);
 	}
 	return check_launch("pcppx_ab_parse_device", stream);

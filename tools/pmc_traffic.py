@@ -37,7 +37,8 @@ c = line["config"]
 out = {
     "config": int(c["workload"].split("config ")[1].split(":")[0]), "packets": int(c["packets_per_gpu"]),
     "max_layers": int(c["max_layers"]), "checksums": bool(c["checksums"]), "layout": c.get("layout", "fixed"),
-    "records": c.get("records", "summary"), "window": c.get("window", "default"), "kernel_sha": kernel_sha(),
+    "records": c.get("records", "summary"), "window": c.get("window", "default"), "sizes": c.get("sizes", "imix"),
+    "kernel_sha": kernel_sha(),
     "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "launches": [nf, nw],
     "read_bytes_corrected": 2 * fetch_kib * 1024, "write_bytes": write_kib * 1024,
     "hbm_bytes_per_launch": int(2 * fetch_kib * 1024 + write_kib * 1024),
