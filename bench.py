@@ -464,7 +464,7 @@ def main() -> None:
                       f"not the reference's", file=sys.stderr, flush=True)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region (every rank's), so N>1 lines carry it too
         cpu = cpu_baseline(batch, opts, args.cpu_sample, args.cpu_seconds)
 
     if rank == 0:

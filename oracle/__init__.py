@@ -400,8 +400,8 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
 
 
 # protocols the engine builds itself (include/pcppx.h: everything else is a host layer); HTTPRequest /
-# HTTPResponse (6/7), DNS (13) and SSL (18) as a classified first L7 layer and the layers behind it
-ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16, 17, 18, 19, 21, 25, 26, 30, 32, 33, 44, 52)
+# HTTPResponse (6/7), DNS (13), SSL (18), SSH (35) and MySQL (63) as a classified first L7 layer and the layers behind it
+ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16, 17, 18, 19, 21, 25, 26, 30, 32, 33, 35, 44, 52, 63)
 
 
 def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:
@@ -409,8 +409,10 @@ def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:
       - every packet whose reference chain holds a layer the engine does not build is flagged
         (NEEDS_HOST_L7 / NEEDS_HOST_PROTO, or not parsed at all: OVERSIZE / BAD_DESC);
       - a flagged packet whose reference chain holds no such layer is one where the host's dissector, at the
-        point the engine stopped, built nothing or fell back to a Payload layer (the engine cannot tell without
-        the dissector's own validity rules): the reference layer at index n_layers is GenericPayload or absent.
+        point the engine stopped, built nothing or fell back to a Payload layer, or (port 3306 beside another trigger
+        port) the earlier dissector declined and the chain fell through to MySQL -- the engine cannot tell without
+        that dissector's own validity rules: the reference layer at index n_layers is GenericPayload, MySQL or
+        absent.
     Returns counters {flagged, foreign, payload_fallback}."""
     host = (eng_sum["flags"] & (abi.F_NEEDS_HOST_L7 | abi.F_NEEDS_HOST_PROTO)) != 0
     unparsed = (eng_sum["flags"] & (abi.F_OVERSIZE | abi.F_BAD_DESC)) != 0
@@ -426,7 +428,7 @@ def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:
     over = np.nonzero(host & ~foreign)[0]
     en = eng_sum["n_layers"][over].astype(np.int64)
     nxt = np.where(en < rn[over], ref_lay["proto"][over, np.minimum(en, ml - 1)], 25)
-    bad = over[nxt != 25]
+    bad = over[(nxt != 25) & (nxt != 63)]
     if len(bad):
         i = int(bad[0])
         raise AssertionError(f"{len(bad)} flagged packets whose reference chain continues with an engine layer; "

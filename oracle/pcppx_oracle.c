@@ -205,6 +205,9 @@ static int ssl_record(const uint8_t* d, uint32_t n)
 }
 static int dns_port(uint16_t x) { return x == 53 || x == 5353 || x == 5355; } /* DnsLayer::isDnsPort, DnsLayer.h:468-479 */
 
+/* engine-internal class bits (never in a summary's flags): the payload is a MySqlLayer / SSH messages the engine builds */
+#define L7_MYSQL 0x4000
+#define L7_SSH 0x8000
 /* TCP payload (sp/dp host order): 0 = plain Payload, else PCPPX_F_NEEDS_HOST_L7 | class bits */
 static uint16_t tcp_l7(const uint8_t* d, uint32_t n, uint16_t sp, uint16_t dp)
 {
@@ -219,6 +222,22 @@ static uint16_t tcp_l7(const uint8_t* d, uint32_t n, uint16_t sp, uint16_t dp)
 		if (tcp_l7_port(x) && !http_port(x) && !ssl_port(x)) other = 1;
 	}
 	if (!other) return 0;
+	/* SSH (TcpLayer.cpp:407-410): port 22 on either side builds SSH messages (SSHLayer::createSSHMessage never fails,
+	 * SSHLayer.cpp:18-30) unless the other port is SIP's or BGP's, whose branches (:387-406) come first and take the
+	 * payload */
+	if (sp == 22 || dp == 22) {
+		const uint16_t o = sp == 22 ? dp : sp;
+		if (o != 5060 && o != 5061 && o != 179) return PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN | L7_SSH;
+	}
+	/* MySQL (TcpLayer.cpp:469-478): MySqlLayer's factory never fails (MySqlLayer.cpp:462-470), so port 3306 on either
+	 * side builds it whenever the other port gates no dissector ahead of it in the chain (GTPv2 2123 and Modbus 502
+	 * come after it); the engine builds that layer (L7_MYSQL). With another trigger port the earlier dissector's own
+	 * validity decides, and the packet stays the host's. */
+	if (sp == 3306 || dp == 3306) {
+		const uint16_t o = sp == 3306 ? dp : sp;
+		if (o == 3306 || o == 2123 || o == 502 || !tcp_l7_port(o) || http_port(o) || ssl_port(o))
+			return PCPPX_F_NEEDS_HOST_L7 | PCPPX_F_L7_KNOWN | L7_MYSQL;
+	}
 	/* SIP (TcpLayer.cpp:387-402), BGP (:403-406) and SSH (:407-410) come before DNS and always take the payload;
 	 * DnsOverTcpLayer needs 14 bytes (DnsLayer::isDataValid(.., true), DnsLayer.h:481-485); nothing after DNS
 	 * builds an HTTP, DNS or SSL layer */
@@ -249,7 +268,7 @@ static uint16_t udp_l7(uint32_t n, uint16_t sp, uint16_t dp, int sip)
  * With no parse-until family, a payload classified HTTP / SSL / DNS above (the layer the reference builds is then
  * certain) gets the reference's layers instead of NEEDS_HOST_L7. Each layer's data runs to the end of the L4
  * payload, so the trailer rule is the plain Payload's. */
-enum { P_HTTP_REQ = 6, P_HTTP_RESP = 7, P_DNS = 13, P_SSL = 18 };
+enum { P_HTTP_REQ = 6, P_HTTP_RESP = 7, P_DNS = 13, P_SSL = 18, P_SSH = 35, P_MYSQL = 63 };
 typedef struct {
 	uint8_t proto, osi;
 	uint32_t off, hdr, dlen;
@@ -303,7 +322,11 @@ static uint32_t http_response_line(const uint8_t* d, uint32_t n)
  *         (TextBasedProtocolMessage::parseNextLayer, TextBasedProtocol.cpp:427-434);
  *   SSL:  one SSLLayer per record (SSLLayer::getHeaderLen / parseNextLayer, SSLLayer.cpp:88-106; every record type
  *         has protocol SSL, OSI presentation, SSLLayer.h:246-249) while the rest is another record header;
- *   DNS:  DnsLayer / DnsOverTcpLayer, header = the whole data, no next layer (DnsLayer.h:353-372).
+ *   DNS:  DnsLayer / DnsOverTcpLayer, header = the whole data, no next layer (DnsLayer.h:353-372);
+ *   MySQL: MySqlLayer, header = the whole data, application layer, no next layer (MySqlLayer.h:362-379);
+ *   SSH:  one layer per message (SSHLayer::createSSHMessage / parseNextLayer, SSHLayer.cpp:18-40): an identification
+ *         message ("SSH-" ... '\n', SSHLayer.cpp:46-56) or an encrypted one takes the rest, a handshake message
+ *         (:135-170) its packet length + 4; application layer (SSHLayer.h:107-110).
  * Each layer passes the stop rules of Packet::parsePacket (Packet.cpp:134-155) before it is kept; the first one
  * that fails is rolled back (:168-175) and ends the chain (*stopped). Returns the new count; *last is the last
  * layer kept. */
@@ -344,6 +367,26 @@ static int l7_layers(const uint8_t* pkt, uint32_t off, uint32_t n, uint16_t cls,
 			L.proto = P_SSL; L.osi = 6; L.off = ro; L.hdr = hl; L.dlen = rem;
 			EMIT();
 			if (rem <= hl || !ssl_record(pkt + ro + hl, rem - hl)) break;
+			ro += hl;
+			rem -= hl;
+		}
+	} else if (cls & L7_MYSQL) {
+		L.proto = P_MYSQL; L.hdr = n;
+		EMIT();
+	} else if (cls & L7_SSH) {
+		uint32_t ro = off, rem = n;
+		for (;;) {
+			const uint8_t* m = pkt + ro;
+			uint32_t hl = rem;
+			const int ident = rem >= 5 && memcmp(m, "SSH-", 4) == 0 && m[rem - 1] == '\n';
+			if (!ident && rem >= 6) {
+				const uint32_t ml4 = ((uint32_t)m[0] << 24) | ((uint32_t)m[1] << 16) | ((uint32_t)m[2] << 8) | m[3];
+				if ((uint64_t)ml4 + 4 <= rem && m[4] <= ml4 && (m[5] == 20 || m[5] == 21 || (m[5] >= 30 && m[5] <= 49)))
+					hl = ml4 + 4;
+			}
+			L.proto = P_SSH; L.osi = 7; L.off = ro; L.hdr = hl; L.dlen = rem;
+			EMIT();
+			if (rem <= hl) break;
 			ro += hl;
 			rem -= hl;
 		}
@@ -398,7 +441,7 @@ static uint8_t udp_l7_min_osi(uint16_t sp, uint16_t dp, int sip_content)
 static uint8_t l7_osi(uint16_t cls, uint8_t min_osi)
 {
 	if (cls & PCPPX_F_L7_SSL) return 6;
-	if (cls & (PCPPX_F_L7_HTTP | PCPPX_F_L7_DNS)) return 7;
+	if (cls & (PCPPX_F_L7_HTTP | PCPPX_F_L7_DNS | L7_MYSQL | L7_SSH)) return 7;
 	return min_osi;
 }
 /* the protocols the engine builds itself (ProtocolType.h:42-258), GenericPayload excluded */
@@ -409,7 +452,7 @@ static int engine_proto(uint32_t p)
 	case P_GREV0: case P_GREV1: case P_PPTP: case P_TRAILER: case P_DOT3: case P_LLC: case P_ICMP: return 1;
 	case P_VXLAN: case P_GTPV1: return 1; /* decided exactly at the UDP layer, never a host candidate */
 	/* a classified first L7 layer is built, an unclassified one is none of these */
-	case P_HTTP_REQ: case P_HTTP_RESP: case P_DNS: case P_SSL: return 1;
+	case P_HTTP_REQ: case P_HTTP_RESP: case P_DNS: case P_SSL: case P_MYSQL: case P_SSH: return 1;
 	default: return 0;
 	}
 }
@@ -877,7 +920,7 @@ static void parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t linktype,
 		if (k == K_OUT || k == K_L7) {
 			/* a classified HTTP / SSL / DNS layer: the engine builds it and the layers behind it, each under the
 			 * stop rules */
-			if (k == K_L7 && (kcls & (PCPPX_F_L7_HTTP | PCPPX_F_L7_SSL | PCPPX_F_L7_DNS))) {
+			if (k == K_L7 && (kcls & (PCPPX_F_L7_HTTP | PCPPX_F_L7_SSL | PCPPX_F_L7_DNS | L7_MYSQL | L7_SSH))) {
 				const lay l4l = last;
 				count = l7_layers(pkt, off, len, kcls, &l4l, opts, &found, &stopped_by_rule, layers, cap, count,
 				                  &mask, &last);

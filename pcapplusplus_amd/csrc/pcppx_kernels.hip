@@ -216,6 +216,8 @@ __device__ __forceinline__ bool sip_key(uint32_t k)
 }
 
 // ---- the first L7 layer behind TCP/UDP (restated in oracle/pcppx_oracle.c: tcp_l7 / udp_l7) ----
+// engine-internal class bits of l7_flags (never in a summary's flags: the layers are built): a MySqlLayer, SSH messages
+constexpr uint32_t kL7MySql = 0x4000u, kL7Ssh = 0x8000u;
 // TcpLayer::parseNextLayer (TcpLayer.cpp:372-491) tries HTTP request (dst 80/8080 + known method), HTTP response
 // (src 80/8080 + known version + supported status code), SSL (SSL port + record header), then dissectors gated by
 // their own ports, then Payload: a payload whose only trigger ports are HTTP / SSL ports and that fails those
@@ -343,6 +345,22 @@ __device__ uint32_t l7_flags(const Pkt& p, bool tcp, uint32_t o, uint32_t n, uin
 	// the rest of the chain is gated by ports other than HTTP's and SSL's
 	if (!(port_bit(kL7.tcp_other, sp) | port_bit(kL7.tcp_other, dp)))
 		return 0;
+	// SSH (TcpLayer.cpp:407-410): port 22 on either side builds SSH messages (SSHLayer::createSSHMessage never fails)
+	// unless the other port is SIP's or BGP's, whose branches come first and always take the payload
+	if (sp == 22 || dp == 22)
+	{
+		const uint32_t o = sp == 22 ? dp : sp;
+		if (o != 5060 && o != 5061 && o != 179)
+			return known | kL7Ssh;
+	}
+	// MySQL (TcpLayer.cpp:469-478): MySqlLayer's factory never fails (MySqlLayer.cpp:462-470), so port 3306 on either
+	// side builds it whenever the other port gates no dissector ahead of it (GTPv2 2123 and Modbus 502 come after it)
+	if (sp == 3306 || dp == 3306)
+	{
+		const uint32_t o = sp == 3306 ? dp : sp;
+		if (o == 3306 || o == 2123 || o == 502 || !port_bit(kL7.tcp_other, o))
+			return known | kL7MySql;
+	}
 	// SIP / BGP / SSH (TcpLayer.cpp:387-410) come before DNS over TCP (14 bytes, DnsLayer.h:481-485) and take the
 	// payload; nothing after DNS builds an HTTP, DNS or SSL layer
 	const bool sbs = sp == 5060 || sp == 5061 || sp == 179 || sp == 22 || dp == 5060 || dp == 5061 || dp == 179 || dp == 22;
@@ -352,8 +370,8 @@ __device__ uint32_t l7_flags(const Pkt& p, bool tcp, uint32_t o, uint32_t n, uin
 // ---- the layers of a classified first L7 layer, built on the device (restated in oracle/pcppx_oracle.c:
 // l7_layers): with no parse-until family, an HTTP / SSL / DNS class names the layer the reference builds, and its
 // rules are short length walks. Each layer's data runs to the end of the L4 payload (no effect on the trailer). ----
-constexpr uint32_t P_HTTP_REQ = 6, P_HTTP_RESP = 7, P_DNS = 13, P_SSL = 18;
-constexpr uint32_t kL7Built = PCPPX_F_L7_HTTP | PCPPX_F_L7_SSL | PCPPX_F_L7_DNS;
+constexpr uint32_t P_HTTP_REQ = 6, P_HTTP_RESP = 7, P_DNS = 13, P_SSL = 18, P_SSH = 35, P_MYSQL = 63;
+constexpr uint32_t kL7Built = PCPPX_F_L7_HTTP | PCPPX_F_L7_SSL | PCPPX_F_L7_DNS | kL7MySql | kL7Ssh;
 
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t v)
 {
@@ -444,9 +462,10 @@ __device__ __forceinline__ bool family_has(uint32_t family, uint32_t proto)
 }
 // The layers of a classified L7 payload at [o, o+n) (HTTP: HttpRequestLayer / HttpResponseLayer + a Payload body,
 // HttpLayer.cpp:62-68,666-672,897-920; SSL: one SSLLayer per record, SSLLayer.cpp:88-106; DNS: DnsLayer, header =
-// data, DnsLayer.h:353-372), appended at index `count`, each kept only if it passes the stop rules (Packet.cpp:
-// 134-155; the first that fails is rolled back and ends the chain); stops counting once past cap_layers (every
-// further layer is another SSL record: same mask, same DEPTH_OVERFLOW).
+// data, DnsLayer.h:353-372; MySQL: MySqlLayer, header = data, MySqlLayer.h:362-379; SSH: one message per layer,
+// SSHLayer.cpp:18-40,46-56,135-170), appended at index `count`, each kept only if it passes the stop rules
+// (Packet.cpp:134-155; the first that fails is rolled back and ends the chain); stops counting once past cap_layers
+// (every further layer is another SSL record / SSH message: same mask, same DEPTH_OVERFLOW).
 __device__ uint32_t l7_build(const Pkt& p, uint32_t lf, uint32_t o, uint32_t n, uint32_t dp, uint32_t count, uint32_t ml,
                              uint32_t cap_layers, uint32_t family, uint32_t until_osi, uint32_t& found,
                              uint32_t& stopped, uint64_t& mask, uint2* lay_out)
@@ -490,6 +509,32 @@ __device__ uint32_t l7_build(const Pkt& p, uint32_t lf, uint32_t o, uint32_t n, 
 			uint32_t hl = 5 + ((rb(p, ro + 3) << 8) | rb(p, ro + 4));
 			hl = hl < rem ? hl : rem;
 			if (!emit(P_SSL, 6, ro, hl, rem) || rem <= hl || count > cap_layers || !ssl_record(p, ro + hl, rem - hl))
+				break;
+			ro += hl;
+			rem -= hl;
+		}
+	}
+	else if (lf & kL7MySql)
+		emit(P_MYSQL, 7, o, n, n);
+	else if (lf & kL7Ssh)
+	{
+		// createSSHMessage: an identification message ("SSH-" ... '\n': the rest), else a handshake message (packet
+		// length + 4 within the data, padding <= packet length, a known message code: packet length + 4), else an
+		// encrypted message (the rest); each message's next one follows it (SSHLayer::parseNextLayer)
+		uint32_t ro = o, rem = n;
+		for (;;)
+		{
+			uint32_t hl = rem;
+			const bool ident = rem >= 5 && rb(p, ro) == 'S' && rb(p, ro + 1) == 'S' && rb(p, ro + 2) == 'H' &&
+			                   rb(p, ro + 3) == '-' && rb(p, ro + rem - 1) == '\n';
+			if (!ident && rem >= 6)
+			{
+				const uint32_t ml4 = (rb(p, ro) << 24) | (rb(p, ro + 1) << 16) | (rb(p, ro + 2) << 8) | rb(p, ro + 3);
+				const uint32_t pad = rb(p, ro + 4), code = rb(p, ro + 5);
+				if ((uint64_t)ml4 + 4 <= rem && pad <= ml4 && (code == 20 || code == 21 || (code >= 30 && code <= 49)))
+					hl = ml4 + 4;
+			}
+			if (!emit(P_SSH, 7, ro, hl, rem) || rem <= hl || count > cap_layers)
 				break;
 			ro += hl;
 			rem -= hl;
@@ -3017,7 +3062,7 @@ bool family_engine_only(uint32_t fam)
 		                 b == P_VLAN || b == P_MPLS || b == P_GREV0 || b == P_GREV1 || b == P_PPTP ||
 		                 b == P_TRAILER || b == P_DOT3 || b == P_LLC || b == P_ICMP ||
 		                 // a classified first L7 layer is built, an unclassified one is none of these
-		                 b == P_HTTP_REQ || b == P_HTTP_RESP || b == P_DNS || b == P_SSL;
+		                 b == P_HTTP_REQ || b == P_HTTP_RESP || b == P_DNS || b == P_SSL || b == P_MYSQL || b == P_SSH;
 		if (b != 0 && !own)
 			return false;
 	}

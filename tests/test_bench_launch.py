@@ -102,3 +102,32 @@ def test_bench_small_run_checks_its_records(cfg):
         assert c["flow_table"]["exact"] and c["flow_table"]["conserved"] and c["collect_stats"]["consistent"]
     if cfg == 5:
         assert c["records"] == "summary" and c["layout"] == "packed" and c["window"] == "default"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [4, 3])
+def test_bench_two_ranks_self_launch(cfg):
+    """`bench.py --gpus 2` through its own launch (a child torch.distributed.run, two ranks over gloo sharing the
+    box's one card: a code-path check of the N>1 path, not a scaling number): one line from rank 0 with n_gpus 2 and
+    both ranks' times; config 4 merges the two ranks' flow tables exactly with every packet conserved and sums both
+    ranks' collectStats; the line carries rank 0's CPU baseline (measured after the timed region)."""
+    import json
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--config",
+                        str(cfg), "--packets", "200000", "--steps", "3", "--warmup", "1", "--no-e2e", "--no-traffic",
+                        "--cpu-sample", "20000", "--cpu-seconds", "0.5"],
+                       capture_output=True, text=True, timeout=400, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c = line["config"]
+    assert line["n_gpus"] == 2 and c["ranks"] == 2 and c["dist_backend"] == "gloo"
+    assert len(c["per_rank_kernel_ms"]) == 2 and all(t > 0 for t in c["per_rank_kernel_ms"])
+    assert line["value"] > 0 and c["flagged_packets"] == 0
+    assert line["cpu_baseline"] is not None and line["cpu_baseline"]["value"] > 0
+    if cfg == 4:
+        ft = c["flow_table"]
+        assert ft["ranks_merged"] == 2 and ft["exact"] and ft["conserved"]
+        assert ft["packets_counted"] == ft["expected"] == 2 * 200000 * 4
+        cs = c["collect_stats"]
+        assert cs["consistent"] and cs["ranks_merged"] == 2 and cs["packet_count"] == 2 * 200000

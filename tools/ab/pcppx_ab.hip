@@ -174,7 +174,9 @@ using namespace pcppx;
  * 3 / 4 tile-shaped / grid-stride read of the batch bytes (results written over summary[]); 7 tile-shaped read + the
  * parse's record stores; 29 gather-only diagnostic; 30 / 31 the checksum / parse-only instance marking fast-path
  * packets (flags bit 0x8000); 44 / 52 skip-generic diagnostics; 70 the DEEP checksum instance with the early second
- * stream window; anything else: the product kernel. Records equal the product's for 1, 70 (30 / 31 up to the mark).
+ * stream window; 80 / 81 / 82 parse-only windows of 144 / 128 / 160 B gathered in one round; 83 a 96 + 32-B two-round
+ * parse-only window; anything else: the product kernel. Records equal the product's for 1, 70, 80-83 (30 / 31 up to
+ * the mark).
  * The shape variants measured in rounds 1-3 are in git history (profiles/r0*_ab_*.txt hold their results). */
 PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, void* hip_stream,
                                        int variant)
@@ -226,6 +228,12 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 52: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	// the PCPPX_WINDOW_DEEP checksum instance with the early second stream window (the product's runs it late)
 	case 70: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 9, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	// parse-only windows gathered in ONE round for every packet (no dependent second round): 144 B, 128 B, 160 B
+	case 80: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 9>), grid, dim3(kTile), 0, stream, prm); break;
+	case 81: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 8, false, 8>), grid, dim3(kTile), 0, stream, prm); break;
+	case 82: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, false, 10>), grid, dim3(kTile), 0, stream, prm); break;
+	// two rounds 128 B (96 + 32)
+	case 83: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 8, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	default: return launch_parse(b, o, r, stream);
 	}
 	return check_launch("pcppx_ab_parse_device", stream);

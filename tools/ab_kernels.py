@@ -1,7 +1,8 @@
 """Interleaved A/B timing of kernel variants in one process (cdna guide §5.4 rule 24), through the tools-only
-library tools/ab/libpcppx_ab.so (variant 0 = the product kernel).
+library tools/ab/libpcppx_ab.so (variant 0 = the product kernel). Records of every full variant are checked equal to
+the first listed case with the same record options before timing.
 
-  python tools/ab_kernels.py [packets] [rounds]
+  AB_CASES=po/packed,po/packed-one144 AB_ML=12 python tools/ab_kernels.py [packets] [rounds] [config]
 """
 import sys
 from pathlib import Path
@@ -24,70 +25,35 @@ summ = torch.empty(n * 32, dtype=torch.uint8, device="cuda:0")
 lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device="cuda:0")
 st = torch.cuda.current_stream()
 read_bytes = int(b.caplens.sum(dtype=np.int64)) + 12 * n  # the checksum runs' algorithmic read
+_ml = int(__import__("os").environ.get("AB_ML", "8"))
+PK = abi.LAYOUT_PACKED
 cases = {
-    "tile/ml8/csum": (abi.make_opts(0, 8, True, 8), 0),
-    "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
-    "prev/ml8/csum": (abi.make_opts(0, 8, True, 8), -2),
+    # checksum instances (configs 1 / 3)
+    "tile/product": (abi.make_opts(0, 8, True, 8), 0),
+    "tile/packed": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
     "tile/deepwin": (abi.make_opts(0, 8, True, 8, abi.WINDOW_DEEP), 0),
+    "tile/deepwin-earlyB": (abi.make_opts(0, 8, True, 8, abi.WINDOW_DEEP), 70),
     "tile/skip-generic": (abi.make_opts(0, 8, True, 8), 52),
-    "tile/earlyB": (abi.make_opts(0, 8, True, 8), 54),
-    "tile/earlyB-w4": (abi.make_opts(0, 8, True, 8), 55),
-    "tile/packed": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 0),
-    "tile/packed-earlyB": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 54),
-    "tile/packed-skipgen": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 52),
-    "tile/packed-sf": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 56),
-    "tile/packed-sf-cached": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 57),
-    "tile/packed-sf-w6": (abi.make_opts(0, 8, True, 8, layout=abi.LAYOUT_PACKED), 58),
-    "tile/late-generic": (abi.make_opts(0, 8, True, 8), 53),
-    "tile/chaintails": (abi.make_opts(0, 8, True, 8), 12),
-    "tile/ring": (abi.make_opts(0, 8, True, 8), 40),
-    "tile/ring-win256": (abi.make_opts(0, 8, True, 8), 41),
-    "tile/ring-w6c6": (abi.make_opts(0, 8, True, 8), 42),
-    "tile/ring-c6": (abi.make_opts(0, 8, True, 8), 43),
-    "tile/c6": (abi.make_opts(0, 8, True, 8), 45),
-    "tile/c6w6": (abi.make_opts(0, 8, True, 8), 46),
-    "tile/c7r6": (abi.make_opts(0, 8, True, 8), 47),
-    "tile/c6w6win64": (abi.make_opts(0, 8, True, 8), 48),
-    "tile/c6win64": (abi.make_opts(0, 8, True, 8), 49),
     "lane/ml8/csum": (abi.make_opts(0, 8, True, 8), 1),
-    "tile/ml0/csum": (abi.make_opts(0, 8, True, 0), 0),
-    "tile/ml8/nocsum": (abi.make_opts(0, 8, False, 8), 0),
-    "tile/w5win256": (abi.make_opts(0, 8, True, 8), 5),
-    "tile/w4win128": (abi.make_opts(0, 8, True, 8), 6),
-    "tile/w4win256": (abi.make_opts(0, 8, True, 8), 8),
-    "tile/cached": (abi.make_opts(0, 8, True, 8), 11),
+    "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
     "tile/stream-only": (abi.make_opts(0, 8, True, 0), 2),
     "diag/tile-read": (abi.make_opts(0, 8, True, 0), 3),
     "diag/grid-read": (abi.make_opts(0, 8, True, 0), 4),
     "diag/tile-rw": (abi.make_opts(0, 8, True, 16), 7),
-}
-# parse-only instances (checksums off): LDS window chunks / first-round chunks; records per packet AB_ML
-_ml = int(__import__("os").environ.get("AB_ML", "8"))
-cases.update({
+    # parse-only instances (checksums off; configs 2 / 4 / 5): records per packet AB_ML
     "po/product": (abi.make_opts(0, 8, False, _ml), 0),
-    "po/packed": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 0),
-    "po/w7": (abi.make_opts(0, 8, False, _ml), 20),
-    "po/w10": (abi.make_opts(0, 8, False, _ml), 21),
-    "po/w10r6": (abi.make_opts(0, 8, False, _ml), 22),
-    "po/w9r6": (abi.make_opts(0, 8, False, _ml), 23),
-    "po/w10r5": (abi.make_opts(0, 8, False, _ml), 24),
-    "po/w7r5": (abi.make_opts(0, 8, False, _ml), 25),
-    "po/r01": (abi.make_opts(0, 8, False, _ml), -1),
-    "po/prev": (abi.make_opts(0, 8, False, _ml), -2),
-    "po/r2full": (abi.make_opts(0, 8, False, _ml), 50),
-    "po/norealign": (abi.make_opts(0, 8, False, _ml), 51),
-    "po/c6w5": (abi.make_opts(0, 8, False, _ml), 45),  # the checksum instance's single 96-B window, 5 waves/SIMD
-    "po/chaintails": (abi.make_opts(0, 8, False, _ml), 26),
-    "po/w9r5": (abi.make_opts(0, 8, False, _ml), 27),
-    "po/w9r5chain": (abi.make_opts(0, 8, False, _ml), 28),
-    "po/c6": (abi.make_opts(0, 8, False, _ml), 60),
-    "po/packed-cached": (abi.make_opts(0, 8, False, _ml, layout=abi.LAYOUT_PACKED), 68),
-    "po/c6-cached": (abi.make_opts(0, 8, False, _ml), 69),
-    "po/c6w6": (abi.make_opts(0, 8, False, _ml), 61),
-    "po/c5w6": (abi.make_opts(0, 8, False, _ml), 63),
+    "po/packed": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),
+    "po/short": (abi.make_opts(0, 8, False, _ml, abi.WINDOW_SHORT), 0),
+    "po/packed-short": (abi.make_opts(0, 8, False, _ml, abi.WINDOW_SHORT, PK), 0),
+    "po/one144": (abi.make_opts(0, 8, False, _ml), 80),
+    "po/packed-one144": (abi.make_opts(0, 8, False, _ml, layout=PK), 80),
+    "po/packed-one128": (abi.make_opts(0, 8, False, _ml, layout=PK), 81),
+    "po/packed-one160": (abi.make_opts(0, 8, False, _ml, layout=PK), 82),
+    "po/packed-w8r6": (abi.make_opts(0, 8, False, _ml, layout=PK), 83),
     "po/gather-only": (abi.make_opts(0, 8, False, _ml), 29),
+    "po/packed-gather-only": (abi.make_opts(0, 8, False, _ml, layout=PK), 29),
     "po/skip-generic": (abi.make_opts(0, 8, False, _ml), 44),
-})
+}
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")
 if only:
@@ -98,7 +64,7 @@ want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
     first = next(iter(cases.values()))[0]
     if o.max_layers != first.max_layers or o.want_checksums != want_csum_ref or o.layout != first.layout or \
-            v in (2, 3, 4, 7, 29, 44, 52, -2):  # diagnostics with wrong records; -2: L7 records of an older contract
+            v in (2, 3, 4, 7, 29, 44, 52):  # diagnostics with wrong records
         continue
     summ.zero_()
     lay.zero_()
