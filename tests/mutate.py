@@ -333,9 +333,20 @@ def crafted_l7(seed: int = 13) -> list[bytes]:
                bytes([23, 3, 3, 0, 40]) + b"e" * 10, bytes([21, 3, 3, 0, 2, 1, 0]) * 12,
                bytes([23, 3, 4, 0, 1, 7]) * 30, bytes([22, 3, 3, 0, 4, 1, 0, 0, 0, 22, 0x7f, 0x10, 0, 1, 1, 22, 3, 6, 0, 1, 1]),
                b"\x12\x34\x01\x00\x00\x01\x00\x00\x00\x00\x00\x00\x03www\x01a\x00\x00\x01\x00\x01",
-               b"\x00\x1d\x12\x34\x01\x00\x00\x01\x00\x00\x00\x00\x00\x00\x03www\x01a\x00\x00\x01\x00\x01"]
+               b"\x00\x1d\x12\x34\x01\x00\x00\x01\x00\x00\x00\x00\x00\x00\x03www\x01a\x00\x00\x01\x00\x01",
+               # SSH messages (SSHLayer.cpp:18-56,135-170): identification, handshake chains, encrypted fall-backs
+               b"SSH-2.0-OpenSSH_8.9\r\n", b"SSH-2.0-x", b"SSH-\n", b"SSH\n", b"SSH-1.99-a\n" + b"z" * 200,
+               struct.pack(">IBB", 12, 4, 20) + b"k" * 10, struct.pack(">IBB", 6, 2, 21) + b"ab" + struct.pack(">IBB", 2, 0, 30),
+               struct.pack(">IBB", 6, 2, 31) + b"ab" + b"\x99" * 33, struct.pack(">IBB", 60, 4, 20) + b"k" * 10,
+               struct.pack(">IBB", 8, 9, 20) + b"k" * 6, struct.pack(">IBB", 8, 2, 50) + b"k" * 6,
+               struct.pack(">IBB", 8, 2, 49) + b"k" * 6 + struct.pack(">IBB", 0, 0, 20),
+               struct.pack(">IBB", 0xFFFFFFFC, 2, 20) + b"k" * 6, (struct.pack(">IBB", 2, 0, 21)) * 25,
+               # MySQL (MySqlLayer.cpp:200-340: the layer is the whole payload whatever its messages)
+               b"\x05\x00\x00\x00\x03SELECT 1", b"\x07\x00\x00\x01\x00\x00\x00\x02\x00\x00\x00", b"\x01"]
     tcp_ports = [(40000, 80), (80, 40000), (8080, 8080), (443, 40000), (40000, 993), (80, 443), (53, 40000),
-                 (40000, 5353), (22, 80), (443, 179), (5060, 80), (102, 443), (21, 8080), (40000, 40001), (2123, 53)]
+                 (40000, 5353), (22, 80), (443, 179), (5060, 80), (102, 443), (21, 8080), (40000, 40001), (2123, 53),
+                 (22, 40000), (40000, 22), (22, 5060), (179, 22), (22, 3306), (3306, 40000), (40000, 3306), (3306, 53),
+                 (3306, 2123), (502, 3306), (3306, 3306), (5432, 3306), (3306, 443), (23, 3306)]
     udp_ports = [(40000, 53), (53, 40000), (5355, 5355), (68, 67), (67, 53), (40000, 4789), (2152, 53), (53, 2123),
                  (40000, 5060), (40000, 40001), (123, 53), (40000, 9)]
     pk = []
