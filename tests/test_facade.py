@@ -257,9 +257,17 @@ def test_gpu_host_completion_every_golden_record(built, tmp_path):
         pytest.skip("reference library not built")
     from conftest import golden_files
 
+    from pcapplusplus_amd.engine import PcapReader
+
     checked = completed = 0
     for path in golden_files():
         b, variants = load_golden(path)
+        f = tmp_path / "lt.pcap"
+        write_pcap(f, b.slice(0, 1))
+        with PcapReader(f) as r:
+            lt = r.linktype
+        if lt != b.linktype:
+            continue  # a link-type value no capture file carries through the readers (the reference's map it to invalid)
         for v, (opts, rs, rl) in variants.items():
             if v not in GOLDEN_PLAN:
                 continue
