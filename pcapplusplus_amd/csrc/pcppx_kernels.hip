@@ -2549,8 +2549,10 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 }
 
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
+// kPeel: before the LDS inserts of a round, the wave's lanes holding the key of its first live lane are combined into that
+// lane (one CAS + one add for the wave's most frequent Zipf keys instead of one per lane), kPeel keys per round.
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false>
+          bool kPart = false, bool kDense = false, uint32_t kPeel = 0>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -2597,16 +2599,40 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		for (uint32_t r = 0; r < kR; ++r)
 		{
 			const uint64_t i = base + r * kFB + t;
-			if (kPrefetch ? !((pvalid >> r) & 1u) : i >= n)
-				break;
-			const uint32_t key = kPrefetch ? pkey[r] : (kDense ? dkeys[i] : sum[i].hash5);
-			const uint32_t len = kPrefetch ? plen[r] : caplens[i];
-			if (key == 0)
+			const bool valid = kPrefetch ? ((pvalid >> r) & 1u) != 0 : i < n;
+			const uint32_t key = !valid ? 0u : (kPrefetch ? pkey[r] : (kDense ? dkeys[i] : sum[i].hash5));
+			const uint32_t len = !valid ? 0u : (kPrefetch ? plen[r] : caplens[i]);
+			if (valid && key == 0)  // flow key 0 (PacketUtils.cpp:141-148): counted, not tabled
 			{
 				z_pk += 1;
 				z_by += len;
-				continue;
 			}
+			bool todo = valid && key != 0;
+			unsigned long long add = (1ull << 40) | len;
+			if constexpr (kPeel > 0)
+			{
+				// every lane of the wave takes part (no lane has left the round): the lanes holding the key of the first
+				// lane still to insert hand their packets and bytes to it, kPeel keys per round
+#pragma unroll
+				for (uint32_t pk = 0; pk < kPeel; ++pk)
+				{
+					const uint64_t act = __ballot(todo);
+					if (act == 0)
+						break;
+					const int lead = __ffsll((unsigned long long)act) - 1;
+					const uint32_t k0 = (uint32_t)__shfl((int)key, lead, 64);
+					const bool same = todo && key == k0;
+					if (__popcll(__ballot(same)) < 2)
+						break;
+					const unsigned long long tot = wave_sum_u64(same ? add : 0ull);
+					if ((int)(threadIdx.x & 63) == lead)
+						add = tot;  // the leader inserts every matched lane's packets and bytes
+					else if (same)
+						todo = false;
+				}
+			}
+			if (!todo)
+				continue;
 			static_assert(kFlowBatch < kFlowLds && kFlowBatch % kFB == 0 && (kFlowLds & (kFlowLds - 1)) == 0, "flow shape");
 			uint32_t slot = (key * 0x9E3779B1u) >> (32 - log2u(kFlowLds));  // top bits
 			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
@@ -2614,7 +2640,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				const uint32_t prev = atomicCAS(&s_key[slot], 0u, key);
 				if (prev == 0u || prev == key)
 				{
-					atomicAdd(&s_cnt[slot], (1ull << 40) | len);
+					atomicAdd(&s_cnt[slot], add);
 					break;
 				}
 				slot = (slot + 1) & (kFlowLds - 1);
