@@ -10,7 +10,7 @@
 #   prof:<cfgs>                    the bench line under rocprofv3 --kernel-trace, plus the timed-launch-only summary
 #                                  (tools/timed_stats.py) -> <tag>_prof_cfg<c>/, <tag>_kernel_stats_cfg<c>.csv
 #   traffic:<cfgs>                 PMC FETCH/WRITE passes -> <tag>_traffic_cfg<c>.json (tools/measure_traffic.sh)
-#   sq:<cfg>                       SQ issue counters (tools/sq_counters.sh)
+#   sq:<cfg>                       SQ issue counters (tools/sq_counters.sh); sqlds:<cfg> the LDS-wait / bank-conflict set
 #   cmd:<shell command>            anything else, under a 600 s limit
 set -o pipefail
 TAG=$1
@@ -69,6 +69,9 @@ for step in "$@"; do
       done ;;
     sq)
       tools/sq_counters.sh "$TAG" "$arg" || exit 7 ;;
+    sqlds)  # LDS / memory-wait counters (the flow-table kernels)
+      SQ_COUNTERS="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD" \
+        tools/sq_counters.sh "${TAG}lds" "$arg" || exit 7 ;;
     cmd)
       timeout -k 10 600 bash -c "$arg" || exit 8 ;;
     *)
