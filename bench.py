@@ -513,6 +513,10 @@ def main() -> None:
                 "traffic_source": traffic_note,
                 "algorithmic_read_bytes": read_bytes,
                 "record_write_bytes": write_bytes,
+                # the kernel also writes its records: algorithmic read + record bytes over the same launch time (the
+                # kernel's total algorithmic traffic against the same peak; `frac` above is the read side alone)
+                "rw_achieved": round((read_bytes + write_bytes) / (kern_ms * 1e-3) / 1e9, 1),
+                "rw_frac": round((read_bytes + write_bytes) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             },
             "cpu_baseline": cpu,
         }
