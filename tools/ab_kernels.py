@@ -58,6 +58,23 @@ import os  # noqa: E402
 only = os.environ.get("AB_CASES")
 if only:
     cases = {k: v for k, v in cases.items() if k in only.split(",")}
+
+
+def layer_records(o, s, l):
+    """The layer records a launch defines: FIXED, the whole n x max_layers array; PACKED, each tile's run of entries
+    (entries past a tile's run are not written, and a generic-walk lane's fixed-slot scratch may lie there)."""
+    ml = o.max_layers
+    if o.layout != PK:
+        return l[: n * 8 * ml]
+    nl = s.view(n, 32)[:, 14].to(torch.int64).clamp(max=ml)
+    tiles = (n + 63) // 64
+    cnt = torch.zeros(tiles * 64, dtype=torch.int64, device=s.device)
+    cnt[:n] = nl
+    tot = cnt.view(tiles, 64).sum(1)
+    idx = torch.arange(n * ml, device=s.device)
+    return l[: n * 8 * ml].view(torch.int64)[(idx % (64 * ml)) < tot[idx // (64 * ml)]]
+
+
 # records of every full variant must equal the first listed variant's (same checksum mode), byte for byte
 ref_s = ref_l = None
 want_csum_ref = next(iter(cases.values()))[0].want_checksums
@@ -71,9 +88,9 @@ for name, (o, v) in cases.items():
     ab.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream, v)
     torch.cuda.synchronize()
     if ref_s is None:
-        ref_s, ref_l = summ.clone(), lay[: n * 8 * o.max_layers].clone()
+        ref_s, ref_l = summ.clone(), layer_records(o, summ, lay).clone()
     else:
-        same = torch.equal(summ, ref_s) and torch.equal(lay[: n * 8 * o.max_layers], ref_l)
+        same = torch.equal(summ, ref_s) and torch.equal(layer_records(o, summ, lay), ref_l)
         print(f"{name:18s} records identical to first variant: {same}", flush=True)
         if not same:
             raise SystemExit(f"{name}: records differ")

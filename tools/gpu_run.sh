@@ -11,6 +11,7 @@
 #                                  (tools/timed_stats.py) -> <tag>_prof_cfg<c>/, <tag>_kernel_stats_cfg<c>.csv
 #   traffic:<cfgs>                 PMC FETCH/WRITE passes -> <tag>_traffic_cfg<c>.json (tools/measure_traffic.sh)
 #   sq:<cfg>                       SQ issue counters (tools/sq_counters.sh); sqlds:<cfg> the LDS-wait / bank-conflict set
+#   sqab:<cases>                   SQ issue counters of tools/ab_kernels.py cases on config 5 -> <tag>_sqab/
 #   cmd:<shell command>            anything else, under a 600 s limit
 set -o pipefail
 TAG=$1
@@ -24,6 +25,7 @@ cfgargs() {  # "3s512" -> --config 3 --sizes 512
     *) echo "--config $1" ;;
   esac
 }
+SQ_DEFAULT="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD"
 tr() { [ -f "$ROOT/$OUT/${TAG}_traffic_cfg$1.json" ] && echo "--traffic $ROOT/$OUT/${TAG}_traffic_cfg$1.json"; }
 for step in "$@"; do
   name=${step%%:*}
@@ -72,6 +74,12 @@ for step in "$@"; do
     sqlds)  # LDS / memory-wait counters (the flow-table kernels)
       SQ_COUNTERS="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD" \
         tools/sq_counters.sh "${TAG}lds" "$arg" || exit 7 ;;
+    sqab)  # SQ issue counters of tools/ab_kernels.py cases (AB_CASES comma list) on config 5, one rocprofv3 --pmc pass
+      mkdir -p "$OUT/${TAG}_sqab"
+      (cd /tmp && AB_CASES="$arg" AB_ML=12 timeout -s KILL 240 rocprofv3 --pmc $SQ_DEFAULT -d "$ROOT/$OUT/${TAG}_sqab" -o p \
+        --output-format csv -- python3 "$ROOT/tools/ab_kernels.py" 10000000 2 5 > "$ROOT/$OUT/${TAG}_sqab/ab.txt" \
+        2> "$ROOT/$OUT/${TAG}_sqab/err.log") || { tail -20 "$OUT/${TAG}_sqab/err.log"; exit 7; }
+      python3 tools/pmc_summary.py "$OUT/${TAG}_sqab" | tee "$OUT/${TAG}_sqab/summary.txt" ;;
     cmd)
       timeout -k 10 600 bash -c "$arg" || exit 8 ;;
     *)
