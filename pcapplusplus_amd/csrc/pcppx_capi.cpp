@@ -69,10 +69,10 @@ public:
 		m_quit = false;
 	}
 
-	// one part per >= 4 MiB, at most kThreads parts
+	// one part per >= 1 MiB, at most kThreads parts
 	void copy(void* dst, const void* src, size_t bytes)
 	{
-		unsigned parts = (unsigned)(bytes >> 22);
+		unsigned parts = (unsigned)(bytes >> 20);
 		parts = parts < 1 ? 1 : (parts > kThreads ? kThreads : parts);
 		if (parts == 1 || m_threads.empty())
 		{

@@ -524,7 +524,10 @@ extern "C"
 			close(fd);
 			return PCPPX_E_INVAL;
 		}
-		void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+		// a small capture is mapped populated (one kernel call instead of a page fault per 4 KiB on the first walk)
+		constexpr off_t kPopulateMax = 64 << 20;
+		void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | (st.st_size <= kPopulateMax ? MAP_POPULATE : 0),
+		               fd, 0);
 		close(fd);
 		if (m == MAP_FAILED)
 			return PCPPX_E_NOMEM;

@@ -9,9 +9,14 @@
  *       list of variants, applied to packet i in turn: full | tcp | ip | osi2 | osi3 | osi4 | own | copy | free);
  *       writes per packet and variant the pcppx_summary (32 B) and the PCPPX_MAX_LAYERS layer records the Packet
  *       holds (zero past its chain).  (GPU.)
+ *   facade_check time <capture> <reps>
+ *       the phases of the reference benchmark's packet loop (open, first getNextPacket, first Packet(&raw, TCP), the
+ *       rest of the loop, close), averaged over reps after one untimed run; one JSON line, microseconds.  (GPU.)
  *   env PCPPX_CHECK_HOST_PARSER=<lib.so>: register that library's pcppx_host_parse with setHostParser.
  */
 #include <dlfcn.h>
+
+#include <chrono>
 
 #include <cstdio>
 #include <cstdlib>
@@ -175,6 +180,56 @@ int parseMode(const char* capture, const char* outfile, const std::string& plan)
 	std::fclose(f);
 	return 0;
 }
+int timeMode(const char* capture, int reps)
+{
+	using clk = std::chrono::steady_clock;
+	double acc[5] = { 0, 0, 0, 0, 0 };
+	size_t packets = 0;
+	for (int r = 0; r <= reps; ++r)
+	{
+		const auto t0 = clk::now();
+		pcppx::PcapFileReaderDevice reader(capture);
+		if (!reader.open())
+			return 4;
+		const auto t1 = clk::now();
+		pcppx::RawPacket raw;
+		size_t n = 0, tcp = 0;
+		auto t2 = t1, t3 = t1;
+		if (reader.getNextPacket(raw))
+		{
+			t2 = clk::now();
+			{
+				pcppx::Packet p(&raw, pcppx::TCP);
+				tcp += p.isPacketOfType(pcppx::TCP) ? 1 : 0;
+			}
+			t3 = clk::now();
+			++n;
+			while (reader.getNextPacket(raw))
+			{
+				pcppx::Packet p(&raw, pcppx::TCP);
+				tcp += p.isPacketOfType(pcppx::TCP) ? 1 : 0;
+				++n;
+			}
+		}
+		const auto t4 = clk::now();
+		reader.close();
+		const auto t5 = clk::now();
+		if (r == 0)
+			continue;  // untimed: HIP initialisation, pinned pools
+		packets = n;
+		const double d[5] = { std::chrono::duration<double, std::micro>(t1 - t0).count(),
+			                  std::chrono::duration<double, std::micro>(t2 - t1).count(),
+			                  std::chrono::duration<double, std::micro>(t3 - t2).count(),
+			                  std::chrono::duration<double, std::micro>(t4 - t3).count(),
+			                  std::chrono::duration<double, std::micro>(t5 - t4).count() };
+		for (int k = 0; k < 5; ++k)
+			acc[k] += d[k];
+	}
+	std::printf("{\"packets\": %zu, \"reps\": %d, \"open_us\": %.1f, \"first_packet_us\": %.1f, \"first_parse_us\": %.1f, "
+	            "\"loop_us\": %.1f, \"close_us\": %.1f}\n",
+	            packets, reps, acc[0] / reps, acc[1] / reps, acc[2] / reps, acc[3] / reps, acc[4] / reps);
+	return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv)
@@ -191,6 +246,8 @@ int main(int argc, char** argv)
 		}
 		if (argc >= 4 && std::string(argv[1]) == "read")
 			return readMode(argv[2], argv[3], argc - 4, argv + 4);
+		if (argc == 4 && std::string(argv[1]) == "time")
+			return timeMode(argv[2], std::atoi(argv[3]));
 		if (argc == 5 && std::string(argv[1]) == "parse")
 			return parseMode(argv[2], argv[3], argv[4]);
 	}
