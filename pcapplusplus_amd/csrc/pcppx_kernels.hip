@@ -2549,13 +2549,8 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 }
 
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
-// kPeel: before the LDS inserts of a round, the wave's lanes holding the key of its first live lane are combined into that
-// lane (one CAS + one add for the wave's most frequent Zipf keys instead of one per lane), kPeel keys per round.
-// kHotKeys: up to kHotKeys keys that hold at least kFlowBatch / 128 packets of the block's first batch (a Zipf head: the
-// same flows in every block) are counted from then on in per-lane registers -- a compare per key instead of LDS atomics
-// that all lanes of a wave would aim at one slot -- and queued once per block at the end.
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false, uint32_t kPeel = 0, uint32_t kHotKeys = 0>
+          bool kPart = false, bool kDense = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -2567,14 +2562,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
 	__shared__ uint32_t s_kept;
-	constexpr uint32_t kHK = kHotKeys > 0 ? kHotKeys : 1;
-	__shared__ uint32_t s_hot[kHK], s_nhot;
-	__shared__ unsigned long long s_hsum[kHK];
-	static_assert(kHotKeys == 0 || kPart, "register-counted hot keys are queued: partitioned flush only");
-	uint32_t hk[kHK], hp[kHK], hb[kHK];  // hot keys (0: none; no counted key is 0), their packets and bytes in this lane
-#pragma unroll
-	for (uint32_t h = 0; h < kHK; ++h)
-		hk[h] = hp[h] = hb[h] = 0;
 	const uint32_t t = threadIdx.x;
 	const uint32_t m = capacity - 1;
 	unsigned long long z_pk = 0, z_by = 0, lost = 0;  // flow key 0 (PacketUtils.cpp:141-148); table full
@@ -2586,10 +2573,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	if (kPart)
 		for (uint32_t j = t; j < kFlowMaxParts; j += kFB)
 			s_bin[j] = 0;
-	if (t < kHK)
-		s_hsum[t] = 0;
-	if (t == 0)
-		s_nhot = 0;
 	__syncthreads();
 	// kPrefetch: the next batch's keys and lengths are loaded into registers before this batch's flush,
 	// so their latency overlaps the flush's HBM reads and atomics
@@ -2622,43 +2605,9 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				z_pk += 1;
 				z_by += len;
 			}
-			bool todo = valid && key != 0;
-			unsigned long long add = (1ull << 40) | len;
-			if constexpr (kHotKeys > 0)
-			{
-#pragma unroll
-				for (uint32_t h = 0; h < kHotKeys; ++h)
-				{
-					const bool m = todo && key == hk[h];
-					hp[h] += m ? 1u : 0u;
-					hb[h] += m ? len : 0u;
-					todo = todo && !m;
-				}
-			}
-			if constexpr (kPeel > 0)
-			{
-				// every lane of the wave takes part (no lane has left the round): the lanes holding the key of the first
-				// lane still to insert hand their packets and bytes to it, kPeel keys per round
-#pragma unroll
-				for (uint32_t pk = 0; pk < kPeel; ++pk)
-				{
-					const uint64_t act = __ballot(todo);
-					if (act == 0)
-						break;
-					const int lead = __ffsll((unsigned long long)act) - 1;
-					const uint32_t k0 = (uint32_t)__shfl((int)key, lead, 64);
-					const bool same = todo && key == k0;
-					if (__popcll(__ballot(same)) < 2)
-						break;
-					const unsigned long long tot = wave_sum_u64(same ? add : 0ull);
-					if ((int)(threadIdx.x & 63) == lead)
-						add = tot;  // the leader inserts every matched lane's packets and bytes
-					else if (same)
-						todo = false;
-				}
-			}
-			if (!todo)
+			if (!valid || key == 0)
 				continue;
+			const unsigned long long add = (1ull << 40) | len;
 			static_assert(kFlowBatch < kFlowLds && kFlowBatch % kFB == 0 && (kFlowLds & (kFlowLds - 1)) == 0, "flow shape");
 			uint32_t slot = (key * 0x9E3779B1u) >> (32 - log2u(kFlowLds));  // top bits
 			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
@@ -2683,31 +2632,14 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		// block meets the top Zipf flows in every batch, and same-address atomics serialise. They are
 		// kept only while they fill at most half of the table, so the next batch always fits.
 		const bool last = base + (uint64_t)gridDim.x * kFlowBatch >= n;  // uniform
-		const bool first = base == (uint64_t)blockIdx.x * kFlowBatch;    // uniform
 		constexpr uint32_t kPer = kFlowLds / kFB;
 		uint32_t hot = 0;
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
-		{
-			const unsigned long long c = s_cnt[u * kFB + t] >> 40;
-			hot |= (c > kHot ? 1u : 0u) << u;
-			if (kHotKeys > 0 && first && !last && c >= kFlowBatch / 128)
-			{
-				const uint32_t h = atomicAdd(&s_nhot, 1u);
-				if (h < kHotKeys)
-					s_hot[h] = s_key[u * kFB + t];
-			}
-		}
+			hot |= ((s_cnt[u * kFB + t] >> 40) > kHot ? 1u : 0u) << u;
 		if (!last && hot)
 			atomicAdd(&s_kept, (uint32_t)__popc(hot));
 		__syncthreads();
-		if (kHotKeys > 0 && first)  // uniform: the block's hot set, fixed from here on
-		{
-			const uint32_t nh = s_nhot < kHotKeys ? s_nhot : kHotKeys;
-#pragma unroll
-			for (uint32_t h = 0; h < kHK; ++h)
-				hk[h] = h < nh ? s_hot[h] : 0u;
-		}
 		const bool keep_hot = !last && s_kept <= kFlowLds / 2 - kFlowBatch / 2;  // uniform
 		uint32_t fk[kPer], fs[kPer], fseen[kPer];
 		if constexpr (kPart)
@@ -2786,29 +2718,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 			s_cnt[j] = 0;
 		}
 		__syncthreads();
-	}
-	if constexpr (kHotKeys > 0)
-	{
-		// the register counts of the hot keys: wave sums -> LDS -> one queue record per key that counted a packet
-#pragma unroll
-		for (uint32_t h = 0; h < kHotKeys; ++h)
-		{
-			const unsigned long long tot = wave_sum_u64(((unsigned long long)hp[h] << 40) | hb[h]);
-			if ((t & 63) == 0 && tot)
-				atomicAdd(&s_hsum[h], tot);
-		}
-		__syncthreads();
-		const uint32_t nh = s_nhot < kHotKeys ? s_nhot : kHotKeys;
-		if (t < nh && s_hsum[t])
-		{
-			const uint32_t key = s_hot[t], part = flow_part(key, fpart.log2p);
-			const unsigned long long c = s_hsum[t];
-			const uint32_t pos = atomicAdd(&fpart.fill[part], 1u);
-			if (pos < fpart.rec_cap)
-				fpart.recs[(size_t)part * fpart.rec_cap + pos] = make_uint4(key, 0u, (uint32_t)c, (uint32_t)(c >> 32));
-			else if (!flow_region_add_atomic(keys, packets, bytes, fpart, key, c >> 40, c & ((1ull << 40) - 1)))
-				lost += c >> 40;
-		}
 	}
 	z_pk = wave_sum_u64(z_pk);
 	z_by = wave_sum_u64(z_by);

@@ -264,12 +264,6 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 1: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true, true, true>, 512, 2048, 768); break;
 	case 2: go(flow_count_kernel<256, 2048, 1024, kFlowHot, true, true, true>, 256, 1024, 1536); break;
 	case 3: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 512); break;
-	case 8: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, 1>, 1024, 4096, 256); break;  // peel 1 key
-	case 9: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, 2>, 1024, 4096, 256); break;  // peel 2 keys
-	case 10: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, 4>, 1024, 4096, 256); break;  // peel 4
-	case 11: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, 0, 8>, 1024, 4096, 256); break;  // 8 hot keys in registers
-	case 12: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, 0, 16>, 1024, 4096, 256); break;  // 16 hot keys
-	case 13: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, 1, 8>, 1024, 4096, 256); break;  // 8 hot + peel 1
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);

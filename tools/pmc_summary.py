@@ -15,9 +15,9 @@ def short(kn: str) -> str:
     for x in ("parse_tile_kernel", "parse_lane_kernel", "diag_tile_read", "diag_grid_read", "flow_count_kernel",
               "flow_merge_kernel", "proto_stats_reduce_kernel"):
         if x in kn:
+            kn = re.sub(r"pcppx::\(anonymous namespace\)::", "", kn)
             m = re.search(re.escape(x) + r"<([^()]*)>", kn)
             args = m.group(1) if m else ""
-            args = re.sub(r"pcppx::\(anonymous namespace\)::", "", args)
             return f"{x}<{args}>" if args else x
     return kn[:40]
 
