@@ -2753,7 +2753,8 @@ __global__ __launch_bounds__(kBlock) void flow_unpack_kernel(unsigned long long*
 // thread per round; flushed whenever more than half full), then adds each distinct key's counts into its own table
 // region -- which no other block touches, so the counts take plain loads and stores (a CAS only claims a new key's
 // slot against the block's other threads). Resets the queue length for the next launch.
-template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT>
+// kAhead: rounds of queue records in flight ahead of the round being inserted.
+template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT, uint32_t kAhead = 1>
 __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* keys, unsigned long long* packets,
                                                          unsigned long long* bytes, unsigned long long* stats)
 {
@@ -2774,24 +2775,32 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 		s_used = 0;
 	__syncthreads();
 	unsigned long long lost = 0;
-	// the next round's records are loaded before this round's inserts (their latency hides behind them)
-	uint4 nxt[kPerT];
-	auto fetch = [&](uint32_t base) {
+	// the next kAhead rounds' records are loaded before this round's inserts (their latency hides behind them)
+	static_assert(kAhead >= 1, "merge lookahead");
+	uint4 nxt[kAhead][kPerT];
+	auto fetch = [&](uint4 (&v)[kPerT], uint32_t base) {
 #pragma unroll
 		for (uint32_t k = 0; k < kPerT; ++k)
 		{
 			const uint32_t idx = base + k * kMB + t;
-			nxt[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
+			v[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
 		}
 	};
-	fetch(0);
+#pragma unroll
+	for (uint32_t a = 0; a < kAhead; ++a)
+		fetch(nxt[a], a * kMB * kPerT);
 	for (uint32_t base = 0; base < cnt; base += kMB * kPerT)
 	{
 		uint4 rec[kPerT];
 #pragma unroll
 		for (uint32_t k = 0; k < kPerT; ++k)
-			rec[k] = nxt[k];
-		fetch(base + kMB * kPerT);
+			rec[k] = nxt[0][k];
+#pragma unroll
+		for (uint32_t a = 0; a + 1 < kAhead; ++a)
+#pragma unroll
+			for (uint32_t k = 0; k < kPerT; ++k)
+				nxt[a][k] = nxt[a + 1][k];
+		fetch(nxt[kAhead - 1], base + kAhead * kMB * kPerT);
 #pragma unroll
 		for (uint32_t k = 0; k < kPerT; ++k)
 		{
