@@ -344,10 +344,10 @@ uint32_t contiguous_chunk(const pcppx_batch* b, uint32_t i, uint64_t* base, size
 constexpr uint32_t kMinRun = 4096;  // a shorter run that stops at a discontinuity is gathered per packet instead
 
 // gather packets [i, j) of a host batch into the slot's pinned staging, rebasing offsets; returns j.
-// Contiguous runs are staged with one multi-threaded copy, or not at all when the caller's bytes are
-// already pinned (*direct is then the source of the H2D copy).
-uint32_t stage_chunk(CopyPool& cp, Slot& s, const pcppx_batch* b, uint32_t i, size_t* pos_out, const uint8_t** direct,
-                     bool pinned_in)
+// Contiguous runs are not staged: *direct is then the source of the H2D copy, page-locked or not (the runtime DMAs a
+// pageable range as fast as a page-locked one, 56 GB/s from a file map, profiles/r04f_h2d_probe.txt, where a copy
+// into staging first ran at 30 GB/s per thread); scattered packets are gathered into the staging.
+uint32_t stage_chunk(Slot& s, const pcppx_batch* b, uint32_t i, size_t* pos_out, const uint8_t** direct)
 {
 	*direct = nullptr;
 	{
@@ -361,10 +361,7 @@ uint32_t stage_chunk(CopyPool& cp, Slot& s, const pcppx_batch* b, uint32_t i, si
 				s.h_off[k - i] = b->offsets[k] - base;
 				s.h_cap[k - i] = b->caplens[k];
 			}
-			if (pinned_in)
-				*direct = b->data + base;
-			else
-				cp.copy(s.h_data, b->data + base, bytes);
+			*direct = b->data + base;
 			*pos_out = bytes;
 			return j;
 		}
@@ -448,7 +445,6 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 {
 	int rc = PCPPX_OK;
 	const uint32_t ml = o->max_layers;
-	const bool pinned_in = is_pinned(b->data);
 	// a NIC ring / pcppx_host_alloc result buffer: records come back by DMA straight into the caller's arrays
 	const bool direct_out = is_pinned(r->summary) && (ml == 0 || r->layers == nullptr || is_pinned(r->layers));
 	uint32_t i = 0, k = 0;
@@ -463,7 +459,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		}
 		size_t pos = 0;
 		const uint8_t* direct = nullptr;
-		const uint32_t j = stage_chunk(c->copier, s, b, i, &pos, &direct, pinned_in);
+		const uint32_t j = stage_chunk(s, b, i, &pos, &direct);
 		const uint32_t cnt = j - i;
 		if (!upload_chunk(s, pos, cnt, direct))
 			return PCPPX_E_HIP;
@@ -505,7 +501,6 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 	pcppx_default_opts(&o);
 	o.want_checksums = 0;  // the worker reads addresses, ports and the protocol mask only
 	const uint32_t ml = o.max_layers;
-	const bool pinned_in = is_pinned(b->data);
 	uint32_t i = 0, k = 0;
 	Slot* prev = nullptr;
 	while (i < b->n)
@@ -520,7 +515,7 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 		}
 		size_t pos = 0;
 		const uint8_t* direct = nullptr;
-		const uint32_t j = stage_chunk(c->copier, s, b, i, &pos, &direct, pinned_in);
+		const uint32_t j = stage_chunk(s, b, i, &pos, &direct);
 		const uint32_t cnt = j - i;
 		if (!upload_chunk(s, pos, cnt, direct))
 			return PCPPX_E_HIP;

@@ -265,6 +265,9 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 2: go(flow_count_kernel<256, 2048, 1024, kFlowHot, true, true, true>, 256, 1024, 1536); break;
 	case 3: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 512); break;
 	case 12: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true, true, true>, 1024, 6144, 256); break;
+	case 13: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, true>, 1024, 4096, 256); break;  // listed slots
+	case 14: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true, true, true, true>, 1024, 6144, 256); break;
+	case 15: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, true>, 1024, 4096, 256); break;  // + merge 8
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);
@@ -274,7 +277,7 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 		hipLaunchKernelGGL((flow_merge_kernel<1024, 4096, 1>), dim3(1u << lp), dim3(1024), 0, stream, fp, keys, pk, by, st);
 	else if (shape >= 5 && shape <= 7)
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
-	else if (shape == 8)  // merge lookahead: 2 / 3 rounds of queue records in flight
+	else if (shape == 8 || shape == 15)  // merge lookahead: 2 / 3 rounds of queue records in flight
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 2>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 9)
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 3>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
