@@ -2549,10 +2549,8 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 }
 
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
-// kList (partitioned flush only): the slots a batch claims are listed as they are claimed (one LDS append per wave and
-// probe step), so the flush visits the batch's distinct keys instead of every LDS slot.
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false, bool kList = false>
+          bool kPart = false, bool kDense = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -2564,10 +2562,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
 	__shared__ uint32_t s_kept;
-	static_assert(!kList || kPart, "listed slots: partitioned flush only");
-	__shared__ uint32_t s_list[kList ? kFlowLds : 1];      // claimed slots [0, s_nlist): kept ones first
-	__shared__ uint32_t s_keep[kList ? kFlowLds / 2 : 1];  // slots a flush keeps (hot flows)
-	__shared__ uint32_t s_nlist, s_nkeep;
 	const uint32_t t = threadIdx.x;
 	const uint32_t m = capacity - 1;
 	unsigned long long z_pk = 0, z_by = 0, lost = 0;  // flow key 0 (PacketUtils.cpp:141-148); table full
@@ -2579,8 +2573,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	if (kPart)
 		for (uint32_t j = t; j < kFlowMaxParts; j += kFB)
 			s_bin[j] = 0;
-	if (t == 0)
-		s_nlist = s_nkeep = 0;
 	__syncthreads();
 	// kPrefetch: the next batch's keys and lengths are loaded into registers before this batch's flush,
 	// so their latency overlaps the flush's HBM reads and atomics
@@ -2621,21 +2613,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
 			{
 				const uint32_t prev = atomicCAS(&s_key[slot], 0u, key);
-				if constexpr (kList)
-				{
-					// the lanes of this probe step that claimed a slot append it: one LDS atomic per wave
-					const uint64_t fm = __ballot(prev == 0u);
-					if (fm)
-					{
-						uint32_t at = 0;
-						if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(true)) - 1))
-							at = atomicAdd(&s_nlist, (uint32_t)__popcll(fm));
-						at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
-						if (prev == 0u)
-							s_list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-							                                      __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] = slot;
-					}
-				}
 				if (prev == 0u || prev == key)
 				{
 					atomicAdd(&s_cnt[slot], add);
@@ -2656,70 +2633,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		// kept only while they fill at most half of the table, so the next batch always fits.
 		const bool last = base + (uint64_t)gridDim.x * kFlowBatch >= n;  // uniform
 		constexpr uint32_t kPer = kFlowLds / kFB;
-		if constexpr (kList)
-		{
-			// the listed slots only (every claimed slot is listed once: a flush clears what it does not keep)
-			const uint32_t nl = s_nlist;
-			uint32_t lhot = 0;
-#pragma unroll
-			for (uint32_t u = 0; u < kPer; ++u)
-			{
-				const uint32_t e = u * kFB + t;
-				lhot += (e < nl && (s_cnt[s_list[e]] >> 40) > kHot) ? 1u : 0u;
-			}
-			if (!last && lhot)
-				atomicAdd(&s_kept, lhot);
-			__syncthreads();
-			const bool keep_hot = !last && s_kept <= kFlowLds / 2 - kFlowBatch / 2;  // uniform
-			uint32_t fk[kPer], fsl[kPer], fs[kPer], fseen[kPer];
-#pragma unroll
-			for (uint32_t u = 0; u < kPer; ++u)
-			{
-				const uint32_t e = u * kFB + t;
-				fsl[u] = e < nl ? s_list[e] : 0u;
-				const bool keep = e < nl && keep_hot && (s_cnt[fsl[u]] >> 40) > kHot;
-				if (keep)
-					s_keep[atomicAdd(&s_nkeep, 1u)] = fsl[u];
-				fk[u] = (e < nl && !keep) ? s_key[fsl[u]] : 0u;
-				fs[u] = flow_part(fk[u], fpart.log2p);
-				fseen[u] = fk[u] ? atomicAdd(&s_bin[fs[u]], 1u) : 0u;
-			}
-			__syncthreads();
-			for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
-			{
-				const uint32_t c = s_bin[b];
-				s_base[b] = c ? atomicAdd(&fpart.fill[b], c) : 0u;
-				s_bin[b] = 0;
-			}
-			__syncthreads();
-#pragma unroll
-			for (uint32_t u = 0; u < kPer; ++u)
-			{
-				const uint32_t key = fk[u];
-				if (key == 0)
-					continue;
-				const uint32_t j = fsl[u];
-				const uint32_t pos = s_base[fs[u]] + fseen[u];
-				const unsigned long long c = s_cnt[j];
-				if (pos < fpart.rec_cap)
-					fpart.recs[(size_t)fs[u] * fpart.rec_cap + pos] = make_uint4(key, 0u, (uint32_t)c, (uint32_t)(c >> 32));
-				else if (!flow_region_add_atomic(keys, packets, bytes, fpart, key, c >> 40, c & ((1ull << 40) - 1)))
-					lost += c >> 40;
-				s_key[j] = 0;
-				s_cnt[j] = 0;
-			}
-			__syncthreads();
-			// the kept slots start the next batch's list
-			const uint32_t nk = s_nkeep;
-			for (uint32_t e = t; e < nk; e += kFB)
-				s_list[e] = s_keep[e];
-			if (t == 0)
-				s_nlist = nk;
-			__syncthreads();
-			if (t == 0)
-				s_nkeep = 0;
-			continue;
-		}
 		uint32_t hot = 0;
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
@@ -3221,13 +3134,16 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 // the flow-table shape: 1024-thread blocks, 8192 LDS slots, 4096-packet batches with the next batch prefetched,
 // 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)
 #define PCPPX_FLOW_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true>
-// the partitioned flush (product): the same aggregation, then per-partition queues and one merge block per partition
-#define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true>
-#define PCPPX_FLOW_PART_DENSE_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true>
+// the partitioned flush (product): the same aggregation over 6144-packet batches (fewer flushes: count + merge
+// 0.178 -> 0.168 ms on config 4, profiles/r04g_ab_flow_list.txt shape 12), then per-partition queues and one merge
+// block per partition
+#define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true>
+#define PCPPX_FLOW_PART_DENSE_KERNEL flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true>
 // merge: 512-thread blocks with a 4096-slot LDS table (48 KiB: 3 blocks per CU) over 512 partitions -- count + merge
-// 0.194 -> 0.181 ms on config 4 against 1024 threads / 8192 slots / 256 partitions (profiles/r03_ab_flow_merge.txt)
-#define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<kFlowMergeThreads, 4096, 2>
-constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 4096, kFlowBlocks = 256;
+// 0.194 -> 0.181 ms on config 4 against 1024 threads / 8192 slots / 256 partitions (profiles/r03_ab_flow_merge.txt);
+// three rounds of queue records in flight (-1 to -2%, profiles/r04f_ab_flow_merge_batch.txt shape 9)
+#define PCPPX_FLOW_MERGE_KERNEL flow_merge_kernel<kFlowMergeThreads, 4096, 2, 3>
+constexpr uint32_t kFlowThreads = 1024, kFlowBatchPk = 6144, kFlowBlocks = 256;
 constexpr uint32_t kPackedMax = (1u << 24) - 1;  // packets per launch the packed LDS/HBM counters hold
 constexpr uint32_t kFlowPartLog2 = 9;            // flow-table partitions (merge blocks); at most kFlowMaxParts
 constexpr uint32_t kFlowMinRegionLog2 = 12;      // slots per partition at least (capacity 2^21+ -> 512 partitions)

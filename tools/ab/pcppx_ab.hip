@@ -241,7 +241,8 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 
 /* The partitioned flow table over a dense key column with count-kernel shape `shape` (0: the product's
  * 1024 threads / 8192 LDS slots / 4096-packet batches / 256 blocks; 1: 512 / 4096 / 2048 / 768; 2: 256 / 2048 / 1024 /
- * 1536; 3: 1024 / 8192 / 4096 / 512; 12: 1024 / 8192 / 6144 / 256), then the product's merge (shapes 4-11: merge variants). queues / fill: scratch as pcppx_capi.cpp sizes it. */
+ * 1536; 3: 1024 / 8192 / 6144 / 512; 12: the round-3 product, 4096-packet batches and a one-round-ahead merge), then the
+ * product's merge (shapes 4-11: merge variants; 9: one round ahead). queues / fill: scratch as pcppx_capi.cpp sizes it. */
 PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caplens, uint32_t n, uint32_t* keys,
                                     uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats, void* queues,
                                     uint32_t rec_cap, uint32_t* fill, void* hip_stream, int shape)
@@ -263,12 +264,9 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	{
 	case 1: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true, true, true>, 512, 2048, 768); break;
 	case 2: go(flow_count_kernel<256, 2048, 1024, kFlowHot, true, true, true>, 256, 1024, 1536); break;
-	case 3: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 512); break;
-	case 12: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true, true, true>, 1024, 6144, 256); break;
-	case 13: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, true>, 1024, 4096, 256); break;  // listed slots
-	case 14: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true, true, true, true>, 1024, 6144, 256); break;
-	case 15: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, true>, 1024, 4096, 256); break;  // + merge 8
-	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, 4096, 256); break;
+	case 3: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 512); break;
+	case 12: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true>, 1024, 4096, 256); break;  // r03 batch
+	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);
 	if (rc != PCPPX_OK)
@@ -277,10 +275,10 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 		hipLaunchKernelGGL((flow_merge_kernel<1024, 4096, 1>), dim3(1u << lp), dim3(1024), 0, stream, fp, keys, pk, by, st);
 	else if (shape >= 5 && shape <= 7)
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
-	else if (shape == 8 || shape == 15)  // merge lookahead: 2 / 3 rounds of queue records in flight
+	else if (shape == 8)  // merge lookahead: 2 / 3 rounds of queue records in flight
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 2>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
-	else if (shape == 9)
-		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 3>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
+	else if (shape == 9 || shape == 12)  // 12: the r03 product merge (one round ahead)
+		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 1>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 10)  // 256 threads x 4 records per round, 2 rounds ahead
 		hipLaunchKernelGGL((flow_merge_kernel<256, 4096, 4, 2>), dim3(1u << lp), dim3(256), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 11)  // 512 threads x 4 records, 8192-slot LDS table
@@ -327,7 +325,7 @@ PCPPX_AB_API int pcppx_ab_flow_count_device(const pcppx_summary* sum, const uint
 	case 10: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true>, 512, 2048, 512); break;
 	case 11: go(flow_count_kernel<1024, 4096, 2048, kFlowHot, true>, 1024, 2048, 512); break;
 	case 12: go(flow_count_kernel<1024, 8192, 6144, kFlowHot, true>, 1024, 6144, 256); break;
-	default: go(PCPPX_FLOW_KERNEL, kFlowThreads, kFlowBatchPk, kFlowBlocks); break;
+	default: go(PCPPX_FLOW_KERNEL, kFlowThreads, 4096, kFlowBlocks); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_count_device", stream);
 	if (rc != PCPPX_OK || pc == nullptr)
