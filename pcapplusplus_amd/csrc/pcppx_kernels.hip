@@ -1986,14 +1986,17 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //   diagnostics (wrong or marked records; static_assert'ed out of libpcppx.so): StreamOnly (no header gather / parse;
 //     L4 range = [14, caplen)), MarkFast (flags bit 0x8000 on the packets the fast path took), GatherOnly (descriptors,
 //     both gather rounds for every packet and the record stores, no parse: the memory time of the access pattern),
-//     SkipGeneric (packets off the fast path are not walked: the time the generic walk costs)
+//     SkipGeneric (packets off the fast path are not walked: the time the generic walk costs), Skip (a fast-path stage
+//     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
-          bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false>
+          bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
+          int kSkip = 0>
 struct ParseShape
 {
 	static constexpr bool NT = kNT, FillTails = kFillTails, TightR2 = kTightR2, Realign = kRealign, EarlyB = kEarlyB;
 	static constexpr bool StreamOnly = kStreamOnly, MarkFast = kMarkFast, GatherOnly = kGatherOnly,
 	                      SkipGeneric = kSkipGeneric;
+	static constexpr int Skip = kSkip;
 };
 
 // One wave = one 64-packet tile. MinWaves: __launch_bounds__ minimum waves per SIMD (1 = the compiler's choice).
@@ -2019,7 +2022,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 #ifndef PCPPX_TOOLS_AB
 	// the diagnostic switches write wrong or marked records: only tools/ab/libpcppx_ab.so (built with PCPPX_TOOLS_AB)
 	// may instantiate them, never libpcppx.so; and every product instance can stage a PACKED run
-	static_assert(!S::MarkFast && !S::GatherOnly && !S::SkipGeneric && !S::StreamOnly, "tools-only parse_tile_kernel switch");
+	static_assert(!S::MarkFast && !S::GatherOnly && !S::SkipGeneric && !S::StreamOnly && S::Skip == 0,
+	              "tools-only parse_tile_kernel switch");
 	static_assert(kPackedOk, "a product instance must stage PCPPX_LAYOUT_PACKED rows");
 #endif
 	constexpr bool NT = S::NT, StreamOnly = S::StreamOnly, MarkFast = S::MarkFast, FillTails = S::FillTails,
@@ -2195,8 +2199,10 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	{
 		if (fast)
 		{
-			fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
-			fast_l7(p, f, cap);
+			if (!(S::Skip & 1))
+				fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
+			if (!(S::Skip & 2))
+				fast_l7(p, f, cap);
 			// a classified HTTP / SSL / DNS payload or a UDP tunnel (VXLAN, GTPv1: an unclassified L7 flag): the
 			// generic walk builds their layers
 			const uint32_t l7 = f.l7();
@@ -2345,7 +2351,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		u32x2* dst = reinterpret_cast<u32x2*>(prm.layers) + (size_t)blockIdx.x * kTile * ml;
 		__syncthreads();  // every lane is done with the header stage
 		lptr64w rows = (lptr64w)(stage);
-		if (fast)
+		if (fast && !(S::Skip & 4))
 			fast_emit(f, cap, ml, [&](uint32_t k, uint2 r) {
 				u32x2 e;
 				e.x = r.x;

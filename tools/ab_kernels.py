@@ -53,6 +53,10 @@ cases = {
     "po/gather-only": (abi.make_opts(0, 8, False, _ml), 29),
     "po/packed-gather-only": (abi.make_opts(0, 8, False, _ml, layout=PK), 29),
     "po/skip-generic": (abi.make_opts(0, 8, False, _ml), 44),
+    "po/packed-no-hash": (abi.make_opts(0, 8, False, _ml, layout=PK), 90),
+    "po/packed-no-l7": (abi.make_opts(0, 8, False, _ml, layout=PK), 91),
+    "po/packed-no-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 92),
+    "po/packed-no-hash-l7-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 93),
 }
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")
@@ -81,7 +85,7 @@ want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
     first = next(iter(cases.values()))[0]
     if o.max_layers != first.max_layers or o.want_checksums != want_csum_ref or o.layout != first.layout or \
-            v in (2, 3, 4, 7, 29, 44, 52):  # diagnostics with wrong records
+            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93):  # diagnostics with wrong records
         continue
     summ.zero_()
     lay.zero_()
