@@ -1576,9 +1576,35 @@ __device__ __forceinline__ bool fast_walk(const Pkt& p, uint32_t cap, const Para
 	return ok;
 }
 
+// The table words the L7 trigger of a fast-path packet needs (tcp_l7 / udp_l7 / sip_key: port bitmap words and the
+// SIP key slot), loaded ahead of the hashes so that their latency hides behind them (fast_l7 consumes them).
+struct L7Pre
+{
+	uint32_t ws, wd, wu, sk;  // src / dst port words of the TCP or UDP bitmap, dst word of udp_dst, SIP slot key
+};
+__device__ __forceinline__ L7Pre fast_l7_pre(const Pkt& p, const Fast& f)
+{
+	L7Pre r{ 0u, 0u, 0u, 0u };
+	if (f.payload() && f.l4())
+	{
+		const uint32_t pw = lds_u32(p, f.l4o());
+		const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
+		const uint32_t* t = f.tcp() ? kL7.tcp : kL7.udp;
+		r.ws = t[sport >> 5];
+		r.wd = t[dport >> 5];
+		if (!f.tcp())
+		{
+			r.wu = kL7.udp_dst[dport >> 5];
+			if (f.l4dlen() - 8 >= 4)  // the SIP heuristic's 4 payload bytes (in the window: fast_walk)
+				r.sk = kSip.key[(__builtin_bswap32(lds_u32(p, f.l4o() + 8)) * kSipMul) >> 27];
+		}
+	}
+	return r;
+}
+
 // L7 dispatch of a fast-path packet (same rules as walk_chain's): an L7 payload ends the chain after the
-// L4 layer, with no Payload and no trailer
-__device__ __forceinline__ void fast_l7(const Pkt& p, Fast& f, uint32_t cap)
+// L4 layer, with no Payload and no trailer. `pre`: fast_l7_pre's words (the same tests as tcp_l7 / udp_l7 / sip_key)
+__device__ __forceinline__ void fast_l7(const Pkt& p, Fast& f, uint32_t cap, const L7Pre& pre)
 {
 	const bool payload = f.payload() != 0, tcp = f.tcp() != 0;
 	const uint32_t l4o = f.l4o(), l4dlen = f.l4dlen();
@@ -1587,8 +1613,16 @@ __device__ __forceinline__ void fast_l7(const Pkt& p, Fast& f, uint32_t cap)
 	{
 		const uint32_t pw = lds_u32(p, l4o);
 		const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
-		const bool sip = !tcp && l4dlen - 8 >= 4 && sip_key(__builtin_bswap32(lds_u32(p, l4o + 8)));
-		const bool trig = tcp ? tcp_l7(sport, dport) : (udp_l7(sport, dport) || sip);
+		const uint32_t pb = ((pre.ws >> (sport & 31)) | (pre.wd >> (dport & 31))) & 1u;
+		bool sip = false;
+		if (!tcp && l4dlen - 8 >= 4)
+		{
+			const uint32_t k = __builtin_bswap32(lds_u32(p, l4o + 8)), h = (k * kSipMul) >> 27;
+			sip = ((kSip.valid >> h) & 1u) && pre.sk == k;
+		}
+		const uint32_t pr = (sport << 16) | dport;  // DHCP 68->67, 67->68, 67->67
+		const bool dhcp = pr == ((68u << 16) | 67u) || pr == ((67u << 16) | 68u) || pr == ((67u << 16) | 67u);
+		const bool trig = tcp ? pb != 0 : (pb != 0 || dhcp || ((pre.wu >> (dport & 31)) & 1u) || sip);
 		if (trig)
 			lf = l7_flags(p, tcp, l4o + f.l4hdr(), l4dlen - f.l4hdr(), sport, dport, sip, true);
 	}
@@ -1987,7 +2021,8 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     L4 range = [14, caplen)), MarkFast (flags bit 0x8000 on the packets the fast path took), GatherOnly (descriptors,
 //     both gather rounds for every packet and the record stores, no parse: the memory time of the access pattern),
 //     SkipGeneric (packets off the fast path are not walked: the time the generic walk costs), Skip (a fast-path stage
-//     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows)
+//     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows; bit 3: the L7 table reads
+//     after the hashes instead of before, records unchanged)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
           int kSkip = 0>
@@ -2199,10 +2234,14 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	{
 		if (fast)
 		{
+			// the L7 table reads first: their latency hides behind the hashes
+			L7Pre pre = (S::Skip & 8) ? L7Pre{ 0u, 0u, 0u, 0u } : fast_l7_pre(p, f);
 			if (!(S::Skip & 1))
-				fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);  // before the L7 decision: its table reads overlap
+				fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);
+			if (S::Skip & 8)  // diagnostic: the round-3 order (table reads after the hashes)
+				pre = fast_l7_pre(p, f);
 			if (!(S::Skip & 2))
-				fast_l7(p, f, cap);
+				fast_l7(p, f, cap, pre);
 			// a classified HTTP / SSL / DNS payload or a UDP tunnel (VXLAN, GTPv1: an unclassified L7 flag): the
 			// generic walk builds their layers
 			const uint32_t l7 = f.l7();

@@ -412,12 +412,6 @@ struct pcppx_pcap
 		lo[S] = region_end;
 		std::vector<Chain> seg(S);
 		run_parallel(T, [&](unsigned t) {
-				// map this thread's part of the region in one call (a page fault per 4 KiB otherwise; ignored where the
-				// kernel lacks MADV_POPULATE_READ)
-				const uintptr_t a0 = (uintptr_t)(map + lo[t * kParChains]) & ~(uintptr_t)4095;
-				const uintptr_t a1 = (uintptr_t)(map + lo[t * kParChains + kParChains]);
-				if (a1 > a0)
-					(void)madvise(reinterpret_cast<void*>(a0), a1 - a0, MADV_POPULATE_READ);
 				struct Cur
 				{
 					size_t p, hi;
