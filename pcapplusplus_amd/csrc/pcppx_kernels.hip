@@ -2022,7 +2022,8 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     both gather rounds for every packet and the record stores, no parse: the memory time of the access pattern),
 //     SkipGeneric (packets off the fast path are not walked: the time the generic walk costs), Skip (a fast-path stage
 //     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows; bit 3: the L7 table reads
-//     after the hashes instead of before, records unchanged)
+//     after the hashes instead of before; bit 4: default-policy span-stream loads instead of non-temporal ones; records
+//     unchanged by bits 3-4)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
           int kSkip = 0>
@@ -2092,7 +2093,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// traffic); their values lie after every prefix target, so they are inert
 			const uint32_t c = win * SWin + 64 * k + lane;
 			const uintptr_t a = smin + 16ull * (c < nchunks ? c : nchunks - 1);
-			if (NT)
+			if (NT && !(S::Skip & 16))
 			{
 				const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<gptr16>(a));
 				v[k] = make_uint4(t.x, t.y, t.z, t.w);
