@@ -148,6 +148,20 @@ def test_gpu_synthetic_configs(engine, cfg, n):
         assert not (g[0]["flags"] & abi.F_NEEDS_HOST).any()
 
 
+@pytest.mark.parametrize("size", [64, 512, 1500])
+def test_gpu_sized_batches(engine, size):
+    """bench.py --sizes 64|512|1500: config 3's batch at one packet size (the per-size lines), checksums on, the
+    summary + PACKED rows as the bench writes them, and FIXED rows; every record equal to the restatement's."""
+    b = synth.imix(200_000, 3, sizes=(size,), weights=(1,))
+    for layout in (abi.LAYOUT_PACKED, abi.LAYOUT_FIXED):
+        opts = abi.make_opts(0, 8, True, 8, layout=layout)
+        g = parse_on_device(engine, b, opts)
+        o = oracle.oracle_parse(b, abi.make_opts(0, 8, True, 8), threads=8)
+        lay = abi.unpack_layers(g[0], g[1], 8) if layout == abi.LAYOUT_PACKED else g[1]
+        oracle.compare_exact(g[0], lay, o[0], o[1])
+        assert not (g[0]["flags"] & abi.F_NEEDS_HOST).any()
+
+
 def test_gpu_host_path_matches_device_path(engine):
     """pcppx_parse_batch_host (chunked, three slots) equals the device path: packed pageable input
     (staged by the copy threads), pinned input (DMA straight from the caller's bytes), pinned input and
