@@ -1188,9 +1188,19 @@ __device__ __forceinline__ uint32_t fnv4(uint32_t h, uint32_t v)
 // header at ipo (s/d: na little-endian dwords each) and the raw port word pw of the L4 layer (has_l4).
 // Byte sequences: [port_a port_b ip_a ip_b proto] and [ip_a ip_b], the pair ordered as the reference
 // orders it (raw-order port compare, then LE u32 (IPv4) / memcmp (IPv6) address compare).
+// The address dwords past the first (IPv6) are hashed under a select, not a branch: a wave mixing IPv4 and IPv6 lanes
+// runs them either way, and the selects spare the exec-mask bookkeeping of 24 branches (kBranchy: the branches, a
+// tools-only diagnostic).
+template <bool kBranchy = false>
 __device__ __forceinline__ void tuple_hashes(const uint32_t (&s)[4], const uint32_t (&d)[4], uint32_t na, bool has_l4,
                                              uint32_t pw, uint32_t proto, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
 {
+	auto add4 = [&](uint32_t h, uint32_t k, uint32_t v) -> uint32_t {
+		if (kBranchy)
+			return k < na ? fnv4(h, v) : h;
+		const uint32_t y = fnv4(h, v);
+		return k < na ? y : h;
+	};
 	int cmp = 0;  // sign of memcmp(dst, src) (IPv6) / (dst <=> src) as LE u32 (IPv4)
 	if (na == 1)
 		cmp = d[0] < s[0] ? -1 : (d[0] > s[0] ? 1 : 0);
@@ -1207,10 +1217,10 @@ __device__ __forceinline__ void tuple_hashes(const uint32_t (&s)[4], const uint3
 	uint32_t x = 2166136261u;
 #pragma unroll
 	for (int k = 0; k < 4; ++k)
-		if ((uint32_t)k < na) x = fnv4(x, sw2 ? d[k] : s[k]);
+		x = add4(x, (uint32_t)k, sw2 ? d[k] : s[k]);
 #pragma unroll
 	for (int k = 0; k < 4; ++k)
-		if ((uint32_t)k < na) x = fnv4(x, sw2 ? s[k] : d[k]);
+		x = add4(x, (uint32_t)k, sw2 ? s[k] : d[k]);
 	h2 = x;
 	h5 = h5d = 0;
 	if (!has_l4)
@@ -1225,10 +1235,10 @@ __device__ __forceinline__ void tuple_hashes(const uint32_t (&s)[4], const uint3
 		y = fnv(fnv(y, sp2 & 0xFF), sp2 >> 8);
 #pragma unroll
 		for (int k = 0; k < 4; ++k)
-			if ((uint32_t)k < na) y = fnv4(y, swap ? d[k] : s[k]);
+			y = add4(y, (uint32_t)k, swap ? d[k] : s[k]);
 #pragma unroll
 		for (int k = 0; k < 4; ++k)
-			if ((uint32_t)k < na) y = fnv4(y, swap ? s[k] : d[k]);
+			y = add4(y, (uint32_t)k, swap ? s[k] : d[k]);
 		y = fnv(y, proto);
 		if (dir) h5d = y; else h5 = y;
 	}
@@ -1701,6 +1711,7 @@ __device__ __forceinline__ void fast_emit(const Fast& f, uint32_t cap, uint32_t 
 
 // hash5Tuple x2 + hash2Tuple of a fast-path packet (every byte in the LDS window): the first IPv4 (else the first
 // IPv6) layer's addresses and protocol / next-header byte, the L4 layer's ports
+template <bool kBranchy = false>
 __device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, const Walk& w, uint32_t& h5, uint32_t& h5d,
                                             uint32_t& h2)
 {
@@ -1716,7 +1727,7 @@ __device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, const W
 		d[k] = (uint32_t)k < na ? lds_u32(p, dofs + 4 * k) : 0;
 	}
 	const uint32_t proto = (lds_u32(p, ipo + (v4 ? 8 : 4)) >> (v4 ? 8 : 16)) & 0xFF;
-	tuple_hashes(s, d, na, f.l4() != 0, lds_u32(p, f.l4o()), proto, h5, h5d, h2);
+	tuple_hashes<kBranchy>(s, d, na, f.l4() != 0, lds_u32(p, f.l4o()), proto, h5, h5d, h2);
 }
 
 // IPv4 header checksum of the first IPv4 layer, from dword reads of the (fully staged) header
@@ -2022,8 +2033,8 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     both gather rounds for every packet and the record stores, no parse: the memory time of the access pattern),
 //     SkipGeneric (packets off the fast path are not walked: the time the generic walk costs), Skip (a fast-path stage
 //     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows; bit 3: the L7 table reads
-//     after the hashes instead of before; bit 4: default-policy span-stream loads instead of non-temporal ones; records
-//     unchanged by bits 3-4)
+//     after the hashes instead of before; bit 4: default-policy span-stream loads instead of non-temporal ones; bit 5:
+//     the IPv6 address dwords hashed under branches instead of selects; records unchanged by bits 3-5)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
           int kSkip = 0>
@@ -2238,7 +2249,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// the L7 table reads first: their latency hides behind the hashes
 			L7Pre pre = (S::Skip & 8) ? L7Pre{ 0u, 0u, 0u, 0u } : fast_l7_pre(p, f);
 			if (!(S::Skip & 1))
-				fast_hashes(p, f, fast_to_walk(f, ml), h5, h5d, h2);
+				fast_hashes<(S::Skip & 32) != 0>(p, f, fast_to_walk(f, ml), h5, h5d, h2);
 			if (S::Skip & 8)  // diagnostic: the round-3 order (table reads after the hashes)
 				pre = fast_l7_pre(p, f);
 			if (!(S::Skip & 2))

@@ -232,6 +232,8 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 94: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 8>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 95: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 8>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 96: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 16>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 97: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 98: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 44: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 52: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	// the PCPPX_WINDOW_DEEP checksum instance with the early second stream window (the product's runs it late)
