@@ -2019,7 +2019,9 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 
 // The shape switches of one parse_tile_kernel instance. The product instances use ParseShape<> (below: only the
 // checksum instance of PCPPX_WINDOW_DEEP differs, in EarlyB); the diagnostics exist for tools/ab/libpcppx_ab.so only.
-//   NT: non-temporal span-stream loads and record stores (read-once / write-once data; profiles/r01_ab_nontemporal.txt)
+//   NT: non-temporal record stores (write-once data; profiles/r01_ab_nontemporal.txt); the span-stream loads use the
+//     default policy since round 4 (their lines are the ones the header gather reads too: config 3 -1.7%,
+//     profiles/r04k_ab_cfg3.txt)
 //   FillTails: the staged FIXED layer rows are zero-filled past n_layers and stored whole: full-line stores, 3.5% faster
 //     on config 3 than storing only the chain's records (profiles/r02_ab_tails.txt)
 //   TightR2: the second gather round reads only up to the deep stack's header extent (deep_extent) instead of the whole
@@ -2033,7 +2035,8 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     both gather rounds for every packet and the record stores, no parse: the memory time of the access pattern),
 //     SkipGeneric (packets off the fast path are not walked: the time the generic walk costs), Skip (a fast-path stage
 //     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows; bit 3: the L7 table reads
-//     after the hashes instead of before; bit 4: default-policy span-stream loads instead of non-temporal ones; bit 5:
+//     after the hashes instead of before; bit 4: non-temporal span-stream loads (rounds 1-3) instead of default-policy
+//     ones; bit 5:
 //     the IPv6 address dwords hashed under branches instead of selects; records unchanged by bits 3-5)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
@@ -2104,7 +2107,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// traffic); their values lie after every prefix target, so they are inert
 			const uint32_t c = win * SWin + 64 * k + lane;
 			const uintptr_t a = smin + 16ull * (c < nchunks ? c : nchunks - 1);
-			if (NT && !(S::Skip & 16))
+			if (NT && (S::Skip & 16))  // diagnostic: the round 1-3 non-temporal stream loads
 			{
 				const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<gptr16>(a));
 				v[k] = make_uint4(t.x, t.y, t.z, t.w);

@@ -55,7 +55,7 @@ cases = {
     "po/skip-generic": (abi.make_opts(0, 8, False, _ml), 44),
     "po/packed-l7-late": (abi.make_opts(0, 8, False, _ml, layout=PK), 94),
     "tile/packed-l7-late": (abi.make_opts(0, 8, True, 8, layout=PK), 95),
-    "tile/packed-cached-stream": (abi.make_opts(0, 8, True, 8, layout=PK), 96),
+    "tile/packed-nt-stream": (abi.make_opts(0, 8, True, 8, layout=PK), 96),
     "po/packed-hash-branchy": (abi.make_opts(0, 8, False, _ml, layout=PK), 97),
     "tile/packed-hash-branchy": (abi.make_opts(0, 8, True, 8, layout=PK), 98),
     "po/packed-no-hash": (abi.make_opts(0, 8, False, _ml, layout=PK), 90),
