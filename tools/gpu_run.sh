@@ -12,6 +12,7 @@
 #   traffic:<cfgs>                 PMC FETCH/WRITE passes -> <tag>_traffic_cfg<c>.json (tools/measure_traffic.sh)
 #   sq:<cfg>                       SQ issue counters (tools/sq_counters.sh); sqlds:<cfg> the LDS-wait / bank-conflict set
 #   sqab:<cases>                   SQ issue counters of tools/ab_kernels.py cases on config 5 -> <tag>_sqab/
+#   pmcab:<cases>                  one --pmc pass (PMC_COUNTERS) over tools/ab_kernels.py cases (config AB_CFG) -> <tag>_pmcab/
 #   cmd:<shell command>            anything else, under a 600 s limit
 set -o pipefail
 TAG=$1
@@ -80,6 +81,12 @@ for step in "$@"; do
         --output-format csv -- python3 "$ROOT/tools/ab_kernels.py" 10000000 2 5 > "$ROOT/$OUT/${TAG}_sqab/ab.txt" \
         2> "$ROOT/$OUT/${TAG}_sqab/err.log") || { tail -20 "$OUT/${TAG}_sqab/err.log"; exit 7; }
       python3 tools/pmc_summary.py "$OUT/${TAG}_sqab" | tee "$OUT/${TAG}_sqab/summary.txt" ;;
+    pmcab)  # one rocprofv3 --pmc pass (counters: PMC_COUNTERS) over tools/ab_kernels.py cases (AB_CASES=<arg>) on config AB_CFG
+      mkdir -p "$OUT/${TAG}_pmcab"
+      (cd /tmp && AB_CASES="$arg" timeout -s KILL 240 rocprofv3 --pmc $PMC_COUNTERS -d "$ROOT/$OUT/${TAG}_pmcab" -o p \
+        --output-format csv -- python3 "$ROOT/tools/ab_kernels.py" 10000000 2 ${AB_CFG:-3} > "$ROOT/$OUT/${TAG}_pmcab/ab.txt" \
+        2> "$ROOT/$OUT/${TAG}_pmcab/err.log") || { tail -20 "$OUT/${TAG}_pmcab/err.log"; exit 7; }
+      python3 tools/pmc_summary.py "$OUT/${TAG}_pmcab" | tee "$OUT/${TAG}_pmcab/summary.txt" ;;
     cmd)
       timeout -k 10 600 bash -c "$arg" || exit 8 ;;
     *)
