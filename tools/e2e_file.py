@@ -104,7 +104,7 @@ def main() -> None:
         res["benchmark_example_pcap"] = bench_pair(exf, (10, 410), ex.n, trials=7)
         print("example.pcap", json.dumps(res["benchmark_example_pcap"]), flush=True)
         exf.unlink()
-        res["benchmark_imix_10M"] = bench_pair(big, (1, 3), args.packets)
+        res["benchmark_imix_10M"] = bench_pair(big, (1, 3), args.packets, trials=3)
         print("imix", json.dumps(res["benchmark_imix_10M"]), flush=True)
     finally:
         big.unlink(missing_ok=True)
