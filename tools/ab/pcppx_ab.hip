@@ -234,6 +234,11 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 96: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 16>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 97: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 98: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
+	// checksum-instance shapes re-tuned under the default-policy stream loads: occupancy 4 / 6, stream window 192 / 64 chunks
+	case 100: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	case 101: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	case 102: hipLaunchKernelGGL((parse_tile_kernel<5, 192, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	case 103: hipLaunchKernelGGL((parse_tile_kernel<5, 64, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 44: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 52: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	// the PCPPX_WINDOW_DEEP checksum instance with the early second stream window (the product's runs it late)
