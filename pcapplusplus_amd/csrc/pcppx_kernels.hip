@@ -2609,8 +2609,10 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 }
 
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
+// kOnePass (partitioned flush): the hot-flow decision is taken in the partition pass (a hot slot is kept while the kept
+// count stays within the bound, first come first kept) instead of in a pass and a barrier of its own.
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false>
+          bool kPart = false, bool kDense = false, bool kOnePass = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -2693,6 +2695,48 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		// kept only while they fill at most half of the table, so the next batch always fits.
 		const bool last = base + (uint64_t)gridDim.x * kFlowBatch >= n;  // uniform
 		constexpr uint32_t kPer = kFlowLds / kFB;
+		if constexpr (kPart && kOnePass)
+		{
+			uint32_t fk[kPer], fs[kPer], fseen[kPer];
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; ++u)
+			{
+				const uint32_t j = u * kFB + t;
+				const uint32_t key = s_key[j];
+				// kept only while at most half the table minus half a batch is kept, so the next batch always fits
+				const bool keep = key != 0 && !last && (s_cnt[j] >> 40) > kHot &&
+				                  atomicAdd(&s_kept, 1u) < kFlowLds / 2 - kFlowBatch / 2;
+				fk[u] = keep ? 0u : key;
+				fs[u] = flow_part(fk[u], fpart.log2p);
+				fseen[u] = fk[u] ? atomicAdd(&s_bin[fs[u]], 1u) : 0u;
+			}
+			__syncthreads();
+			for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
+			{
+				const uint32_t c = s_bin[b];
+				s_base[b] = c ? atomicAdd(&fpart.fill[b], c) : 0u;
+				s_bin[b] = 0;
+			}
+			__syncthreads();
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; ++u)
+			{
+				const uint32_t j = u * kFB + t;
+				const uint32_t key = fk[u];
+				if (key == 0)
+					continue;
+				const uint32_t pos = s_base[fs[u]] + fseen[u];
+				const unsigned long long c = s_cnt[j];
+				if (pos < fpart.rec_cap)
+					fpart.recs[(size_t)fs[u] * fpart.rec_cap + pos] = make_uint4(key, 0u, (uint32_t)c, (uint32_t)(c >> 32));
+				else if (!flow_region_add_atomic(keys, packets, bytes, fpart, key, c >> 40, c & ((1ull << 40) - 1)))
+					lost += c >> 40;
+				s_key[j] = 0;
+				s_cnt[j] = 0;
+			}
+			__syncthreads();
+			continue;
+		}
 		uint32_t hot = 0;
 #pragma unroll
 		for (uint32_t u = 0; u < kPer; ++u)
