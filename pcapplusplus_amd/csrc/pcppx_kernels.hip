@@ -3253,10 +3253,10 @@ constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
 // 256 persistent blocks (profiles/r01_ab_flow_shape.txt, r01_ab_flow_grid.txt)
 #define PCPPX_FLOW_KERNEL flow_count_kernel<1024, 8192, 4096, kFlowHot, true>
 // the partitioned flush (product): the same aggregation over 6144-packet batches (fewer flushes: count + merge
-// 0.178 -> 0.168 ms on config 4, profiles/r04g_ab_flow_list.txt shape 12), then per-partition queues and one merge
-// block per partition
-#define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true>
-#define PCPPX_FLOW_PART_DENSE_KERNEL flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true>
+// 0.178 -> 0.168 ms on config 4, profiles/r04g_ab_flow_list.txt shape 12) with the one-pass flush (-4.6%,
+// profiles/r04r_ab_flow_onepass.txt), then per-partition queues and one merge block per partition
+#define PCPPX_FLOW_PART_KERNEL flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, false, true>
+#define PCPPX_FLOW_PART_DENSE_KERNEL flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, true>
 // merge: 512-thread blocks with a 4096-slot LDS table (48 KiB: 3 blocks per CU) over 512 partitions -- count + merge
 // 0.194 -> 0.181 ms on config 4 against 1024 threads / 8192 slots / 256 partitions (profiles/r03_ab_flow_merge.txt);
 // three rounds of queue records in flight (-1 to -2%, profiles/r04f_ab_flow_merge_batch.txt shape 9)
