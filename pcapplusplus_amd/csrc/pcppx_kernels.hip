@@ -2857,10 +2857,8 @@ __global__ __launch_bounds__(kBlock) void flow_unpack_kernel(unsigned long long*
 // thread per round; flushed whenever more than half full), then adds each distinct key's counts into its own table
 // region -- which no other block touches, so the counts take plain loads and stores (a CAS only claims a new key's
 // slot against the block's other threads). Resets the queue length for the next launch.
-// kAhead: rounds of queue records in flight ahead of the round being inserted. kPreCnt: the flush loads each key's home
-// slot counters with its key (one dependent HBM round trip fewer for a key found at its home slot, the common case once
-// the table holds the flows).
-template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT, uint32_t kAhead = 1, bool kPreCnt = false>
+// kAhead: rounds of queue records in flight ahead of the round being inserted.
+template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT, uint32_t kAhead = 1>
 __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* keys, unsigned long long* packets,
                                                          unsigned long long* bytes, unsigned long long* stats)
 {
@@ -2935,18 +2933,12 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 			// the home slot of every distinct key is read first (all loads in flight together), then claimed / added
 			constexpr uint32_t kPerF = kMLds / kMB;
 			uint32_t fkey[kPerF], fr[kPerF], fprev[kPerF];
-			unsigned long long fpk[kPreCnt ? kPerF : 1], fby[kPreCnt ? kPerF : 1];
 #pragma unroll
 			for (uint32_t u = 0; u < kPerF; ++u)
 			{
 				fkey[u] = s_key[u * kMB + t];
 				fr[u] = flow_region_slot(fkey[u], fp.log2r);
 				fprev[u] = fkey[u] ? keys[rbase + fr[u]] : 0u;
-				if constexpr (kPreCnt)
-				{
-					fpk[u] = fkey[u] ? packets[rbase + fr[u]] : 0ull;
-					fby[u] = fkey[u] ? bytes[rbase + fr[u]] : 0ull;
-				}
 			}
 #pragma unroll
 			for (uint32_t u = 0; u < kPerF; ++u)
@@ -2957,13 +2949,7 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 				const unsigned long long c = s_cnt[j];
 				uint32_t r = fr[u], prev = fprev[u];
 				bool done = false;
-				if (kPreCnt && prev == key)  // at its home slot: the counters are in registers already
-				{
-					packets[rbase + r] = fpk[kPreCnt ? u : 0] + (c >> 40);
-					bytes[rbase + r] = fby[kPreCnt ? u : 0] + (c & ((1ull << 40) - 1));
-					done = true;
-				}
-				for (uint32_t probe = 0; !done && probe <= rm; ++probe)
+				for (uint32_t probe = 0; probe <= rm; ++probe)
 				{
 					if (probe > 0)
 						prev = keys[rbase + r];
