@@ -2015,15 +2015,6 @@ __device__ __forceinline__ uint32_t deep_extent(const Pkt& p, uint32_t et, uint3
 	return ok ? l4 + 20 : 0xFFFFu;
 }
 
-// the generic walk + hashes as a real call (ParseShape Skip bit 6, a tools-only diagnostic): the fast path's code kept
-// compact in the instruction cache, the rare generic packets paying a call
-__device__ __noinline__ Walk generic_walk_call(const Pkt& p, uint32_t cap, const Params& prm, uint2* lay_out, uint32_t* h)
-{
-	Walk w = walk_chain(p, cap, prm, lay_out);
-	hashes(p, w, h[0], h[1], h[2]);
-	return w;
-}
-
 constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_layers; beyond, direct stores
 
 // The shape switches of one parse_tile_kernel instance. The product instances use ParseShape<> (below: only the
@@ -2046,8 +2037,7 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows; bit 3: the L7 table reads
 //     after the hashes instead of before; bit 4: non-temporal span-stream loads (rounds 1-3) instead of default-policy
 //     ones; bit 5:
-//     the IPv6 address dwords hashed under branches instead of selects; bit 6: the generic walk as a real call; records
-//     unchanged by bits 3-6)
+//     the IPv6 address dwords hashed under branches instead of selects; records unchanged by bits 3-5)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
           int kSkip = 0>
@@ -2284,19 +2274,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		else if (!SkipGeneric)
 		{
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
-			if (S::Skip & 64)
-			{
-				uint32_t h[3];
-				w = generic_walk_call(p, cap, prm, lay_out, h);
-				h5 = h[0];
-				h5d = h[1];
-				h2 = h[2];
-			}
-			else
-			{
-				w = walk_chain(p, cap, prm, lay_out);
-				hashes(p, w, h5, h5d, h2);
-			}
+			w = walk_chain(p, cap, prm, lay_out);
+			hashes(p, w, h5, h5d, h2);
 			if (want_csum && w.v4 >= 0)
 			{
 				ipc = ipv4_checksum(p, w, &ips);
