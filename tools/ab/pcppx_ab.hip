@@ -275,6 +275,20 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 		hipLaunchKernelGGL(kern, dim3(batches < blocks ? batches : blocks), dim3(threads), 0, stream, nullptr, caplens, n,
 		                   keys, pk, by, capacity, st, nullptr, fp, dkeys);
 	};
+	if (shape == 20)  // no partitions: each batch's distinct keys go straight to the table (packed 64-bit atomics into
+	{                 // `queues` taken as a zeroed u64[capacity] accumulator), then one unpack pass over the table
+		const uint32_t batches = (n + kFlowBatchPk - 1) / kFlowBatchPk;
+		auto* acc = static_cast<unsigned long long*>(queues);
+		hipLaunchKernelGGL((flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, false, true>),
+		                   dim3(batches < kFlowBlocks ? batches : kFlowBlocks), dim3(1024), 0, stream, nullptr, caplens, n, keys,
+		                   pk, by, capacity, st, acc, FlowPart{}, dkeys);
+		int rc = check_launch("pcppx_ab_flow_part(unpartitioned)", stream);
+		if (rc != PCPPX_OK)
+			return rc;
+		const uint32_t ub = (capacity + kBlock - 1) / kBlock;
+		hipLaunchKernelGGL(flow_unpack_kernel, dim3(ub < 2048 ? ub : 2048), dim3(kBlock), 0, stream, pk, by, acc, capacity);
+		return check_launch("flow_unpack_kernel", stream);
+	}
 	switch (shape)
 	{
 	case 1: go(flow_count_kernel<512, 4096, 2048, kFlowHot, true, true, true>, 512, 2048, 768); break;

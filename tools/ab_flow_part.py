@@ -28,6 +28,7 @@ eng.parse_device(data, offs, caps, n, b.linktype, abi.make_opts(0, 8, False, 0),
 cap = 1 << 21
 PARTS = {6: 256, 7: 1024}  # partitions per shape (tools/ab pcppx_ab_flow_part's `want`); else 512
 queues = torch.empty(1024 * (2 * ((n + 1023) // 1024) + 4096) * 4, dtype=torch.int32, device=dev)
+acc = torch.zeros(cap, dtype=torch.int64, device=dev)  # shape 20's accumulator (its unpack pass leaves it zeroed)
 fill = torch.zeros(512 * 256, dtype=torch.int32, device=dev)
 
 
@@ -39,7 +40,8 @@ def run(shape):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     abi.check(ab.lib().pcppx_ab_flow_part(abi.ptr(fk), abi.ptr(caps), n, abi.ptr(t[0]), abi.ptr(t[1]), abi.ptr(t[2]), cap,
-                                          abi.ptr(t[3]), abi.ptr(queues), rec_cap, abi.ptr(fill), st.cuda_stream, shape),
+                                          abi.ptr(t[3]), abi.ptr(acc if shape == 20 else queues), rec_cap, abi.ptr(fill),
+                                          st.cuda_stream, shape),
               "pcppx_ab_flow_part")
     e1.record(st)
     torch.cuda.synchronize()
