@@ -311,6 +311,12 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 2>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 9 || shape == 12)  // 12: the r03 product merge (one round ahead)
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 1>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
+	else if (shape == 17)  // deeper merge lookahead: 4 / 6 rounds of queue records in flight
+		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 4>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
+	else if (shape == 18)
+		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 6>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
+	else if (shape == 19)  // 1 record per thread, 6 rounds ahead
+		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 1, 6>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 10)  // 256 threads x 4 records per round, 2 rounds ahead
 		hipLaunchKernelGGL((flow_merge_kernel<256, 4096, 4, 2>), dim3(1u << lp), dim3(256), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 11)  // 512 threads x 4 records, 8192-slot LDS table
