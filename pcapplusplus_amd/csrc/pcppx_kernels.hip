@@ -2611,10 +2611,8 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
 // kOnePass (partitioned flush): the hot-flow decision is taken in the partition pass (a hot slot is kept while the kept
 // count stays within the bound, first come first kept) instead of in a pass and a barrier of its own.
-// kGroup4: the LDS table is probed four slots (one 16-B read) at a time: a key is looked for in the whole group before
-// the group's first free slot is claimed, so a probe sequence at high load takes a quarter of the dependent LDS reads.
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false, bool kOnePass = false, bool kGroup4 = false>
+          bool kPart = false, bool kDense = false, bool kOnePass = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -2623,7 +2621,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
                                                             FlowPart fpart = FlowPart{}, const uint32_t* dkeys = nullptr)
 {
 	__shared__ uint32_t s_bin[kPart ? kFlowMaxParts : 1], s_base[kPart ? kFlowMaxParts : 1];  // per-partition counts / offsets
-	__shared__ __attribute__((aligned(16))) uint32_t s_key[kFlowLds];
+	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
 	__shared__ uint32_t s_kept;
 	const uint32_t t = threadIdx.x;
@@ -2674,12 +2672,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 			const unsigned long long add = (1ull << 40) | len;
 			static_assert(kFlowBatch < kFlowLds && kFlowBatch % kFB == 0 && (kFlowLds & (kFlowLds - 1)) == 0, "flow shape");
 			uint32_t slot = (key * 0x9E3779B1u) >> (32 - log2u(kFlowLds));  // top bits
-			if constexpr (kGroup4)
-			{
-				// a group holds K only once: a claimer takes the first free slot of the group as it reads it, so a second
-				// claimer of K reads either K (a hit) or the same free slot (its CAS then returns K)
-				uint32_t g = slot & ~3u;
-				while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
+			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
 				{
 					typedef uint32_t u32x4l __attribute__((ext_vector_type(4)));
 					const u32x4l k4 = *reinterpret_cast<const u32x4l*>(&s_key[g]);  // one 16-B LDS read

@@ -296,7 +296,6 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 3: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 512); break;
 	case 12: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true>, 1024, 4096, 256); break;  // r03 batch
 	case 13: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, false>, 1024, kFlowBatchPk, 256); break;  // two-pass flush (r04 before r04r)
-	case 21: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // 4-slot group probing
 	case 14: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 4, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 4
 	case 15: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 1, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 1
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 256); break;
