@@ -2673,32 +2673,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 			static_assert(kFlowBatch < kFlowLds && kFlowBatch % kFB == 0 && (kFlowLds & (kFlowLds - 1)) == 0, "flow shape");
 			uint32_t slot = (key * 0x9E3779B1u) >> (32 - log2u(kFlowLds));  // top bits
 			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
-				{
-					typedef uint32_t u32x4l __attribute__((ext_vector_type(4)));
-					const u32x4l k4 = *reinterpret_cast<const u32x4l*>(&s_key[g]);  // one 16-B LDS read
-					const int hit = k4.x == key ? 0 : (k4.y == key ? 1 : (k4.z == key ? 2 : (k4.w == key ? 3 : -1)));
-					if (hit >= 0)
-					{
-						atomicAdd(&s_cnt[g + hit], add);
-						break;
-					}
-					const int fr = k4.x == 0u ? 0 : (k4.y == 0u ? 1 : (k4.z == 0u ? 2 : (k4.w == 0u ? 3 : -1)));
-					if (fr < 0)
-					{
-						g = (g + 4) & (kFlowLds - 1);
-						continue;
-					}
-					const uint32_t prev = atomicCAS(&s_key[g + fr], 0u, key);
-					if (prev == 0u || prev == key)
-					{
-						atomicAdd(&s_cnt[g + fr], add);
-						break;
-					}
-					// lost the slot to another key: read the group again
-				}
-				continue;
-			}
-			while (true)  // at most kFlowBatch keys in kFlowLds slots: always terminates
 			{
 				const uint32_t prev = atomicCAS(&s_key[slot], 0u, key);
 				if (prev == 0u || prev == key)
