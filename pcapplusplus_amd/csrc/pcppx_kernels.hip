@@ -2037,8 +2037,7 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows; bit 3: the L7 table reads
 //     after the hashes instead of before; bit 4: non-temporal span-stream loads (rounds 1-3) instead of default-policy
 //     ones; bit 5:
-//     the IPv6 address dwords hashed under branches instead of selects; bit 6: PACKED runs stored one 8-B entry per
-//     lane instead of two; records unchanged by bits 3-6)
+//     the IPv6 address dwords hashed under branches instead of selects; records unchanged by bits 3-5)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
           int kSkip = 0>
@@ -2417,23 +2416,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			for (uint32_t k = 0; k < cnt; ++k)  // the generic walk wrote this lane's chain at its fixed-layout slot
 				rows[excl + k] = dst[lane * ml + k];
 		__syncthreads();
-		if (S::Skip & 64)  // diagnostic: one 8-B entry per lane and store (rounds 3-4)
-		{
-			for (uint32_t r = lane; r < total; r += kTile)
-				__builtin_nontemporal_store(rows[r], &dst[r]);
-		}
-		else
-		{
-			// two entries per lane and 16-B store (the run starts 16-B aligned: 64 * ml entries per tile)
-			typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
-			typedef __attribute__((address_space(3))) u32x4s* lptr128w;
-			const lptr128w rows2 = (lptr128w)(stage);
-			u32x4s* dst2 = reinterpret_cast<u32x4s*>(dst);
-			for (uint32_t q = lane; q < total / 2; q += kTile)
-				__builtin_nontemporal_store(rows2[q], &dst2[q]);
-			if ((total & 1) && lane == 0)
-				__builtin_nontemporal_store(rows[total - 1], &dst[total - 1]);
-		}
+		for (uint32_t r = lane; r < total; r += kTile)
+			__builtin_nontemporal_store(rows[r], &dst[r]);
 	}
 	else if (stage_layers && ml > kRowMl)  // uniform: deep records, each fast lane stores its own row
 	{

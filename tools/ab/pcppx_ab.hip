@@ -239,8 +239,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 101: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 102: hipLaunchKernelGGL((parse_tile_kernel<5, 192, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 103: hipLaunchKernelGGL((parse_tile_kernel<5, 64, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	case 106: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 64>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 107: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 64>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 44: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 52: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	// the PCPPX_WINDOW_DEEP checksum instance with the early second stream window (the product's runs it late)

@@ -56,8 +56,6 @@ cases = {
     "po/packed-l7-late": (abi.make_opts(0, 8, False, _ml, layout=PK), 94),
     "tile/packed-l7-late": (abi.make_opts(0, 8, True, 8, layout=PK), 95),
     "tile/packed-nt-stream": (abi.make_opts(0, 8, True, 8, layout=PK), 96),
-    "tile/packed-8b-stores": (abi.make_opts(0, 8, True, 8, layout=PK), 106),
-    "po/packed-8b-stores": (abi.make_opts(0, 8, False, _ml, layout=PK), 107),
     "tile/packed-w4": (abi.make_opts(0, 8, True, 8, layout=PK), 100),
     "tile/packed-w6": (abi.make_opts(0, 8, True, 8, layout=PK), 101),
     "tile/packed-swin192": (abi.make_opts(0, 8, True, 8, layout=PK), 102),
