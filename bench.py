@@ -335,7 +335,8 @@ def main() -> None:
     wall = time.perf_counter() - w0
     step_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
     # the parse kernel is the dominant kernel of every config; config 4 also runs the flow-table kernels
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, mids)])) if mids else step_ms
+    kern_each = [s.elapsed_time(e) for s, e in zip(starts, mids if mids else ends)]
+    kern_ms = float(np.mean(kern_each))
     flow_ms = step_ms - kern_ms if mids else None
 
     tdev = dev if args.dist_backend == "nccl" else "cpu"
@@ -499,6 +500,11 @@ def main() -> None:
                 "per_rank_wall_ms_per_step": [round(p[0] * 1e3 / args.steps, 4) for p in per_rank],
                 "wire_GBps": round(wire * world * args.steps / wall_max / 1e9, 2),
                 "kernel_ms": round(kern_max, 4),
+                # the timed launches' spread (rank 0): the mean above averages the chip's clock transient over the
+                # first launches of a run (profiles/r05_transient.txt); median and minimum beside it, nothing hidden
+                "kernel_ms_median": round(float(np.median(kern_each)), 4),
+                "kernel_ms_min": round(float(np.min(kern_each)), 4),
+                "kernel_ms_max": round(float(np.max(kern_each)), 4),
                 "step_kernel_ms": round(step_ms, 4),
                 "flagged_packets": flagged,
                 "gen_seconds": round(gen_s, 1),

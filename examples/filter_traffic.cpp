@@ -228,12 +228,12 @@ public:
 	/* the whole worker on the GPU: flow table, matching and statistics in HBM (pcppx_filter_batch_host) */
 	bool runOnDevice(pcppx::PcapFileReaderDevice& reader, pcpp::PcapFileWriterDevice* pcapWriter)
 	{
-		pcppx::RawPacketVector packetArr;
+		pcppx::RawBatch packetArr;
 		std::vector<uint8_t> matched;
 		pcppx_packet_stats s{};
 		m_Engine.resetFilter();
 		const pcppx::MatchSpec spec = m_PacketMatchingEngine.spec();
-		while (reader.getNextPackets(packetArr, (int)m_Burst) > 0)
+		while (reader.getNextBatch(packetArr, (int)m_Burst) > 0)
 		{
 			s = m_Engine.filter(packetArr, spec, matched);
 			if (pcapWriter != nullptr)

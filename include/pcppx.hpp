@@ -28,7 +28,7 @@
  * exact layer prefix; with a host parser registered (pcppx::setHostParser: the caller's own Packet++ parse of one
  * packet) they are completed before the caller sees them. libpcppx.so never links Packet++.
  *
- * The batch API remains for callers that want it: RawPacketVector + Engine::parse -> ParsedBatch of Packet views.
+ * The batch API remains for callers that want it: RawBatch + Engine::parse -> ParsedBatch of Packet views.
  *
  * Errors are reported as pcppx::Error (a std::runtime_error carrying the PCPPX_E_* code).
  */
@@ -222,6 +222,8 @@ inline void setHostParser(pcppx_host_parse_fn fn)
 	detail::hostParser().store(fn);
 }
 
+class RawPacket;
+
 namespace detail
 {
 /* Page-locked blocks for record pages, reused across pages and readers (pinning memory is slow). Blocks go back to
@@ -295,10 +297,19 @@ public:
 	{
 		std::lock_guard<std::mutex> g(m_Mu);
 		check(pcppx_parse_batch_host(m_Ctx, &b, &o, &r), "pcppx_parse_batch_host");
+		++counter();
 	}
+	/* GPU parses the per-packet entry points have made (one per page, group or re-parse) */
+	uint64_t parses() const { return counter().load(); }
+	static uint64_t parsesSoFar() { return counter().load(); }  // without opening the device
 
 private:
 	explicit Service(int device) { check(pcppx_open(device, &m_Ctx), "pcppx_open"); }
+	static std::atomic<uint64_t>& counter()
+	{
+		static std::atomic<uint64_t> c{ 0 };
+		return c;
+	}
 	std::mutex m_Mu;
 	pcppx_ctx* m_Ctx = nullptr;
 };
@@ -362,9 +373,11 @@ private:
 	size_t m_Bytes = 0;
 };
 
-/* records of one packet parsed on its own (a RawPacket that did not come from a reader) */
-struct OwnedRecords
+/* one packet's records, copied out of its page when its RawPacket is copied (the copy owns its bytes and keeps no
+ * page alive, as a copied pcpp::RawPacket owns a copy of the bytes: RawPacket.cpp copyDataFrom) */
+struct CopiedRecords
 {
+	ParseKey key;
 	pcppx_summary sum{};
 	pcppx_layer lay[PCPPX_MAX_LAYERS]{};
 };
@@ -378,11 +391,17 @@ struct MapHandle
 
 class ReaderCore;
 
-/* A run of consecutive packets of one capture and one link type, pointing into the map, with its GPU records. */
+/* A run of consecutive packets of one capture and one link type, pointing into the map, with its GPU records -- or
+ * (a group, `group` set) the caller's own RawPackets of one link type that were parsed together: base is the lowest
+ * of their byte addresses and offsets[i] the distance of packet i's bytes from it (a gapped batch, legal in
+ * pcppx_batch). A group member that is released or given other bytes leaves the group: its caplen becomes 0 under
+ * groupMu, so a later parse of the group (other options) never reads bytes the caller has freed. */
 struct Page
 {
-	std::shared_ptr<MapHandle> map;  // keeps the bytes valid
+	std::shared_ptr<MapHandle> map;  // keeps the bytes valid (reader pages)
 	std::weak_ptr<ReaderCore> core;  // the reader, to learn the parse options from the caller's Packets
+	bool group = false;
+	mutable std::mutex groupMu;      // a group's parse vs. its members leaving
 	const uint8_t* base = nullptr;
 	uint64_t dataLen = 0;
 	uint16_t linkType = LINKTYPE_ETHERNET;
@@ -609,16 +628,47 @@ inline const Records* Page::recordsFor(ParseKey k)
 	for (const auto& e : extra)
 		if (e->key == k)
 			return e.get();
+	std::unique_lock<std::mutex> gl(groupMu, std::defer_lock);
+	if (group)
+		gl.lock();  // the members still alive: a released member's caplen is 0
 	extra.push_back(parseRecords(k));
 	return extra.back().get();
 }
+
+/* The caller's own RawPackets (not from a reader) that no Packet has been built on yet. The first Packet built on
+ * one of them parses every pending RawPacket in one GPU batch per link type (a group, above), so that a caller
+ * that fills a RawPacketVector itself and then builds Packets on it -- BM_PacketPureParsing's pattern,
+ * Examples/PcapPlusPlus-benchmark/benchmark-google.cpp:231-260 -- pays one GPU round trip for the whole vector, not
+ * one per packet. The mutex guards the pending list and the group membership fields of registered RawPackets. */
+class OwnedRegistry
+{
+public:
+	static OwnedRegistry& instance()
+	{
+		static OwnedRegistry* r = new OwnedRegistry();  // never destroyed, like the Service
+		return *r;
+	}
+	inline void add(RawPacket* r);
+	inline void remove(RawPacket* r);
+	/* the group and index of r's records for k (r is registered; parses the pending RawPackets if r is one) */
+	inline const Records* recordsFor(RawPacket* r, ParseKey k, uint32_t* index);
+
+private:
+	static constexpr size_t npos = ~(size_t)0;
+	std::mutex m_Mu;
+	std::vector<RawPacket*> m_Pending;  // nullptr: removed since
+	size_t m_Removed = 0;
+	inline void compact();
+};
 }  // namespace detail
 
 /* pcpp::RawPacket (Packet++/header/RawPacket.h:288-566): a packet's bytes, lengths, timestamp and link type.
- * A RawPacket filled by PcapFileReaderDevice::getNextPacket refers to the packet's bytes in the reader's memory map
- * and to the page of GPU records they were parsed into; it keeps both alive (no copy is made). One made from the
- * caller's bytes (the constructors / setRawData) owns them when takeOwnership is set, as in the reference. The
- * bytes are read-only (packet crafting is outside the engine). */
+ * A RawPacket filled by a reader (getNextPacket / getNextPackets) refers to the packet's bytes in the reader's memory
+ * map and to the page of GPU records they were parsed into; it keeps both alive (no copy is made). One made from the
+ * caller's bytes (the constructors / setRawData) owns them when takeOwnership is set, as in the reference, and is
+ * parsed on the GPU together with the caller's other pending RawPackets when the first Packet is built on one of them
+ * (detail::OwnedRegistry). A copy owns a copy of the bytes and of the packet's records, never the page (RawPacket.cpp
+ * copyDataFrom). The bytes are read-only (packet crafting is outside the engine). */
 class RawPacket
 {
 public:
@@ -634,7 +684,6 @@ public:
 		setRawData(pRawData, rawDataLen, takeOwnership, timestamp, layerType);
 	}
 	virtual ~RawPacket() { release(); }
-	/* copies share a reader page (its bytes are immutable); the caller's own bytes are copied (RawPacket.cpp) */
 	RawPacket(const RawPacket& other) { copyFrom(other); }
 	RawPacket& operator=(const RawPacket& other)
 	{
@@ -664,6 +713,8 @@ public:
 		m_OwnsRawData = takeOwnership;
 		m_LinkLayerType = layerType;
 		m_RawPacketSet = true;
+		if (m_RawData != nullptr)
+			detail::OwnedRegistry::instance().add(this);
 		return true;
 	}
 
@@ -681,9 +732,12 @@ public:
 private:
 	friend class PcapFileReaderDevice;
 	friend class Packet;
+	friend class detail::OwnedRegistry;
 
 	void release()
 	{
+		if (m_Registered)
+			detail::OwnedRegistry::instance().remove(this);
 		if (m_OwnsRawData)
 			delete[] m_RawData;
 		m_RawData = nullptr;
@@ -692,6 +746,23 @@ private:
 		m_OwnsRawData = m_RawPacketSet = false;
 		m_Page.reset();
 		m_Index = 0;
+		m_Copied.reset();
+	}
+	/* the records of this packet for its page's parse options, if that page has been parsed */
+	std::shared_ptr<const detail::CopiedRecords> copyRecords() const
+	{
+		if (m_Copied != nullptr)
+			return m_Copied;
+		if (m_Registered || m_Page == nullptr)
+			return nullptr;  // the caller's own bytes: a group's fields are written under the registry's lock
+		const detail::Records* r = m_Page->primary.load(std::memory_order_acquire);
+		if (r == nullptr)
+			return nullptr;
+		auto c = std::make_shared<detail::CopiedRecords>();
+		c->key = r->key;
+		c->sum = r->sum[m_Index];
+		std::memcpy(c->lay, r->lay + (size_t)m_Index * PCPPX_MAX_LAYERS, sizeof(c->lay));
+		return c;
 	}
 	void copyFrom(const RawPacket& o)
 	{
@@ -700,23 +771,23 @@ private:
 		m_TsNs = o.m_TsNs;
 		m_LinkLayerType = o.m_LinkLayerType;
 		m_RawPacketSet = o.m_RawPacketSet;
-		m_Page = o.m_Page;
-		m_Index = o.m_Index;
-		if (o.m_Page != nullptr || o.m_RawData == nullptr)
-		{
-			m_RawData = o.m_RawData;
-			m_OwnsRawData = false;
+		if (o.m_RawData == nullptr)
 			return;
-		}
 		uint8_t* copy = new uint8_t[o.m_RawDataLen > 0 ? o.m_RawDataLen : 1];
 		std::memcpy(copy, o.m_RawData, o.m_RawDataLen > 0 ? (size_t)o.m_RawDataLen : 0);
 		m_RawData = copy;
 		m_OwnsRawData = true;
+		m_Copied = o.copyRecords();
+		detail::OwnedRegistry::instance().add(this);
 	}
 	/* getNextPacket's per-packet step: point at packet i of a page (the page pointer changes once per page) */
 	void setFromPage(const std::shared_ptr<detail::Page>& pg, uint32_t i)
 	{
-		if (m_OwnsRawData)
+		if (m_Registered || m_Copied != nullptr || (m_Page != nullptr && m_Page->group))
+		{
+			release();
+		}
+		else if (m_OwnsRawData)
 		{
 			delete[] m_RawData;
 			m_OwnsRawData = false;
@@ -739,14 +810,303 @@ private:
 	uint64_t m_TsNs = 0;
 	bool m_OwnsRawData = false;
 	bool m_RawPacketSet = false;
+	bool m_Registered = false;  // the caller's own bytes: in detail::OwnedRegistry (pending or in a group)
 	LinkLayerType m_LinkLayerType = LINKTYPE_ETHERNET;
-	std::shared_ptr<detail::Page> m_Page;  // set when the packet came from a reader
+	std::shared_ptr<detail::Page> m_Page;  // a reader's page, or (registered) the group this packet was parsed in
 	uint32_t m_Index = 0;
+	size_t m_PendingSlot = ~(size_t)0;                   // registered, not yet parsed: the pending-list slot
+	std::shared_ptr<const detail::CopiedRecords> m_Copied;  // records copied with the bytes (copy constructor)
 };
 
-/* A batch of raw packets back to back in one buffer: packet i = data[offsets[i], offsets[i] + caplens[i]).
- * The batch prepass's container (the role of pcpp::RawPacketVector, Packet++/header/RawPacket.h) for Engine::parse. */
-struct RawPacketVector
+namespace detail
+{
+inline void OwnedRegistry::add(RawPacket* r)
+{
+	std::lock_guard<std::mutex> g(m_Mu);
+	r->m_Registered = true;
+	r->m_PendingSlot = m_Pending.size();
+	m_Pending.push_back(r);
+}
+
+inline void OwnedRegistry::compact()
+{
+	size_t w = 0;
+	for (RawPacket* p : m_Pending)
+		if (p != nullptr)
+		{
+			p->m_PendingSlot = w;
+			m_Pending[w++] = p;
+		}
+	m_Pending.resize(w);
+	m_Removed = 0;
+}
+
+inline void OwnedRegistry::remove(RawPacket* r)
+{
+	std::shared_ptr<Page> grp;
+	uint32_t idx = 0;
+	{
+		std::lock_guard<std::mutex> g(m_Mu);
+		if (r->m_PendingSlot != npos)
+		{
+			m_Pending[r->m_PendingSlot] = nullptr;
+			if (++m_Removed > 4096 && m_Removed * 2 > m_Pending.size())
+				compact();
+		}
+		r->m_PendingSlot = npos;
+		r->m_Registered = false;
+		if (r->m_Page != nullptr && r->m_Page->group)
+		{
+			grp = std::move(r->m_Page);
+			idx = r->m_Index;
+		}
+	}
+	if (grp != nullptr)
+	{
+		std::lock_guard<std::mutex> gl(grp->groupMu);  // waits for a parse of the group in flight
+		grp->caplens[idx] = 0;
+	}
+}
+
+inline const Records* OwnedRegistry::recordsFor(RawPacket* r, ParseKey k, uint32_t* index)
+{
+	std::shared_ptr<Page> grp;
+	std::vector<std::shared_ptr<Page>> fresh;  // groups made here, parsed below (their groupMu held)
+	{
+		std::lock_guard<std::mutex> g(m_Mu);
+		if (r->m_PendingSlot != npos)
+		{
+			// every pending RawPacket -> one group per link type, in the order they were registered
+			std::map<LinkLayerType, std::vector<RawPacket*>> byType;
+			for (RawPacket* p : m_Pending)
+				if (p != nullptr)
+					byType[p->m_LinkLayerType].push_back(p);
+			m_Pending.clear();
+			m_Removed = 0;
+			for (auto& kv : byType)
+			{
+				auto pg = std::make_shared<Page>();
+				pg->group = true;
+				pg->linkType = kv.first;
+				const std::vector<RawPacket*>& mem = kv.second;
+				uintptr_t lo = ~(uintptr_t)0, hi = 0;
+				for (RawPacket* p : mem)
+				{
+					const uintptr_t a = reinterpret_cast<uintptr_t>(p->m_RawData);
+					const uint32_t len = p->m_RawDataLen > 0 ? (uint32_t)p->m_RawDataLen : 0;
+					lo = a < lo ? a : lo;
+					hi = a + len > hi ? a + len : hi;
+				}
+				pg->n = (uint32_t)mem.size();
+				pg->base = reinterpret_cast<const uint8_t*>(lo);
+				pg->dataLen = hi - lo;
+				pg->offsets.resize(mem.size());
+				pg->caplens.resize(mem.size());
+				for (uint32_t i = 0; i < pg->n; ++i)
+				{
+					RawPacket* p = mem[i];
+					pg->offsets[i] = reinterpret_cast<uintptr_t>(p->m_RawData) - lo;
+					pg->caplens[i] = p->m_RawDataLen > 0 ? (uint32_t)p->m_RawDataLen : 0;
+					p->m_Page = pg;
+					p->m_Index = i;
+					p->m_PendingSlot = npos;
+				}
+				pg->state.store(1);  // parsed below; a Packet on another member waits for it
+				pg->groupMu.lock();
+				fresh.push_back(std::move(pg));
+			}
+		}
+		grp = r->m_Page;
+		*index = r->m_Index;
+	}
+	for (auto& pg : fresh)
+	{
+		std::unique_ptr<Records> rec;
+		int err = PCPPX_OK;
+		try
+		{
+			rec = pg->parseRecords(k);
+		}
+		catch (const Error& e)
+		{
+			err = e.code();
+		}
+		catch (const std::bad_alloc&)
+		{
+			err = PCPPX_E_NOMEM;
+		}
+		pg->groupMu.unlock();
+		{
+			std::lock_guard<std::mutex> g(pg->mu);
+			pg->primaryOwned = std::move(rec);
+			pg->error = err;
+			pg->primary.store(pg->primaryOwned.get(), std::memory_order_release);
+			pg->state.store(2);
+		}
+		pg->cv.notify_all();
+	}
+	const Records* rec = grp->primary.load(std::memory_order_acquire);
+	if (rec != nullptr && rec->key == k)
+		return rec;
+	return grp->recordsFor(k);
+}
+}  // namespace detail
+
+/* pcpp::PointerVector (Common++/header/PointerVector.h:44-350): a vector of owned pointers; the elements are freed
+ * when removed or when the vector is destroyed, and a copy of the vector copies the elements (clone() for polymorphic
+ * ones). */
+template <typename T, typename Deleter = std::default_delete<T>>
+class PointerVector
+{
+public:
+	using VectorIterator = typename std::vector<T*>::iterator;
+	using ConstVectorIterator = typename std::vector<T*>::const_iterator;
+
+	PointerVector() = default;
+	PointerVector(const PointerVector& other) : m_Vector(deepCopy(other.m_Vector)) {}
+	PointerVector(PointerVector&& other) noexcept : m_Vector(std::move(other.m_Vector)) { other.m_Vector.clear(); }
+	~PointerVector() { freeAll(); }
+	PointerVector& operator=(const PointerVector& other)
+	{
+		if (this != &other)
+		{
+			std::vector<T*> copy = deepCopy(other.m_Vector);
+			freeAll();
+			m_Vector = std::move(copy);
+		}
+		return *this;
+	}
+	PointerVector& operator=(PointerVector&& other) noexcept
+	{
+		if (this != &other)
+		{
+			freeAll();
+			m_Vector = std::move(other.m_Vector);
+			other.m_Vector.clear();
+		}
+		return *this;
+	}
+
+	void clear()
+	{
+		freeAll();
+		m_Vector.clear();
+	}
+	void pushBack(std::nullptr_t, bool = true) = delete;
+	/* takes ownership of element (freed here if the push fails and freeElementOnError is set) */
+	void pushBack(T* element, bool freeElementOnError = true)
+	{
+		if (element == nullptr)
+			throw std::invalid_argument("Element is nullptr");
+		try
+		{
+			m_Vector.push_back(element);
+		}
+		catch (const std::exception&)
+		{
+			if (freeElementOnError)
+				Deleter()(element);
+			throw;
+		}
+	}
+	void pushBack(std::unique_ptr<T> element)
+	{
+		if (!element)
+			throw std::invalid_argument("Element is nullptr");
+		m_Vector.push_back(element.get());
+		element.release();
+	}
+	VectorIterator begin() { return m_Vector.begin(); }
+	ConstVectorIterator begin() const { return m_Vector.begin(); }
+	VectorIterator end() { return m_Vector.end(); }
+	ConstVectorIterator end() const { return m_Vector.end(); }
+	size_t size() const { return m_Vector.size(); }
+	size_t capacity() const { return m_Vector.capacity(); }
+	void reserve(size_t newSize) { m_Vector.reserve(newSize); }
+	T* front() const { return m_Vector.front(); }
+	T* back() const { return m_Vector.back(); }
+	/* frees the element at position; returns the iterator after it */
+	VectorIterator erase(VectorIterator position)
+	{
+		Deleter()(*position);
+		return m_Vector.erase(position);
+	}
+	VectorIterator erase(ConstVectorIterator first, ConstVectorIterator last)
+	{
+		for (auto it = first; it != last; ++it)
+			Deleter()(*it);
+		return m_Vector.erase(first, last);
+	}
+	/* removes the element at position without freeing it (the caller owns it); position moves to the next one */
+	T* getAndRemoveFromVector(VectorIterator& position)
+	{
+		T* result = *position;
+		position = m_Vector.erase(position);
+		return result;
+	}
+	std::unique_ptr<T> getAndDetach(size_t index)
+	{
+		auto it = m_Vector.begin() + (std::ptrdiff_t)index;
+		return getAndDetach(it);
+	}
+	std::unique_ptr<T> getAndDetach(VectorIterator& position)
+	{
+		std::unique_ptr<T> result(*position);
+		position = m_Vector.erase(position);
+		return result;
+	}
+	std::unique_ptr<T> getAndDetach(const VectorIterator& position)
+	{
+		std::unique_ptr<T> result(*position);
+		m_Vector.erase(position);
+		return result;
+	}
+	T* at(int index) const { return m_Vector.at((size_t)index); }
+	T** data() { return m_Vector.data(); }
+
+private:
+	template <class U>
+	static auto copyOne(const U& obj, int) -> decltype(obj.clone(), (U*)nullptr)
+	{
+		return obj.clone();
+	}
+	template <class U>
+	static U* copyOne(const U& obj, long)
+	{
+		return new U(obj);
+	}
+	static std::vector<T*> deepCopy(const std::vector<T*>& src)
+	{
+		std::vector<T*> out;
+		out.reserve(src.size());
+		try
+		{
+			for (T* p : src)
+				out.push_back(copyOne<T>(*p, 0));
+		}
+		catch (...)
+		{
+			for (T* p : out)
+				Deleter()(p);
+			throw;
+		}
+		return out;
+	}
+	void freeAll()
+	{
+		for (T* p : m_Vector)
+			Deleter()(p);
+	}
+	std::vector<T*> m_Vector;
+};
+
+/* pcpp::RawPacketVector (Pcap++/header/Device.h:14): what IFileReaderDevice::getNextPackets fills */
+using RawPacketVector = PointerVector<RawPacket>;
+
+/* A batch of raw packets back to back in one buffer: packet i = data[offsets[i], offsets[i] + caplens[i]). The batch
+ * API's container (Engine::parse / Engine::filter, PcapFileReaderDevice::getNextBatch): one copy of the bytes in
+ * one buffer, the shape pcppx_batch takes. */
+struct RawBatch
 {
 	buffer<uint8_t> data;
 	buffer<uint64_t> offsets;
@@ -780,7 +1140,6 @@ struct RawPacketVector
 			                linkType, 0 };
 	}
 };
-using RawBatch = RawPacketVector;
 
 /* PcapFileReaderDevice / PcapNgFileReaderDevice (Pcap++/header/PcapFileDevice.h): the format (pcap or pcapng) comes
  * from the file's first bytes (IFileReaderDevice::createReader, PcapFileDevice.cpp:546-583). open() starts the
@@ -851,10 +1210,30 @@ public:
 		return k;
 	}
 
-	/* IFileReaderDevice::getNextPackets(RawPacketVector&, int numOfPacketsToRead) (PcapFileDevice.cpp:604-624), into
-	 * the batch container: replaces `batch` with the next packets (at most numOfPacketsToRead, -1 = as many as
-	 * maxBytes holds; one link type per batch); returns the count, 0 at the end of the capture. */
-	int getNextPackets(RawPacketVector& batch, int numOfPacketsToRead = -1, uint64_t maxBytes = 256ull << 20)
+	/* IFileReaderDevice::getNextPackets(RawPacketVector&, int numOfPacketsToRead = -1) (PcapFileDevice.cpp:604-624):
+	 * appends the next packets (all that remain when numOfPacketsToRead < 0) to packetVec as new RawPackets and returns
+	 * how many. Each refers to its bytes in the map and to its page of GPU records (no copy), like getNextPacket's. */
+	int getNextPackets(RawPacketVector& packetVec, int numOfPacketsToRead = -1)
+	{
+		int numOfPacketsRead = 0;
+		for (; numOfPacketsToRead < 0 || numOfPacketsRead < numOfPacketsToRead; numOfPacketsRead++)
+		{
+			if (m_Cur == nullptr || m_Pos >= m_Cur->n)
+			{
+				if (!advance())
+					break;
+			}
+			std::unique_ptr<RawPacket> p(new RawPacket());
+			p->setFromPage(m_Cur, m_Pos++);
+			packetVec.pushBack(std::move(p));
+		}
+		return numOfPacketsRead;
+	}
+
+	/* The batch API's read (one copy of the bytes into one buffer, the shape pcppx_batch takes): replaces `batch` with
+	 * the next packets (at most numOfPacketsToRead, -1 = as many as maxBytes holds; one link type per batch); returns
+	 * the count, 0 at the end of the capture. */
+	int getNextBatch(RawBatch& batch, int numOfPacketsToRead = -1, uint64_t maxBytes = 256ull << 20)
 	{
 		batch.clear();
 		int n = 0;
@@ -886,6 +1265,52 @@ public:
 			++n;
 		}
 		return n;
+	}
+
+	/* IFileDevice::getFileSize (PcapFileDevice.cpp:598-602) */
+	uint64_t getFileSize() const
+	{
+		std::ifstream f(m_FileName, std::ifstream::ate | std::ifstream::binary);
+		return f ? (uint64_t)f.tellg() : 0;
+	}
+
+	/* IFileReaderDevice::createReader (PcapFileDevice.cpp:546-583): the reader for the file's format, from its first
+	 * bytes (detectFileFormat, :403-458) -- pcap (micro- or nanosecond magic, either byte order) and pcapng. Throws
+	 * std::runtime_error when the file cannot be opened or its format is not one of those: Kuznetzov's modified pcap
+	 * (the reference's switch has no case for it either), zstd-compressed pcapng (as a reference build without zstd
+	 * support) and snoop (outside this engine). The device is not opened. */
+	static std::unique_ptr<PcapFileReaderDevice> createReader(const std::string& fileName)
+	{
+		std::ifstream f(fileName, std::ios_base::binary);
+		if (f.fail())
+			throw std::runtime_error("Could not open file: " + fileName);
+		uint8_t b[8] = { 0 };
+		f.read(reinterpret_cast<char*>(b), sizeof(b));
+		const std::streamsize got = f.gcount();
+		uint32_t magic = 0;
+		std::memcpy(&magic, b, 4);
+		if (got >= 4)
+		{
+			if (magic == 0xa1b2c3d4u || magic == 0xd4c3b2a1u || magic == 0xa1b23c4du || magic == 0x4d3cb2a1u ||
+			    magic == 0x0A0D0D0Au)
+				return std::unique_ptr<PcapFileReaderDevice>(new PcapFileReaderDevice(fileName));
+			if (magic == 0x28B52FFDu || magic == 0xFD2FB528u)
+				throw std::runtime_error("PcapNG Zstd compressed files are not supported in this build of PcapPlusPlus");
+		}
+		throw std::runtime_error("File format of " + fileName + " is not supported");
+	}
+	/* IFileReaderDevice::tryCreateReader (PcapFileDevice.cpp:585-596): createReader, or nullptr where it throws */
+	static std::unique_ptr<PcapFileReaderDevice> tryCreateReader(const std::string& fileName)
+	{
+		try
+		{
+			return createReader(fileName);
+		}
+		catch (const std::runtime_error& e)
+		{
+			std::fprintf(stderr, "%s\n", e.what());  // PCPP_LOG_ERROR
+			return nullptr;
+		}
 	}
 
 private:
@@ -1176,6 +1601,21 @@ private:
 		m_Raw = raw->m_RawData;
 		m_Caplen = raw->m_RawDataLen > 0 ? (uint32_t)raw->m_RawDataLen : 0;
 		const detail::ParseKey k{ parseUntil, parseUntilLayer };
+		if (raw->m_Copied != nullptr && raw->m_Copied->key == k)
+		{
+			m_Sum = &raw->m_Copied->sum;  // records copied with the bytes
+			m_Layers = raw->m_Copied->lay;
+			return;
+		}
+		if (raw->m_Registered)
+		{
+			// the caller's own bytes: parsed with every other pending RawPacket in one batch, or already in a group
+			uint32_t idx = 0;
+			const detail::Records* r = detail::OwnedRegistry::instance().recordsFor(raw, k, &idx);
+			m_Sum = r->sum + idx;
+			m_Layers = r->lay + (size_t)idx * PCPPX_MAX_LAYERS;
+			return;
+		}
 		if (detail::Page* p = raw->m_Page.get())
 		{
 			const detail::Records* r = p->primary.load(std::memory_order_acquire);
@@ -1183,23 +1623,8 @@ private:
 				r = p->recordsFor(k);
 			m_Sum = r->sum + raw->m_Index;
 			m_Layers = r->lay + (size_t)raw->m_Index * PCPPX_MAX_LAYERS;
-			return;
 		}
-		if (m_Raw == nullptr)
-			return;  // no data: createFirstLayer builds nothing (Packet.cpp:88-94)
-		// the caller's own bytes: a one-packet batch
-		m_Own = std::make_shared<detail::OwnedRecords>();
-		const pcppx_opts o = k.opts();
-		const uint64_t off = 0;
-		const pcppx_batch b{ m_Raw, &off, &m_Caplen, m_Caplen, 1, raw->m_LinkLayerType, 0 };
-		pcppx_records rec{};
-		rec.summary = &m_Own->sum;
-		rec.layers = m_Own->lay;
-		detail::Service::instance().parse(b, o, rec);
-		detail::completeOnHost(detail::hostParser().load(), m_Raw, &off, &m_Caplen, 1, raw->m_LinkLayerType, o,
-		                       &m_Own->sum, m_Own->lay);
-		m_Sum = &m_Own->sum;
-		m_Layers = m_Own->lay;
+		// else no data: createFirstLayer builds nothing (Packet.cpp:88-94)
 	}
 
 	const pcppx_summary* m_Sum = nullptr;
@@ -1207,7 +1632,6 @@ private:
 	uint8_t m_MaxLayers = 0;
 	const uint8_t* m_Raw = nullptr;
 	uint32_t m_Caplen = 0;
-	std::shared_ptr<detail::OwnedRecords> m_Own;  // a RawPacket that did not come from a reader
 	std::shared_ptr<RawPacket> m_OwnedRaw;        // freeRawPacket
 };
 using ParsedPacket = Packet;
@@ -1223,11 +1647,11 @@ inline uint32_t hash2Tuple(const Packet* packet)
 	return packet->summary().hash2;
 }
 
-/* Records of one parsed batch (owns them); indexes into the RawPacketVector it was parsed from. */
+/* Records of one parsed batch (owns them); indexes into the RawBatch it was parsed from. */
 class ParsedBatch
 {
 public:
-	ParsedBatch(const RawPacketVector& raw, uint8_t maxLayers)
+	ParsedBatch(const RawBatch& raw, uint8_t maxLayers)
 	    : m_Raw(&raw), m_MaxLayers(maxLayers), summaries(raw.size()), layers(raw.size() * (size_t)maxLayers)
 	{}
 	size_t size() const { return summaries.size(); }
@@ -1259,7 +1683,7 @@ public:
 	size_t hostParsed = 0;
 
 private:
-	const RawPacketVector* m_Raw;
+	const RawBatch* m_Raw;
 	uint8_t m_MaxLayers;
 
 public:
@@ -1316,13 +1740,13 @@ public:
 
 	/* Packet(&rawPacket, options) for every packet of the batch, host to host through HBM; flagged packets are
 	 * completed by the host parser when one is set */
-	ParsedBatch parse(const RawPacketVector& batch, const PacketParseOptions& options = PacketParseOptions()) const
+	ParsedBatch parse(const RawBatch& batch, const PacketParseOptions& options = PacketParseOptions()) const
 	{
 		ParsedBatch out(batch, options.maxLayers);
 		parseInto(batch, options, out);
 		return out;
 	}
-	void parseInto(const RawPacketVector& batch, const PacketParseOptions& options, ParsedBatch& out) const
+	void parseInto(const RawBatch& batch, const PacketParseOptions& options, ParsedBatch& out) const
 	{
 		const pcppx_batch b = batch.toC();
 		const pcppx_opts o = options.toC();
@@ -1337,7 +1761,7 @@ public:
 
 	/* FilterTraffic's whole worker on the device (AppWorkerThread.h:85-139): matched[i] = 1 for packets to send on;
 	 * the flow table persists across calls until resetFilter() */
-	pcppx_packet_stats filter(const RawPacketVector& batch, const MatchSpec& spec, std::vector<uint8_t>& matched)
+	pcppx_packet_stats filter(const RawBatch& batch, const MatchSpec& spec, std::vector<uint8_t>& matched)
 	{
 		matched.assign(batch.size(), 0);
 		const pcppx_batch b = batch.toC();

@@ -9,6 +9,15 @@
  *       list of variants, applied to packet i in turn: full | tcp | ip | osi2 | osi3 | osi4 | own | copy | free);
  *       writes per packet and variant the pcppx_summary (32 B) and the PCPPX_MAX_LAYERS layer records the Packet
  *       holds (zero past its chain).  (GPU.)
+ *   facade_check parsevec <capture> <outfile> <plan> <reader|own|copy>
+ *       the RawPacketVector forms (Examples/PcapPlusPlus-benchmark/benchmark-google.cpp:231-260): reader =
+ *       IFileReaderDevice::tryCreateReader + getNextPackets(vector) and Packet(vector.at(i), ...) per packet; own = the
+ *       caller's own RawPackets (heap copies of the bytes, takeOwnership) pushed into a RawPacketVector, then the
+ *       Packets; copy = a copy of the reader's vector (PointerVector's deep copy: every RawPacket copied, records
+ *       with it). Writes the records as `parse` does; prints {"gpu_parses": N} (pcppx_parse_batch_host calls the
+ *       per-packet entry points made).  (GPU.)
+ *   facade_check create <file>
+ *       IFileReaderDevice::tryCreateReader: prints "null", "noopen" or "packets N" (getNextPacket to the end).  (CPU.)
  *   facade_check time <capture> <reps>
  *       the phases of the reference benchmark's packet loop (open, first getNextPacket, first Packet(&raw, TCP), the
  *       rest of the loop, close), averaged over reps after one untimed run; one JSON line, microseconds.  (GPU.)
@@ -21,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -85,11 +95,22 @@ int readMode(const std::string& mode, const std::string& outdir, int nfiles, cha
 			for (auto* p : arr)
 				delete p;
 		}
+		else if (mode == "vector" || mode.rfind("vector:", 0) == 0)
+		{
+			// getNextPackets(RawPacketVector&) appends page-bound RawPackets: all at once, or N per call
+			const int n = mode == "vector" ? -1 : std::atoi(mode.c_str() + 7);
+			pcppx::RawPacketVector v;
+			while (reader.getNextPackets(v, n) > 0 && n > 0)
+			{
+			}
+			for (pcppx::RawPacket* p : v)
+				putRaw(f, *p);
+		}
 		else if (mode.rfind("batch:", 0) == 0)
 		{
 			const int n = std::atoi(mode.c_str() + 6);
-			pcppx::RawPacketVector b;
-			while (reader.getNextPackets(b, n) > 0)
+			pcppx::RawBatch b;
+			while (reader.getNextBatch(b, n) > 0)
 				for (size_t i = 0; i < b.size(); ++i)
 				{
 					const uint64_t t = b.timestampsNs[i];
@@ -180,6 +201,78 @@ int parseMode(const char* capture, const char* outfile, const std::string& plan)
 	std::fclose(f);
 	return 0;
 }
+void putVariant(std::FILE* f, pcppx::RawPacket* raw, const std::string& v)
+{
+	if (v == "full")
+		putPacket(f, pcppx::Packet(raw));
+	else if (v == "tcp")
+		putPacket(f, pcppx::Packet(raw, pcppx::TCP));
+	else if (v == "ip")
+		putPacket(f, pcppx::Packet(raw, pcppx::IP));
+	else if (v == "osi3")
+		putPacket(f, pcppx::Packet(raw, pcppx::OsiModelNetworkLayer));
+	else if (v == "osi2")
+		putPacket(f, pcppx::Packet(raw, pcppx::OsiModelDataLinkLayer));
+	else if (v == "osi4")
+		putPacket(f, pcppx::Packet(raw, false, pcppx::UnknownProtocol, pcppx::OsiModelTransportLayer));
+	else
+		throw std::runtime_error("variant " + v);
+}
+
+int parseVecMode(const char* capture, const char* outfile, const std::string& plan, const std::string& how)
+{
+	std::vector<std::string> variants;
+	for (size_t a = 0; a <= plan.size();)
+	{
+		size_t b = plan.find(',', a);
+		if (b == std::string::npos)
+			b = plan.size();
+		variants.push_back(plan.substr(a, b - a));
+		a = b + 1;
+	}
+	auto reader = pcppx::IFileReaderDevice::tryCreateReader(capture);
+	if (reader == nullptr || !reader->open())
+		return 4;
+	pcppx::RawPacketVector rawPackets;
+	reader->getNextPackets(rawPackets);
+	pcppx::RawPacketVector other;
+	pcppx::RawPacketVector* use = &rawPackets;
+	if (how == "own")
+	{
+		for (pcppx::RawPacket* p : rawPackets)
+		{
+			const int len = p->getRawDataLen();
+			uint8_t* bytes = new uint8_t[len > 0 ? len : 1];
+			std::memcpy(bytes, p->getRawData(), (size_t)(len > 0 ? len : 0));
+			other.pushBack(new pcppx::RawPacket(bytes, len, p->getPacketTimeStamp(), true, p->getLinkLayerType()));
+		}
+		rawPackets.clear();  // the reader's pages go: only the caller's own bytes remain
+		use = &other;
+	}
+	else if (how == "copy")
+	{
+		// build the first Packet on the reader's vector (its first page parsed), then copy the whole vector
+		{
+			pcppx::Packet first(rawPackets.at(0));
+			(void)first;
+		}
+		other = rawPackets;
+		rawPackets.clear();
+		use = &other;
+	}
+	else if (how != "reader")
+		return 1;
+	std::FILE* f = std::fopen(outfile, "wb");
+	if (f == nullptr)
+		return 2;
+	for (size_t i = 0; i < use->size(); ++i)
+		putVariant(f, use->at((int)i), variants[i % variants.size()]);
+	std::fclose(f);
+	std::printf("{\"packets\": %zu, \"gpu_parses\": %llu}\n", use->size(),
+	            (unsigned long long)pcppx::detail::Service::instance().parses());
+	return 0;
+}
+
 int timeMode(const char* capture, int reps)
 {
 	using clk = std::chrono::steady_clock;
@@ -248,6 +341,28 @@ int main(int argc, char** argv)
 			return readMode(argv[2], argv[3], argc - 4, argv + 4);
 		if (argc == 4 && std::string(argv[1]) == "time")
 			return timeMode(argv[2], std::atoi(argv[3]));
+		if (argc == 3 && std::string(argv[1]) == "create")
+		{
+			auto reader = pcppx::IFileReaderDevice::tryCreateReader(argv[2]);
+			if (reader == nullptr)
+			{
+				std::printf("null\n");
+				return 0;
+			}
+			if (!reader->open())
+			{
+				std::printf("noopen\n");
+				return 0;
+			}
+			pcppx::RawPacket raw;
+			size_t n = 0;
+			while (reader->getNextPacket(raw))
+				++n;
+			std::printf("packets %zu\n", n);
+			return 0;
+		}
+		if (argc == 6 && std::string(argv[1]) == "parsevec")
+			return parseVecMode(argv[2], argv[3], argv[4], argv[5]);
 		if (argc == 5 && std::string(argv[1]) == "parse")
 			return parseMode(argv[2], argv[3], argv[4]);
 	}
@@ -255,6 +370,11 @@ int main(int argc, char** argv)
 	{
 		std::fprintf(stderr, "%s\n", e.what());
 		return 6;
+	}
+	catch (const std::exception& e)
+	{
+		std::fprintf(stderr, "%s\n", e.what());
+		return 7;
 	}
 	std::fprintf(stderr, "usage: facade_check read <mode> <outdir> <capture>... | parse <capture> <out> <plan>\n");
 	return 1;

@@ -60,10 +60,11 @@ def _read_dump(path: Path):
     return out
 
 
-@pytest.mark.parametrize("mode", ["packet", "burst:64", "batch:333"])
+@pytest.mark.parametrize("mode", ["packet", "burst:64", "batch:333", "vector", "vector:333"])
 def test_reader_entry_points_equal_reference(built, tmp_path, mode):
-    """getNextPacket(RawPacket&) / receivePackets(RawPacket**, 64) / getNextPackets(RawPacketVector&, 333) over every
-    fixture, crafted case and mutation of the ingest golden set: the reference readers' packets, field for field."""
+    """getNextPacket(RawPacket&) / receivePackets(RawPacket**, 64) / getNextBatch(RawBatch&, 333) /
+    getNextPackets(RawPacketVector&) (all at once, and 333 per call) over every fixture, crafted case and mutation of the
+    ingest golden set: the reference readers' packets, field for field."""
     from test_ingest import _case_bytes, _golden
 
     g, starts = _golden()
@@ -132,6 +133,54 @@ def test_benchmark_packet_loop_is_the_references():
                  "m_Stats.collectStats(parsedPacket);", "pcapWriter->writePacket(*packetArr[i]);"):
         w = tok(line)
         assert any(ft[i:i + len(w)] == w for i in range(len(ft))), line
+
+
+def test_benchmark_google_loops_are_the_references():
+    """examples/benchmark_google_loops.inc holds BM_FileRead, BM_PacketParsing and BM_PacketPureParsing of
+    Examples/PcapPlusPlus-benchmark/benchmark-google.cpp:15-64,149-207,209-264 token for token (signature and body;
+    comments aside): the parse loops of the reference's third caller compile unchanged against the facade
+    (examples/benchmark_google.cpp, `namespace pcpp = pcppx`) and against the reference (oracle/ref_benchmark_google.cpp)."""
+    ref = REF / "Examples" / "PcapPlusPlus-benchmark" / "benchmark-google.cpp"
+    if not ref.exists():
+        pytest.skip("/root/reference absent")
+    strip = lambda s: re.sub(r"//[^\n]*", "", s)  # noqa: E731
+    tok = lambda s: re.findall(r"[A-Za-z_][A-Za-z_0-9]*|::|->|\"(?:[^\"\\]|\\.)*\"|[^\s\w]", strip(s))  # noqa: E731
+    lines = ref.read_text().splitlines(keepends=True)
+    ours = tok((ROOT / "examples" / "benchmark_google_loops.inc").read_text())
+    for lo, hi, name in ((15, 64, "BM_FileRead"), (149, 207, "BM_PacketParsing"), (209, 264, "BM_PacketPureParsing")):
+        want = tok("".join(lines[lo - 1:hi]))
+        assert want[:4] == ["static", "void", name, "("] and want[-1] == "}", name
+        assert any(ours[i:i + len(want)] == want for i in range(len(ours))), f"{name} differs from the reference's"
+    # both programs include the same loops; the engine's aliases the namespace and nothing else
+    eng = (ROOT / "examples" / "benchmark_google.cpp").read_text()
+    assert '#include "benchmark_google_loops.inc"' in eng and "namespace pcpp = pcppx;" in eng
+    assert '#include "../examples/benchmark_google_loops.inc"' in (ROOT / "oracle" / "ref_benchmark_google.cpp").read_text()
+
+
+def test_create_reader_by_content(built, tmp_path):
+    """IFileReaderDevice::createReader / tryCreateReader (PcapFileDevice.cpp:546-596) pick the reader from the first
+    bytes: pcap (micro / nano, either byte order) and pcapng open; zstd, snoop, Kuznetzov-modified pcap, short and
+    missing files give nullptr (tryCreateReader), as in the reference built without zstd and (here) without snoop."""
+    b = synth.config(2, 10)
+    good = tmp_path / "a.pcap"
+    write_pcap(good, b)
+    raw = good.read_bytes()
+    cases = {"pcap": (raw, 10), "pcap_renamed.pcapng": (raw, 10),
+             "nano.pcap": (bytes.fromhex("4d3cb2a1") + raw[4:], 10),
+             "zstd.pcapng": (bytes.fromhex("28b52ffd") + raw[4:], None),
+             "kuz.pcap": (bytes.fromhex("34cdb2a1") + raw[4:], None),
+             "snoop": (b"snoop\0\0\0" + raw[8:], None), "short": (b"\xd4\xc3", None)}
+    import os
+    for name, (content, want) in cases.items():
+        f = tmp_path / name
+        f.write_bytes(content)
+        r = subprocess.run([str(built), "create", str(f)], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        got = r.stdout.strip()
+        assert got == ("null" if want is None else f"packets {want}"), (name, got)
+    r = subprocess.run([str(built), "create", str(tmp_path / "missing.pcap")], capture_output=True, text=True, timeout=60)
+    assert r.stdout.strip() == "null" and "Could not open file" in r.stderr
+    assert os.path.exists(good)
 
 
 # ---- GPU: Packet(RawPacket*, ...) records ----
@@ -207,6 +256,66 @@ def test_gpu_packet_from_own_bytes(built, tmp_path):
     rec = _run_plan(built, tmp_path, b, "own,full")
     ws, wl = _expected(b, "own,full")
     oracle.compare_exact(rec["sum"], rec["lay"], ws, wl)
+
+
+def _run_vec(built, tmp_path, batch, plan, how, host_parser=False):
+    f, o = tmp_path / "in.pcap", tmp_path / "rec.bin"
+    write_pcap(f, batch)
+    env = None
+    if host_parser:
+        import os
+
+        env = dict(os.environ, PCPPX_CHECK_HOST_PARSER=str(oracle.REF_SO))
+    r = subprocess.run([str(built), "parsevec", str(f), str(o), plan, how], capture_output=True, text=True, timeout=600,
+                       env=env)
+    assert r.returncode == 0, r.stderr
+    import json
+
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    rec = np.frombuffer(o.read_bytes(), REC)
+    assert len(rec) == batch.n == info["packets"]
+    return rec, info
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["reader", "own", "copy"])
+def test_gpu_packet_vector_equals_restatement(built, tmp_path, how):
+    """benchmark-google.cpp's preload-then-parse pattern (:231-260): getNextPackets(RawPacketVector&) into page-bound
+    RawPackets (reader), the caller's own RawPackets in a RawPacketVector (own: parsed together on the first Packet,
+    one GPU batch per link type and options -- never one per packet), and a deep copy of the reader's vector (copy:
+    bytes and records copied, no page kept); every Packet(vector.at(i), ...) equals the restatement's records."""
+    for plan in ("full", "full,tcp,osi3"):
+        for name, b in _captures():
+            rec, info = _run_vec(built, tmp_path, b, plan, how)
+            ws, wl = _expected(b, plan)
+            try:
+                oracle.compare_exact(rec["sum"], rec["lay"], ws, wl)
+            except AssertionError as e:
+                raise AssertionError(f"{name}/{plan}/{how}: {e}") from None
+            variants = len(set(plan.split(",")))
+            if how == "own":  # one group (one link type) parsed once per option set
+                assert info["gpu_parses"] == variants, (name, plan, info)
+            else:  # pages of 16k, 64k, 256k packets: each parsed once per option set (plus copies' groups)
+                pages = 1 + (b.n > 16384) + (b.n > 16384 + 65536)
+                assert info["gpu_parses"] <= pages * variants + (variants if how == "copy" else 0), (name, plan, info)
+
+
+@pytest.mark.gpu
+def test_gpu_packet_vector_host_parser_equals_reference(built, tmp_path):
+    """The caller's own RawPacketVector with the reference registered as host parser: every Packet equals the reference
+    Packet++'s chain and hashes (flagged packets completed on the host)."""
+    if not oracle.ref_available():
+        pytest.skip("reference library not built")
+    for name, b in _captures()[:-1]:
+        rec, _ = _run_vec(built, tmp_path, b, "full", "own", host_parser=True)
+        ws, wl = _expected(b, "full", reference=True)
+        nl = np.minimum(ws["n_layers"], abi.MAX_LAYERS)
+        for f in ("hash5", "hash5_dir", "hash2"):
+            assert np.array_equal(rec["sum"][f], ws[f]), f"{name}: {f}"
+        assert np.array_equal(rec["sum"]["n_layers"], nl), name
+        valid = np.arange(abi.MAX_LAYERS)[None, :] < nl[:, None]
+        for f in ("proto", "offset", "hdr_len", "data_len"):
+            assert not ((rec["lay"][f] != wl[f]) & valid).any(), f"{name}: layers.{f}"
 
 
 @pytest.mark.gpu

@@ -5,7 +5,10 @@ host memory (north_star: "the rate including the H2D/D2H copies must also be mea
    examples/bin/pcap_parse -- the engine's reader (zero-copy map batches, or the copying reader into page-locked
    buffers with --copy) overlapped with pcppx_parse_batch_host (chunked H2D, parse on the GPU, D2H into page-locked
    record arrays) -- for 8 layer rows + checksums and for summaries only.
-2. the drop-in benchmark: examples/bin/benchmark (the reference's PcapPlusPlus-benchmark loop with the batch prepass)
+2. the reference's Google-benchmark parse loops (benchmark-google.cpp:15-64,149-264, examples/benchmark_google_loops.inc)
+   over the facade (examples/bin/benchmark_google) beside the same loops over the reference Packet++
+   (oracle/_ref/benchmark_google_ref), on example.pcap and the 10M IMIX pcap (--only google: this part alone).
+3. the drop-in benchmark: examples/bin/benchmark (the reference's PcapPlusPlus-benchmark loop with the batch prepass)
    beside oracle/_ref/benchmark_ref (the reference's benchmark.cpp compiled unchanged, one core) on the config-1 10k
    pcap, the reference's example.pcap (frozen in tests/golden/capture_example.npz) and the 10M IMIX pcap.
 
@@ -65,11 +68,42 @@ def bench_pair(pcap: Path, reps: tuple[int, int], n: int, trials: int = 1) -> di
     return out
 
 
+def google_pair(pcap: Path, args: list[str], trials: int = 1) -> dict:
+    """The reference's Google-benchmark parse loops (examples/benchmark_google_loops.inc) over the engine's facade
+    (examples/bin/benchmark_google) and over the reference Packet++ built from source (oracle/_ref/benchmark_google_ref,
+    one core), alternating trial by trial; per benchmark the median of the trials' ns per iteration."""
+    progs = [(name, exe) for name, exe in (("reference", ROOT / "oracle" / "_ref" / "benchmark_google_ref"),
+                                           ("engine", ROOT / "examples" / "bin" / "benchmark_google")) if exe.exists()]
+    per: dict = {}
+    for _ in range(trials):
+        for name, exe in progs:
+            for ln in run([exe, "--pcap-file", pcap, *args], timeout=1500).strip().splitlines():
+                d = json.loads(ln)
+                if "name" in d and "ns_per_iteration" in d:
+                    per.setdefault(d["name"].split("/")[0], {}).setdefault(name, []).append(d)
+                elif "gpu_parses" in d:
+                    per.setdefault("gpu_parses", []).append(d["gpu_parses"])
+    out = {"file": pcap.name, "args": args, "trials": trials}
+    for bm, by in per.items():
+        if bm == "gpu_parses":
+            out[bm] = by
+            continue
+        out[bm] = {}
+        for name, ds in by.items():
+            ns = sorted(d["ns_per_iteration"] for d in ds)
+            out[bm][name] = {"ns_per_packet": ns[len(ns) // 2], "trials_ns": ns, "iterations": ds[-1]["iterations"]}
+        if "reference" in out[bm] and "engine" in out[bm]:
+            out[bm]["speedup"] = round(out[bm]["reference"]["ns_per_packet"] / out[bm]["engine"]["ns_per_packet"], 2)
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--packets", type=int, default=10_000_000)
     ap.add_argument("--out", default=None)
     ap.add_argument("--shm", default="/dev/shm")
+    ap.add_argument("--only", choices=("all", "google"), default="all",
+                    help="google: only the benchmark-google loops (example.pcap and the IMIX pcap)")
     args = ap.parse_args()
     res = {"cores": len(os.sched_getaffinity(0))}
     big = Path(args.shm) / f"pcppx_e2e_{os.getpid()}.pcap"
@@ -81,6 +115,23 @@ def main() -> None:
                             "gen_write_seconds": round(time.time() - t, 1), "where": "tmpfs (/dev/shm)"}
         del b
         print(json.dumps(res["imix_pcap"]), flush=True)
+        from conftest import GOLDEN, load_golden
+
+        ex, _ = load_golden(GOLDEN / "capture_example.npz")
+        exf = Path(args.shm) / f"pcppx_example_{os.getpid()}.pcap"
+        write_pcap(exf, ex)
+        # benchmark-google.cpp's loops: all three on example.pcap (the library's 0.5-s runs); the two parse loops on the
+        # IMIX pcap at fixed counts (the pure loop: three passes over the preloaded 10M packets)
+        res["google_example_pcap"] = google_pair(exf, ["--min-time", "0.5"], trials=3)
+        print("google_example", json.dumps(res["google_example_pcap"]), flush=True)
+        res["google_imix_pure"] = google_pair(big, ["--benchmark", "BM_PacketPureParsing", "--iterations",
+                                                    str(3 * args.packets)])
+        print("google_imix_pure", json.dumps(res["google_imix_pure"]), flush=True)
+        res["google_imix_parsing"] = google_pair(big, ["--benchmark", "BM_PacketParsing", "--iterations",
+                                                       str(args.packets)])
+        print("google_imix_parsing", json.dumps(res["google_imix_parsing"]), flush=True)
+        if args.only == "google":
+            raise StopIteration
         runs = {}
         for tag, extra in (("map_l8_csum", []), ("copy_l8_csum", ["--copy"]),
                            ("map_summary", ["--layers", "0", "--checksums", "0"]),
@@ -96,18 +147,16 @@ def main() -> None:
         res["benchmark_config1"] = bench_pair(c1, (10, 510), b1.n, trials=7)
         print("config1", json.dumps(res["benchmark_config1"]), flush=True)
         c1.unlink()
-        from conftest import GOLDEN, load_golden
-
-        ex, _ = load_golden(GOLDEN / "capture_example.npz")
-        exf = Path(args.shm) / f"pcppx_example_{os.getpid()}.pcap"
-        write_pcap(exf, ex)
         res["benchmark_example_pcap"] = bench_pair(exf, (10, 410), ex.n, trials=7)
         print("example.pcap", json.dumps(res["benchmark_example_pcap"]), flush=True)
-        exf.unlink()
         res["benchmark_imix_10M"] = bench_pair(big, (1, 3), args.packets, trials=3)
         print("imix", json.dumps(res["benchmark_imix_10M"]), flush=True)
+    except StopIteration:
+        pass
     finally:
         big.unlink(missing_ok=True)
+        for f in Path(args.shm).glob(f"pcppx_example_{os.getpid()}.pcap"):
+            f.unlink()
     line = json.dumps(res, indent=1)
     if args.out:
         Path(args.out).write_text(line + "\n")

@@ -13,6 +13,8 @@
 #   sq:<cfg>                       SQ issue counters (tools/sq_counters.sh); sqlds:<cfg> the LDS-wait / bank-conflict set
 #   sqab:<cases>                   SQ issue counters of tools/ab_kernels.py cases on config 5 -> <tag>_sqab/
 #   pmcab:<cases>                  one --pmc pass (PMC_COUNTERS) over tools/ab_kernels.py cases (config AB_CFG) -> <tag>_pmcab/
+#   transient                      tools/transient.py plain and under rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES
+#                                  SQ_BUSY_CYCLES -> <tag>_transient.json, <tag>_transient_pmc/, <tag>_transient.txt
 #   cmd:<shell command>            anything else, under a 600 s limit
 set -o pipefail
 TAG=$1
@@ -46,7 +48,7 @@ for step in "$@"; do
     e2e)
       timeout -k 10 1000 python -u tools/e2e_file.py --out "$OUT/${TAG}_e2e_file.json" $arg > "$OUT/${TAG}_e2e.log" 2>&1 \
         || { tail -20 "$OUT/${TAG}_e2e.log"; exit 3; }
-      grep -E "^map|^copy|^config1|^example|^imix|^filter" "$OUT/${TAG}_e2e.log" | cut -c1-500 ;;
+      grep -E "^map|^copy|^config1|^example|^imix|^filter|^google" "$OUT/${TAG}_e2e.log" | cut -c1-500 ;;
     bench)
       for c in ${arg//,/ }; do
         timeout -k 10 400 python -u bench.py $(cfgargs "$c") $(tr "$c") > "$OUT/${TAG}_bench_cfg$c.json" \
@@ -87,6 +89,16 @@ for step in "$@"; do
         --output-format csv -- python3 "$ROOT/tools/ab_kernels.py" 10000000 2 ${AB_CFG:-3} > "$ROOT/$OUT/${TAG}_pmcab/ab.txt" \
         2> "$ROOT/$OUT/${TAG}_pmcab/err.log") || { tail -20 "$OUT/${TAG}_pmcab/err.log"; exit 7; }
       python3 tools/pmc_summary.py "$OUT/${TAG}_pmcab" | tee "$OUT/${TAG}_pmcab/summary.txt" ;;
+    transient)
+      timeout -k 10 300 python -u tools/transient.py --launches 100 --idle 3 > "$OUT/${TAG}_transient.json" \
+        2> "$OUT/${TAG}_transient.err" || { tail -20 "$OUT/${TAG}_transient.err"; exit 10; }
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        -d "$ROOT/$OUT/${TAG}_transient_pmc" -o p --output-format csv -- python3 "$ROOT/tools/transient.py" --launches 100 \
+        --idle 3 > "$ROOT/$OUT/${TAG}_transient_pmc.json" 2> "$ROOT/$OUT/${TAG}_transient_pmc.err") \
+        || { tail -20 "$OUT/${TAG}_transient_pmc.err"; exit 10; }
+      python3 tools/transient_summary.py "$OUT/${TAG}_transient_pmc" "$OUT/${TAG}_transient.json" \
+        > "$OUT/${TAG}_transient.txt" || exit 10
+      tail -8 "$OUT/${TAG}_transient.txt" ;;
     cmd)
       timeout -k 10 600 bash -c "$arg" || exit 8 ;;
     *)
