@@ -8,7 +8,8 @@ One step = one pass of the parse kernel over the whole batch already resident in
 --config selects the other BASELINE configs as extra bench lines (not the driver's default):
   2: 1M x 64 B Eth/IPv4/{TCP,UDP}: parse + hash5Tuple (5-tuple extract), no checksums;
   4: 12.5M IMIX packets/GPU with Zipf(1.1) 5-tuples over 1M flows: parse + hash5Tuple + per-flow
-     {packets, bytes} counters in an HBM flow table (DpdkExample-FilterTraffic's flow table);
+     {packets, bytes} counters in an HBM flow table (DpdkExample-FilterTraffic's flow table); the ranks' shards are
+     contiguous ranges of ONE stream over ONE flow universe (synth.flow_stream), merged on the host after timing;
   5: 10M deep-encapsulation packets (QinQ / MPLS stacks / GREv0 / IPv6 extension chains): parse + hashes.
 Without checksums the algorithmic read is each packet's header extent (end of its last L2-L4 header,
 SURVEY.md §8d) + the 12-B descriptor, computed from the records the kernel wrote.
@@ -72,6 +73,8 @@ def parse_args():
                     help="per-packet record: the 32-B summary, the 48-B 5-tuple extract (pcppx_tuple) alone, or (config "
                          "4) only what the flow table reads: the dense hash5 column + collectStats, no summary (auto: "
                          "tuples for config 2's 5-tuple extract, keys for config 4's flow table, else summary)")
+    ap.add_argument("--dump-flows", default=None,
+                    help="config 4: write the merged flow table (rank 0, after the timed region) to this .npz")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: a multi-rank rehearsal on fewer GPUs than ranks (ranks share cards round-robin); "
                          "the timed numbers of such a run are not a scaling measurement")
@@ -81,6 +84,7 @@ def parse_args():
 CONFIG_PACKETS = {2: 1_000_000, 3: 10_000_000, 4: 12_500_000, 5: 10_000_000}
 SIZED_PACKETS = {64: 10_000_000, 512: 10_000_000, 1500: 5_000_000}  # config 3 at one size: 0.6 / 5.1 / 7.5 GB per GPU
 CONFIG_MAX_LAYERS = {2: 0, 3: 8, 4: 0, 5: 12}
+CONFIG4_FLOWS = 1_000_000  # config 4's flow universe (one for all ranks)
 CONFIG_LAYOUT = {3: "packed", 5: "packed"}  # configs with layer records
 # plain Eth / VLAN / IP / L4 stacks (configs 2 and 4): the one-round parse-only window (PCPPX_WINDOW_SHORT)
 CONFIG_WINDOW = {2: "short", 4: "short"}
@@ -133,7 +137,8 @@ WORKLOADS = {
     2: "config 2: 64 B Eth/IPv4/{TCP,UDP} 50/50; parse + hash5Tuple, 5-tuple extract",
     3: "config 3: IMIX 64/512/1500 B 7:4:1, 25% VLAN, 70/30 IPv4/IPv6, TCP/UDP 50/50, 1% bad checksums; "
        "parse + hashes + IPv4/L4 checksum verify",
-    4: "config 4: IMIX as config 3 with 5-tuples Zipf(1.1) over 1M flows, both directions; parse + hash5Tuple + "
+    4: "config 4: IMIX as config 3 with 5-tuples Zipf(1.1) over 1M flows, both directions, one stream cut into "
+       "contiguous per-GPU shards; parse + hash5Tuple + "
        "per-flow {packets, bytes} counters (FilterTraffic flow table) + collectStats protocol histogram",
     5: "config 5: deep encapsulation (QinQ, 1-3 MPLS labels, GREv0 C/K/S over IPv4|IPv6, IPv6 1-3 extension "
        "headers) then TCP/UDP, 64/512/1500 B; parse + hashes",
@@ -268,7 +273,9 @@ def main() -> None:
     if cfg == 3:
         batch = synth.imix(npk, seed, sizes=(sized,), weights=(1,)) if sized else synth.imix(npk, seed)
     elif cfg == 4:
-        batch = synth.imix(npk, seed, flows=1_000_000, corrupt_frac=0.0)
+        # one config-4 stream over one 1M-flow universe, cut into contiguous shards: rank r parses packets
+        # [npk*r, npk*(r+1)) of it, so a flow spans ranks and the host merge adds them up
+        batch = synth.flow_stream(npk * rank, npk * (rank + 1), 4, flows=CONFIG4_FLOWS)
     elif cfg == 5:
         batch = synth.deep(npk, seed)
     else:
@@ -454,7 +461,15 @@ def main() -> None:
             merged = shard.merge_device_tables(tables)
             counted = int(merged["packets"].sum()) + merged["key0_packets"] + merged["dropped"]
             expected = n * world * (args.warmup + args.steps)
+            if args.dump_flows:
+                np.savez(args.dump_flows, keys=merged["keys"], packets=merged["packets"], bytes=merged["bytes"],
+                         key0=np.array([merged["key0_packets"], merged["key0_bytes"], merged["dropped"]], np.uint64),
+                         launches=np.array([args.warmup + args.steps]))
             flow_check = {"merged_flows": int(len(merged["keys"])), "ranks_merged": len(tables),
+                          "stream": f"one seed-4 stream over {CONFIG4_FLOWS} flows; rank r = packets [{n}r, {n}(r+1))",
+                          "flow_universe": CONFIG4_FLOWS,
+                          "merged_within_universe": int(len(merged["keys"])) <= CONFIG4_FLOWS,
+                          "flows_spanning_ranks": int(sum(len(t["keys"]) for t in tables) - len(merged["keys"])),
                           "per_rank_flows": [int(len(t["keys"])) for t in tables],
                           "packets_counted": counted, "expected": expected, "conserved": counted == expected,
                           # exact: no packet fell to the no-free-slot count, i.e. the table is the reference's map

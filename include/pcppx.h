@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PCPPX_ABI_VERSION 6
+#define PCPPX_ABI_VERSION 7
 /* the library is built with hidden visibility: exactly the functions declared here are exported */
 #define PCPPX_API __attribute__((visibility("default")))
 #define PCPPX_MAX_LAYERS 16     /* fixed depth cap; deeper chains set PCPPX_F_DEPTH_OVERFLOW */
@@ -105,6 +105,19 @@ typedef struct pcppx_summary {
 	uint16_t l4_csum_stored; /* be16 of that layer's checksum field */
 } pcppx_summary;
 
+/* The summary's first 16 bytes alone (ABI 7): what a caller that reads the layer records needs besides them. The
+ * protocol mask is the OR of the recorded chain's protocols (pcppx_chain_proto_mask below: exact when the chain is
+ * recorded whole -- no PCPPX_F_DEPTH_OVERFLOW and n_layers <= max_layers), and the checksum verdicts are the flags
+ * (PCPPX_F_IP_CSUM[_OK], PCPPX_F_L4_CSUM[_OK]); only the computed / stored checksum values are not carried. */
+typedef struct pcppx_brief {
+	uint32_t hash5;     /* = pcppx_summary.hash5 */
+	uint32_t hash5_dir; /* = pcppx_summary.hash5_dir */
+	uint32_t hash2;     /* = pcppx_summary.hash2 */
+	uint16_t flags;     /* = pcppx_summary.flags */
+	uint8_t n_layers;   /* = pcppx_summary.n_layers */
+	uint8_t l4_layer;   /* = pcppx_summary.l4_layer */
+} pcppx_brief;
+
 /* A batch of packets: bytes of packet i are data[offsets[i] .. offsets[i] + caplens[i]).
  * For the fast path packets should be stored back to back in ascending offset order (any order and
  * gaps are legal; they only cost bandwidth). */
@@ -145,14 +158,20 @@ typedef struct pcppx_opts {
  *   PACKED: only the chain's entries are written, densely per 64-packet tile: the entries of tile t (packets
  *           64t .. 64t+63) start at layers[64 * t * max_layers], and packet i's entries follow those of the packets
  *           before it in its tile: layers[64 * t * max_layers + sum_{64t <= j < i} min(n_layers_j, max_layers) + k].
- *           The buffer is sized as for FIXED (n * max_layers entries); the summary is required (its n_layers
- *           decode the positions: pcppx_unpack_layers below, pcppx::unpackLayers in include/pcppx.hpp). The write
+ *           The buffer is sized as for FIXED (n * max_layers entries); the summary or the brief is required (its
+ *           n_layers decode the positions: pcppx_unpack_layers[_brief] below, pcppx::unpackLayers in include/pcppx.hpp). The write
  *           traffic is the chain, not max_layers rows per packet. max_layers <= PCPPX_PACKED_MAX_LAYERS. Device parse
  *           only; the consumers of a parse's records (pcppx_filter_device, pcppx_reasm_device) read FIXED records and
  *           refuse PACKED ones (pcppx_records.layout). */
 #define PCPPX_LAYOUT_FIXED 0
 #define PCPPX_LAYOUT_PACKED 1
 #define PCPPX_PACKED_MAX_LAYERS 12
+/*   DENSE (ABI 7, host path): the chains back to back over the whole batch, in packet order: packet i's entries are
+ *           layers[sum_{j < i} min(n_layers_j, max_layers) + k]; pcppx_records.layers_written returns the total. The
+ *           buffer must hold the total (n * max_layers entries always do; unwritten memory is never touched), and
+ *           only the chains cross PCIe (config 3: 4.2 entries = 34 B per packet instead of 8 * max_layers).
+ *           max_layers <= PCPPX_MAX_LAYERS. pcppx_parse_batch_host only. */
+#define PCPPX_LAYOUT_DENSE 2
 
 /* The 5-tuple extract (the compact record of the bandwidth runs), 48 bytes per packet: exactly the
  * fields pcpp::hash5Tuple reads (Packet++/src/PacketUtils.cpp:139-210), from the same layers as the summary's
@@ -194,8 +213,9 @@ typedef struct pcppx_tuple {
 
 /* Output arrays (same memory space as the batch for the _device call, host for the _host call). */
 typedef struct pcppx_records {
-	pcppx_summary* summary; /* n entries; may be NULL on the device path when max_layers is 0 and one of tuples /
-	                           flow_keys / proto_stats is set (e.g. a flow table's launch: dense keys + collectStats) */
+	pcppx_summary* summary; /* n entries, or NULL when `brief` is set; may also be NULL on the device path when max_layers
+	                           is 0 and one of tuples / flow_keys / proto_stats is set (e.g. a flow table's launch: dense
+	                           keys + collectStats) */
 	pcppx_layer* layers;    /* n * max_layers entries in pcppx_opts.layout, or NULL when max_layers == 0 */
 	uint32_t* flow_keys;    /* optional (NULL): n entries, flow_keys[i] = summary[i].hash5 -- the dense column
 	                           FilterTraffic's flow table is keyed by (pcppx_flow_count_keys_device reads 8 B per
@@ -207,7 +227,20 @@ typedef struct pcppx_records {
 	                           pcppx_filter_device / pcppx_reasm_device, which refuse PCPPX_LAYOUT_PACKED records.
 	                           Zero-initialised records are FIXED. */
 	uint8_t reserved[7];
+	pcppx_brief* brief;     /* optional (NULL), ABI 7: n 16-B briefs (the summary's first half), beside or instead of
+	                           the summary -- the record a layer-reading caller needs (device and host paths) */
+	uint64_t layers_written; /* out: layer entries written (PCPPX_LAYOUT_DENSE: the total of the chains) */
 } pcppx_records;
+
+/* Packet::isPacketOfType's mask (bit p for every protocol p of the chain) from a packet's recorded layers: equals
+ * pcppx_summary.proto_mask when the chain is recorded whole (pcppx_brief) */
+static inline uint64_t pcppx_chain_proto_mask(const pcppx_layer* chain, unsigned n_layers)
+{
+	uint64_t m = 0;
+	for (unsigned k = 0; k < n_layers; ++k)
+		m |= chain[k].proto < 64 ? 1ull << chain[k].proto : 0ull;
+	return m;
+}
 
 /* The caller's own host parse of ONE packet — its Packet++ (`pcpp::Packet packet(&raw, parseUntil...)`) turned
  * into this engine's records: summary + up to opts->max_layers layers, as the engine would write them had it
@@ -238,8 +271,8 @@ PCPPX_API int pcppx_parse_batch_device(pcppx_ctx* ctx, const pcppx_batch* batch,
                              pcppx_records* out, void* hip_stream);
 
 /* Host-to-host parse: batch and records hold host pointers. The context stages the bytes through pinned
- * buffers in chunks, overlapping H2D copies, kernels and D2H copies; returns when out is filled. The FIXED layout
- * only; records.tuples and records.proto_stats must be NULL (device-path outputs). */
+ * buffers in chunks, overlapping H2D copies, kernels and D2H copies; returns when out is filled. The FIXED or the DENSE
+ * layout; a summary and / or a brief; records.tuples and records.proto_stats must be NULL (device-path outputs). */
 PCPPX_API int pcppx_parse_batch_host(pcppx_ctx* ctx, const pcppx_batch* batch, const pcppx_opts* opts,
                            pcppx_records* out);
 
@@ -395,6 +428,9 @@ PCPPX_API void pcppx_pcap_close(pcppx_pcap* reader);
  * for k < min(summary[i].n_layers, max_layers), zero past each chain. max_layers <= PCPPX_PACKED_MAX_LAYERS. */
 PCPPX_API int pcppx_unpack_layers(const pcppx_summary* summary, const pcppx_layer* packed, uint64_t n,
                                   uint32_t max_layers, pcppx_layer* fixed);
+/* the same with the chain lengths from briefs (ABI 7) */
+PCPPX_API int pcppx_unpack_layers_brief(const pcppx_brief* brief, const pcppx_layer* packed, uint64_t n,
+                                        uint32_t max_layers, pcppx_layer* fixed);
 PCPPX_API void* pcppx_host_alloc(size_t bytes); /* page-locked host memory (hipHostMalloc) */
 PCPPX_API void pcppx_host_free(void* p);
 

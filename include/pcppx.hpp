@@ -37,7 +37,9 @@
 
 #include <sys/time.h>
 
+#include <algorithm>
 #include <atomic>
+#include <iterator>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
@@ -208,6 +210,11 @@ inline std::atomic<pcppx_host_parse_fn>& hostParser()
 	static std::atomic<pcppx_host_parse_fn> f{ nullptr };
 	return f;
 }
+inline std::atomic<bool>& pageChecksums()
+{
+	static std::atomic<bool> c{ false };
+	return c;
+}
 }  // namespace detail
 
 /* The GPU the per-packet entry points (readers, Packet(RawPacket*)) use; set before the first one runs. */
@@ -220,6 +227,13 @@ inline void setDefaultDevice(int device)
 inline void setHostParser(pcppx_host_parse_fn fn)
 {
 	detail::hostParser().store(fn);
+}
+/* Packet(RawPacket*, ...) computes no checksum in Packet++ (Packet.cpp:66-196), so the per-packet entry points parse
+ * without them; with this set they also verify the IPv4 / TCP / UDP checksums (Packet::isIPv4ChecksumValid ... carry
+ * the computed values). Set before the Packets it should apply to. */
+inline void setPageChecksums(bool on)
+{
+	detail::pageChecksums().store(on);
 }
 
 class RawPacket;
@@ -334,52 +348,105 @@ inline size_t completeOnHost(pcppx_host_parse_fn fn, const uint8_t* data, const 
 	return done;
 }
 
-/* Packet::parsePacket's options (Packet.cpp:66-196): what a page's records were parsed for */
+/* Packet::parsePacket's options (Packet.cpp:66-196): what a page's records were parsed for (+ whether the checksums
+ * were verified, setPageChecksums) */
 struct ParseKey
 {
 	ProtocolTypeFamily family = UnknownProtocol;
 	uint8_t osi = OsiModelLayerUnknown;
-	bool operator==(const ParseKey& o) const { return family == o.family && osi == o.osi; }
-	/* the reader's parse: every layer record (PCPPX_MAX_LAYERS, FIXED) and the checksums */
+	bool csum = false;
+	bool operator==(const ParseKey& o) const { return family == o.family && osi == o.osi && csum == o.csum; }
+	/* the per-packet parse: every layer of the chain (PCPPX_MAX_LAYERS) in the DENSE layout, with the 16-B brief -- or
+	 * the 32-B summary when checksums are verified (the computed values ride in it) */
 	pcppx_opts opts() const
 	{
 		pcppx_opts o;
 		pcppx_default_opts(&o);
 		o.parse_until_family = family;
 		o.parse_until_osi = osi;
+		o.want_checksums = csum ? 1 : 0;
+		o.layout = PCPPX_LAYOUT_DENSE;
 		return o;
 	}
 };
 
-/* one page's records for one ParseKey, in page-locked memory: summary[n] then layers[n][PCPPX_MAX_LAYERS] */
-struct Records
-{
-	ParseKey key;
-	pcppx_summary* sum = nullptr;
-	pcppx_layer* lay = nullptr;
-	Records(ParseKey k, uint32_t n) : key(k)
-	{
-		m_Block = PinnedPool::instance().take((size_t)n * (sizeof(pcppx_summary) + PCPPX_MAX_LAYERS * sizeof(pcppx_layer)),
-		                                      &m_Bytes);
-		sum = static_cast<pcppx_summary*>(m_Block);
-		lay = reinterpret_cast<pcppx_layer*>(sum + n);
-	}
-	~Records() { PinnedPool::instance().give(m_Block, m_Bytes); }
-	Records(const Records&) = delete;
-	Records& operator=(const Records&) = delete;
-
-private:
-	void* m_Block = nullptr;
-	size_t m_Bytes = 0;
-};
-
-/* one packet's records, copied out of its page when its RawPacket is copied (the copy owns its bytes and keeps no
- * page alive, as a copied pcpp::RawPacket owns a copy of the bytes: RawPacket.cpp copyDataFrom) */
+/* one packet's complete records: a summary (proto_mask included) and its first PCPPX_MAX_LAYERS layers -- a packet the
+ * host parser completed, one whose chain is deeper than the records hold, or a copied RawPacket's (the copy owns its
+ * bytes and keeps no page alive, as a copied pcpp::RawPacket owns a copy of the bytes: RawPacket.cpp copyDataFrom) */
 struct CopiedRecords
 {
 	ParseKey key;
 	pcppx_summary sum{};
 	pcppx_layer lay[PCPPX_MAX_LAYERS]{};
+};
+
+/* One page's records for one ParseKey (ABI 7): per packet the 16-B brief (or, checksums verified, the 32-B summary,
+ * whose first half is the brief) and the chain's layer entries back to back (PCPPX_LAYOUT_DENSE: only the chains cross
+ * PCIe, 50 B per config-3 packet), both DMA'd into page-locked memory; first[i] = packet i's first entry. Packets whose
+ * records the chain alone cannot give -- completed by the host parser (F_HOST_PARSED) or deeper than PCPPX_MAX_LAYERS
+ * (PCPPX_F_DEPTH_OVERFLOW: the protocol mask then covers layers the entries do not hold) -- carry complete records in
+ * `side`, looked up by index. */
+struct Records
+{
+	ParseKey key;
+	uint32_t n = 0;
+	pcppx_brief* brief = nullptr;   // n (the summaries' first halves when sum is set)
+	pcppx_summary* sum = nullptr;   // n when key.csum
+	pcppx_layer* lay = nullptr;     // the chains (up to n * PCPPX_MAX_LAYERS entries)
+	std::unique_ptr<uint32_t[]> first;
+	uint64_t entries = 0;           // layers_written
+	std::vector<uint32_t> sideIdx;  // ascending
+	std::vector<CopiedRecords> side;
+
+	Records(ParseKey k, uint32_t count) : key(k), n(count), first(new uint32_t[count ? count : 1])
+	{
+		const size_t head = (size_t)n * (k.csum ? sizeof(pcppx_summary) : sizeof(pcppx_brief));
+		m_Block = PinnedPool::instance().take(head + (size_t)n * PCPPX_MAX_LAYERS * sizeof(pcppx_layer), &m_Bytes);
+		if (k.csum)
+			sum = static_cast<pcppx_summary*>(m_Block);
+		brief = static_cast<pcppx_brief*>(m_Block);  // stride: briefOf()
+		lay = reinterpret_cast<pcppx_layer*>(static_cast<uint8_t*>(m_Block) + head);
+	}
+	~Records() { PinnedPool::instance().give(m_Block, m_Bytes); }
+	Records(const Records&) = delete;
+	Records& operator=(const Records&) = delete;
+
+	const pcppx_brief* briefOf(uint32_t i) const
+	{
+		return sum ? reinterpret_cast<const pcppx_brief*>(sum + i) : brief + i;
+	}
+	pcppx_brief* briefOf(uint32_t i) { return sum ? reinterpret_cast<pcppx_brief*>(sum + i) : brief + i; }
+	const CopiedRecords* sideFor(uint32_t i) const
+	{
+		auto it = std::lower_bound(sideIdx.begin(), sideIdx.end(), i);
+		return it != sideIdx.end() && *it == i ? &side[(size_t)(it - sideIdx.begin())] : nullptr;
+	}
+	/* packet i's complete records (a copy's): the side entry, or the summary / the brief + the chain's mask */
+	void complete(uint32_t i, CopiedRecords* c) const
+	{
+		if (const CopiedRecords* s = sideFor(i))
+		{
+			*c = *s;
+			return;
+		}
+		c->key = key;
+		const pcppx_brief* b = briefOf(i);
+		const uint32_t cnt = b->n_layers < PCPPX_MAX_LAYERS ? b->n_layers : PCPPX_MAX_LAYERS;
+		std::memset(c->lay, 0, sizeof(c->lay));
+		std::memcpy(c->lay, lay + first[i], cnt * sizeof(pcppx_layer));
+		if (sum != nullptr)
+			c->sum = sum[i];
+		else
+		{
+			c->sum = pcppx_summary{};
+			std::memcpy(&c->sum, b, sizeof(pcppx_brief));
+			c->sum.proto_mask = pcppx_chain_proto_mask(c->lay, cnt);
+		}
+	}
+
+private:
+	void* m_Block = nullptr;
+	size_t m_Bytes = 0;
 };
 
 /* the capture map: closed when the reader and every page of it are gone */
@@ -424,11 +491,79 @@ struct Page
 		const pcppx_opts o = k.opts();
 		const pcppx_batch b{ base, offsets.data(), caplens.data(), dataLen, n, linkType, 0 };
 		pcppx_records rec{};
-		rec.summary = r->sum;
+		if (k.csum)
+			rec.summary = r->sum;
+		else
+			rec.brief = r->brief;
 		rec.layers = r->lay;
 		Service::instance().parse(b, o, rec);
-		completeOnHost(hostParser().load(), base, offsets.data(), caplens.data(), n, linkType, o, r->sum, r->lay);
+		r->entries = rec.layers_written;
+		// each chain's first entry; the packets that need complete records beside the chain
+		std::vector<uint32_t> deep, host;
+		const pcppx_host_parse_fn fn = hostParser().load();
+		uint32_t pos = 0;
+		for (uint32_t i = 0; i < n; ++i)
+		{
+			r->first[i] = pos;
+			const pcppx_brief* bi = r->briefOf(i);
+			pos += bi->n_layers < PCPPX_MAX_LAYERS ? bi->n_layers : PCPPX_MAX_LAYERS;
+			if (fn != nullptr && (bi->flags & PCPPX_F_NEEDS_HOST) && !(bi->flags & PCPPX_F_BAD_DESC))
+				host.push_back(i);
+			else if (!k.csum && (bi->flags & PCPPX_F_DEPTH_OVERFLOW))
+				deep.push_back(i);
+		}
+		if (pos != r->entries)
+			throw Error(PCPPX_E_HIP, "page records: chain entries do not add up");
+		completeSide(*r, k, deep, host, fn);
 		return r;
+	}
+	/* complete records of the few packets the chain alone does not describe: chains deeper than the records (their
+	 * summaries from one small FIXED parse of just those packets), and packets the host parser completes */
+	void completeSide(Records& r, ParseKey k, const std::vector<uint32_t>& deep, const std::vector<uint32_t>& host,
+	                  pcppx_host_parse_fn fn) const
+	{
+		std::vector<uint32_t> all;
+		std::merge(deep.begin(), deep.end(), host.begin(), host.end(), std::back_inserter(all));
+		if (all.empty())
+			return;
+		r.sideIdx = all;
+		r.side.resize(all.size());
+		pcppx_opts o = k.opts();
+		o.layout = PCPPX_LAYOUT_FIXED;
+		if (!deep.empty())
+		{
+			buffer<uint64_t> off(deep.size());
+			buffer<uint32_t> cap(deep.size());
+			for (size_t j = 0; j < deep.size(); ++j)
+			{
+				off[j] = offsets[deep[j]];
+				cap[j] = caplens[deep[j]];
+			}
+			std::vector<pcppx_summary> ds(deep.size());
+			std::vector<pcppx_layer> dl(deep.size() * PCPPX_MAX_LAYERS);
+			const pcppx_batch b{ base, off.data(), cap.data(), dataLen, (uint32_t)deep.size(), linkType, 0 };
+			pcppx_records rec{};
+			rec.summary = ds.data();
+			rec.layers = dl.data();
+			Service::instance().parse(b, o, rec);
+			for (size_t j = 0; j < deep.size(); ++j)
+			{
+				CopiedRecords& c = r.side[(size_t)(std::lower_bound(all.begin(), all.end(), deep[j]) - all.begin())];
+				c.key = k;
+				c.sum = ds[j];
+				std::memcpy(c.lay, dl.data() + j * PCPPX_MAX_LAYERS, sizeof(c.lay));
+			}
+		}
+		for (uint32_t i : host)
+		{
+			CopiedRecords& c = r.side[(size_t)(std::lower_bound(all.begin(), all.end(), i) - all.begin())];
+			c.key = k;
+			std::memset(&c.sum, 0, sizeof(c.sum));
+			check(fn(base + offsets[i], caplens[i], linkType, &o, &c.sum, c.lay), "host parser");
+			c.sum.flags = (uint16_t)(c.sum.flags | F_HOST_PARSED);
+			pcppx_brief* bi = r.briefOf(i);
+			bi->flags = (uint16_t)(bi->flags | F_HOST_PARSED);  // Packet: look the packet up in `side`
+		}
 	}
 	/* parse for k unless another thread has started: false if it has */
 	bool tryParse(ParseKey k)
@@ -759,9 +894,7 @@ private:
 		if (r == nullptr)
 			return nullptr;
 		auto c = std::make_shared<detail::CopiedRecords>();
-		c->key = r->key;
-		c->sum = r->sum[m_Index];
-		std::memcpy(c->lay, r->lay + (size_t)m_Index * PCPPX_MAX_LAYERS, sizeof(c->lay));
+		r->complete(m_Index, c.get());
 		return c;
 	}
 	void copyFrom(const RawPacket& o)
@@ -1525,7 +1658,8 @@ public:
 	}
 	/* a view into records the caller holds (ParsedBatch) */
 	Packet(const pcppx_summary* s, const pcppx_layer* layers, uint8_t maxLayers, const uint8_t* raw, uint32_t caplen)
-	    : m_Sum(s), m_Layers(layers), m_MaxLayers(maxLayers), m_Raw(raw), m_Caplen(caplen)
+	    : m_Brief(reinterpret_cast<const pcppx_brief*>(s)), m_Sum(s), m_Layers(layers), m_MaxLayers(maxLayers), m_Raw(raw),
+	      m_Caplen(caplen)
 	{}
 
 	/* Packet::isPacketOfType (Packet.cpp:614-640), for a protocol or a family. On a packet the engine left to the
@@ -1533,10 +1667,11 @@ public:
 	 * of its first L7 layer when the device named it (PCPPX_F_L7_KNOWN) */
 	bool isPacketOfType(ProtocolTypeFamily family) const
 	{
-		uint64_t mask = m_Sum->proto_mask;
-		if (m_Sum->flags & PCPPX_F_L7_KNOWN)
-			mask |= ((m_Sum->flags & PCPPX_F_L7_HTTP) ? (1ull << HTTPRequest) | (1ull << HTTPResponse) : 0) |
-			        ((m_Sum->flags & PCPPX_F_L7_SSL) ? 1ull << SSL : 0) | ((m_Sum->flags & PCPPX_F_L7_DNS) ? 1ull << DNS : 0);
+		uint64_t mask = protoMask();
+		const uint16_t fl = m_Brief->flags;
+		if (fl & PCPPX_F_L7_KNOWN)
+			mask |= ((fl & PCPPX_F_L7_HTTP) ? (1ull << HTTPRequest) | (1ull << HTTPResponse) : 0) |
+			        ((fl & PCPPX_F_L7_SSL) ? 1ull << SSL : 0) | ((fl & PCPPX_F_L7_DNS) ? 1ull << DNS : 0);
 		for (int k = 0; k < 4; ++k)
 		{
 			const uint32_t p = (family >> (8 * k)) & 0xFF;
@@ -1545,9 +1680,9 @@ public:
 		}
 		return false;
 	}
-	size_t getLayerCount() const { return m_Sum->n_layers; }
+	size_t getLayerCount() const { return m_Brief->n_layers; }
 	/* records held for the first min(getLayerCount(), maxLayers) layers */
-	size_t getRecordedLayerCount() const { return m_Sum->n_layers < m_MaxLayers ? m_Sum->n_layers : m_MaxLayers; }
+	size_t getRecordedLayerCount() const { return m_Brief->n_layers < m_MaxLayers ? m_Brief->n_layers : m_MaxLayers; }
 	Layer getLayer(size_t k) const { return Layer(m_Layers + k, m_Raw); }
 	Layer getFirstLayer() const { return getRecordedLayerCount() ? getLayer(0) : Layer(); }
 	Layer getLastLayer() const { return getRecordedLayerCount() ? getLayer(getRecordedLayerCount() - 1) : Layer(); }
@@ -1570,19 +1705,32 @@ public:
 	uint32_t getRawDataLen() const { return m_Caplen; }
 
 	/* engine flags: the host must finish the packet (an L7 or an out-of-scope L2/L3 layer) and no host parser did */
-	bool needsHost() const { return (m_Sum->flags & PCPPX_F_NEEDS_HOST) != 0; }
+	bool needsHost() const { return (m_Brief->flags & PCPPX_F_NEEDS_HOST) != 0; }
 	/* the records come from the caller's host parser (setHostParser / Engine::setHostParser) */
-	bool wasHostParsed() const { return (m_Sum->flags & F_HOST_PARSED) != 0; }
-	bool hasTrailer() const { return (m_Sum->flags & PCPPX_F_TRAILER) != 0; }
-	/* IPv4Layer::computeCalculateFields checksum vs the stored one (IPv4Layer.cpp:410-412) */
-	bool hasIPv4Checksum() const { return (m_Sum->flags & PCPPX_F_IP_CSUM) != 0; }
-	bool isIPv4ChecksumValid() const { return (m_Sum->flags & PCPPX_F_IP_CSUM_OK) != 0; }
+	bool wasHostParsed() const { return (m_Brief->flags & F_HOST_PARSED) != 0; }
+	bool hasTrailer() const { return (m_Brief->flags & PCPPX_F_TRAILER) != 0; }
+	/* IPv4Layer::computeCalculateFields checksum vs the stored one (IPv4Layer.cpp:410-412): verified where the parse
+	 * computed checksums (setPageChecksums, PacketParseOptions::computeChecksums) */
+	bool hasIPv4Checksum() const { return (m_Brief->flags & PCPPX_F_IP_CSUM) != 0; }
+	bool isIPv4ChecksumValid() const { return (m_Brief->flags & PCPPX_F_IP_CSUM_OK) != 0; }
 	/* TcpLayer/UdpLayer::calculateChecksum(false) vs the stored checksum (TcpLayer.cpp:271, UdpLayer.cpp:47) */
-	bool hasL4Checksum() const { return (m_Sum->flags & PCPPX_F_L4_CSUM) != 0; }
-	bool isL4ChecksumValid() const { return (m_Sum->flags & PCPPX_F_L4_CSUM_OK) != 0; }
-	uint16_t calculatedL4Checksum() const { return m_Sum->l4_csum_calc; }
-	uint16_t calculatedIPv4Checksum() const { return m_Sum->ip_csum_calc; }
-	const pcppx_summary& summary() const { return *m_Sum; }
+	bool hasL4Checksum() const { return (m_Brief->flags & PCPPX_F_L4_CSUM) != 0; }
+	bool isL4ChecksumValid() const { return (m_Brief->flags & PCPPX_F_L4_CSUM_OK) != 0; }
+	uint16_t calculatedL4Checksum() const { return m_Sum ? m_Sum->l4_csum_calc : 0; }
+	uint16_t calculatedIPv4Checksum() const { return m_Sum ? m_Sum->ip_csum_calc : 0; }
+	/* hashes, flags, chain length, port layer (pcppx_brief) */
+	const pcppx_brief& brief() const { return *m_Brief; }
+	/* the whole summary: the records' own, or built from the brief with the chain's protocol mask (checksum values 0:
+	 * the parse computed none) */
+	const pcppx_summary& summary() const
+	{
+		if (m_Sum != nullptr)
+			return *m_Sum;
+		m_Full = pcppx_summary{};
+		std::memcpy(&m_Full, m_Brief, sizeof(pcppx_brief));
+		m_Full.proto_mask = protoMask();
+		return m_Full;
+	}
 
 private:
 	static const pcppx_summary* emptySummary()
@@ -1590,9 +1738,30 @@ private:
 		static const pcppx_summary s{ 0, 0, 0, 0, 0, 0xFF, 0, 0, 0, 0, 0 };
 		return &s;
 	}
+	uint64_t protoMask() const
+	{
+		return m_Sum ? m_Sum->proto_mask : pcppx_chain_proto_mask(m_Layers, (unsigned)getRecordedLayerCount());
+	}
+	/* packet i of a page's / group's records */
+	void bindRecords(const detail::Records* r, uint32_t i)
+	{
+		const pcppx_brief* b = r->briefOf(i);
+		if (b->flags & (F_HOST_PARSED | PCPPX_F_DEPTH_OVERFLOW))
+			if (const detail::CopiedRecords* c = r->sideFor(i))
+			{
+				m_Sum = &c->sum;  // complete records beside the chain
+				m_Brief = reinterpret_cast<const pcppx_brief*>(m_Sum);
+				m_Layers = c->lay;
+				return;
+			}
+		m_Brief = b;
+		m_Sum = r->sum ? r->sum + i : nullptr;
+		m_Layers = r->lay + r->first[i];
+	}
 	void bind(RawPacket* raw, bool freeRawPacket, ProtocolTypeFamily parseUntil, OsiModelLayer parseUntilLayer)
 	{
 		m_Sum = emptySummary();
+		m_Brief = reinterpret_cast<const pcppx_brief*>(m_Sum);
 		m_MaxLayers = PCPPX_MAX_LAYERS;
 		if (raw == nullptr)
 			return;  // Packet::setRawPacket: no RawPacket, no layers (Packet.cpp:60-61)
@@ -1600,10 +1769,11 @@ private:
 			m_OwnedRaw.reset(raw);
 		m_Raw = raw->m_RawData;
 		m_Caplen = raw->m_RawDataLen > 0 ? (uint32_t)raw->m_RawDataLen : 0;
-		const detail::ParseKey k{ parseUntil, parseUntilLayer };
+		const detail::ParseKey k{ parseUntil, parseUntilLayer, detail::pageChecksums().load(std::memory_order_relaxed) };
 		if (raw->m_Copied != nullptr && raw->m_Copied->key == k)
 		{
 			m_Sum = &raw->m_Copied->sum;  // records copied with the bytes
+			m_Brief = reinterpret_cast<const pcppx_brief*>(m_Sum);
 			m_Layers = raw->m_Copied->lay;
 			return;
 		}
@@ -1611,9 +1781,7 @@ private:
 		{
 			// the caller's own bytes: parsed with every other pending RawPacket in one batch, or already in a group
 			uint32_t idx = 0;
-			const detail::Records* r = detail::OwnedRegistry::instance().recordsFor(raw, k, &idx);
-			m_Sum = r->sum + idx;
-			m_Layers = r->lay + (size_t)idx * PCPPX_MAX_LAYERS;
+			bindRecords(detail::OwnedRegistry::instance().recordsFor(raw, k, &idx), idx);
 			return;
 		}
 		if (detail::Page* p = raw->m_Page.get())
@@ -1621,18 +1789,19 @@ private:
 			const detail::Records* r = p->primary.load(std::memory_order_acquire);
 			if (r == nullptr || !(r->key == k))
 				r = p->recordsFor(k);
-			m_Sum = r->sum + raw->m_Index;
-			m_Layers = r->lay + (size_t)raw->m_Index * PCPPX_MAX_LAYERS;
+			bindRecords(r, raw->m_Index);
 		}
 		// else no data: createFirstLayer builds nothing (Packet.cpp:88-94)
 	}
 
-	const pcppx_summary* m_Sum = nullptr;
+	const pcppx_brief* m_Brief = nullptr;  // always set (a summary's first half where m_Sum is)
+	const pcppx_summary* m_Sum = nullptr;  // complete records, where the parse or the side table has them
 	const pcppx_layer* m_Layers = nullptr;
 	uint8_t m_MaxLayers = 0;
 	const uint8_t* m_Raw = nullptr;
 	uint32_t m_Caplen = 0;
-	std::shared_ptr<RawPacket> m_OwnedRaw;        // freeRawPacket
+	mutable pcppx_summary m_Full{};       // summary() of brief-backed records
+	std::shared_ptr<RawPacket> m_OwnedRaw;  // freeRawPacket
 };
 using ParsedPacket = Packet;
 using ParsedLayer = Layer;
@@ -1640,11 +1809,11 @@ using ParsedLayer = Layer;
 /* pcpp::hash5Tuple / hash2Tuple (Packet++/header/PacketUtils.h:58-91) */
 inline uint32_t hash5Tuple(const Packet* packet, bool const& directionUnique = false)
 {
-	return directionUnique ? packet->summary().hash5_dir : packet->summary().hash5;
+	return directionUnique ? packet->brief().hash5_dir : packet->brief().hash5;
 }
 inline uint32_t hash2Tuple(const Packet* packet)
 {
-	return packet->summary().hash2;
+	return packet->brief().hash2;
 }
 
 /* Records of one parsed batch (owns them); indexes into the RawBatch it was parsed from. */

@@ -15,11 +15,11 @@ PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 ENGINE_SO = PKG_DIR / "libpcppx.so"
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_LAYERS = 16
 MAX_CAPLEN = 65535
 WINDOW_DEFAULT, WINDOW_DEEP, WINDOW_SHORT = 0, 1, 2  # pcppx_opts.window (PCPPX_WINDOW_*)
-LAYOUT_FIXED, LAYOUT_PACKED = 0, 1  # pcppx_opts.layout (PCPPX_LAYOUT_*)
+LAYOUT_FIXED, LAYOUT_PACKED, LAYOUT_DENSE = 0, 1, 2  # pcppx_opts.layout (PCPPX_LAYOUT_*); DENSE: host path
 PACKED_MAX_LAYERS = 12
 TILE = 64  # packets per tile of the PACKED layout
 
@@ -68,6 +68,7 @@ SUMMARY_DTYPE = np.dtype(
         ("l4_csum_stored", "<u2"),
     ]
 )
+BRIEF_DTYPE = np.dtype(SUMMARY_DTYPE.descr[:6])  # pcppx_brief (ABI 7): the summary's first 16 bytes
 LAYER_DTYPE = np.dtype(
     [("proto", "u1"), ("osi", "u1"), ("offset", "<u2"), ("hdr_len", "<u2"), ("data_len", "<u2")]
 )
@@ -81,6 +82,7 @@ TUPLE_DTYPE = np.dtype(
      ("n_layers", "u1"), ("reserved", "u1")]
 )
 assert SUMMARY_DTYPE.itemsize == 32 and LAYER_DTYPE.itemsize == 8 and REASM_DTYPE.itemsize == 16
+assert BRIEF_DTYPE.itemsize == 16
 assert TUPLE_DTYPE.itemsize == 48
 
 # pcppx_records.proto_stats words (PCPPX_PS_*): PacketStats::collectStats, Common.h:83-104
@@ -121,7 +123,8 @@ class Opts(C.Structure):
 
 class Records(C.Structure):
     _fields_ = [("summary", C.c_void_p), ("layers", C.c_void_p), ("flow_keys", C.c_void_p), ("tuples", C.c_void_p),
-                ("proto_stats", C.c_void_p), ("layout", C.c_uint8), ("reserved", C.c_uint8 * 7)]
+                ("proto_stats", C.c_void_p), ("layout", C.c_uint8), ("reserved", C.c_uint8 * 7),
+                ("brief", C.c_void_p), ("layers_written", C.c_uint64)]
 
 
 class MatchSpec(C.Structure):
@@ -159,8 +162,10 @@ def make_opts(parse_until_family: int = 0, parse_until_osi: int = 8, want_checks
         raise ValueError(f"max_layers must be in [0, {MAX_LAYERS}]")
     if window not in (WINDOW_DEFAULT, WINDOW_DEEP, WINDOW_SHORT):
         raise ValueError("window must be WINDOW_DEFAULT, WINDOW_DEEP or WINDOW_SHORT")
-    if layout not in (LAYOUT_FIXED, LAYOUT_PACKED) or (layout == LAYOUT_PACKED and max_layers > PACKED_MAX_LAYERS):
-        raise ValueError(f"layout must be LAYOUT_FIXED, or LAYOUT_PACKED with max_layers <= {PACKED_MAX_LAYERS}")
+    if layout not in (LAYOUT_FIXED, LAYOUT_PACKED, LAYOUT_DENSE) or \
+            (layout == LAYOUT_PACKED and max_layers > PACKED_MAX_LAYERS):
+        raise ValueError(f"layout must be LAYOUT_FIXED, LAYOUT_DENSE (host path), or LAYOUT_PACKED with max_layers <= "
+                         f"{PACKED_MAX_LAYERS}")
     o = Opts(parse_until_family, parse_until_osi, 1 if want_checksums else 0, max_layers, window)
     o.layout = layout
     return o
@@ -190,6 +195,37 @@ def unpack_layers(summary: np.ndarray, packed: np.ndarray, max_layers: int) -> n
         m = cnt > k
         out[m, k] = flat[start[m] + k]
     return out
+
+
+def dense_positions(n_layers: np.ndarray, max_layers: int) -> np.ndarray:
+    """Start entry of every packet's chain in a DENSE layer array (PCPPX_LAYOUT_DENSE): the chains of the packets
+    before it, whole batch."""
+    cnt = np.minimum(n_layers.astype(np.int64), max_layers)
+    return np.cumsum(cnt) - cnt
+
+
+def unpack_dense(n_layers: np.ndarray, dense: np.ndarray, max_layers: int) -> np.ndarray:
+    """DENSE layer entries -> the FIXED [n, max_layers] array (entries past a chain zero)."""
+    n = len(n_layers)
+    out = np.zeros((n, max_layers), dtype=LAYER_DTYPE)
+    if n == 0 or max_layers == 0:
+        return out
+    cnt = np.minimum(n_layers.astype(np.int64), max_layers)
+    start = dense_positions(n_layers, max_layers)
+    flat = dense.reshape(-1)
+    for k in range(max_layers):
+        m = cnt > k
+        out[m, k] = flat[start[m] + k]
+    return out
+
+
+def chain_proto_mask(fixed: np.ndarray, n_layers: np.ndarray) -> np.ndarray:
+    """pcppx_chain_proto_mask over FIXED rows: Packet::isPacketOfType's mask from the recorded chain."""
+    n, ml = fixed.shape
+    k = np.arange(ml)[None, :] < np.minimum(n_layers.astype(np.int64), ml)[:, None]
+    bits = np.where(k & (fixed["proto"] < 64), np.left_shift(np.uint64(1), fixed["proto"].astype(np.uint64)),
+                    np.uint64(0))
+    return np.bitwise_or.reduce(bits, axis=1) if ml else np.zeros(n, np.uint64)
 
 
 def _declare(lib: C.CDLL) -> C.CDLL:
@@ -245,6 +281,8 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_host_free.restype = None
     lib.pcppx_unpack_layers.argtypes = [P, P, C.c_uint64, C.c_uint32, P]
     lib.pcppx_unpack_layers.restype = C.c_int
+    lib.pcppx_unpack_layers_brief.argtypes = [P, P, C.c_uint64, C.c_uint32, P]
+    lib.pcppx_unpack_layers_brief.restype = C.c_int
     for name in ("pcppx_device_count", "pcppx_open", "pcppx_sync", "pcppx_parse_batch_device",
                  "pcppx_parse_batch_host", "pcppx_flow_count_device"):
         getattr(lib, name).restype = C.c_int
@@ -259,7 +297,7 @@ EXPORTED_SYMBOLS = (
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
     "pcppx_flow_count_device", "pcppx_flow_count_keys_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_parse_batch_device_reasm", "pcppx_pcap_open", "pcppx_pcap_linktype",
     "pcppx_pcap_read_batch", "pcppx_pcap_read_batch_ex", "pcppx_pcap_map_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
-    "pcppx_unpack_layers",
+    "pcppx_unpack_layers", "pcppx_unpack_layers_brief",
 )
 
 

@@ -31,16 +31,24 @@ struct Slot
 	uint64_t* h_off = nullptr;
 	uint32_t* h_cap = nullptr;
 	pcppx_summary* h_sum = nullptr;
-	pcppx_layer* h_lay = nullptr;
+	pcppx_layer* h_lay = nullptr;  // FIXED rows, or (DENSE) the chunk's chains
+	pcppx_brief* h_brief = nullptr;
+	uint32_t* h_total = nullptr;   // DENSE: the chunk's chain entries
 	uint8_t* d_data = nullptr;
 	uint64_t* d_off = nullptr;
 	uint32_t* d_cap = nullptr;
 	pcppx_summary* d_sum = nullptr;
 	pcppx_layer* d_lay = nullptr;
+	pcppx_brief* d_brief = nullptr;
+	pcppx_layer* d_dense = nullptr;  // DENSE: the chunk's chains back to back
+	uint32_t* d_dsum = nullptr;      // DENSE: per-block chain totals + the chunk's total (last word)
+	hipEvent_t parsed = nullptr;     // DENSE: the chunk's records and total are on the host
 	uint8_t* h_match = nullptr;  // host filter path: per-packet verdicts
 	uint8_t* d_match = nullptr;
 	bool busy = false;
 	uint32_t first = 0, count = 0, ml = 0;
+	uint64_t dense_first = 0;  // DENSE: the chunk's first entry in the caller's array
+	uint32_t dense_count = 0;
 };
 
 // memcpy split over persistent host threads (started with the host path, joined at pcppx_close): a single
@@ -184,7 +192,7 @@ bool ok(hipError_t e)
 int valid_opts(const pcppx_opts* o)
 {
 	if (o == nullptr || o->max_layers > PCPPX_MAX_LAYERS || o->window > PCPPX_WINDOW_SHORT ||
-	    o->layout > PCPPX_LAYOUT_PACKED || (o->layout == PCPPX_LAYOUT_PACKED && o->max_layers > PCPPX_PACKED_MAX_LAYERS))
+	    o->layout > PCPPX_LAYOUT_DENSE || (o->layout == PCPPX_LAYOUT_PACKED && o->max_layers > PCPPX_PACKED_MAX_LAYERS))
 		return PCPPX_E_INVAL;
 	return PCPPX_OK;
 }
@@ -197,10 +205,10 @@ bool valid_device_records(const pcppx_opts* o, const pcppx_records* r)
 {
 	if (o->max_layers != 0 && r->layers == nullptr)
 		return false;
-	if (r->summary == nullptr &&
+	if (r->summary == nullptr && r->brief == nullptr &&
 	    (o->max_layers != 0 || (r->tuples == nullptr && r->flow_keys == nullptr && r->proto_stats == nullptr)))
 		return false;
-	return true;
+	return o->layout != PCPPX_LAYOUT_DENSE;  // DENSE: the host path's layout
 }
 
 // Scratch owned by a context and shared by its calls: a call waits (on its own stream) for the previous call's
@@ -255,6 +263,12 @@ void free_slot(Slot& s)
 {
 	if (s.st) (void)hipStreamDestroy(s.st);
 	if (s.done) (void)hipEventDestroy(s.done);
+	if (s.parsed) (void)hipEventDestroy(s.parsed);
+	(void)hipHostFree(s.h_brief);
+	(void)hipHostFree(s.h_total);
+	(void)hipFree(s.d_brief);
+	(void)hipFree(s.d_dense);
+	(void)hipFree(s.d_dsum);
 	(void)hipHostFree(s.h_data);
 	(void)hipHostFree(s.h_off);
 	(void)hipHostFree(s.h_cap);
@@ -293,7 +307,15 @@ int init_host_path(pcppx_ctx* c)
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_lay),
 		                         (size_t)kChunkPackets * PCPPX_MAX_LAYERS * sizeof(pcppx_layer))) &&
 		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_match), kChunkPackets)) &&
-		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_match), kChunkPackets));
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_match), kChunkPackets)) &&
+		            ok(hipEventCreateWithFlags(&s.parsed, hipEventDisableTiming)) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_brief), kChunkPackets * sizeof(pcppx_brief))) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_total), sizeof(uint32_t))) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_brief), kChunkPackets * sizeof(pcppx_brief))) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_dense),
+		                         (size_t)kChunkPackets * PCPPX_MAX_LAYERS * sizeof(pcppx_layer))) &&
+		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_dsum),
+		                         (pcppx::dense_blocks(kChunkPackets) + 1) * sizeof(uint32_t)));
 		if (!good)
 		{
 			for (Slot& t : c->slots)
@@ -427,26 +449,51 @@ void abandon_slots(pcppx_ctx* c)
 
 // copy a finished chunk's records from pinned memory to the caller's arrays (nothing to copy when the
 // caller's arrays are pinned: the chunk's D2H wrote them directly)
-void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out)
+void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out, bool dense)
 {
 	if (!direct_out)
 	{
-		cp.copy(out->summary + s.first, s.h_sum, (size_t)s.count * sizeof(pcppx_summary));
-		if (s.ml && out->layers)
+		if (out->summary)
+			cp.copy(out->summary + s.first, s.h_sum, (size_t)s.count * sizeof(pcppx_summary));
+		if (out->brief)
+			cp.copy(out->brief + s.first, s.h_brief, (size_t)s.count * sizeof(pcppx_brief));
+		if (s.ml && out->layers && dense)
+			cp.copy(out->layers + s.dense_first, s.h_lay, (size_t)s.dense_count * sizeof(pcppx_layer));
+		else if (s.ml && out->layers)
 			cp.copy(out->layers + (size_t)s.first * s.ml, s.h_lay, (size_t)s.count * s.ml * sizeof(pcppx_layer));
 	}
-	if (out->flow_keys)  // the dense hash5 column, from the host copy of the summaries
+	if (out->flow_keys)  // the dense hash5 column, from the host copy of the summaries / briefs
 		for (uint32_t k = 0; k < s.count; ++k)
-			out->flow_keys[s.first + k] = out->summary[s.first + k].hash5;
+			out->flow_keys[s.first + k] = out->summary ? out->summary[s.first + k].hash5 : out->brief[s.first + k].hash5;
 	s.busy = false;
 }
+
+// DENSE, second half of a chunk: once its total is on the host, its chains are copied out behind the chunks before it
+bool finish_dense(Slot& p, pcppx_records* r, bool direct_out, uint64_t* written)
+{
+	if (!ok(hipEventSynchronize(p.parsed)))
+		return false;
+	p.dense_count = *p.h_total;
+	p.dense_first = *written;
+	*written += p.dense_count;
+	pcppx_layer* dst = direct_out ? r->layers + p.dense_first : p.h_lay;
+	return (p.dense_count == 0 ||
+	        ok(hipMemcpyAsync(dst, p.d_dense, (size_t)p.dense_count * sizeof(pcppx_layer), hipMemcpyDeviceToHost, p.st))) &&
+	       ok(hipEventRecord(p.done, p.st));
+}
+
 // pcppx_parse_batch_host's chunk pipeline (argument checks done; slots idle on entry)
 int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r)
 {
 	int rc = PCPPX_OK;
 	const uint32_t ml = o->max_layers;
+	const bool rows = ml != 0 && r->layers != nullptr;
+	const bool dense = rows && o->layout == PCPPX_LAYOUT_DENSE;
 	// a NIC ring / pcppx_host_alloc result buffer: records come back by DMA straight into the caller's arrays
-	const bool direct_out = is_pinned(r->summary) && (ml == 0 || r->layers == nullptr || is_pinned(r->layers));
+	const bool direct_out = (r->summary == nullptr || is_pinned(r->summary)) &&
+	                        (r->brief == nullptr || is_pinned(r->brief)) && (!rows || is_pinned(r->layers));
+	uint64_t written = 0;
+	Slot* pend = nullptr;  // DENSE: the previous chunk, its chains not yet copied out
 	uint32_t i = 0, k = 0;
 	while (i < b->n)
 	{
@@ -455,7 +502,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(c->copier, s, r, direct_out);
+			drain(c->copier, s, r, direct_out, dense);
 		}
 		size_t pos = 0;
 		const uint8_t* direct = nullptr;
@@ -464,34 +511,66 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		if (!upload_chunk(s, pos, cnt, direct))
 			return PCPPX_E_HIP;
 		pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
-		pcppx_records dr{ s.d_sum, ml ? s.d_lay : nullptr, nullptr };
-		rc = pcppx::launch_parse(&db, o, &dr, s.st);
+		pcppx_records dr{};
+		dr.summary = r->summary ? s.d_sum : nullptr;
+		dr.brief = r->brief ? s.d_brief : nullptr;
+		dr.layers = ml ? s.d_lay : nullptr;
+		pcppx_opts fo = *o;
+		fo.layout = PCPPX_LAYOUT_FIXED;  // DENSE is compacted from the chunk's FIXED rows below
+		rc = pcppx::launch_parse(&db, &fo, &dr, s.st);
+		if (rc == PCPPX_OK && dense)
+			rc = pcppx::launch_dense_compact(s.d_lay,
+			                                 dr.brief ? reinterpret_cast<const uint8_t*>(s.d_brief) + 14
+			                                          : reinterpret_cast<const uint8_t*>(s.d_sum) + 14,
+			                                 dr.brief ? sizeof(pcppx_brief) : sizeof(pcppx_summary), cnt, ml, s.d_dense,
+			                                 s.d_dsum, s.d_dsum + pcppx::dense_blocks(kChunkPackets), s.st);
 		if (rc != PCPPX_OK)
 			return rc;
-		pcppx_summary* hs = direct_out ? r->summary + i : s.h_sum;
-		pcppx_layer* hl = direct_out && r->layers ? r->layers + (size_t)i * ml : s.h_lay;
-		const bool good = ok(hipMemcpyAsync(hs, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st)) &&
-		       (ml == 0 || r->layers == nullptr ||
-		        ok(hipMemcpyAsync(hl, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer), hipMemcpyDeviceToHost, s.st))) &&
-		       ok(hipEventRecord(s.done, s.st));
+		pcppx_summary* hs = direct_out && r->summary ? r->summary + i : s.h_sum;
+		pcppx_brief* hb = direct_out && r->brief ? r->brief + i : s.h_brief;
+		pcppx_layer* hl = direct_out && rows ? r->layers + (size_t)i * ml : s.h_lay;
+		bool good = (!r->summary ||
+		             ok(hipMemcpyAsync(hs, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st))) &&
+		            (!r->brief || ok(hipMemcpyAsync(hb, s.d_brief, cnt * sizeof(pcppx_brief), hipMemcpyDeviceToHost, s.st)));
+		if (dense)
+			good = good &&
+			       ok(hipMemcpyAsync(s.h_total, s.d_dsum + pcppx::dense_blocks(kChunkPackets), sizeof(uint32_t),
+			                         hipMemcpyDeviceToHost, s.st)) &&
+			       ok(hipEventRecord(s.parsed, s.st));
+		else
+			good = good &&
+			       (!rows ||
+			        ok(hipMemcpyAsync(hl, s.d_lay, (size_t)cnt * ml * sizeof(pcppx_layer), hipMemcpyDeviceToHost, s.st))) &&
+			       ok(hipEventRecord(s.done, s.st));
 		if (!good)
 			return PCPPX_E_HIP;
 		s.busy = true;
 		s.first = i;
 		s.count = cnt;
 		s.ml = ml;
+		if (dense)
+		{
+			// chunk k-1's total is known by now (or soon: its kernels ran ahead of this chunk's upload)
+			if (pend != nullptr && !finish_dense(*pend, r, direct_out, &written))
+				return PCPPX_E_HIP;
+			pend = &s;
+		}
 		i = j;
 		++k;
 	}
+	if (pend != nullptr && !finish_dense(*pend, r, direct_out, &written))
+		return PCPPX_E_HIP;
 	for (Slot& s : c->slots)
 		if (s.busy)
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(c->copier, s, r, direct_out);
+			drain(c->copier, s, r, direct_out, dense);
 		}
+	r->layers_written = dense ? written : (rows ? (uint64_t)b->n * ml : 0);
 	return PCPPX_OK;
 }
+
 // pcppx_filter_batch_host's chunk pipeline (argument checks done; slots idle on entry)
 int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* spec, uint8_t* matched,
                     pcppx_packet_stats* stats)
@@ -523,7 +602,9 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 		if (prev != nullptr && !ok(hipStreamWaitEvent(s.st, prev->done, 0)))
 			return PCPPX_E_HIP;
 		pcppx_batch db{ s.d_data, s.d_off, s.d_cap, pos, cnt, b->linktype, 0 };
-		pcppx_records dr{ s.d_sum, s.d_lay, nullptr };
+		pcppx_records dr{};
+		dr.summary = s.d_sum;
+		dr.layers = s.d_lay;
 		rc = pcppx::launch_parse(&db, &o, &dr, s.st);
 		if (rc == PCPPX_OK)
 			rc = pcppx::launch_filter(&db, &dr, ml, spec, c->seq + i, c->d_keys, c->d_first, c->flow_slots,
@@ -704,6 +785,7 @@ extern "C"
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
 		r->layout = o->layout;
+		r->layers_written = o->max_layers ? (uint64_t)b->n * o->max_layers : 0;
 		return device_parse(c, b, o, r, nullptr, static_cast<hipStream_t>(hip_stream));
 	}
 
@@ -713,13 +795,14 @@ extern "C"
 			return PCPPX_E_INVAL;
 		if (b->n == 0)
 			return PCPPX_OK;
-		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || r->summary == nullptr ||
-		    (o->max_layers != 0 && r->layers == nullptr))
+		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr ||
+		    (r->summary == nullptr && r->brief == nullptr) || (o->max_layers != 0 && r->layers == nullptr))
 			return PCPPX_E_INVAL;
 		// device-path-only outputs
-		if (r->tuples != nullptr || r->proto_stats != nullptr || o->layout != PCPPX_LAYOUT_FIXED)
+		if (r->tuples != nullptr || r->proto_stats != nullptr || o->layout == PCPPX_LAYOUT_PACKED)
 			return PCPPX_E_INVAL;
-		r->layout = PCPPX_LAYOUT_FIXED;
+		r->layout = o->layout;
+		r->layers_written = 0;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
 		int rc = init_host_path(c);
@@ -893,6 +976,29 @@ int flow_count(pcppx_ctx* c, const pcppx_summary* summary, const uint32_t* keys_
 	}
 }
 
+namespace
+{
+// PCPPX_LAYOUT_PACKED -> FIXED, the chain lengths at n_layers[i * stride]
+int unpack_packed(const uint8_t* n_layers, size_t stride, const pcppx_layer* packed, uint64_t n, uint32_t max_layers,
+                  pcppx_layer* fixed)
+{
+	if (packed == nullptr || fixed == nullptr || max_layers == 0 || max_layers > PCPPX_PACKED_MAX_LAYERS)
+		return PCPPX_E_INVAL;
+	uint64_t pos = 0;
+	for (uint64_t i = 0; i < n; ++i)
+	{
+		if (i % 64 == 0)
+			pos = i * max_layers;  // tile t's run starts at entry 64 * t * max_layers
+		const uint32_t nl = n_layers[i * stride];
+		const uint32_t cnt = nl < max_layers ? nl : max_layers;
+		for (uint32_t k = 0; k < max_layers; ++k)
+			fixed[i * max_layers + k] = k < cnt ? packed[pos + k] : pcppx_layer{};
+		pos += cnt;
+	}
+	return PCPPX_OK;
+}
+}  // namespace
+
 extern "C"
 {
 	void* pcppx_host_alloc(size_t bytes)
@@ -914,19 +1020,18 @@ extern "C"
 	{
 		if (n == 0)
 			return PCPPX_OK;
-		if (summary == nullptr || packed == nullptr || fixed == nullptr || max_layers == 0 ||
-		    max_layers > PCPPX_PACKED_MAX_LAYERS)
+		if (summary == nullptr)
 			return PCPPX_E_INVAL;
-		uint64_t pos = 0;
-		for (uint64_t i = 0; i < n; ++i)
-		{
-			if (i % 64 == 0)
-				pos = i * max_layers;  // tile t's run starts at entry 64 * t * max_layers
-			const uint32_t cnt = summary[i].n_layers < max_layers ? summary[i].n_layers : max_layers;
-			for (uint32_t k = 0; k < max_layers; ++k)
-				fixed[i * max_layers + k] = k < cnt ? packed[pos + k] : pcppx_layer{};
-			pos += cnt;
-		}
-		return PCPPX_OK;
+		return unpack_packed(&summary->n_layers, sizeof(pcppx_summary), packed, n, max_layers, fixed);
+	}
+
+	int pcppx_unpack_layers_brief(const pcppx_brief* brief, const pcppx_layer* packed, uint64_t n, uint32_t max_layers,
+	                              pcppx_layer* fixed)
+	{
+		if (n == 0)
+			return PCPPX_OK;
+		if (brief == nullptr)
+			return PCPPX_E_INVAL;
+		return unpack_packed(&brief->n_layers, sizeof(pcppx_brief), packed, n, max_layers, fixed);
 	}
 }

@@ -25,4 +25,10 @@ int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* dkeys, cons
 int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
                        hipStream_t stream, void* wave_stats = nullptr);
 int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcppx_reasm_info* info, hipStream_t stream);
+// PCPPX_LAYOUT_DENSE on the host path: a chunk's FIXED rows (n x ml) -> its chains back to back (dense), the chain
+// lengths read from n_layers[i * nl_stride] (a summary's or a brief's byte 14); *total = the entries written.
+// block_sums: dense_blocks(n) words of scratch.
+uint32_t dense_blocks(uint32_t n);
+int launch_dense_compact(const pcppx_layer* fixed, const uint8_t* n_layers, uint32_t nl_stride, uint32_t n, uint32_t ml,
+                         pcppx_layer* dense, uint32_t* block_sums, uint32_t* total, hipStream_t stream);
 }  // namespace pcppx

@@ -997,6 +997,7 @@ struct Params
 	pcppx_tuple* tuples;      // optional 5-tuple extracts (pcppx_records.tuples)
 	uint4* wave_stats;        // optional per-wave collectStats counters (16 x u8), reduced by proto_stats_reduce_kernel
 	uint32_t packed;          // PCPPX_LAYOUT_PACKED: the chain's layer entries dense per 64-packet tile
+	pcppx_brief* brief;       // optional 16-B brief (pcppx_records.brief): the summary's first half
 };
 
 // Everything the summary needs after the chain walk.
@@ -2383,6 +2384,15 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	}
 	else if (in && prm.summary != nullptr)
 		write_summary(prm.summary + i, h5, h5d, h2, w.flags, w.n_layers, w.l4i, w.mask, ipc, ips, l4c, l4s);
+	// the 16-B brief: the summary's first half (hashes, flags, chain length, port layer) -- one coalesced 16-B store per
+	// lane; a caller that reads the layer rows derives isPacketOfType from them and the checksum verdicts are the flags
+	if (in && prm.brief != nullptr)
+	{
+		const uint32_t l4b = w.l4i >= 0 ? (uint32_t)w.l4i : 0xFFu;
+		u32x4 s0;
+		s0.x = h5; s0.y = h5d; s0.z = h2; s0.w = w.flags | (MarkFast && fast ? 0x8000u : 0u) | (w.n_layers << 16) | (l4b << 24);
+		__builtin_nontemporal_store(s0, reinterpret_cast<u32x4*>(prm.brief + i));
+	}
 	if (in && prm.flow_keys != nullptr)
 		__builtin_nontemporal_store(h5, prm.flow_keys + i);
 	if (in && prm.tuples != nullptr)  // the LDS window is still intact here (the rows below reuse it)
@@ -3204,6 +3214,7 @@ Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, 
 	prm.tuples = r->tuples;
 	prm.wave_stats = nullptr;
 	prm.packed = o->layout == PCPPX_LAYOUT_PACKED ? 1u : 0u;
+	prm.brief = r->brief;
 	return prm;
 }
 
@@ -3253,6 +3264,111 @@ constexpr uint32_t kFlowPartLog2 = 9;            // flow-table partitions (merge
 constexpr uint32_t kFlowMinRegionLog2 = 12;      // slots per partition at least (capacity 2^21+ -> 512 partitions)
 constexpr uint32_t kFlowMergeThreads = 512;
 
+// ---- PCPPX_LAYOUT_DENSE (host path): FIXED rows -> the chains back to back ----
+// Two small kernels per host-path chunk (<= 256k packets): dense_count_kernel sums each 1024-packet block's chain
+// lengths; dense_copy_kernel takes its block's base as the sum of the blocks before it (at most 256 words), scans its
+// threads' counts (4 consecutive packets per thread) and copies each chain's entries to its dense position. On-device
+// traffic is the FIXED rows once (8 * ml B per packet, ~6 us per chunk at HBM rates); what crosses PCIe is the chains.
+constexpr uint32_t kDenseThreads = 256, kDensePer = 4, kDenseBlockPk = kDenseThreads * kDensePer;
+
+__device__ __forceinline__ uint32_t block_sum_256(uint32_t v, uint32_t* lds)
+{
+	for (int o = 32; o > 0; o >>= 1)
+		v += __shfl_xor(v, o);
+	const uint32_t wv = threadIdx.x >> 6;
+	if ((threadIdx.x & 63) == 0)
+		lds[wv] = v;
+	__syncthreads();
+	const uint32_t t = lds[0] + lds[1] + lds[2] + lds[3];
+	__syncthreads();
+	return t;
+}
+
+__global__ __launch_bounds__(kDenseThreads) void dense_count_kernel(const uint8_t* __restrict__ nl, uint32_t stride,
+                                                                    uint32_t n, uint32_t ml, uint32_t* __restrict__ bsum)
+{
+	__shared__ uint32_t lds[4];
+	uint32_t s = 0;
+	for (uint32_t k = 0; k < kDensePer; ++k)
+	{
+		const uint32_t i = blockIdx.x * kDenseBlockPk + k * kDenseThreads + threadIdx.x;
+		if (i < n)
+			s += min((uint32_t)nl[(size_t)i * stride], ml);
+	}
+	s = block_sum_256(s, lds);
+	if (threadIdx.x == 0)
+		bsum[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kDenseThreads) void dense_copy_kernel(const uint2* __restrict__ fixed,
+                                                                   const uint8_t* __restrict__ nl, uint32_t stride,
+                                                                   uint32_t n, uint32_t ml,
+                                                                   const uint32_t* __restrict__ bsum, uint2* __restrict__ dense,
+                                                                   uint32_t* __restrict__ total)
+{
+	__shared__ uint32_t lds[4];
+	__shared__ uint32_t wsum[4];
+	// the block's base: the chain lengths of every block before it
+	uint32_t b = 0;
+	for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kDenseThreads)
+		b += bsum[j];
+	const uint32_t base = block_sum_256(b, lds);
+	// this thread's 4 consecutive packets, their counts and the thread's exclusive offset in the block
+	const uint32_t i0 = blockIdx.x * kDenseBlockPk + threadIdx.x * kDensePer;
+	uint32_t c[kDensePer], mine = 0;
+	for (uint32_t k = 0; k < kDensePer; ++k)
+	{
+		c[k] = i0 + k < n ? min((uint32_t)nl[(size_t)(i0 + k) * stride], ml) : 0u;
+		mine += c[k];
+	}
+	uint32_t incl = mine;  // inclusive wave scan, then the waves' totals
+	const uint32_t lane = threadIdx.x & 63;
+	for (uint32_t o = 1; o < 64; o <<= 1)
+	{
+		const uint32_t t = __shfl_up(incl, o);
+		incl += lane >= o ? t : 0u;
+	}
+	if (lane == 63)
+		wsum[threadIdx.x >> 6] = incl;
+	__syncthreads();
+	uint32_t wbase = 0;
+	for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w)
+		wbase += wsum[w];
+	uint32_t pos = base + wbase + incl - mine;
+	for (uint32_t k = 0; k < kDensePer; ++k)
+	{
+		const uint2* src = fixed + (size_t)(i0 + k) * ml;
+		for (uint32_t e = 0; e < c[k]; ++e)
+			dense[pos + e] = src[e];
+		pos += c[k];
+	}
+	if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kDenseThreads - 1)
+		*total = pos;  // the last thread of the last block ends the batch's chains
+}
+
+}  // namespace
+
+uint32_t dense_blocks(uint32_t n)
+{
+	return (n + kDenseBlockPk - 1) / kDenseBlockPk;
+}
+
+int launch_dense_compact(const pcppx_layer* fixed, const uint8_t* n_layers, uint32_t nl_stride, uint32_t n, uint32_t ml,
+                         pcppx_layer* dense, uint32_t* block_sums, uint32_t* total, hipStream_t stream)
+{
+	if (n == 0 || ml == 0)
+		return hipMemsetAsync(total, 0, sizeof(uint32_t), stream) == hipSuccess ? PCPPX_OK : PCPPX_E_HIP;
+	const uint32_t g = dense_blocks(n);
+	hipLaunchKernelGGL(dense_count_kernel, dim3(g), dim3(kDenseThreads), 0, stream, n_layers, nl_stride, n, ml,
+	                   block_sums);
+	hipLaunchKernelGGL(dense_copy_kernel, dim3(g), dim3(kDenseThreads), 0, stream,
+	                   reinterpret_cast<const uint2*>(fixed), n_layers, nl_stride, n, ml, block_sums,
+	                   reinterpret_cast<uint2*>(dense), total);
+	return check_launch("dense_compact", stream);
+}
+
+namespace
+{
 }  // namespace
 
 int check_launch(const char* what, hipStream_t /*stream*/)

@@ -57,9 +57,41 @@ class Engine:
                   "pcppx_parse_batch_host")
         return summary, layers[: batch.n * opts.max_layers].reshape(batch.n, opts.max_layers)
 
+    def parse_host_ex(self, batch: PacketBatch, opts: abi.Opts, want_summary: bool = True, want_brief: bool = False,
+                      pinned: bool = False):
+        """Host parse with the ABI-7 outputs: the summary and / or the 16-B brief, and the layer entries in opts.layout
+        (LAYOUT_FIXED: [n, max_layers]; LAYOUT_DENSE: the chains back to back, pcppx_records.layers_written of them).
+        Returns (summary | None, brief | None, layers, layers_written). pinned: page-locked output arrays (records
+        DMA'd straight into them)."""
+        n, ml = batch.n, opts.max_layers
+        keep = []
+
+        def arr(count, dt):
+            if not pinned:
+                return np.zeros(count, dtype=dt)
+            buf = PinnedBuffer(max(count, 1) * dt.itemsize)
+            keep.append(buf)
+            return buf.array.view(dt)[:count]
+
+        summary = arr(n, abi.SUMMARY_DTYPE) if want_summary else None
+        brief = arr(n, abi.BRIEF_DTYPE) if want_brief else None
+        layers = arr(max(n * ml, 1), abi.LAYER_DTYPE)
+        rec = abi.Records(summary.ctypes.data if summary is not None else None, layers.ctypes.data if ml else None)
+        rec.brief = brief.ctypes.data if brief is not None else None
+        b = batch.c_batch()
+        abi.check(self.lib.pcppx_parse_batch_host(self.ctx, C.byref(b), C.byref(opts), C.byref(rec)),
+                  "pcppx_parse_batch_host")
+        w = int(rec.layers_written)
+        out = (None if summary is None else summary.copy() if pinned else summary,
+               None if brief is None else brief.copy() if pinned else brief,
+               layers[:w].copy() if pinned else layers[:w], w)
+        for k in keep:
+            k.free()
+        return out
+
     # ---- device-resident batches (torch tensors on this GPU) ----
     def parse_device(self, data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers=None,
-                     stream: int | None = None, flow_keys=None, tuples=None, proto_stats=None) -> None:
+                     stream: int | None = None, flow_keys=None, tuples=None, proto_stats=None, brief=None) -> None:
         """Queue a parse of device tensors on `stream` (a hipStream_t handle, e.g.
         torch.cuda.current_stream().cuda_stream). summary: uint8 tensor of n*32 bytes (or None with no layers when
         tuples / flow_keys / proto_stats is given); layers: n*max_layers*8; flow_keys: n int32 (hash5); tuples: n*48
@@ -68,6 +100,7 @@ class Engine:
         opt = lambda t: abi.ptr(t) if t is not None else None  # noqa: E731
         rec = abi.Records(opt(summary), abi.ptr(layers) if (layers is not None and opts.max_layers) else None,
                           opt(flow_keys), opt(tuples), opt(proto_stats))
+        rec.brief = opt(brief)
         abi.check(self.lib.pcppx_parse_batch_device(self.ctx, C.byref(b), C.byref(opts), C.byref(rec),
                                                     C.c_void_p(stream or 0)), "pcppx_parse_batch_device")
 
@@ -257,9 +290,11 @@ def records_from_device(summary_t, layers_t, n: int, max_layers: int):
 
 
 def parse_on_device_ex(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = None, device: str = "cuda:0",
-                       summary: bool = True, tuples: bool = False, proto_stats: bool = False, flow_keys: bool = False):
-    """parse_on_device with the optional outputs: {"summary", "layers" (FIXED [n, max_layers], decoded when the
-    layout is PACKED), "packed" (the raw PACKED entries), "tuples", "proto_stats" (dict), "flow_keys" (u32 hash5)}."""
+                       summary: bool = True, tuples: bool = False, proto_stats: bool = False, flow_keys: bool = False,
+                       brief: bool = False):
+    """parse_on_device with the optional outputs: {"summary", "brief" (16-B pcppx_brief), "layers" (FIXED
+    [n, max_layers], decoded when the layout is PACKED, through the summary or else the brief), "packed" (the raw PACKED
+    entries), "tuples", "proto_stats" (dict), "flow_keys" (u32 hash5)}."""
     import torch
 
     opts = opts or abi.make_opts()
@@ -270,17 +305,20 @@ def parse_on_device_ex(eng: Engine, batch: PacketBatch, opts: abi.Opts | None = 
     tp = torch.zeros(max(n, 1) * 48, dtype=torch.uint8, device=device) if tuples else None
     ps = torch.zeros(abi.PROTO_STATS, dtype=torch.int64, device=device) if proto_stats else None
     fk = torch.zeros(max(n, 1), dtype=torch.int32, device=device) if flow_keys else None
+    br = torch.zeros(max(n, 1) * 16, dtype=torch.uint8, device=device) if brief else None
     eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, st, lay if opts.max_layers else None,
-                     torch.cuda.current_stream(device).cuda_stream, flow_keys=fk, tuples=tp, proto_stats=ps)
+                     torch.cuda.current_stream(device).cuda_stream, flow_keys=fk, tuples=tp, proto_stats=ps, brief=br)
     torch.cuda.synchronize(device)
     out = {}
     if st is not None:
         out["summary"] = st.cpu().numpy().view(abi.SUMMARY_DTYPE)[:n]
-    if opts.max_layers and st is not None:
+    if br is not None:
+        out["brief"] = br.cpu().numpy().view(abi.BRIEF_DTYPE)[:n]
+    if opts.max_layers and (st is not None or br is not None):
         raw = lay.cpu().numpy().view(abi.LAYER_DTYPE)[: n * opts.max_layers]
         if opts.layout == abi.LAYOUT_PACKED:
             out["packed"] = raw
-            out["layers"] = abi.unpack_layers(out["summary"], raw, opts.max_layers)
+            out["layers"] = abi.unpack_layers(out["summary"] if st is not None else out["brief"], raw, opts.max_layers)
         else:
             out["layers"] = raw.reshape(n, opts.max_layers)
     if tp is not None:

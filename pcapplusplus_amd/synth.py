@@ -347,10 +347,10 @@ def _corrupt(batch: PacketBatch, rng: np.random.Generator, frac: float, info: di
     batch.meta["corrupted"] = int(len(half) + len(v4))
 
 
-def imix(n: int, seed: int, vlan_frac: float = 0.25, v6_frac: float = 0.30, corrupt_frac: float = 0.01,
-         sizes=IMIX_SIZES, weights=IMIX_WEIGHTS, flows: int | None = None) -> PacketBatch:
-    """Config 3 (flows=None) / config 4 (flows=N: 5-tuples Zipf(1.1) over N flows, both directions)."""
-    rng = np.random.default_rng(seed)
+def _imix_attrs(rng: np.random.Generator, n: int, vlan_frac: float, v6_frac: float, sizes, weights,
+                flows: int | None, univ: dict | None) -> dict:
+    """Per-packet draws of an IMIX batch: size, VLAN, IPv6, TCP, and with a flow universe the Zipf(1.1) flow and the
+    direction (the flow then fixes IPv6 / TCP)."""
     w = np.array(weights, dtype=np.float64)
     size_of = np.array(sizes)[rng.choice(len(sizes), size=n, p=w / w.sum())]
     vlan = rng.random(n) < vlan_frac
@@ -367,20 +367,31 @@ def imix(n: int, seed: int, vlan_frac: float = 0.25, v6_frac: float = 0.30, corr
         pz /= pz.sum()
         flow_id = rng.choice(flows, size=n, p=pz)
         dirn = rng.random(n) < 0.5
-        frng = np.random.default_rng(seed + 1000)
-        f_v6 = frng.random(flows) < v6_frac
-        f_tcp = frng.random(flows) < 0.5
-        f_src4 = frng.integers(0, 256, size=(flows, 4), dtype=np.uint8)
-        f_dst4 = frng.integers(0, 256, size=(flows, 4), dtype=np.uint8)
-        f_src6 = frng.integers(0, 256, size=(flows, 16), dtype=np.uint8)
-        f_dst6 = frng.integers(0, 256, size=(flows, 16), dtype=np.uint8)
-        f_sp, f_dp = safe_ports(frng, flows), safe_ports(frng, flows)
-        v6 = f_v6[flow_id]
-        tcp = f_tcp[flow_id]
+        v6 = univ["v6"][flow_id]
+        tcp = univ["tcp"][flow_id]
         # a flow keeps its protocol: 64 B cannot hold IPv6/TCP, so those packets become 512 B
         size_of = np.where(small & v6 & tcp, sizes[1], size_of)
         small = size_of < 14 + 4 + 40 + 20 + 2
         vlan = np.where(small & v6, False, vlan)
+    return {"size_of": size_of, "vlan": vlan, "v6": v6, "tcp": tcp, "flow_id": flow_id, "dirn": dirn}
+
+
+def _flow_universe(seed: int, flows: int, v6_frac: float) -> dict:
+    """The flows' 5-tuples (protocol, addresses, ports), drawn from the config's seed alone."""
+    frng = np.random.default_rng(seed + 1000)
+    u = {"v6": frng.random(flows) < v6_frac, "tcp": frng.random(flows) < 0.5}
+    u["src4"] = frng.integers(0, 256, size=(flows, 4), dtype=np.uint8)
+    u["dst4"] = frng.integers(0, 256, size=(flows, 4), dtype=np.uint8)
+    u["src6"] = frng.integers(0, 256, size=(flows, 16), dtype=np.uint8)
+    u["dst6"] = frng.integers(0, 256, size=(flows, 16), dtype=np.uint8)
+    u["sp"], u["dp"] = safe_ports(frng, flows), safe_ports(frng, flows)
+    return u
+
+
+def _imix_rows(at: dict, univ: dict | None, n: int, row_seed, sizes, rng: np.random.Generator,
+               corrupt_frac: float) -> PacketBatch:
+    """Build and interleave the packets the attribute draws describe (groups of one size / VLAN / IP / L4 shape)."""
+    size_of, vlan, v6, tcp, flow_id, dirn = (at[k] for k in ("size_of", "vlan", "v6", "tcp", "flow_id", "dirn"))
     groups = []
     info_l4 = np.zeros(n, dtype=np.int64)
     info_ip = np.zeros(n, dtype=np.int64)
@@ -392,19 +403,19 @@ def imix(n: int, seed: int, vlan_frac: float = 0.25, v6_frac: float = 0.30, corr
                     if len(idx) == 0:
                         continue
                     tuples = None
-                    if flows:
+                    if univ is not None:
                         fid = flow_id[idx]
                         fwd = ~dirn[idx]
                         if ip6:
-                            a, b = f_src6[fid], f_dst6[fid]
+                            a, b = univ["src6"][fid], univ["dst6"][fid]
                         else:
-                            a, b = f_src4[fid], f_dst4[fid]
+                            a, b = univ["src4"][fid], univ["dst4"][fid]
                         src = np.where(fwd[:, None], a, b)
                         dst = np.where(fwd[:, None], b, a)
-                        sp = np.where(fwd, f_sp[fid], f_dp[fid]).astype(np.uint16)
-                        dp = np.where(fwd, f_dp[fid], f_sp[fid]).astype(np.uint16)
+                        sp = np.where(fwd, univ["sp"][fid], univ["dp"][fid]).astype(np.uint16)
+                        dp = np.where(fwd, univ["dp"][fid], univ["sp"][fid]).astype(np.uint16)
                         tuples = {"src": src, "dst": dst, "sport": sp, "dport": dp}
-                    grng = np.random.default_rng([seed, s, int(vl), int(ip6), int(t)])
+                    grng = np.random.default_rng([*row_seed, s, int(vl), int(ip6), int(t)])
                     rows = build_rows(grng, len(idx), s, vl, ip6, t, tuples)
                     groups.append((rows, idx))
                     l2 = 18 if vl else 14
@@ -415,9 +426,49 @@ def imix(n: int, seed: int, vlan_frac: float = 0.25, v6_frac: float = 0.30, corr
     del groups
     if corrupt_frac:
         _corrupt(batch, rng, corrupt_frac, {"l4_csum_off": info_l4, "ip_csum_off": info_ip})
+    return batch
+
+
+def imix(n: int, seed: int, vlan_frac: float = 0.25, v6_frac: float = 0.30, corrupt_frac: float = 0.01,
+         sizes=IMIX_SIZES, weights=IMIX_WEIGHTS, flows: int | None = None) -> PacketBatch:
+    """Config 3 (flows=None) / an IMIX batch with 5-tuples Zipf(1.1) over `flows` flows, both directions."""
+    rng = np.random.default_rng(seed)
+    univ = _flow_universe(seed, flows, v6_frac) if flows else None
+    at = _imix_attrs(rng, n, vlan_frac, v6_frac, sizes, weights, flows, univ)
+    batch = _imix_rows(at, univ, n, [seed], sizes, rng, corrupt_frac)
     batch.meta.update(config="imix", seed=seed, flows=flows)
     if flows:
-        batch.meta["flow_id"] = flow_id
+        batch.meta["flow_id"] = at["flow_id"]
+    return batch
+
+
+FLOW_STREAM_BLOCK = 500_000  # packets per independently drawn block of the config-4 stream
+
+
+def flow_stream(lo: int, hi: int, seed: int = 4, flows: int = 1_000_000, v6_frac: float = 0.30,
+                sizes=IMIX_SIZES, weights=IMIX_WEIGHTS) -> PacketBatch:
+    """Packets [lo, hi) of BASELINE config 4's ONE IMIX stream (100M packets over one universe
+    of 1M flows, Zipf(1.1) 5-tuples in both directions, cut into contiguous shards, §8e). The stream is drawn in blocks
+    of FLOW_STREAM_BLOCK packets, block b from its own seed (seed, b), so any range is generated without the packets
+    before it; the flow universe comes from the config's seed alone, so every rank's shard draws from the same 1M
+    flows and a flow spans shards. A packet's size, direction and flow -- hence its caplen and hash5Tuple key -- are
+    those of the stream position, whichever rank generates it."""
+    if not 0 <= lo <= hi:
+        raise ValueError("bad stream range")
+    n = hi - lo
+    univ = _flow_universe(seed, flows, v6_frac)
+    parts = []
+    for blk in range(lo // FLOW_STREAM_BLOCK, -(-hi // FLOW_STREAM_BLOCK) if n else lo // FLOW_STREAM_BLOCK):
+        b0 = blk * FLOW_STREAM_BLOCK
+        at = _imix_attrs(np.random.default_rng([seed, 7, blk]), FLOW_STREAM_BLOCK, 0.25, v6_frac, sizes, weights, flows,
+                         univ)
+        a, e = max(lo, b0) - b0, min(hi, b0 + FLOW_STREAM_BLOCK) - b0
+        parts.append({k: v[a:e] for k, v in at.items()})
+    at = {k: np.concatenate([p[k] for p in parts]) if parts else np.zeros(0) for k in parts[0]} if parts else \
+        _imix_attrs(np.random.default_rng([seed, 7]), 0, 0.25, v6_frac, sizes, weights, flows, univ)
+    batch = _imix_rows(at, univ, n, [seed, 7, lo], sizes, np.random.default_rng([seed, 8, lo]), 0.0)
+    batch.meta.update(config="flow-stream", seed=seed, flows=flows, stream_lo=lo, stream_hi=hi,
+                      flow_id=at["flow_id"])
     return batch
 
 
@@ -455,8 +506,8 @@ def config(cfg: int, n: int | None = None) -> PacketBatch:
         return small64(n or 1_000_000, 2)
     if cfg == 3:
         return imix(n or 10_000_000, 3)
-    if cfg == 4:
-        return imix(n or 12_500_000, 4, flows=1_000_000, corrupt_frac=0.0)
+    if cfg == 4:  # the first n packets of the one config-4 stream (rank 0's shard)
+        return flow_stream(0, n or 12_500_000, 4)
     if cfg == 5:
         return deep(n or 10_000_000, 5)
     raise ValueError(f"unknown config {cfg}")

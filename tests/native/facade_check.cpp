@@ -22,6 +22,7 @@
  *       the phases of the reference benchmark's packet loop (open, first getNextPacket, first Packet(&raw, TCP), the
  *       rest of the loop, close), averaged over reps after one untimed run; one JSON line, microseconds.  (GPU.)
  *   env PCPPX_CHECK_HOST_PARSER=<lib.so>: register that library's pcppx_host_parse with setHostParser.
+ *   env PCPPX_CHECK_PAGE_CHECKSUMS=1: setPageChecksums(true) (the records then carry the checksum verdicts and values).
  */
 #include <dlfcn.h>
 
@@ -329,6 +330,8 @@ int main(int argc, char** argv)
 {
 	try
 	{
+		if (std::getenv("PCPPX_CHECK_PAGE_CHECKSUMS") != nullptr)
+			pcppx::setPageChecksums(true);
 		if (const char* lib = std::getenv("PCPPX_CHECK_HOST_PARSER"))
 		{
 			void* h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);

@@ -106,7 +106,7 @@ def test_bench_small_run_checks_its_records(cfg):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [4, 3])
-def test_bench_two_ranks_self_launch(cfg):
+def test_bench_two_ranks_self_launch(cfg, tmp_path):
     """`bench.py --gpus 2` through its own launch (a child torch.distributed.run, two ranks over gloo sharing the
     box's one card: a code-path check of the N>1 path, not a scaling number): one line from rank 0 with n_gpus 2 and
     both ranks' times; config 4 merges the two ranks' flow tables exactly with every packet conserved and sums both
@@ -114,9 +114,10 @@ def test_bench_two_ranks_self_launch(cfg):
     import json
 
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dump = tmp_path / "flows.npz"
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--config",
                         str(cfg), "--packets", "200000", "--steps", "3", "--warmup", "1", "--no-e2e", "--no-traffic",
-                        "--cpu-sample", "20000", "--cpu-seconds", "0.5"],
+                        "--cpu-sample", "20000", "--cpu-seconds", "0.5", "--dump-flows", str(dump)],
                        capture_output=True, text=True, timeout=400, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -129,5 +130,23 @@ def test_bench_two_ranks_self_launch(cfg):
         ft = c["flow_table"]
         assert ft["ranks_merged"] == 2 and ft["exact"] and ft["conserved"]
         assert ft["packets_counted"] == ft["expected"] == 2 * 200000 * 4
+        assert ft["merged_within_universe"] and ft["flows_spanning_ranks"] > 1000
         cs = c["collect_stats"]
         assert cs["consistent"] and cs["ranks_merged"] == 2 and cs["packet_count"] == 2 * 200000
+        # the merged table equals a single-pass map over the union of the two shards (the stream's first 400k
+        # packets), key for key: the restatement's hash5Tuple grouped on the host, times the 4 launches per rank
+        import numpy as np
+
+        import oracle
+        from pcapplusplus_amd import abi, shard, synth
+
+        m = np.load(dump)
+        whole = synth.flow_stream(0, 400_000, 4, flows=bench.CONFIG4_FLOWS)
+        s, _ = oracle.oracle_parse(whole, abi.make_opts(0, 8, False, 0), threads=8)
+        want = shard.flow_table(s["hash5"], whole.caplens)
+        launches = int(m["launches"][0])
+        got = {int(k): (int(p) // launches, int(b) // launches) for k, p, b in zip(m["keys"], m["packets"], m["bytes"])}
+        assert all(int(p) % launches == 0 for p in m["packets"])
+        if m["key0"][0]:
+            got[-1] = (int(m["key0"][0]) // launches, int(m["key0"][1]) // launches)
+        assert got == want and int(m["key0"][2]) == 0

@@ -193,14 +193,21 @@ VARIANTS = {  # facade_check plan name -> (parse_until_family, parse_until_osi)
 REC = np.dtype([("sum", abi.SUMMARY_DTYPE), ("lay", abi.LAYER_DTYPE, (abi.MAX_LAYERS,))])
 
 
-def _run_plan(built, tmp_path, batch, plan, host_parser=False):
+def _env(host_parser=False, checksums=False):
+    import os
+
+    env = dict(os.environ)
+    if host_parser:
+        env["PCPPX_CHECK_HOST_PARSER"] = str(oracle.REF_SO)
+    if checksums:
+        env["PCPPX_CHECK_PAGE_CHECKSUMS"] = "1"
+    return env
+
+
+def _run_plan(built, tmp_path, batch, plan, host_parser=False, checksums=False):
     f, o = tmp_path / "in.pcap", tmp_path / "rec.bin"
     write_pcap(f, batch)
-    env = None
-    if host_parser:
-        import os
-
-        env = dict(os.environ, PCPPX_CHECK_HOST_PARSER=str(oracle.REF_SO))
+    env = _env(host_parser, checksums)
     r = subprocess.run([str(built), "parse", str(f), str(o), plan], capture_output=True, text=True, timeout=600,
                        env=env)
     assert r.returncode == 0, r.stderr
@@ -209,14 +216,15 @@ def _run_plan(built, tmp_path, batch, plan, host_parser=False):
     return rec
 
 
-def _expected(batch, plan, reference=False):
-    """per packet the records of the variant the plan applies to it: from the restatement (or the reference)"""
+def _expected(batch, plan, reference=False, checksums=False):
+    """per packet the records of the variant the plan applies to it: from the restatement (or the reference). The
+    per-packet entry points compute no checksum (as Packet(&raw) in Packet++) unless setPageChecksums is on."""
     names = plan.split(",")
     want_sum = np.zeros(batch.n, abi.SUMMARY_DTYPE)
     want_lay = np.zeros((batch.n, abi.MAX_LAYERS), abi.LAYER_DTYPE)
     for v in set(names):
         fam, osi = VARIANTS[v]
-        opts = abi.make_opts(fam, osi, True, abi.MAX_LAYERS)
+        opts = abi.make_opts(fam, osi, checksums, abi.MAX_LAYERS)
         s, lay = oracle.ref_parse(batch, opts) if reference else oracle.oracle_parse(batch, opts, threads=8)
         idx = np.array([i for i in range(batch.n) if names[i % len(names)] == v], np.int64)
         want_sum[idx] = s[idx]
@@ -235,13 +243,17 @@ def _captures():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("plan", ["full", "tcp", "osi3", "full,tcp,ip,osi3,osi4", "copy,free,tcp"])
-def test_gpu_packet_from_reader_equals_restatement(built, tmp_path, plan):
+@pytest.mark.parametrize("plan,checksums", [("full", False), ("tcp", False), ("osi3", False),
+                                            ("full,tcp,ip,osi3,osi4", False), ("copy,free,tcp", False),
+                                            ("full", True), ("full,tcp,copy", True)])
+def test_gpu_packet_from_reader_equals_restatement(built, tmp_path, plan, checksums):
     """Every Packet a reader's RawPacket builds equals the restatement's records for its options, bit for bit
-    (flagged packets: their exact prefix, as the device writes it); mixed plans force page re-parses."""
+    (flagged packets: their exact prefix, as the device writes it); mixed plans force page re-parses. Pages hold the
+    16-B brief + the chains (DENSE) and Packet::summary() rebuilds the protocol mask from the chain; with
+    setPageChecksums the 32-B summaries with the checksum values."""
     for name, b in _captures():
-        rec = _run_plan(built, tmp_path, b, plan)
-        ws, wl = _expected(b, plan)
+        rec = _run_plan(built, tmp_path, b, plan, checksums=checksums)
+        ws, wl = _expected(b, plan, checksums=checksums)
         try:
             oracle.compare_exact(rec["sum"], rec["lay"], ws, wl)
         except AssertionError as e:
@@ -261,13 +273,9 @@ def test_gpu_packet_from_own_bytes(built, tmp_path):
 def _run_vec(built, tmp_path, batch, plan, how, host_parser=False):
     f, o = tmp_path / "in.pcap", tmp_path / "rec.bin"
     write_pcap(f, batch)
-    env = None
-    if host_parser:
-        import os
-
-        env = dict(os.environ, PCPPX_CHECK_HOST_PARSER=str(oracle.REF_SO))
+    env = _env(host_parser)
     r = subprocess.run([str(built), "parsevec", str(f), str(o), plan, how], capture_output=True, text=True, timeout=600,
-                       env=env)
+                       env=env or _env())
     assert r.returncode == 0, r.stderr
     import json
 
@@ -380,7 +388,7 @@ def test_gpu_host_completion_every_golden_record(built, tmp_path):
         for v, (opts, rs, rl) in variants.items():
             if v not in GOLDEN_PLAN:
                 continue
-            rec = _run_plan(built, tmp_path, b, GOLDEN_PLAN[v], host_parser=True)
+            rec = _run_plan(built, tmp_path, b, GOLDEN_PLAN[v], host_parser=True, checksums=bool(opts.want_checksums))
             s, lay = rec["sum"], rec["lay"]
             ml = int(opts.max_layers)
             host = (s["flags"] & F_HOST) != 0

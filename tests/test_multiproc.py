@@ -83,8 +83,9 @@ def _device_format(hash5: np.ndarray, caplens: np.ndarray, capacity: int):
 
 
 def _device_worker(rank: int, world: int, port: int, q):
-    """Each rank holds a device-format flow table of its shard; rank 0 merges the compact tables (the bench's
-    config-4 host merge) and compares with one table over the whole batch."""
+    """Each rank holds a device-format flow table of its contiguous shard of the one config-4 stream; rank 0 merges the
+    compact tables (the bench's config-4 host merge) and compares with one table over the union of the shards, key for
+    key; flows span the shards (the merge adds real counts)."""
     import sys
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
@@ -95,18 +96,22 @@ def _device_worker(rank: int, world: int, port: int, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    b = synth.imix(30_000, 4, flows=3000, corrupt_frac=0.0)
-    lo, hi = shard.shard_range(b.n, world, rank)
-    part = b.slice(lo, hi)
+    # bench.py's config-4 layout: rank r parses packets [n r, n (r+1)) of ONE stream over ONE flow universe
+    n = 30_000
+    part = synth.flow_stream(n * rank, n * (rank + 1), 4, flows=3000)
     s, _ = oracle.oracle_parse(part, abi.make_opts(0, 8, False, 0))
     mine = shard.compact_device_table(*_device_format(s["hash5"], part.caplens, 1 << 13))
     tables = [None] * world
     dist.all_gather_object(tables, mine)
     if rank == 0:
         merged = shard.merge_device_tables(tables)
-        full, _ = oracle.oracle_parse(b, abi.make_opts(0, 8, False, 0))
+        # the single-pass map over the union of the shards: the stream's first n * world packets in one batch
+        whole = synth.flow_stream(0, n * world, 4, flows=3000)
+        full, _ = oracle.oracle_parse(whole, abi.make_opts(0, 8, False, 0))
         counted = int(merged["packets"].sum()) + merged["key0_packets"] + merged["dropped"]
-        q.put((shard.merged_to_dict(merged) == shard.flow_table(full["hash5"], b.caplens), counted == b.n))
+        spanning = sum(len(t["keys"]) for t in tables) - len(merged["keys"])
+        q.put((shard.merged_to_dict(merged) == shard.flow_table(full["hash5"], whole.caplens),
+               counted == whole.n and spanning > 100))
     dist.destroy_process_group()
 
 

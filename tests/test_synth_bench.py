@@ -85,3 +85,29 @@ def test_bench_header_extent_byte_model(cfg):
     ext = np.minimum(np.where(valid, end, 0).max(axis=1), b.caplens)
     assert got == int(ext.sum()) + 12 * b.n
     assert bench.algorithmic_read_bytes(b, True) == int(b.caplens.sum(dtype=np.int64)) + 12 * b.n
+
+
+def test_flow_stream_ranges_are_one_stream():
+    """BASELINE config 4 is ONE stream over ONE flow universe cut into contiguous shards: any range
+    of synth.flow_stream carries the same caplens, flows and hash5Tuple keys as that range of a longer call, across
+    block boundaries, and shards share flows."""
+    import numpy as np
+
+    import oracle
+    from pcapplusplus_amd import abi, synth
+
+    blk = synth.FLOW_STREAM_BLOCK
+    lo, hi = blk - 20_000, blk + 30_000
+    whole = synth.flow_stream(0, hi, 4, flows=5000)
+    part = synth.flow_stream(lo, hi, 4, flows=5000)
+    assert part.n == hi - lo
+    assert np.array_equal(part.caplens, whole.caplens[lo:hi])
+    assert np.array_equal(part.meta["flow_id"], whole.meta["flow_id"][lo:hi])
+    opts = abi.make_opts(0, 8, False, 0)
+    sp, _ = oracle.oracle_parse(part, opts, threads=8)
+    sw, _ = oracle.oracle_parse(whole.slice(lo, hi), opts, threads=8)
+    assert np.array_equal(sp["hash5"], sw["hash5"]) and (sp["hash5"] != 0).all()
+    a = set(synth.flow_stream(0, 20_000, 4, flows=5000).meta["flow_id"].tolist())
+    b = set(synth.flow_stream(20_000, 40_000, 4, flows=5000).meta["flow_id"].tolist())
+    assert len(a & b) > 500  # the Zipf head: flows span shards
+    assert synth.config(4, 1000).meta["stream_lo"] == 0
