@@ -39,7 +39,7 @@ DESC_BYTES = 12          # u64 offset + u32 caplen per packet
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=None, help="packets per GPU (default: the config's size)")
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 4, 5))
@@ -69,10 +69,12 @@ def parse_args():
                     help="layer-record layout (pcppx_opts.layout): fixed = max_layers entries per packet; packed = only the "
                          "chain's entries, dense per 64-packet tile (the same entries; auto: " + ", ".join(
                              f"config {c} {v}" for c, v in sorted(CONFIG_LAYOUT.items())) + ")")
-    ap.add_argument("--records", choices=("auto", "summary", "tuples", "keys"), default="auto",
-                    help="per-packet record: the 32-B summary, the 48-B 5-tuple extract (pcppx_tuple) alone, or (config "
-                         "4) only what the flow table reads: the dense hash5 column + collectStats, no summary (auto: "
-                         "tuples for config 2's 5-tuple extract, keys for config 4's flow table, else summary)")
+    ap.add_argument("--records", choices=("auto", "summary", "brief", "tuples", "keys"), default="auto",
+                    help="per-packet record: the 32-B summary, the 16-B brief (pcppx_brief: the summary's first half -- "
+                         "hashes, flags incl. the checksum verdicts, chain length, port layer; isPacketOfType from the "
+                         "layer rows), the 48-B 5-tuple extract (pcppx_tuple) alone, or (config 4) only what the flow table "
+                         "reads: the dense hash5 column + collectStats, no summary (auto: " + ", ".join(
+                             f"config {c} {v}" for c, v in sorted(CONFIG_RECORDS.items())) + ")")
     ap.add_argument("--dump-flows", default=None,
                     help="config 4: write the merged flow table (rank 0, after the timed region) to this .npz")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -86,6 +88,7 @@ SIZED_PACKETS = {64: 10_000_000, 512: 10_000_000, 1500: 5_000_000}  # config 3 a
 CONFIG_MAX_LAYERS = {2: 0, 3: 8, 4: 0, 5: 12}
 CONFIG4_FLOWS = 1_000_000  # config 4's flow universe (one for all ranks)
 CONFIG_LAYOUT = {3: "packed", 5: "packed"}  # configs with layer records
+CONFIG_RECORDS = {2: "tuples", 3: "summary", 4: "keys", 5: "summary"}
 # plain Eth / VLAN / IP / L4 stacks (configs 2 and 4): the one-round parse-only window (PCPPX_WINDOW_SHORT)
 CONFIG_WINDOW = {2: "short", 4: "short"}
 KERNEL_SRC = ROOT / "pcapplusplus_amd" / "csrc" / "pcppx_kernels.hip"
@@ -283,7 +286,9 @@ def main() -> None:
     gen_s = time.time() - t0
     want_csum = args.checksums == "on" or (args.checksums == "auto" and cfg == 3)
     layout = args.layout if args.layout != "auto" else CONFIG_LAYOUT.get(cfg, "fixed")
-    rec_kind = args.records if args.records != "auto" else {2: "tuples", 4: "keys"}.get(cfg, "summary")
+    rec_kind = args.records if args.records != "auto" else CONFIG_RECORDS[cfg]
+    if rec_kind == "brief" and not ml:
+        sys.exit("bench.py: --records brief goes with layer records (isPacketOfType comes from them)")
     if rec_kind in ("tuples", "keys") and ml:
         sys.exit(f"bench.py: --records {rec_kind} writes no layer records (use --max-layers 0)")
     if rec_kind == "keys" and cfg != 4:
@@ -296,6 +301,7 @@ def main() -> None:
     eng = Engine(local)
     data, offsets, caplens = to_device(batch, dev)
     summary = torch.empty(n * 32, dtype=torch.uint8, device=dev) if rec_kind == "summary" else None
+    brief = torch.empty(n * 16, dtype=torch.uint8, device=dev) if rec_kind == "brief" else None
     tuples = torch.empty(n * 48, dtype=torch.uint8, device=dev) if rec_kind == "tuples" else None
     layers = torch.empty(max(n * ml, 1) * 8, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -315,7 +321,7 @@ def main() -> None:
 
     def step(k=None):
         eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh, flow_keys, tuples,
-                         proto_stats)
+                         proto_stats, brief)
         if flows is not None:
             if k is not None:
                 mids[k].record(stream)
@@ -373,8 +379,8 @@ def main() -> None:
         del ext_lay
     nl16 = ext_sum.view(n, 32)[:, 14].to(torch.int64)
     chain_entries = int(torch.clamp(nl16, max=ml).sum().item()) if ml else 0
-    per_pkt = (32 if summary is not None else 0) + (48 if tuples is not None else 0) + \
-        (4 if flow_keys is not None else 0)
+    per_pkt = (32 if summary is not None else 0) + (16 if brief is not None else 0) + \
+        (48 if tuples is not None else 0) + (4 if flow_keys is not None else 0)
     write_bytes = n * per_pkt + {"fixed": 8 * n * ml, "packed": 8 * chain_entries}[layout]
     achieved = read_bytes / (kern_ms * 1e-3) / 1e9
 
@@ -390,6 +396,8 @@ def main() -> None:
         tuple_check = None
     # the flow table's keys: the timed launches' dense hash5 column equals the full parse's summary hash5
     keys_equal = bool(torch.equal(flow_keys, s[:, 0])) if flow_keys is not None else None
+    # the timed launches' briefs: the first half of the full parse's summaries, byte for byte
+    brief_equal = bool(torch.equal(brief.view(n, 16), ext_sum.view(n, 32)[:, :16])) if brief is not None else None
     stats_line = None
     if proto_stats is not None:  # collectStats over every launch (warmup + timed): the histogram of one pass
         launches = args.warmup + args.steps
@@ -547,6 +555,8 @@ def main() -> None:
             line["config"]["flow_table"] = flow_check
         if keys_equal is not None:
             line["config"]["flow_keys_equal_hash5"] = keys_equal
+        if brief_equal is not None:
+            line["config"]["brief_equal_summary_half"] = brief_equal
         if stats_line is not None:
             line["config"]["collect_stats"] = stats_line
         if tuple_check is not None:

@@ -22,7 +22,8 @@
  * PPP_PPTP, ARP, ICMP (+ the IPv4 header an error message quotes), TCP, UDP, the VXLAN and GTPv1 tunnels
  * (+ the inner packet), Payload, Trailer, the first layers of link types Ethernet, raw IP (RAW, DLT_RAW1/2,
  * IPV4, IPV6), Linux SLL / SLL2 and Null/Loopback, and the first L7 layers it can name: HTTPRequest /
- * HTTPResponse (+ the Payload body), SSL records and DNS.
+ * HTTPResponse (+ the Payload body), SSL records, DNS, SSH messages (port 22) and MySQL (port 3306, where no
+ * dissector ahead of it in TcpLayer::parseNextLayer takes the other port).
  * Packets for which the reference would build a layer outside this scope (other L7 dissectors, IGMP, PPPoE,
  * NFLOG / Cisco HDLC first layers, ...) are flagged PCPPX_F_NEEDS_HOST_L7 / PCPPX_F_NEEDS_HOST_PROTO: their
  * layer prefix is exact, and the host owns the rest.
@@ -142,9 +143,13 @@ typedef struct pcppx_opts {
 	uint8_t layout;              /* PCPPX_LAYOUT_*: how pcppx_records.layers is laid out */
 	uint8_t reserved[3];
 } pcppx_opts;
-#define PCPPX_WINDOW_DEFAULT 0 /* checksum launches: one 96-B window, 5 waves/SIMD (the fastest for Eth / VLAN / IP /
-                                  L4 traffic); parse-only launches: 96 B plus a second gather round up to 144 B for the
-                                  stacks the first window cannot hold (QinQ, MPLS, GRE, IPv6 extensions) */
+#define PCPPX_WINDOW_DEFAULT 0 /* the engine's choice (ABI 7), from the traffic this context has parsed: one tile in 64
+                                  of every parse counts its deep stacks (after up to two VLAN tags an MPLS label, or an IP
+                                  layer not followed by TCP / UDP); when more than 1 in 256 sampled packets had one, the
+                                  next launches run as DEEP (checksum launches) / with the second round (parse-only),
+                                  otherwise checksum launches gather one 96-B window (5 waves/SIMD) and parse-only ones
+                                  run as SHORT. Until 4096 packets were sampled: one 96-B window for checksum launches,
+                                  96 B + a second round up to 144 B for parse-only ones. pcppx_window_choice() */
 #define PCPPX_WINDOW_DEEP 1    /* checksum launches too gather the two-round 144-B window: deep stacks stay on the
                                   fast path instead of the generic walk; 4 waves/SIMD. Parse-only: as DEFAULT */
 #define PCPPX_WINDOW_SHORT 2   /* parse-only launches: one 96-B gather round and no second one (7 KiB of LDS per wave
@@ -262,6 +267,8 @@ PCPPX_API int pcppx_open(int device_ordinal, pcppx_ctx** out); /* one per host t
 PCPPX_API void pcppx_close(pcppx_ctx* ctx);
 PCPPX_API int pcppx_sync(pcppx_ctx* ctx);                      /* wait for everything queued on ctx's stream */
 PCPPX_API void* pcppx_ctx_stream(pcppx_ctx* ctx);              /* the context's own hipStream_t */
+/* the window a PCPPX_WINDOW_DEFAULT launch with / without checksums would run with now (waits for the last sample) */
+PCPPX_API int pcppx_window_choice(pcppx_ctx* ctx, int want_checksums, int* window);
 PCPPX_API void pcppx_default_opts(pcppx_opts* opts);           /* Packet(RawPacket*) defaults + checksums + 16 layers */
 
 /* Device-resident parse. batch and records hold device pointers; the kernels are queued on

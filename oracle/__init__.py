@@ -404,15 +404,43 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
 ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16, 17, 18, 19, 21, 25, 26, 30, 32, 33, 35, 44, 52, 63)
 
 
-def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:
+# TcpLayer::parseNextLayer's trigger ports (TcpLayer.cpp:372-491; pcppx_oracle.c tcp_l7_port), HTTP's (HttpLayer.h:74-77)
+# and SSL's (SSLLayer.h:488-510)
+TCP_L7_PORTS = frozenset((80, 8080, 5060, 5061, 179, 22, 53, 5353, 5355, 23, 21, 20, 13400, 3496, 30490, 102, 25, 587,
+                          389, 5432, 3306, 2123, 502, 443, 261, 448, 465, 563, 614, 636, 989, 990, 992, 993, 994, 995))
+HTTP_PORTS = frozenset((80, 8080))
+SSL_PORTS = frozenset((443, 261, 448, 465, 563, 614, 636, 989, 990, 992, 993, 994, 995))
+
+
+def _mysql_behind_earlier_dissector(batch, i: int, lay) -> bool:
+    """Packet i's last TCP layer (reference records `lay`, one packet) has port 3306 on one side and on the other a
+    trigger port whose dissector comes ahead of MySQL's in TcpLayer::parseNextLayer and has a validity rule of its own
+    (not 3306, GTPv2 2123, Modbus 502, HTTP or SSL): the only case where the reference may fall through to MySQL after
+    the engine left the payload to the host (pcppx_oracle.c tcp_l7, the MySQL rule)."""
+    tcp = [k for k in range(len(lay)) if lay["proto"][k] == 4]
+    if not tcp:
+        return False
+    off = int(lay["offset"][tcp[-1]])
+    pkt = batch.packet(i)
+    if off + 4 > len(pkt):
+        return False
+    sp, dp = int.from_bytes(pkt[off:off + 2], "big"), int.from_bytes(pkt[off + 2:off + 4], "big")
+    if 3306 not in (sp, dp):
+        return False
+    o = dp if sp == 3306 else sp
+    return o not in (3306, 2123, 502) and o in TCP_L7_PORTS and o not in HTTP_PORTS and o not in SSL_PORTS
+
+
+def check_flag_contract(eng_sum, ref_sum, ref_lay, batch=None) -> dict:
     """The NEEDS_HOST flags against the reference chain (records with max_layers >= 1):
       - every packet whose reference chain holds a layer the engine does not build is flagged
         (NEEDS_HOST_L7 / NEEDS_HOST_PROTO, or not parsed at all: OVERSIZE / BAD_DESC);
       - a flagged packet whose reference chain holds no such layer is one where the host's dissector, at the
         point the engine stopped, built nothing or fell back to a Payload layer, or (port 3306 beside another trigger
         port) the earlier dissector declined and the chain fell through to MySQL -- the engine cannot tell without
-        that dissector's own validity rules: the reference layer at index n_layers is GenericPayload, MySQL or
-        absent.
+        that dissector's own validity rules: the reference layer at index n_layers is GenericPayload or absent, or
+        MySQL exactly where the packet's ports are 3306 beside such a trigger port (checked from the bytes: `batch`
+        is required whenever a reference chain continues with MySQL).
     Returns counters {flagged, foreign, payload_fallback}."""
     host = (eng_sum["flags"] & (abi.F_NEEDS_HOST_L7 | abi.F_NEEDS_HOST_PROTO)) != 0
     unparsed = (eng_sum["flags"] & (abi.F_OVERSIZE | abi.F_BAD_DESC)) != 0
@@ -428,7 +456,11 @@ def check_flag_contract(eng_sum, ref_sum, ref_lay) -> dict:
     over = np.nonzero(host & ~foreign)[0]
     en = eng_sum["n_layers"][over].astype(np.int64)
     nxt = np.where(en < rn[over], ref_lay["proto"][over, np.minimum(en, ml - 1)], 25)
-    bad = over[(nxt != 25) & (nxt != 63)]
+    mysql = over[nxt == 63]
+    ok_mysql = np.array([batch is not None and _mysql_behind_earlier_dissector(batch, int(i), ref_lay[i][: rn[i]])
+                         for i in mysql], dtype=bool)
+    bad = np.concatenate([over[(nxt != 25) & (nxt != 63)], mysql[~ok_mysql]]) if len(mysql) else \
+        over[(nxt != 25) & (nxt != 63)]
     if len(bad):
         i = int(bad[0])
         raise AssertionError(f"{len(bad)} flagged packets whose reference chain continues with an engine layer; "

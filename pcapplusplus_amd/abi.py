@@ -281,6 +281,8 @@ def _declare(lib: C.CDLL) -> C.CDLL:
     lib.pcppx_host_free.restype = None
     lib.pcppx_unpack_layers.argtypes = [P, P, C.c_uint64, C.c_uint32, P]
     lib.pcppx_unpack_layers.restype = C.c_int
+    lib.pcppx_window_choice.argtypes = [P, C.c_int, C.POINTER(C.c_int)]
+    lib.pcppx_window_choice.restype = C.c_int
     lib.pcppx_unpack_layers_brief.argtypes = [P, P, C.c_uint64, C.c_uint32, P]
     lib.pcppx_unpack_layers_brief.restype = C.c_int
     for name in ("pcppx_device_count", "pcppx_open", "pcppx_sync", "pcppx_parse_batch_device",
@@ -297,7 +299,7 @@ EXPORTED_SYMBOLS = (
     "pcppx_sync", "pcppx_ctx_stream", "pcppx_default_opts", "pcppx_parse_batch_device", "pcppx_parse_batch_host",
     "pcppx_flow_count_device", "pcppx_flow_count_keys_device", "pcppx_filter_device", "pcppx_filter_reset", "pcppx_filter_batch_host", "pcppx_reasm_device", "pcppx_parse_batch_device_reasm", "pcppx_pcap_open", "pcppx_pcap_linktype",
     "pcppx_pcap_read_batch", "pcppx_pcap_read_batch_ex", "pcppx_pcap_map_batch", "pcppx_pcap_close", "pcppx_host_alloc", "pcppx_host_free",
-    "pcppx_unpack_layers", "pcppx_unpack_layers_brief",
+    "pcppx_unpack_layers", "pcppx_unpack_layers_brief", "pcppx_window_choice",
 )
 
 

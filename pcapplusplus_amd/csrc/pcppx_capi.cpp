@@ -180,6 +180,16 @@ struct pcppx_ctx
 	uint64_t wave_stats_bytes = 0;
 	hipEvent_t stats_done = nullptr;
 	bool stats_pending = false;
+	// the engine's header-window choice for PCPPX_WINDOW_DEFAULT launches: every parse adds the live packets and deep
+	// stacks of one tile in 64 to d_win (never cleared); after a parse, a private stream copies the counters into a
+	// page-locked mirror, which the next launch reads once the copy is done (no wait on any stream)
+	unsigned long long* d_win = nullptr;
+	unsigned long long* h_win = nullptr;
+	hipStream_t win_stream = nullptr;
+	hipEvent_t win_parsed = nullptr, win_copied = nullptr;
+	bool win_ready = false, win_pending = false;
+	unsigned long long win_live = 0, win_deep = 0;  // the mirror at the last decision
+	int deep_traffic = -1;                            // -1: not known yet; 0: plain stacks; 1: deep stacks
 };
 
 namespace
@@ -187,6 +197,75 @@ namespace
 bool ok(hipError_t e)
 {
 	return e == hipSuccess;
+}
+
+// ---- the engine's header window (PCPPX_WINDOW_DEFAULT) ----
+constexpr unsigned long long kWinMinSample = 4096;  // sampled packets per decision
+constexpr unsigned long long kWinDeepShare = 256;   // deep stacks above 1 in 256 sampled packets: deep traffic
+
+bool ensure_win(pcppx_ctx* c)
+{
+	if (c->win_ready)
+		return true;
+	const bool good = ok(hipMalloc(reinterpret_cast<void**>(&c->d_win), 2 * sizeof(unsigned long long))) &&
+	                  ok(hipMemset(c->d_win, 0, 2 * sizeof(unsigned long long))) &&
+	                  ok(hipHostMalloc(reinterpret_cast<void**>(&c->h_win), 2 * sizeof(unsigned long long))) &&
+	                  ok(hipStreamCreateWithFlags(&c->win_stream, hipStreamNonBlocking)) &&
+	                  ok(hipEventCreateWithFlags(&c->win_parsed, hipEventDisableTiming)) &&
+	                  ok(hipEventCreateWithFlags(&c->win_copied, hipEventDisableTiming));
+	if (!good)
+	{
+		(void)hipGetLastError();
+		return false;
+	}
+	c->h_win[0] = c->h_win[1] = 0;
+	c->win_ready = true;
+	return true;
+}
+
+// fold a finished counter copy into the decision (wait: block until the copy in flight is done)
+void update_window(pcppx_ctx* c, bool wait)
+{
+	if (!c->win_pending)
+		return;
+	if (wait ? !ok(hipEventSynchronize(c->win_copied)) : hipEventQuery(c->win_copied) != hipSuccess)
+		return;
+	c->win_pending = false;
+	const unsigned long long live = c->h_win[0] - c->win_live, deep = c->h_win[1] - c->win_deep;
+	if (live < kWinMinSample)
+		return;
+	c->deep_traffic = deep * kWinDeepShare > live ? 1 : 0;
+	c->win_live = c->h_win[0];
+	c->win_deep = c->h_win[1];
+}
+
+// the window a launch runs with: an explicit DEEP / SHORT as asked; DEFAULT follows the traffic this context has seen
+// (deep stacks: the two-round window for checksum launches too; plain stacks: one round for parse-only launches too).
+// The records are the same whichever window runs.
+pcppx_opts resolve_window(pcppx_ctx* c, const pcppx_opts* o)
+{
+	pcppx_opts e = *o;
+	if (o->window != PCPPX_WINDOW_DEFAULT)
+		return e;
+	update_window(c, false);
+	if (c->deep_traffic == 1 && o->want_checksums)
+		e.window = PCPPX_WINDOW_DEEP;
+	else if (c->deep_traffic == 0 && !o->want_checksums)
+		e.window = PCPPX_WINDOW_SHORT;
+	return e;
+}
+
+// after a parse on st: copy the counters out behind it on the private stream (one copy in flight)
+void note_window(pcppx_ctx* c, hipStream_t st)
+{
+	if (!c->win_ready || c->win_pending)
+		return;
+	if (ok(hipEventRecord(c->win_parsed, st)) && ok(hipStreamWaitEvent(c->win_stream, c->win_parsed, 0)) &&
+	    ok(hipMemcpyAsync(c->h_win, c->d_win, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->win_stream)) &&
+	    ok(hipEventRecord(c->win_copied, c->win_stream)))
+		c->win_pending = true;
+	else
+		(void)hipGetLastError();
 }
 
 int valid_opts(const pcppx_opts* o)
@@ -247,7 +326,11 @@ int device_parse(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_
 			return rc;
 		ws = c->d_wave_stats;
 	}
-	int rc = info ? pcppx::launch_parse_reasm(b, o, r, info, st, ws) : pcppx::launch_parse(b, o, r, st, ws);
+	unsigned long long* win = ensure_win(c) ? c->d_win : nullptr;
+	const pcppx_opts eo = resolve_window(c, o);
+	int rc = info ? pcppx::launch_parse_reasm(b, &eo, r, info, st, ws, win) : pcppx::launch_parse(b, &eo, r, st, ws, win);
+	if (rc == PCPPX_OK)
+		note_window(c, st);
 	if (rc != PCPPX_OK || ws == nullptr)
 		return rc;
 	rc = pcppx::launch_proto_stats_reduce(ws, b->n, r->proto_stats, st);
@@ -494,6 +577,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 	                        (r->brief == nullptr || is_pinned(r->brief)) && (!rows || is_pinned(r->layers));
 	uint64_t written = 0;
 	Slot* pend = nullptr;  // DENSE: the previous chunk, its chains not yet copied out
+	unsigned long long* win = ensure_win(c) ? c->d_win : nullptr;
 	uint32_t i = 0, k = 0;
 	while (i < b->n)
 	{
@@ -515,9 +599,11 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		dr.summary = r->summary ? s.d_sum : nullptr;
 		dr.brief = r->brief ? s.d_brief : nullptr;
 		dr.layers = ml ? s.d_lay : nullptr;
-		pcppx_opts fo = *o;
+		pcppx_opts fo = resolve_window(c, o);
 		fo.layout = PCPPX_LAYOUT_FIXED;  // DENSE is compacted from the chunk's FIXED rows below
-		rc = pcppx::launch_parse(&db, &fo, &dr, s.st);
+		rc = pcppx::launch_parse(&db, &fo, &dr, s.st, nullptr, win);
+		if (rc == PCPPX_OK)
+			note_window(c, s.st);
 		if (rc == PCPPX_OK && dense)
 			rc = pcppx::launch_dense_compact(s.d_lay,
 			                                 dr.brief ? reinterpret_cast<const uint8_t*>(s.d_brief) + 14
@@ -605,7 +691,10 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 		pcppx_records dr{};
 		dr.summary = s.d_sum;
 		dr.layers = s.d_lay;
-		rc = pcppx::launch_parse(&db, &o, &dr, s.st);
+		const pcppx_opts eo = resolve_window(c, &o);
+		rc = pcppx::launch_parse(&db, &eo, &dr, s.st, nullptr, c->win_ready ? c->d_win : nullptr);
+		if (rc == PCPPX_OK)
+			note_window(c, s.st);
 		if (rc == PCPPX_OK)
 			rc = pcppx::launch_filter(&db, &dr, ml, spec, c->seq + i, c->d_keys, c->d_first, c->flow_slots,
 			                          s.d_match, c->d_stats, s.st);
@@ -751,12 +840,35 @@ extern "C"
 		if (c->d_wave_stats)
 			(void)hipFreeAsync(c->d_wave_stats, c->stream);
 		(void)hipStreamSynchronize(c->stream);
+		if (c->win_ready)
+		{
+			(void)hipStreamSynchronize(c->win_stream);
+			(void)hipStreamDestroy(c->win_stream);
+			(void)hipEventDestroy(c->win_parsed);
+			(void)hipEventDestroy(c->win_copied);
+			(void)hipFree(c->d_win);
+			(void)hipHostFree(c->h_win);
+		}
 		if (c->flow_done)
 			(void)hipEventDestroy(c->flow_done);
 		if (c->stats_done)
 			(void)hipEventDestroy(c->stats_done);
 		(void)hipStreamDestroy(c->stream);
 		delete c;
+	}
+
+	int pcppx_window_choice(pcppx_ctx* c, int want_checksums, int* window)
+	{
+		if (c == nullptr || window == nullptr)
+			return PCPPX_E_INVAL;
+		if (!ok(hipSetDevice(c->device)))
+			return PCPPX_E_HIP;
+		update_window(c, true);
+		pcppx_opts o;
+		pcppx_default_opts(&o);
+		o.want_checksums = want_checksums ? 1 : 0;
+		*window = resolve_window(c, &o).window;
+		return PCPPX_OK;
 	}
 
 	void* pcppx_ctx_stream(pcppx_ctx* c)

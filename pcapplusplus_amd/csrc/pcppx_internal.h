@@ -9,8 +9,9 @@ namespace pcppx
 {
 int check_launch(const char* what, hipStream_t stream);
 // wave_stats: null, or parse_waves(n) 16-B per-wave collectStats records, summed by launch_proto_stats_reduce
+// win_stats: null, or the context's two 64-bit counters the parse adds its sampled live / deep-stack packets to
 int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream,
-                 void* wave_stats = nullptr);
+                 void* wave_stats = nullptr, unsigned long long* win_stats = nullptr);
 uint32_t parse_waves(uint32_t n);
 int launch_proto_stats_reduce(const void* wave_stats, uint32_t n, uint64_t* out, hipStream_t stream);
 int launch_filter(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, const pcppx_match_spec* spec,
@@ -23,7 +24,7 @@ int launch_flow_count_part(const pcppx_summary* sum, const uint32_t* dkeys, cons
                            uint32_t* keys, uint64_t* packets, uint64_t* bytes, uint32_t capacity, uint64_t* stats,
                            void* queues, uint32_t rec_cap, uint32_t* fill, hipStream_t stream);
 int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
-                       hipStream_t stream, void* wave_stats = nullptr);
+                       hipStream_t stream, void* wave_stats = nullptr, unsigned long long* win_stats = nullptr);
 int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcppx_reasm_info* info, hipStream_t stream);
 // PCPPX_LAYOUT_DENSE on the host path: a chunk's FIXED rows (n x ml) -> its chains back to back (dense), the chain
 // lengths read from n_layers[i * nl_stride] (a summary's or a brief's byte 14); *total = the entries written.

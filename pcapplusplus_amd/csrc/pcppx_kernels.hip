@@ -998,6 +998,7 @@ struct Params
 	uint4* wave_stats;        // optional per-wave collectStats counters (16 x u8), reduced by proto_stats_reduce_kernel
 	uint32_t packed;          // PCPPX_LAYOUT_PACKED: the chain's layer entries dense per 64-packet tile
 	pcppx_brief* brief;       // optional 16-B brief (pcppx_records.brief): the summary's first half
+	unsigned long long* win_stats;  // engine-chosen window: {sampled live packets, of them deep stacks} (context-owned)
 };
 
 // Everything the summary needs after the chain walk.
@@ -1650,6 +1651,27 @@ __device__ __forceinline__ uint32_t fast_k1(const Fast& f)
 	return 1 + f.nv() + f.nm();
 }
 
+// The deep-stack pre-scan of a packet's first LDS window: Ethernet, up to two VLAN tags, then an MPLS label or an IP
+// layer not followed directly by TCP / UDP (GRE, IPv6 extension headers, ...) -- the stacks the two-round window is for.
+// *et / *o: the ethertype and offset after the VLAN tags.
+__device__ __forceinline__ bool deep_stack(const Pkt& p, uint32_t* et_out, uint32_t* o_out)
+{
+	uint32_t et = swap16(lds_u32(p, 12)), o = 14;
+#pragma unroll
+	for (int t = 0; t < 2; ++t)
+	{
+		const bool vl = (et == 0x8100 || et == 0x88A8) && o + 8 <= p.lim;
+		const uint32_t e2 = swap16(lds_u32(p, vl ? o : 0) >> 16);
+		et = vl ? e2 : et;
+		o = vl ? o + 4 : o;
+	}
+	const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 8 <= p.lim ? o + 8 : 0);
+	const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
+	*et_out = et;
+	*o_out = o;
+	return et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
+}
+
 // the Walk summary of a fast-path packet
 __device__ __forceinline__ Walk fast_to_walk(const Fast& f, uint32_t ml)
 {
@@ -2097,7 +2119,10 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	const uint64_t smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
 	const uint64_t emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
 	const uint64_t wire = uniform_u64(wave_sum_u64(live ? cap : 0));
-	const bool stream = want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
+	// a tile whose every packet lies whole in its first gather round (e.g. 64-B packets: 96-B windows) takes its L4 sums
+	// from the LDS window after the parse: no span stream, no prefix scan (the stream would re-read the gathered lines)
+	const bool in_window = !__ballot(live && ((uint32_t)(pkt_addr & 15) + cap + 15) >> 4 > (uint32_t)Chunks1);  // uniform
+	const bool stream = want_csum && !in_window && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
 	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
 	uint4 va[SWin / 64], vb[SWin / 64];
 	auto load = [&](uint4 (&v)[SWin / 64], uint32_t win) {
@@ -2173,18 +2198,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		// second round before any walk: the rest of the window for the stacks the first round cannot hold (an MPLS
 		// label, or an IP layer not followed directly by TCP / UDP: GRE, IPv6 extension headers, ...), from a
 		// pre-scan of the Ethernet / VLAN / IP fields of the first window
-		uint32_t et = swap16(lds_u32(p, 12)), o = 14;
-#pragma unroll
-		for (int t = 0; t < 2; ++t)
-		{
-			const bool vl = (et == 0x8100 || et == 0x88A8) && o + 8 <= p.lim;
-			const uint32_t e2 = swap16(lds_u32(p, vl ? o : 0) >> 16);
-			et = vl ? e2 : et;
-			o = vl ? o + 4 : o;
-		}
-		const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 8 <= p.lim ? o + 8 : 0);
-		const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
-		const bool deep = et == 0x8847 || ((et == 0x0800 || et == 0x86DD) && nh != 6 && nh != 17);
+		uint32_t et, o;
+		const bool deep = deep_stack(p, &et, &o);
 		uint32_t full = need < (uint32_t)Chunks ? need : (uint32_t)Chunks;
 		bool more = live && !StreamOnly && (deep || GatherOnly) && full > p.nch;
 		uint32_t from = p.nch;  // the second round gathers chunks [from, full)
@@ -2221,6 +2236,19 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			__syncthreads();
 			p.nch = more ? full : p.nch;
 			set_lim();
+		}
+	}
+	// the engine's window choice (pcppx_ctx: the next launches' window follows the traffic): one tile in 64 counts its live
+	// packets and their deep stacks (Ethernet links; two atomics per sampled wave)
+	if (prm.win_stats != nullptr && (blockIdx.x & 63) == 0 && prm.linktype == 1)  // uniform
+	{
+		uint32_t et, o;
+		const bool dp = live && p.lim >= 14 && deep_stack(p, &et, &o);
+		const uint32_t nl = (uint32_t)__popcll(__ballot(live)), nd = (uint32_t)__popcll(__ballot(dp));
+		if (lane == 0 && nl != 0)
+		{
+			atomicAdd(prm.win_stats, (unsigned long long)nl);
+			atomicAdd(prm.win_stats + 1, (unsigned long long)nd);
 		}
 	}
 	Fast f;
@@ -2355,18 +2383,24 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			if (full)
 				fsum = p1 - p0;
 		}
-		else if (full)
+		else if (full && !in_window)
 			fsum = full_chunks_sum(f0, f1);
 		if (need)
 		{
-			uint32_t acc = mod65535(fsum);
-			if (f0 <= f1)
-				acc += edge_sum(p, as, f0) + (tail_done ? tsum : edge_sum(p, f1, ae));
+			uint32_t r;
+			if (in_window)  // uniform: the whole L4 range is in the LDS window
+				r = range_residue(p, w.l4o, w.l4o + w.l4dlen);
 			else
-				acc += edge_sum(p, as, ae);
-			uint32_t r = mod65535(acc);
-			if (as & 1)
-				r = (r * 256u) % 65535u;
+			{
+				uint32_t acc = mod65535(fsum);
+				if (f0 <= f1)
+					acc += edge_sum(p, as, f0) + (tail_done ? tsum : edge_sum(p, f1, ae));
+				else
+					acc += edge_sum(p, as, ae);
+				r = mod65535(acc);
+				if (as & 1)
+					r = (r * 256u) % 65535u;
+			}
 			l4c = l4_checksum(p, w, r, &l4s);
 			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
 		}
@@ -3215,6 +3249,7 @@ Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, 
 	prm.wave_stats = nullptr;
 	prm.packed = o->layout == PCPPX_LAYOUT_PACKED ? 1u : 0u;
 	prm.brief = r->brief;
+	prm.win_stats = nullptr;
 	return prm;
 }
 
@@ -3382,41 +3417,45 @@ int check_launch(const char* what, hipStream_t /*stream*/)
 	return PCPPX_OK;
 }
 
-int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream, void* wave_stats)
+namespace
+{
+// the instance for the (already resolved) window: checksum launches DEFAULT one round / DEEP two rounds; parse-only
+// launches two rounds / SHORT one round
+int launch_instance(const pcppx_opts* o, const Params& prm, uint32_t n, hipStream_t stream, const char* what)
+{
+	const dim3 grid((n + kTile - 1) / kTile);
+	if (o->want_checksums && o->window == PCPPX_WINDOW_DEEP)
+		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else if (o->want_checksums)
+		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else if (o->window == PCPPX_WINDOW_SHORT)
+		hipLaunchKernelGGL(PCPPX_PARSE_SHORT_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	else
+		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
+	return check_launch(what, stream);
+}
+}  // namespace
+
+int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream, void* wave_stats,
+                 unsigned long long* win_stats)
 {
 	if (b->n == 0)
 		return PCPPX_OK;
 	Params prm = make_params(b, o, r, nullptr);
 	prm.wave_stats = static_cast<uint4*>(wave_stats);
-	const dim3 grid((b->n + kTile - 1) / kTile);
-	if (o->want_checksums && o->window == PCPPX_WINDOW_DEEP)
-		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	else if (o->want_checksums)
-		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	else if (o->window == PCPPX_WINDOW_SHORT)
-		hipLaunchKernelGGL(PCPPX_PARSE_SHORT_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	else
-		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	return check_launch("parse_tile_kernel", stream);
+	prm.win_stats = win_stats;
+	return launch_instance(o, prm, b->n, stream, "parse_tile_kernel");
 }
 
 int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
-                       hipStream_t stream, void* wave_stats)
+                       hipStream_t stream, void* wave_stats, unsigned long long* win_stats)
 {
 	if (b->n == 0)
 		return PCPPX_OK;
 	Params prm = make_params(b, o, r, info);
 	prm.wave_stats = static_cast<uint4*>(wave_stats);
-	const dim3 grid((b->n + kTile - 1) / kTile);
-	if (o->want_checksums && o->window == PCPPX_WINDOW_DEEP)
-		hipLaunchKernelGGL(PCPPX_PARSE_DEEP_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	else if (o->want_checksums)
-		hipLaunchKernelGGL(PCPPX_PARSE_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	else if (o->window == PCPPX_WINDOW_SHORT)
-		hipLaunchKernelGGL(PCPPX_PARSE_SHORT_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	else
-		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
-	return check_launch("parse_tile_kernel(reasm)", stream);
+	prm.win_stats = win_stats;
+	return launch_instance(o, prm, b->n, stream, "parse_tile_kernel(reasm)");
 }
 
 uint32_t parse_waves(uint32_t n)

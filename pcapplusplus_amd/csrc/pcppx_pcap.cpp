@@ -45,6 +45,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <thread>
@@ -123,25 +124,42 @@ constexpr size_t kParMin = 4ull << 20;       // fewer bytes left: walk sequentia
 constexpr unsigned kParThreads = 16;         // at most; one per MiB of the region at least
 constexpr unsigned kParChains = 4;           // interleaved chains (segments) per thread
 // fn(t) for t in [0, T): on new threads where they can be started, the rest on the calling thread (a thread that
-// cannot be created never fails the read)
+// cannot be created never fails the read). An out-of-memory in any fn(t) -- a worker's or the caller's -- is caught
+// where it happens, every thread is joined, and then std::bad_alloc is rethrown on the calling thread, where the
+// reader falls back to the sequential walk (an exception leaving a std::thread, or a joinable thread destroyed during
+// unwinding, would call std::terminate).
 template <class F>
 void run_parallel(unsigned T, const F& fn)
 {
+	std::atomic<bool> oom{ false };
+	auto guarded = [&](unsigned t) {
+		try
+		{
+			fn(t);
+		}
+		catch (const std::bad_alloc&)
+		{
+			oom.store(true);
+		}
+	};
 	std::vector<std::thread> th;
 	unsigned started = 1;
 	try
 	{
+		th.reserve(T);
 		for (; started < T; ++started)
-			th.emplace_back(fn, started);
+			th.emplace_back(guarded, started);
 	}
 	catch (...)
 	{
 	}
-	fn(0u);
+	guarded(0u);
 	for (unsigned t = started; t < T; ++t)
-		fn(t);
+		guarded(t);
 	for (auto& x : th)
 		x.join();
+	if (oom.load())
+		throw std::bad_alloc();
 }
 
 unsigned par_threads(size_t bytes)

@@ -89,6 +89,12 @@ class Engine:
             k.free()
         return out
 
+    def window_choice(self, want_checksums: bool) -> int:
+        """pcppx_window_choice: the window a WINDOW_DEFAULT launch would run with now (abi.WINDOW_*)."""
+        w = C.c_int(0)
+        abi.check(self.lib.pcppx_window_choice(self.ctx, 1 if want_checksums else 0, C.byref(w)), "pcppx_window_choice")
+        return w.value
+
     # ---- device-resident batches (torch tensors on this GPU) ----
     def parse_device(self, data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers=None,
                      stream: int | None = None, flow_keys=None, tuples=None, proto_stats=None, brief=None) -> None:

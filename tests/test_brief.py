@@ -138,3 +138,29 @@ def test_gpu_host_dense_layout(engine, pinned, src):
             os_, ol = oracle.oracle_parse(batch, opts)
             assert br.tobytes() == _brief_of(os_).tobytes(), (path.stem, v)
             oracle.compare_exact(os_, abi.unpack_dense(br["n_layers"], dense, opts.max_layers), os_, ol)
+
+
+@pytest.mark.gpu
+def test_gpu_engine_window_choice():
+    """PCPPX_WINDOW_DEFAULT is the engine's choice (ABI 7): after parsing deep stacks (config 5) a context runs checksum
+    launches with the two-round window (as WINDOW_DEEP) and keeps the second round for parse-only ones; after plain
+    stacks (config 3) it runs parse-only launches as SHORT and checksum launches with the one 96-B window. The records are
+    the restatement's whatever was chosen (device and host paths)."""
+    from pcapplusplus_amd.engine import Engine, parse_on_device
+
+    for cfg, want_csum_win, want_po_win in ((5, abi.WINDOW_DEEP, abi.WINDOW_DEFAULT),
+                                            (3, abi.WINDOW_DEFAULT, abi.WINDOW_SHORT)):
+        b = synth.config(cfg, 200_000)
+        with Engine(0) as eng:
+            assert eng.window_choice(True) == abi.WINDOW_DEFAULT  # nothing sampled yet
+            for csum in (True, False, True):
+                o = abi.make_opts(0, 8, csum, 12 if cfg == 5 else 8)
+                s, lay = parse_on_device(eng, b, o)
+                if csum:
+                    os_, ol = oracle.oracle_parse(b, o, threads=8)
+                    oracle.compare_exact(s, lay, os_, ol)
+            assert eng.window_choice(True) == want_csum_win, cfg
+            assert eng.window_choice(False) == want_po_win, cfg
+            hs, hl = eng.parse_host(b, abi.make_opts(0, 8, True, 8))  # the host path follows the same choice
+            os_, ol = oracle.oracle_parse(b, abi.make_opts(0, 8, True, 8), threads=8)
+            oracle.compare_exact(hs, hl, os_, ol)

@@ -300,12 +300,14 @@ def test_gpu_packet_vector_equals_restatement(built, tmp_path, how):
                 oracle.compare_exact(rec["sum"], rec["lay"], ws, wl)
             except AssertionError as e:
                 raise AssertionError(f"{name}/{plan}/{how}: {e}") from None
+            # a parse per page (or group) and option set, plus at most one small parse of its chains deeper than the
+            # records hold (their complete records, Records::side)
             variants = len(set(plan.split(",")))
             if how == "own":  # one group (one link type) parsed once per option set
-                assert info["gpu_parses"] == variants, (name, plan, info)
+                assert variants <= info["gpu_parses"] <= 2 * variants, (name, plan, info)
             else:  # pages of 16k, 64k, 256k packets: each parsed once per option set (plus copies' groups)
-                pages = 1 + (b.n > 16384) + (b.n > 16384 + 65536)
-                assert info["gpu_parses"] <= pages * variants + (variants if how == "copy" else 0), (name, plan, info)
+                pages = 1 + (b.n > 16384) + (b.n > 16384 + 65536) + (how == "copy")
+                assert info["gpu_parses"] <= 2 * pages * variants, (name, plan, info)
 
 
 @pytest.mark.gpu

@@ -34,7 +34,7 @@ def test_crafted_stacks_vs_reference(opt_i):
     os_, ol = oracle.oracle_parse(b, OPTS[opt_i])
     oracle.compare_engine_to_reference(os_, ol, rs, rl)
     if OPTS[opt_i].max_layers >= 8:
-        oracle.check_flag_contract(os_, rs, rl)
+        oracle.check_flag_contract(os_, rs, rl, b)
 
 
 @pytest.mark.parametrize("opt_i", range(len(OPTS)))
@@ -45,7 +45,7 @@ def test_crafted_l7_payloads_vs_reference(opt_i):
     os_, ol = oracle.oracle_parse(b, OPTS[opt_i])
     oracle.compare_engine_to_reference(os_, ol, rs, rl)
     if OPTS[opt_i].max_layers >= 8:
-        st = oracle.check_flag_contract(os_, rs, rl)
+        st = oracle.check_flag_contract(os_, rs, rl, b)
         if opt_i == 0:
             assert st["l7_known"] > 0 and st["flagged"] < b.n
 
@@ -57,7 +57,7 @@ def test_mutations_vs_reference(seed):
         rs, rl = oracle.ref_parse(b, opts)
         os_, ol = oracle.oracle_parse(b, opts)
         oracle.compare_engine_to_reference(os_, ol, rs, rl)
-        oracle.check_flag_contract(os_, rs, rl)
+        oracle.check_flag_contract(os_, rs, rl, b)
 
 
 @pytest.mark.parametrize("linktype", [0, 113, 276])
@@ -78,6 +78,6 @@ def test_link_layers_vs_reference(linktype):
         os_, ol = oracle.oracle_parse(b, opts)
         oracle.compare_engine_to_reference(os_, ol, rs, rl)
         if opts.max_layers >= 8:
-            oracle.check_flag_contract(os_, rs, rl)
+            oracle.check_flag_contract(os_, rs, rl, b)
     s, _ = oracle.oracle_parse(b, OPTS[0])
     assert ((s["flags"] & abi.F_NEEDS_HOST) == 0).mean() > 0.5

@@ -11,10 +11,12 @@ from pcapplusplus_amd import abi
 AB_SO = Path(__file__).resolve().parent / "libpcppx_ab.so"
 R01_SO = Path(__file__).resolve().parent / "r01" / "libpcppx_r01.so"
 PREV_SO = Path(__file__).resolve().parent / "prev" / "libpcppx_prev.so"
+R04_SO = Path(__file__).resolve().parent / "r04" / "libpcppx_r04.so"
 _lib = None
 _r01 = {}
 R01 = -1  # parse_device variant: the round-1 product kernel (tools/ab/r01, rebuilt from git history)
 PREV = -2  # parse_device variant: the r02m product kernel before device-built L7 / ICMP / tunnels (tools/ab/prev)
+R04 = -3  # parse_device variant: the round-4 final product kernel (tools/ab/r04, commit b2a062a)
 
 # pcppx_ab_parse_device variants (tools/ab/pcppx_ab.hip)
 LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ, TILE_W5_WIN256, TILE_W1_WIN128, TILE_W1_WIN256, TILE_CACHED = \
@@ -58,8 +60,8 @@ def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, 
     rec = abi.Records(abi.ptr(summary) if summary is not None else None,
                       abi.ptr(layers) if (layers is not None and opts.max_layers) else None, None,
                       abi.ptr(tuples) if tuples is not None else None)
-    if variant in (R01, PREV):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
-        abi.check(r01_lib(R01_SO if variant == R01 else PREV_SO).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
+    if variant in (R01, PREV, R04):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
+        abi.check(r01_lib({R01: R01_SO, PREV: PREV_SO, R04: R04_SO}[variant]).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
                   "pcppx_r01_parse_device")
         return
     abi.check(lib().pcppx_ab_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0), variant),

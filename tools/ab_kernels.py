@@ -19,7 +19,8 @@ from tools import ab  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-b = synth.config(cfg, n)
+_sizes = __import__("os").environ.get("AB_SIZES")  # config 3 at one packet size (bench.py --sizes)
+b = synth.imix(n, 3, sizes=(int(_sizes),), weights=(1,)) if _sizes else synth.config(cfg, n)
 data, offs, caps = to_device(b)
 summ = torch.empty(n * 32, dtype=torch.uint8, device="cuda:0")
 lay = torch.empty(n * 16 * 8, dtype=torch.uint8, device="cuda:0")
@@ -66,6 +67,9 @@ cases = {
     "po/packed-no-l7": (abi.make_opts(0, 8, False, _ml, layout=PK), 91),
     "po/packed-no-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 92),
     "po/packed-no-hash-l7-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 93),
+    # the round-4 final product kernel (tools/ab/r04): round-5 changes against it in one process
+    "r04/tile-packed": (abi.make_opts(0, 8, True, 8, layout=PK), -3),
+    "r04/po-packed": (abi.make_opts(0, 8, False, _ml, layout=PK), -3),
 }
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")
