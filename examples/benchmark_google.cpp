@@ -18,8 +18,11 @@ int main(int argc, char** argv)
 	try
 	{
 		const int rc = runBenchmarks(argc, argv, "engine");
-		std::printf("{\"impl\": \"engine\", \"gpu_parses\": %llu}\n",
-		            (unsigned long long)pcppx::detail::Service::parsesSoFar());
+		const uint64_t pk = pcppx::detail::Service::packetsParsed(), by = pcppx::detail::Service::recordBytes();
+		std::printf("{\"impl\": \"engine\", \"gpu_parses\": %llu, \"packets_parsed\": %llu, \"record_bytes\": %llu, "
+		            "\"record_bytes_per_packet\": %.2f}\n",
+		            (unsigned long long)pcppx::detail::Service::parsesSoFar(), (unsigned long long)pk, (unsigned long long)by,
+		            pk ? (double)by / (double)pk : 0.0);
 		return rc;
 	}
 	catch (const pcppx::Error& e)

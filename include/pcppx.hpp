@@ -262,6 +262,7 @@ public:
 				void* p = it->second;
 				*got = it->first;
 				m_Cached -= it->first;
+				m_Out += it->first;
 				m_Free.erase(it);
 				return p;
 			}
@@ -270,12 +271,14 @@ public:
 		if (p == nullptr)
 			throw Error(PCPPX_E_NOMEM, "pcppx_host_alloc");
 		*got = bytes;
+		m_Out += bytes;
 		return p;
 	}
 	void give(void* p, size_t bytes)
 	{
 		if (p == nullptr)
 			return;
+		m_Out -= bytes;
 		{
 			std::lock_guard<std::mutex> g(m_Mu);
 			if (m_Cached + bytes <= kKeep)
@@ -288,8 +291,12 @@ public:
 		pcppx_host_free(p);
 	}
 
+	/* page-locked bytes held by live record pages (taken and not given back) */
+	size_t outstanding() const { return m_Out.load(); }
+
 private:
 	static constexpr size_t kGrain = 1u << 20;
+	std::atomic<size_t> m_Out{ 0 };
 	static constexpr size_t kKeep = 2ull << 30;
 	std::mutex m_Mu;
 	std::multimap<size_t, void*> m_Free;
@@ -316,6 +323,14 @@ public:
 	/* GPU parses the per-packet entry points have made (one per page, group or re-parse) */
 	uint64_t parses() const { return counter().load(); }
 	static uint64_t parsesSoFar() { return counter().load(); }  // without opening the device
+	/* packets parsed and record bytes the parses brought back over PCIe (briefs / summaries + layer entries) */
+	static void noteRecords(uint64_t packets, uint64_t bytes)
+	{
+		recordStats()[0] += packets;
+		recordStats()[1] += bytes;
+	}
+	static uint64_t packetsParsed() { return recordStats()[0].load(); }
+	static uint64_t recordBytes() { return recordStats()[1].load(); }
 
 private:
 	explicit Service(int device) { check(pcppx_open(device, &m_Ctx), "pcppx_open"); }
@@ -323,6 +338,11 @@ private:
 	{
 		static std::atomic<uint64_t> c{ 0 };
 		return c;
+	}
+	static std::atomic<uint64_t>* recordStats()
+	{
+		static std::atomic<uint64_t> st[2] = { { 0 }, { 0 } };
+		return st;
 	}
 	std::mutex m_Mu;
 	pcppx_ctx* m_Ctx = nullptr;
@@ -498,6 +518,8 @@ struct Page
 		rec.layers = r->lay;
 		Service::instance().parse(b, o, rec);
 		r->entries = rec.layers_written;
+		Service::noteRecords(n, (uint64_t)n * (k.csum ? sizeof(pcppx_summary) : sizeof(pcppx_brief)) +
+		                            rec.layers_written * sizeof(pcppx_layer));
 		// each chain's first entry; the packets that need complete records beside the chain
 		std::vector<uint32_t> deep, host;
 		const pcppx_host_parse_fn fn = hostParser().load();
@@ -546,6 +568,7 @@ struct Page
 			rec.summary = ds.data();
 			rec.layers = dl.data();
 			Service::instance().parse(b, o, rec);
+			Service::noteRecords(0, deep.size() * (sizeof(pcppx_summary) + PCPPX_MAX_LAYERS * sizeof(pcppx_layer)));
 			for (size_t j = 0; j < deep.size(); ++j)
 			{
 				CopiedRecords& c = r.side[(size_t)(std::lower_bound(all.begin(), all.end(), deep[j]) - all.begin())];
@@ -1781,7 +1804,8 @@ private:
 		{
 			// the caller's own bytes: parsed with every other pending RawPacket in one batch, or already in a group
 			uint32_t idx = 0;
-			bindRecords(detail::OwnedRegistry::instance().recordsFor(raw, k, &idx), idx);
+			const detail::Records* r = detail::OwnedRegistry::instance().recordsFor(raw, k, &idx);  // sets idx
+			bindRecords(r, idx);
 			return;
 		}
 		if (detail::Page* p = raw->m_Page.get())

@@ -459,7 +459,11 @@ uint32_t stage_chunk(Slot& s, const pcppx_batch* b, uint32_t i, size_t* pos_out,
 		uint64_t base = 0;
 		size_t bytes = 0;
 		const uint32_t j = contiguous_chunk(b, i, &base, &bytes);
-		if (j > i && (j == b->n || j - i >= kMinRun || b->offsets[j] + b->caplens[j] - base > kChunkBytes))
+		// a run that ends the batch, a long run, or one that stops only because the next packet (ascending) would not fit
+		// the chunk: copied straight from the caller's bytes. (A next packet below the run -- an unordered batch -- is
+		// no such reason: its offset minus the run's base would wrap.)
+		if (j > i && (j == b->n || j - i >= kMinRun ||
+		              (b->offsets[j] >= base && b->offsets[j] + b->caplens[j] - base > kChunkBytes)))
 		{
 			for (uint32_t k = i; k < j; ++k)
 			{

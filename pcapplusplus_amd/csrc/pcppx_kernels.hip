@@ -2119,10 +2119,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	const uint64_t smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
 	const uint64_t emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
 	const uint64_t wire = uniform_u64(wave_sum_u64(live ? cap : 0));
-	// a tile whose every packet lies whole in its first gather round (e.g. 64-B packets: 96-B windows) takes its L4 sums
-	// from the LDS window after the parse: no span stream, no prefix scan (the stream would re-read the gathered lines)
-	const bool in_window = !__ballot(live && ((uint32_t)(pkt_addr & 15) + cap + 15) >> 4 > (uint32_t)Chunks1);  // uniform
-	const bool stream = want_csum && !in_window && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
+	const bool stream = want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
 	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
 	uint4 va[SWin / 64], vb[SWin / 64];
 	auto load = [&](uint4 (&v)[SWin / 64], uint32_t win) {
@@ -2236,19 +2233,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			__syncthreads();
 			p.nch = more ? full : p.nch;
 			set_lim();
-		}
-	}
-	// the engine's window choice (pcppx_ctx: the next launches' window follows the traffic): one tile in 64 counts its live
-	// packets and their deep stacks (Ethernet links; two atomics per sampled wave)
-	if (prm.win_stats != nullptr && (blockIdx.x & 63) == 0 && prm.linktype == 1)  // uniform
-	{
-		uint32_t et, o;
-		const bool dp = live && p.lim >= 14 && deep_stack(p, &et, &o);
-		const uint32_t nl = (uint32_t)__popcll(__ballot(live)), nd = (uint32_t)__popcll(__ballot(dp));
-		if (lane == 0 && nl != 0)
-		{
-			atomicAdd(prm.win_stats, (unsigned long long)nl);
-			atomicAdd(prm.win_stats + 1, (unsigned long long)nd);
 		}
 	}
 	Fast f;
@@ -2383,24 +2367,18 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			if (full)
 				fsum = p1 - p0;
 		}
-		else if (full && !in_window)
+		else if (full)
 			fsum = full_chunks_sum(f0, f1);
 		if (need)
 		{
-			uint32_t r;
-			if (in_window)  // uniform: the whole L4 range is in the LDS window
-				r = range_residue(p, w.l4o, w.l4o + w.l4dlen);
+			uint32_t acc = mod65535(fsum);
+			if (f0 <= f1)
+				acc += edge_sum(p, as, f0) + (tail_done ? tsum : edge_sum(p, f1, ae));
 			else
-			{
-				uint32_t acc = mod65535(fsum);
-				if (f0 <= f1)
-					acc += edge_sum(p, as, f0) + (tail_done ? tsum : edge_sum(p, f1, ae));
-				else
-					acc += edge_sum(p, as, ae);
-				r = mod65535(acc);
-				if (as & 1)
-					r = (r * 256u) % 65535u;
-			}
+				acc += edge_sum(p, as, ae);
+			uint32_t r = mod65535(acc);
+			if (as & 1)
+				r = (r * 256u) % 65535u;
 			l4c = l4_checksum(p, w, r, &l4s);
 			w.flags |= PCPPX_F_L4_CSUM | (l4c == l4s ? PCPPX_F_L4_CSUM_OK : 0);
 		}
@@ -2433,6 +2411,20 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		write_tuple(p, w, h5, prm.tuples + i);
 	if (prm.wave_stats != nullptr)  // uniform
 		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + blockIdx.x);
+	// the engine's window choice (pcppx_ctx: the next launches' window follows the traffic): one tile in 64 counts its live
+	// packets and their deep stacks (Ethernet links; two atomics per sampled wave), from the first window (still intact:
+	// the rows below reuse the stage)
+	if (prm.win_stats != nullptr && (blockIdx.x & 63) == 0 && prm.linktype == 1)  // uniform
+	{
+		uint32_t et, o;
+		const bool dp = live && p.lim >= 14 && deep_stack(p, &et, &o);
+		const uint32_t nl = (uint32_t)__popcll(__ballot(live)), nd = (uint32_t)__popcll(__ballot(dp));
+		if (lane == 0 && nl != 0)
+		{
+			atomicAdd(prm.win_stats, (unsigned long long)nl);
+			atomicAdd(prm.win_stats + 1, (unsigned long long)nd);
+		}
+	}
 
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
 	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----

@@ -16,6 +16,10 @@
  *       Packets; copy = a copy of the reader's vector (PointerVector's deep copy: every RawPacket copied, records
  *       with it). Writes the records as `parse` does; prints {"gpu_parses": N} (pcppx_parse_batch_host calls the
  *       per-packet entry points made).  (GPU.)
+ *   facade_check retain <capture> <every>
+ *       getNextPacket + Packet(&raw) over the capture, keeping a copy of every <every>-th RawPacket (and building a
+ *       Packet on each copy after the reader is closed); prints {"kept", "pinned_while_reading", "pinned_after"}: the
+ *       page-locked record bytes held by live pages -- copies own their bytes and records, so none after.  (GPU.)
  *   facade_check create <file>
  *       IFileReaderDevice::tryCreateReader: prints "null", "noopen" or "packets N" (getNextPacket to the end).  (CPU.)
  *   facade_check time <capture> <reps>
@@ -344,6 +348,38 @@ int main(int argc, char** argv)
 			return readMode(argv[2], argv[3], argc - 4, argv + 4);
 		if (argc == 4 && std::string(argv[1]) == "time")
 			return timeMode(argv[2], std::atoi(argv[3]));
+		if (argc == 4 && std::string(argv[1]) == "retain")
+		{
+			std::vector<pcppx::RawPacket> kept;
+			size_t peak = 0, i = 0;
+			{
+				pcppx::PcapFileReaderDevice reader(argv[2]);
+				if (!reader.open())
+					return 4;
+				const size_t every = (size_t)std::atoll(argv[3]);
+				pcppx::RawPacket raw;
+				while (reader.getNextPacket(raw))
+				{
+					pcppx::Packet p(&raw);
+					(void)p;
+					if (i++ % every == 0)
+						kept.push_back(raw);
+					const size_t out = pcppx::detail::PinnedPool::instance().outstanding();
+					peak = out > peak ? out : peak;
+				}
+				raw.clear();
+				reader.close();
+			}
+			uint64_t h = 0;
+			for (pcppx::RawPacket& k : kept)
+			{
+				pcppx::Packet p(&k);
+				h += pcppx::hash5Tuple(&p);
+			}
+			std::printf("{\"kept\": %zu, \"pinned_while_reading\": %zu, \"pinned_after\": %zu, \"h\": %llu}\n",
+			            kept.size(), peak, pcppx::detail::PinnedPool::instance().outstanding(), (unsigned long long)h);
+			return 0;
+		}
 		if (argc == 3 && std::string(argv[1]) == "create")
 		{
 			auto reader = pcppx::IFileReaderDevice::tryCreateReader(argv[2]);

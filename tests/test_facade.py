@@ -329,6 +329,24 @@ def test_gpu_packet_vector_host_parser_equals_reference(built, tmp_path):
 
 
 @pytest.mark.gpu
+def test_gpu_copied_rawpackets_keep_no_page(built, tmp_path):
+    """A copy of a reader's RawPacket owns its bytes and its records (RawPacket.cpp copyDataFrom), not the page: after the
+    reader is closed, RawPackets kept from every page hold no page-locked record memory, and Packets built
+    on them afterwards carry the same hashes as the restatement."""
+    import json
+
+    b = synth.config(3, 350_000)
+    f = tmp_path / "in.pcap"
+    write_pcap(f, b)
+    r = subprocess.run([str(built), "retain", str(f), "997"], capture_output=True, text=True, timeout=600, env=_env())
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["kept"] == (b.n + 996) // 997 and d["pinned_while_reading"] > 0 and d["pinned_after"] == 0, d
+    s, _ = oracle.oracle_parse(b, abi.make_opts(0, 8, False, 0), threads=8)
+    assert d["h"] == int(s["hash5"][::997].astype(np.uint64).sum())
+
+
+@pytest.mark.gpu
 def test_gpu_packet_large_capture_pages(built, tmp_path):
     """350k IMIX packets (pages of 16k, 64k, 256k packets, parsed ahead by the pipeline) under Packet(&raw, TCP):
     every record equal to the restatement's."""

@@ -55,11 +55,12 @@ def r01_lib(so: Path = R01_SO) -> C.CDLL:
 
 
 def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers, stream: int,
-                 variant: int, tuples=None) -> None:
+                 variant: int, tuples=None, brief=None) -> None:
     b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
     rec = abi.Records(abi.ptr(summary) if summary is not None else None,
                       abi.ptr(layers) if (layers is not None and opts.max_layers) else None, None,
                       abi.ptr(tuples) if tuples is not None else None)
+    rec.brief = abi.ptr(brief) if brief is not None else None
     if variant in (R01, PREV, R04):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
         abi.check(r01_lib({R01: R01_SO, PREV: PREV_SO, R04: R04_SO}[variant]).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
                   "pcppx_r01_parse_device")

@@ -70,7 +70,11 @@ cases = {
     # the round-4 final product kernel (tools/ab/r04): round-5 changes against it in one process
     "r04/tile-packed": (abi.make_opts(0, 8, True, 8, layout=PK), -3),
     "r04/po-packed": (abi.make_opts(0, 8, False, _ml, layout=PK), -3),
+    # the 16-B brief instead of the 32-B summary (ABI 7): same rows
+    "tile/packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
+    "po/packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),
 }
+brief_t = torch.empty(n * 16, dtype=torch.uint8, device="cuda:0")
 import os  # noqa: E402
 only = os.environ.get("AB_CASES")
 if only:
@@ -98,7 +102,7 @@ want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
     first = next(iter(cases.values()))[0]
     if o.max_layers != first.max_layers or o.want_checksums != want_csum_ref or o.layout != first.layout or \
-            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93):  # diagnostics with wrong records
+            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93) or name.endswith("+brief"):  # diagnostics / other records
         continue
     summ.zero_()
     lay.zero_()
@@ -117,7 +121,10 @@ for r in range(rounds):
     for name, (o, v) in cases.items():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        ab.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream, v)
+        if name.endswith("+brief"):
+            ab.parse_device(data, offs, caps, n, b.linktype, o, None, lay, st.cuda_stream, v, brief=brief_t)
+        else:
+            ab.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream, v)
         e1.record(st)
         torch.cuda.synchronize()
         if r > 0:

@@ -82,7 +82,7 @@ def google_pair(pcap: Path, args: list[str], trials: int = 1) -> dict:
                 if "name" in d and "ns_per_iteration" in d:
                     per.setdefault(d["name"].split("/")[0], {}).setdefault(name, []).append(d)
                 elif "gpu_parses" in d:
-                    per.setdefault("gpu_parses", []).append(d["gpu_parses"])
+                    per.setdefault("gpu_parses", []).append(d)
     out = {"file": pcap.name, "args": args, "trials": trials}
     for bm, by in per.items():
         if bm == "gpu_parses":

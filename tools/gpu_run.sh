@@ -15,6 +15,8 @@
 #   pmcab:<cases>                  one --pmc pass (PMC_COUNTERS) over tools/ab_kernels.py cases (config AB_CFG) -> <tag>_pmcab/
 #   transient                      tools/transient.py plain and under rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES
 #                                  SQ_BUSY_CYCLES -> <tag>_transient.json, <tag>_transient_pmc/, <tag>_transient.txt
+#   ab:<cfg>:<cases>               interleaved A/B of tools/ab_kernels.py cases (comma list) on config <cfg> (3s64: config 3
+#                                  at 64 B), 10M packets, 12 rounds -> <tag>_ab_cfg<cfg>.txt
 #   cmd:<shell command>            anything else, under a 600 s limit
 set -o pipefail
 TAG=$1
@@ -99,6 +101,15 @@ for step in "$@"; do
       python3 tools/transient_summary.py "$OUT/${TAG}_transient_pmc" "$OUT/${TAG}_transient.json" \
         > "$OUT/${TAG}_transient.txt" || exit 10
       tail -8 "$OUT/${TAG}_transient.txt" ;;
+    ab)
+      c=${arg%%:*}; cases=${arg#*:}
+      case "$c" in
+        *s*) sz=${c#*s}; cf=${c%%s*} ;;
+        *) sz=""; cf=$c ;;
+      esac
+      AB_SIZES=$sz AB_ML=${AB_ML:-12} AB_CASES="$cases" timeout -k 10 400 python -u tools/ab_kernels.py 10000000 ${AB_ROUNDS:-12} "$cf" \
+        > "$OUT/${TAG}_ab_cfg$c.txt" 2>&1 || { tail -20 "$OUT/${TAG}_ab_cfg$c.txt"; exit 11; }
+      grep -E "median|identical" "$OUT/${TAG}_ab_cfg$c.txt" ;;
     cmd)
       timeout -k 10 600 bash -c "$arg" || exit 8 ;;
     *)
