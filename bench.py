@@ -3,7 +3,8 @@
 Default workload (BASELINE.json configs[2]): a 10M-packet IMIX batch (64/512/1500 B
 at 7:4:1; 25% VLAN; 70% IPv4 / 30% IPv6; TCP/UDP 50/50; 1% corrupted checksums), synthetic, seed 3 (+rank).
 One step = one pass of the parse kernel over the whole batch already resident in HBM: layer chain
-(8 layer records/packet), hash5Tuple both directions, hash2Tuple, IPv4 + TCP/UDP checksum verify.
+(up to 8 layer records/packet, PACKED), hash5Tuple both directions, hash2Tuple, IPv4 + TCP/UDP checksum verify; records:
+the 16-B brief per packet (hashes, flags incl. the checksum verdicts, chain length, port layer) + the layer rows.
 
 --config selects the other BASELINE configs as extra bench lines (not the driver's default):
   2: 1M x 64 B Eth/IPv4/{TCP,UDP}: parse + hash5Tuple (5-tuple extract), no checksums;
@@ -88,7 +89,10 @@ SIZED_PACKETS = {64: 10_000_000, 512: 10_000_000, 1500: 5_000_000}  # config 3 a
 CONFIG_MAX_LAYERS = {2: 0, 3: 8, 4: 0, 5: 12}
 CONFIG4_FLOWS = 1_000_000  # config 4's flow universe (one for all ranks)
 CONFIG_LAYOUT = {3: "packed", 5: "packed"}  # configs with layer records
-CONFIG_RECORDS = {2: "tuples", 3: "summary", 4: "keys", 5: "summary"}
+# per-packet records: config 2 the 5-tuple extract its name asks for; configs 3 / 5 the 16-B brief beside the layer rows
+# (hashes, flags with the checksum verdicts, chain length, port layer; isPacketOfType from the rows -- ABI 7); config 4
+# what the flow table reads
+CONFIG_RECORDS = {2: "tuples", 3: "brief", 4: "keys", 5: "brief"}
 # plain Eth / VLAN / IP / L4 stacks (configs 2 and 4): the one-round parse-only window (PCPPX_WINDOW_SHORT)
 CONFIG_WINDOW = {2: "short", 4: "short"}
 KERNEL_SRC = ROOT / "pcapplusplus_amd" / "csrc" / "pcppx_kernels.hip"

@@ -181,7 +181,7 @@ struct pcppx_ctx
 	hipEvent_t stats_done = nullptr;
 	bool stats_pending = false;
 	// the engine's header-window choice for PCPPX_WINDOW_DEFAULT launches: every parse adds the live packets and deep
-	// stacks of one tile in 64 to d_win (never cleared); after a parse, a private stream copies the counters into a
+	// stacks of about 64 of its tiles to d_win (never cleared); after a parse, a private stream copies the counters into a
 	// page-locked mirror, which the next launch reads once the copy is done (no wait on any stream)
 	unsigned long long* d_win = nullptr;
 	unsigned long long* h_win = nullptr;
@@ -200,7 +200,7 @@ bool ok(hipError_t e)
 }
 
 // ---- the engine's header window (PCPPX_WINDOW_DEFAULT) ----
-constexpr unsigned long long kWinMinSample = 4096;  // sampled packets per decision
+constexpr unsigned long long kWinMinSample = 2048;  // sampled packets per decision (a launch samples up to ~4096)
 constexpr unsigned long long kWinDeepShare = 256;   // deep stacks above 1 in 256 sampled packets: deep traffic
 
 bool ensure_win(pcppx_ctx* c)

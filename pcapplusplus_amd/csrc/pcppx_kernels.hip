@@ -2411,10 +2411,10 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		write_tuple(p, w, h5, prm.tuples + i);
 	if (prm.wave_stats != nullptr)  // uniform
 		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + blockIdx.x);
-	// the engine's window choice (pcppx_ctx: the next launches' window follows the traffic): one tile in 64 counts its live
-	// packets and their deep stacks (Ethernet links; two atomics per sampled wave), from the first window (still intact:
-	// the rows below reuse the stage)
-	if (prm.win_stats != nullptr && (blockIdx.x & 63) == 0 && prm.linktype == 1)  // uniform
+	// the engine's window choice (pcppx_ctx: the next launches' window follows the traffic): about 64 tiles of a launch,
+	// evenly spread, count their live packets and deep stacks (Ethernet links; two atomics per sampled wave), from the
+	// first window (still intact: the rows below reuse the stage)
+	if (prm.win_stats != nullptr && blockIdx.x % max(1u, gridDim.x >> 6) == 0 && prm.linktype == 1)  // uniform
 	{
 		uint32_t et, o;
 		const bool dp = live && p.lim >= 14 && deep_stack(p, &et, &o);
