@@ -400,8 +400,16 @@ def main() -> None:
         tuple_check = None
     # the flow table's keys: the timed launches' dense hash5 column equals the full parse's summary hash5
     keys_equal = bool(torch.equal(flow_keys, s[:, 0])) if flow_keys is not None else None
-    # the timed launches' briefs: the first half of the full parse's summaries, byte for byte
-    brief_equal = bool(torch.equal(brief.view(n, 16), ext_sum.view(n, 32)[:, :16])) if brief is not None else None
+    # the timed launches' briefs: the first half of the full parse's summaries, byte for byte (a parse-only run against
+    # the checksum parse above: but for its checksum flags)
+    brief_equal = None
+    if brief is not None:
+        want16 = ext_sum.view(n, 32)[:, :16].clone()
+        if not want_csum:
+            csum_flags = abi.F_IP_CSUM | abi.F_IP_CSUM_OK | abi.F_L4_CSUM | abi.F_L4_CSUM_OK
+            w = want16.view(torch.int32)
+            w[:, 3] &= ~csum_flags
+        brief_equal = bool(torch.equal(brief.view(n, 16), want16))
     stats_line = None
     if proto_stats is not None:  # collectStats over every launch (warmup + timed): the histogram of one pass
         launches = args.warmup + args.steps

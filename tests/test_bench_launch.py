@@ -84,7 +84,7 @@ def test_real_launcher_starts_n_ranks(tmp_path):
 def test_bench_small_run_checks_its_records(cfg):
     """bench.py end to end on the GPU at a small size for the configs whose launch differs from the default one: config 2
     (5-tuple extract alone, SHORT window), config 4 (dense keys + collectStats without a summary, SHORT window, the flow
-    table) and config 5 (two-round window, PACKED rows) -- one JSON line whose own checks hold."""
+    table) and config 5 (two-round window, the brief + PACKED rows) -- one JSON line whose own checks hold."""
     import json
 
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", str(cfg), "--packets", "200000", "--steps",
@@ -101,7 +101,8 @@ def test_bench_small_run_checks_its_records(cfg):
         assert c["records"] == "keys" and c["window"] == "short" and c["flow_keys_equal_hash5"]
         assert c["flow_table"]["exact"] and c["flow_table"]["conserved"] and c["collect_stats"]["consistent"]
     if cfg == 5:
-        assert c["records"] == "summary" and c["layout"] == "packed" and c["window"] == "default"
+        assert c["records"] == "brief" and c["layout"] == "packed" and c["window"] == "default"
+        assert c["brief_equal_summary_half"]
 
 
 @pytest.mark.gpu
