@@ -234,6 +234,11 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 96: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 16>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 97: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 98: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
+	// the same stage costs in the checksum instance (the 64-B class, round 5): no hashes / no L7 / no rows / none
+	case 110: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 1>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 111: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 2>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 112: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 4>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 113: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 7>>), grid, dim3(kTile), 0, stream, prm); break;
 	// checksum-instance shapes re-tuned under the default-policy stream loads: occupancy 4 / 6, stream window 192 / 64 chunks
 	case 100: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 101: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;

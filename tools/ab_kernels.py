@@ -63,6 +63,10 @@ cases = {
     "tile/packed-swin64": (abi.make_opts(0, 8, True, 8, layout=PK), 103),
     "po/packed-hash-branchy": (abi.make_opts(0, 8, False, _ml, layout=PK), 97),
     "tile/packed-hash-branchy": (abi.make_opts(0, 8, True, 8, layout=PK), 98),
+    "tile/packed-no-hash": (abi.make_opts(0, 8, True, 8, layout=PK), 110),
+    "tile/packed-no-l7": (abi.make_opts(0, 8, True, 8, layout=PK), 111),
+    "tile/packed-no-rows": (abi.make_opts(0, 8, True, 8, layout=PK), 112),
+    "tile/packed-no-hash-l7-rows": (abi.make_opts(0, 8, True, 8, layout=PK), 113),
     "po/packed-no-hash": (abi.make_opts(0, 8, False, _ml, layout=PK), 90),
     "po/packed-no-l7": (abi.make_opts(0, 8, False, _ml, layout=PK), 91),
     "po/packed-no-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 92),
@@ -102,7 +106,7 @@ want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
     first = next(iter(cases.values()))[0]
     if o.max_layers != first.max_layers or o.want_checksums != want_csum_ref or o.layout != first.layout or \
-            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93) or name.endswith("+brief"):  # diagnostics / other records
+            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93, 110, 111, 112, 113) or name.endswith("+brief"):  # diagnostics / other records
         continue
     summ.zero_()
     lay.zero_()

@@ -60,7 +60,7 @@ for step in "$@"; do
     prof)
       for c in ${arg//,/ }; do
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/${TAG}_prof_cfg$c" \
-          -o bench --output-format csv -- python3 "$ROOT/bench.py" $(cfgargs "$c") --steps 20 --warmup 5 --no-e2e $(tr "$c") \
+          -o bench --output-format csv -- python3 "$ROOT/bench.py" $(cfgargs "$c") --steps 100 --warmup 5 --no-e2e $(tr "$c") \
           > "$ROOT/$OUT/${TAG}_prof_bench_cfg$c.json" 2> "$ROOT/$OUT/${TAG}_prof_cfg$c.err") \
           || { tail -20 "$OUT/${TAG}_prof_cfg$c.err"; exit 5; }
         python3 tools/timed_stats.py "$OUT/${TAG}_prof_cfg$c" "$OUT/${TAG}_prof_bench_cfg$c.json" \
