@@ -369,8 +369,9 @@ def main() -> None:
     wire = int(batch.caplens.sum(dtype=np.int64))
     # the records' chain lengths (packed write bytes), the flag check and -- for parse-only runs -- the header extents
     # (their byte model): from the timed run's own summary when it has one and computes checksums; else from one
-    # untimed parse with full FIXED records through the checksum instance (the same records; a different kernel, so
-    # the timed kernel's rocprof row holds only the timed launches)
+    # untimed parse with full FIXED records through the checksum instance (the same records; for a checksum run that
+    # writes no summary -- configs 3 with the brief -- the same kernel, launched once after the timed region:
+    # tools/timed_stats.py keeps launches warmup+1 .. warmup+steps)
     if want_csum and summary is not None:
         ext_sum = summary
         read_bytes = algorithmic_read_bytes(batch, True)
