@@ -180,9 +180,10 @@ struct pcppx_ctx
 	uint64_t wave_stats_bytes = 0;
 	hipEvent_t stats_done = nullptr;
 	bool stats_pending = false;
-	// the engine's header-window choice for PCPPX_WINDOW_DEFAULT launches: every parse adds the live packets and deep
-	// stacks of about 64 of its tiles to d_win (never cleared); after a parse, a private stream copies the counters into a
-	// page-locked mirror, which the next launch reads once the copy is done (no wait on any stream)
+	// the engine's header-window choice for PCPPX_WINDOW_DEFAULT launches: a sampled parse (every launch until the first
+	// decision, then one in kWinEvery) first adds the live packets and deep stacks of about 64 of its tiles to d_win (never
+	// cleared); after it, a private stream copies the counters into a page-locked mirror, which a later launch reads once
+	// the copy is done (no wait on any stream)
 	unsigned long long* d_win = nullptr;
 	unsigned long long* h_win = nullptr;
 	hipStream_t win_stream = nullptr;
@@ -190,6 +191,7 @@ struct pcppx_ctx
 	bool win_ready = false, win_pending = false;
 	unsigned long long win_live = 0, win_deep = 0;  // the mirror at the last decision
 	int deep_traffic = -1;                            // -1: not known yet; 0: plain stacks; 1: deep stacks
+	uint64_t win_launches = 0;                        // parses since the context was made (the sampling schedule)
 };
 
 namespace
@@ -202,6 +204,7 @@ bool ok(hipError_t e)
 // ---- the engine's header window (PCPPX_WINDOW_DEFAULT) ----
 constexpr unsigned long long kWinMinSample = 2048;  // sampled packets per decision (a launch samples up to ~4096)
 constexpr unsigned long long kWinDeepShare = 256;   // deep stacks above 1 in 256 sampled packets: deep traffic
+constexpr uint64_t kWinEvery = 16;                  // once decided, one parse in 16 is sampled (the traffic may change)
 
 bool ensure_win(pcppx_ctx* c)
 {
@@ -255,10 +258,20 @@ pcppx_opts resolve_window(pcppx_ctx* c, const pcppx_opts* o)
 	return e;
 }
 
-// after a parse on st: copy the counters out behind it on the private stream (one copy in flight)
-void note_window(pcppx_ctx* c, hipStream_t st)
+// the counters a parse samples into, or null: every parse until the first decision, then one in kWinEvery
+unsigned long long* window_sample(pcppx_ctx* c)
 {
-	if (!c->win_ready || c->win_pending)
+	if (!ensure_win(c))
+		return nullptr;
+	const uint64_t k = c->win_launches++;
+	return (c->deep_traffic < 0 || k % kWinEvery == 0) ? c->d_win : nullptr;
+}
+
+// after a sampled parse on st (win: window_sample's counters): copy the counters out behind it on the private stream
+// (one copy in flight)
+void note_window(pcppx_ctx* c, hipStream_t st, const unsigned long long* win)
+{
+	if (win == nullptr || !c->win_ready || c->win_pending)
 		return;
 	if (ok(hipEventRecord(c->win_parsed, st)) && ok(hipStreamWaitEvent(c->win_stream, c->win_parsed, 0)) &&
 	    ok(hipMemcpyAsync(c->h_win, c->d_win, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->win_stream)) &&
@@ -326,11 +339,11 @@ int device_parse(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_
 			return rc;
 		ws = c->d_wave_stats;
 	}
-	unsigned long long* win = ensure_win(c) ? c->d_win : nullptr;
 	const pcppx_opts eo = resolve_window(c, o);
+	unsigned long long* win = window_sample(c);
 	int rc = info ? pcppx::launch_parse_reasm(b, &eo, r, info, st, ws, win) : pcppx::launch_parse(b, &eo, r, st, ws, win);
 	if (rc == PCPPX_OK)
-		note_window(c, st);
+		note_window(c, st, win);
 	if (rc != PCPPX_OK || ws == nullptr)
 		return rc;
 	rc = pcppx::launch_proto_stats_reduce(ws, b->n, r->proto_stats, st);
@@ -581,7 +594,6 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 	                        (r->brief == nullptr || is_pinned(r->brief)) && (!rows || is_pinned(r->layers));
 	uint64_t written = 0;
 	Slot* pend = nullptr;  // DENSE: the previous chunk, its chains not yet copied out
-	unsigned long long* win = ensure_win(c) ? c->d_win : nullptr;
 	uint32_t i = 0, k = 0;
 	while (i < b->n)
 	{
@@ -605,9 +617,10 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		dr.layers = ml ? s.d_lay : nullptr;
 		pcppx_opts fo = resolve_window(c, o);
 		fo.layout = PCPPX_LAYOUT_FIXED;  // DENSE is compacted from the chunk's FIXED rows below
+		unsigned long long* win = window_sample(c);
 		rc = pcppx::launch_parse(&db, &fo, &dr, s.st, nullptr, win);
 		if (rc == PCPPX_OK)
-			note_window(c, s.st);
+			note_window(c, s.st, win);
 		if (rc == PCPPX_OK && dense)
 			rc = pcppx::launch_dense_compact(s.d_lay,
 			                                 dr.brief ? reinterpret_cast<const uint8_t*>(s.d_brief) + 14
@@ -696,9 +709,10 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 		dr.summary = s.d_sum;
 		dr.layers = s.d_lay;
 		const pcppx_opts eo = resolve_window(c, &o);
-		rc = pcppx::launch_parse(&db, &eo, &dr, s.st, nullptr, c->win_ready ? c->d_win : nullptr);
+		unsigned long long* win = window_sample(c);
+		rc = pcppx::launch_parse(&db, &eo, &dr, s.st, nullptr, win);
 		if (rc == PCPPX_OK)
-			note_window(c, s.st);
+			note_window(c, s.st, win);
 		if (rc == PCPPX_OK)
 			rc = pcppx::launch_filter(&db, &dr, ml, spec, c->seq + i, c->d_keys, c->d_first, c->flow_slots,
 			                          s.d_match, c->d_stats, s.st);

@@ -9,7 +9,8 @@ namespace pcppx
 {
 int check_launch(const char* what, hipStream_t stream);
 // wave_stats: null, or parse_waves(n) 16-B per-wave collectStats records, summed by launch_proto_stats_reduce
-// win_stats: null, or the context's two 64-bit counters the parse adds its sampled live / deep-stack packets to
+// win_stats: null, or the context's two 64-bit counters: a window sample (window_sample_kernel: ~64 tiles' live and
+// deep-stack packets) runs ahead of the parse on the same stream and adds to them
 int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream,
                  void* wave_stats = nullptr, unsigned long long* win_stats = nullptr);
 uint32_t parse_waves(uint32_t n);

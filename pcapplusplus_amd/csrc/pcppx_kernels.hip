@@ -998,7 +998,6 @@ struct Params
 	uint4* wave_stats;        // optional per-wave collectStats counters (16 x u8), reduced by proto_stats_reduce_kernel
 	uint32_t packed;          // PCPPX_LAYOUT_PACKED: the chain's layer entries dense per 64-packet tile
 	pcppx_brief* brief;       // optional 16-B brief (pcppx_records.brief): the summary's first half
-	unsigned long long* win_stats;  // engine-chosen window: {sampled live packets, of them deep stacks} (context-owned)
 };
 
 // Everything the summary needs after the chain walk.
@@ -2411,21 +2410,6 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		write_tuple(p, w, h5, prm.tuples + i);
 	if (prm.wave_stats != nullptr)  // uniform
 		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + blockIdx.x);
-	// the engine's window choice (pcppx_ctx: the next launches' window follows the traffic): about 64 tiles of a launch,
-	// evenly spread, count their live packets and deep stacks (Ethernet links; two atomics per sampled wave), from the
-	// first window (still intact: the rows below reuse the stage)
-	if (prm.win_stats != nullptr && blockIdx.x % max(1u, gridDim.x >> 6) == 0 && prm.linktype == 1)  // uniform
-	{
-		uint32_t et, o;
-		const bool dp = live && p.lim >= 14 && deep_stack(p, &et, &o);
-		const uint32_t nl = (uint32_t)__popcll(__ballot(live)), nd = (uint32_t)__popcll(__ballot(dp));
-		if (lane == 0 && nl != 0)
-		{
-			atomicAdd(prm.win_stats, (unsigned long long)nl);
-			atomicAdd(prm.win_stats + 1, (unsigned long long)nd);
-		}
-	}
-
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,
 	// zero past the chain, with FillTails; the generic walk writes only the chain's records) ----
 	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -2536,6 +2520,52 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		else
 			r = reasm_one(w.flags, w.n_layers, prm.layers + (size_t)i * ml, ml, prm.data + off);
 		reinterpret_cast<uint4*>(prm.reasm)[i] = r;
+	}
+}
+
+// ---- the engine's header-window choice (pcppx_ctx, PCPPX_WINDOW_DEFAULT): a sample of the batch's stacks ----
+// About 64 tiles of a batch, evenly spread (every `stride`-th tile), count their live packets and the deep stacks among
+// them (deep_stack over each packet's first 48 B staged in LDS, as the parse's first window holds them: Ethernet links
+// only); one wave per sampled tile, two atomics per wave into the context's counters `win`. A kernel of its own, which
+// the context launches before some of its parses, so that the parse kernel carries no sampling code.
+__global__ __launch_bounds__(kTile) void window_sample_kernel(Params prm, uint32_t stride, unsigned long long* win)
+{
+	constexpr uint32_t kCh = 3, kSlotDw = 4 * kCh + 1;  // + 1 pad dword: lds_u32's second read stays in the slot
+	__shared__ uint32_t stage[kTile * kSlotDw];
+	const uint32_t lane = threadIdx.x;
+	const uint32_t i = blockIdx.x * stride * kTile + lane;
+	const bool in = i < prm.n;
+	const uint64_t off = in ? prm.offsets[i] : 0;
+	const uint32_t cap = in ? prm.caplens[i] : 0;
+	bool empty = true;
+	const uint32_t bad = in ? desc_flags(off, cap, prm.data_len, &empty) : 0;
+	const bool live = in && !bad && !empty;
+	Pkt p;
+	p.g = (gptr8)(prm.data + (live ? off : 0));
+	p.a0 = (uintptr_t)p.g & ~(uintptr_t)15;
+	p.mis = (uint32_t)((uintptr_t)p.g - p.a0);
+	const uint32_t need = (p.mis + cap + 15) >> 4;  // chunks holding the whole packet (none past the batch)
+	p.nch = live ? (need < kCh ? need : kCh) : 0u;
+	lptr32w slot = (lptr32w)(stage) + lane * kSlotDw;
+	for (uint32_t c = 0; c < kCh; ++c)
+		if (c < p.nch)
+		{
+			const uint4 v = ld16(p.a0 + 16 * c);
+			slot[4 * c] = v.x;
+			slot[4 * c + 1] = v.y;
+			slot[4 * c + 2] = v.z;
+			slot[4 * c + 3] = v.w;
+		}
+	p.s = reinterpret_cast<lptr8>(slot);
+	const uint32_t staged = 16 * p.nch - p.mis;
+	p.lim = (live && p.nch) ? (staged < cap ? staged : cap) : 0u;
+	uint32_t et, o;
+	const bool dp = live && p.lim >= 14 && deep_stack(p, &et, &o);  // reads < 34 B: 48 B - 15 staged at least
+	const uint32_t nl = (uint32_t)__popcll(__ballot(live)), nd = (uint32_t)__popcll(__ballot(dp));
+	if (lane == 0 && nl != 0)
+	{
+		atomicAdd(win, (unsigned long long)nl);
+		atomicAdd(win + 1, (unsigned long long)nd);
 	}
 }
 
@@ -3241,7 +3271,6 @@ Params make_params(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, 
 	prm.wave_stats = nullptr;
 	prm.packed = o->layout == PCPPX_LAYOUT_PACKED ? 1u : 0u;
 	prm.brief = r->brief;
-	prm.win_stats = nullptr;
 	return prm;
 }
 
@@ -3426,6 +3455,16 @@ int launch_instance(const pcppx_opts* o, const Params& prm, uint32_t n, hipStrea
 		hipLaunchKernelGGL(PCPPX_PARSE_ONLY_KERNEL, grid, dim3(kTile), 0, stream, prm);
 	return check_launch(what, stream);
 }
+
+// the window sample (Ethernet batches): about 64 evenly spread tiles of the batch, ahead of its parse on the same stream
+int launch_window_sample(const Params& prm, unsigned long long* win, hipStream_t stream)
+{
+	if (win == nullptr || prm.linktype != 1)
+		return PCPPX_OK;
+	const uint32_t tiles = (prm.n + kTile - 1) / kTile, stride = tiles >> 6 ? tiles >> 6 : 1u;
+	hipLaunchKernelGGL(window_sample_kernel, dim3((tiles + stride - 1) / stride), dim3(kTile), 0, stream, prm, stride, win);
+	return check_launch("window_sample_kernel", stream);
+}
 }  // namespace
 
 int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hipStream_t stream, void* wave_stats,
@@ -3435,8 +3474,8 @@ int launch_parse(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, hi
 		return PCPPX_OK;
 	Params prm = make_params(b, o, r, nullptr);
 	prm.wave_stats = static_cast<uint4*>(wave_stats);
-	prm.win_stats = win_stats;
-	return launch_instance(o, prm, b->n, stream, "parse_tile_kernel");
+	const int rc = launch_window_sample(prm, win_stats, stream);
+	return rc != PCPPX_OK ? rc : launch_instance(o, prm, b->n, stream, "parse_tile_kernel");
 }
 
 int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r, pcppx_reasm_info* info,
@@ -3446,8 +3485,8 @@ int launch_parse_reasm(const pcppx_batch* b, const pcppx_opts* o, pcppx_records*
 		return PCPPX_OK;
 	Params prm = make_params(b, o, r, info);
 	prm.wave_stats = static_cast<uint4*>(wave_stats);
-	prm.win_stats = win_stats;
-	return launch_instance(o, prm, b->n, stream, "parse_tile_kernel(reasm)");
+	const int rc = launch_window_sample(prm, win_stats, stream);
+	return rc != PCPPX_OK ? rc : launch_instance(o, prm, b->n, stream, "parse_tile_kernel(reasm)");
 }
 
 uint32_t parse_waves(uint32_t n)

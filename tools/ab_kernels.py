@@ -74,6 +74,11 @@ cases = {
     # the round-4 final product kernel (tools/ab/r04): round-5 changes against it in one process
     "r04/tile-packed": (abi.make_opts(0, 8, True, 8, layout=PK), -3),
     "r04/po-packed": (abi.make_opts(0, 8, False, _ml, layout=PK), -3),
+    # the round-5 kernel with the window sampling inside the parse (tools/ab/r05s): today's samples in its own kernel
+    "r05s/tile-packed": (abi.make_opts(0, 8, True, 8, layout=PK), -4),
+    "r05s/po-packed": (abi.make_opts(0, 8, False, _ml, layout=PK), -4),
+    "r05s/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -4),
+    "r05s/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -4),
     # the 16-B brief instead of the 32-B summary (ABI 7): same rows
     "tile/packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
     "po/packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),

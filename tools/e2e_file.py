@@ -46,7 +46,9 @@ def bench_pair(pcap: Path, reps: tuple[int, int], n: int, trials: int = 1) -> di
     measurements can land in a busy second)."""
     out = {"packets": n, "pcap_bytes": pcap.stat().st_size}
     progs = [(name, exe) for name, exe in (("reference_benchmark", ROOT / "oracle" / "_ref" / "benchmark_ref"),
-                                           ("engine_benchmark", ROOT / "examples" / "bin" / "benchmark"))
+                                           ("engine_benchmark", ROOT / "examples" / "bin" / "benchmark"),
+                                           # the round-4 drop-in (facade + library of commit b2a062a, tools only)
+                                           ("engine_r04_benchmark", ROOT / "tools" / "ab" / "r04" / "benchmark_r04"))
              if exe.exists()]
     per = {name: [] for name, _ in progs}
     last = {}
@@ -61,7 +63,7 @@ def bench_pair(pcap: Path, reps: tuple[int, int], n: int, trials: int = 1) -> di
     for name, _ in progs:
         ms = sorted(per[name])[len(per[name]) // 2]
         out[name] = {"ms_per_run": round(ms, 4), "Mpackets_per_s": round(n / ms / 1e3, 2), "stdout": last[name],
-                     "threads": 1 if name == "reference_benchmark" else "1 host thread + reader thread + GPU",
+                     "threads": 1 if name == "reference_benchmark" else "1 host thread + mapper + parser threads + GPU",
                      "reps": list(reps), "trials_ms": [round(x, 4) for x in per[name]]}
     if "reference_benchmark" in out and "engine_benchmark" in out:
         out["speedup"] = round(out["reference_benchmark"]["ms_per_run"] / out["engine_benchmark"]["ms_per_run"], 2)
@@ -102,11 +104,13 @@ def main() -> None:
     ap.add_argument("--packets", type=int, default=10_000_000)
     ap.add_argument("--out", default=None)
     ap.add_argument("--shm", default="/dev/shm")
-    ap.add_argument("--only", choices=("all", "google"), default="all",
-                    help="google: only the benchmark-google loops (example.pcap and the IMIX pcap)")
+    ap.add_argument("--only", choices=("all", "google", "dropin"), default="all",
+                    help="google: only the benchmark-google loops (example.pcap and the IMIX pcap); dropin: only the "
+                         "drop-in benchmark.cpp runs (5 IMIX trials)")
     args = ap.parse_args()
     res = {"cores": len(os.sched_getaffinity(0))}
     big = Path(args.shm) / f"pcppx_e2e_{os.getpid()}.pcap"
+    exf = Path(args.shm) / f"pcppx_example_{os.getpid()}.pcap"
     try:
         t = time.time()
         b = synth.config(3, args.packets)
@@ -118,45 +122,44 @@ def main() -> None:
         from conftest import GOLDEN, load_golden
 
         ex, _ = load_golden(GOLDEN / "capture_example.npz")
-        exf = Path(args.shm) / f"pcppx_example_{os.getpid()}.pcap"
         write_pcap(exf, ex)
-        # benchmark-google.cpp's loops: all three on example.pcap (the library's 0.5-s runs); the two parse loops on the
-        # IMIX pcap at fixed counts (the pure loop: three passes over the preloaded 10M packets)
-        res["google_example_pcap"] = google_pair(exf, ["--min-time", "0.5"], trials=3)
-        print("google_example", json.dumps(res["google_example_pcap"]), flush=True)
-        res["google_imix_pure"] = google_pair(big, ["--benchmark", "BM_PacketPureParsing", "--iterations",
-                                                    str(3 * args.packets)])
-        print("google_imix_pure", json.dumps(res["google_imix_pure"]), flush=True)
-        res["google_imix_parsing"] = google_pair(big, ["--benchmark", "BM_PacketParsing", "--iterations",
-                                                       str(args.packets)])
-        print("google_imix_parsing", json.dumps(res["google_imix_parsing"]), flush=True)
-        if args.only == "google":
-            raise StopIteration
-        runs = {}
-        for tag, extra in (("map_l8_csum", []), ("copy_l8_csum", ["--copy"]),
-                           ("map_summary", ["--layers", "0", "--checksums", "0"]),
-                           ("copy_summary", ["--copy", "--layers", "0", "--checksums", "0"])):
-            line = run([ROOT / "examples" / "bin" / "pcap_parse", big, "--reps", "3", *extra], timeout=900)
-            runs[tag] = json.loads(line.strip().splitlines()[-1])
-            print(tag, json.dumps(runs[tag]), flush=True)
-        res["file_to_records"] = runs
-        # the drop-in benchmark beside the reference's own, same host
-        c1 = Path(args.shm) / f"pcppx_cfg1_{os.getpid()}.pcap"
-        b1 = synth.config(1)
-        write_pcap(c1, b1)
-        res["benchmark_config1"] = bench_pair(c1, (10, 510), b1.n, trials=7)
-        print("config1", json.dumps(res["benchmark_config1"]), flush=True)
-        c1.unlink()
-        res["benchmark_example_pcap"] = bench_pair(exf, (10, 410), ex.n, trials=7)
-        print("example.pcap", json.dumps(res["benchmark_example_pcap"]), flush=True)
-        res["benchmark_imix_10M"] = bench_pair(big, (1, 3), args.packets, trials=3)
-        print("imix", json.dumps(res["benchmark_imix_10M"]), flush=True)
-    except StopIteration:
-        pass
+        if args.only in ("all", "google"):
+            # benchmark-google.cpp's loops: all three on example.pcap (the library's 0.5-s runs); the two parse loops on
+            # the IMIX pcap at fixed counts (the pure loop: three passes over the preloaded 10M packets)
+            res["google_example_pcap"] = google_pair(exf, ["--min-time", "0.5"], trials=3)
+            print("google_example", json.dumps(res["google_example_pcap"]), flush=True)
+            res["google_imix_pure"] = google_pair(big, ["--benchmark", "BM_PacketPureParsing", "--iterations",
+                                                        str(3 * args.packets)])
+            print("google_imix_pure", json.dumps(res["google_imix_pure"]), flush=True)
+            res["google_imix_parsing"] = google_pair(big, ["--benchmark", "BM_PacketParsing", "--iterations",
+                                                           str(args.packets)])
+            print("google_imix_parsing", json.dumps(res["google_imix_parsing"]), flush=True)
+        if args.only == "all":
+            runs = {}
+            for tag, extra in (("map_l8_csum", []), ("copy_l8_csum", ["--copy"]),
+                               ("map_summary", ["--layers", "0", "--checksums", "0"]),
+                               ("copy_summary", ["--copy", "--layers", "0", "--checksums", "0"])):
+                line = run([ROOT / "examples" / "bin" / "pcap_parse", big, "--reps", "3", *extra], timeout=900)
+                runs[tag] = json.loads(line.strip().splitlines()[-1])
+                print(tag, json.dumps(runs[tag]), flush=True)
+            res["file_to_records"] = runs
+        if args.only in ("all", "dropin"):
+            # the drop-in benchmark beside the reference's own (and the round-4 drop-in where built), same host
+            c1 = Path(args.shm) / f"pcppx_cfg1_{os.getpid()}.pcap"
+            b1 = synth.config(1)
+            write_pcap(c1, b1)
+            try:
+                res["benchmark_config1"] = bench_pair(c1, (10, 510), b1.n, trials=7)
+            finally:
+                c1.unlink()
+            print("config1", json.dumps(res["benchmark_config1"]), flush=True)
+            res["benchmark_example_pcap"] = bench_pair(exf, (10, 410), ex.n, trials=7)
+            print("example.pcap", json.dumps(res["benchmark_example_pcap"]), flush=True)
+            res["benchmark_imix_10M"] = bench_pair(big, (1, 3), args.packets, trials=5 if args.only == "dropin" else 3)
+            print("imix", json.dumps(res["benchmark_imix_10M"]), flush=True)
     finally:
         big.unlink(missing_ok=True)
-        for f in Path(args.shm).glob(f"pcppx_example_{os.getpid()}.pcap"):
-            f.unlink()
+        exf.unlink(missing_ok=True)
     line = json.dumps(res, indent=1)
     if args.out:
         Path(args.out).write_text(line + "\n")
