@@ -33,7 +33,7 @@ struct Slot
 	pcppx_summary* h_sum = nullptr;
 	pcppx_layer* h_lay = nullptr;  // FIXED rows, or (DENSE) the chunk's chains
 	pcppx_brief* h_brief = nullptr;
-	uint32_t* h_total = nullptr;   // DENSE: the chunk's chain entries
+	uint32_t* h_total = nullptr;   // DENSE: the chunk's chain entries, and the batch's up to the chunk's end
 	uint8_t* d_data = nullptr;
 	uint64_t* d_off = nullptr;
 	uint32_t* d_cap = nullptr;
@@ -41,8 +41,8 @@ struct Slot
 	pcppx_layer* d_lay = nullptr;
 	pcppx_brief* d_brief = nullptr;
 	pcppx_layer* d_dense = nullptr;  // DENSE: the chunk's chains back to back
-	uint32_t* d_dsum = nullptr;      // DENSE: per-block chain totals + the chunk's total (last word)
-	hipEvent_t parsed = nullptr;     // DENSE: the chunk's records and total are on the host
+	uint32_t* d_dsum = nullptr;      // DENSE: per-block chain totals, the chunk's total, the batch's up to the chunk's end
+	hipEvent_t parsed = nullptr;     // DENSE: the chunk's chains pushed (the next chunk's positions follow them)
 	uint8_t* h_match = nullptr;  // host filter path: per-packet verdicts
 	uint8_t* d_match = nullptr;
 	bool busy = false;
@@ -406,12 +406,12 @@ int init_host_path(pcppx_ctx* c)
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_match), kChunkPackets)) &&
 		            ok(hipEventCreateWithFlags(&s.parsed, hipEventDisableTiming)) &&
 		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_brief), kChunkPackets * sizeof(pcppx_brief))) &&
-		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_total), sizeof(uint32_t))) &&
+		            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_total), 2 * sizeof(uint32_t))) &&
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_brief), kChunkPackets * sizeof(pcppx_brief))) &&
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_dense),
 		                         (size_t)kChunkPackets * PCPPX_MAX_LAYERS * sizeof(pcppx_layer))) &&
 		            ok(hipMalloc(reinterpret_cast<void**>(&s.d_dsum),
-		                         (pcppx::dense_blocks(kChunkPackets) + 1) * sizeof(uint32_t)));
+		                         (pcppx::dense_blocks(kChunkPackets) + 2) * sizeof(uint32_t)));
 		if (!good)
 		{
 			for (Slot& t : c->slots)
@@ -434,6 +434,18 @@ bool is_pinned(const void* p)
 		return false;
 	}
 	return a.type == hipMemoryTypeHost;
+}
+
+// the device mapping of page-locked host memory (kernels store into it directly), or null
+void* mapped(void* p)
+{
+	hipPointerAttribute_t a;
+	if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || a.devicePointer == nullptr)
+	{
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	return a.devicePointer;
 }
 
 // Packets [i, j) of a host batch as one byte range [*base, *base + *bytes): ascending, each starting at most kMaxGap
@@ -549,8 +561,14 @@ void abandon_slots(pcppx_ctx* c)
 
 // copy a finished chunk's records from pinned memory to the caller's arrays (nothing to copy when the
 // caller's arrays are pinned: the chunk's D2H wrote them directly)
-void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out, bool dense)
+void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out, bool dense, uint64_t* written)
 {
+	if (dense && s.ml && out->layers)  // the chunk's chains: [batch total up to its end - its own, batch total)
+	{
+		s.dense_count = s.h_total[0];
+		s.dense_first = s.h_total[1] - s.h_total[0];
+		*written = s.h_total[1] > *written ? s.h_total[1] : *written;
+	}
 	if (!direct_out)
 	{
 		if (out->summary)
@@ -568,20 +586,6 @@ void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out, bool dens
 	s.busy = false;
 }
 
-// DENSE, second half of a chunk: once its total is on the host, its chains are copied out behind the chunks before it
-bool finish_dense(Slot& p, pcppx_records* r, bool direct_out, uint64_t* written)
-{
-	if (!ok(hipEventSynchronize(p.parsed)))
-		return false;
-	p.dense_count = *p.h_total;
-	p.dense_first = *written;
-	*written += p.dense_count;
-	pcppx_layer* dst = direct_out ? r->layers + p.dense_first : p.h_lay;
-	return (p.dense_count == 0 ||
-	        ok(hipMemcpyAsync(dst, p.d_dense, (size_t)p.dense_count * sizeof(pcppx_layer), hipMemcpyDeviceToHost, p.st))) &&
-	       ok(hipEventRecord(p.done, p.st));
-}
-
 // pcppx_parse_batch_host's chunk pipeline (argument checks done; slots idle on entry)
 int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_records* r)
 {
@@ -593,7 +597,14 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 	const bool direct_out = (r->summary == nullptr || is_pinned(r->summary)) &&
 	                        (r->brief == nullptr || is_pinned(r->brief)) && (!rows || is_pinned(r->layers));
 	uint64_t written = 0;
-	Slot* pend = nullptr;  // DENSE: the previous chunk, its chains not yet copied out
+	// DENSE: the chains are pushed by a kernel through the device mapping of page-locked memory (the caller's array, or
+	// the slot's staging buffer), their positions chained on the device chunk after chunk -- no host round trip to learn
+	// a chunk's count before its copy
+	const uint32_t kTot = pcppx::dense_blocks(kChunkPackets);  // d_dsum[kTot]: the chunk's, [kTot + 1]: cumulative
+	pcppx_layer* lay_map = nullptr;
+	if (dense && direct_out && (lay_map = static_cast<pcppx_layer*>(mapped(r->layers))) == nullptr)
+		return PCPPX_E_HIP;
+	Slot* prev = nullptr;  // DENSE: the previous chunk (its cumulative count is this chunk's base)
 	uint32_t i = 0, k = 0;
 	while (i < b->n)
 	{
@@ -602,7 +613,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(c->copier, s, r, direct_out, dense);
+			drain(c->copier, s, r, direct_out, dense, &written);
 		}
 		size_t pos = 0;
 		const uint8_t* direct = nullptr;
@@ -636,10 +647,16 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		             ok(hipMemcpyAsync(hs, s.d_sum, cnt * sizeof(pcppx_summary), hipMemcpyDeviceToHost, s.st))) &&
 		            (!r->brief || ok(hipMemcpyAsync(hb, s.d_brief, cnt * sizeof(pcppx_brief), hipMemcpyDeviceToHost, s.st)));
 		if (dense)
-			good = good &&
-			       ok(hipMemcpyAsync(s.h_total, s.d_dsum + pcppx::dense_blocks(kChunkPackets), sizeof(uint32_t),
-			                         hipMemcpyDeviceToHost, s.st)) &&
-			       ok(hipEventRecord(s.parsed, s.st));
+		{
+			pcppx_layer* to = direct_out ? lay_map : static_cast<pcppx_layer*>(mapped(s.h_lay));
+			good = good && to != nullptr && (prev == nullptr || ok(hipStreamWaitEvent(s.st, prev->parsed, 0))) &&
+			       pcppx::launch_dense_push(s.d_dense, s.d_dsum + kTot, prev ? prev->d_dsum + kTot + 1 : nullptr, to,
+			                                direct_out, s.d_dsum + kTot + 1, s.st) == PCPPX_OK &&
+			       ok(hipEventRecord(s.parsed, s.st)) &&
+			       ok(hipMemcpyAsync(s.h_total, s.d_dsum + kTot, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s.st)) &&
+			       ok(hipEventRecord(s.done, s.st));
+			prev = &s;
+		}
 		else
 			good = good &&
 			       (!rows ||
@@ -651,24 +668,15 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		s.first = i;
 		s.count = cnt;
 		s.ml = ml;
-		if (dense)
-		{
-			// chunk k-1's total is known by now (or soon: its kernels ran ahead of this chunk's upload)
-			if (pend != nullptr && !finish_dense(*pend, r, direct_out, &written))
-				return PCPPX_E_HIP;
-			pend = &s;
-		}
 		i = j;
 		++k;
 	}
-	if (pend != nullptr && !finish_dense(*pend, r, direct_out, &written))
-		return PCPPX_E_HIP;
 	for (Slot& s : c->slots)
 		if (s.busy)
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(c->copier, s, r, direct_out, dense);
+			drain(c->copier, s, r, direct_out, dense, &written);
 		}
 	r->layers_written = dense ? written : (rows ? (uint64_t)b->n * ml : 0);
 	return PCPPX_OK;

@@ -33,4 +33,8 @@ int launch_reasm(const pcppx_batch* b, const pcppx_records* r, uint32_t ml, pcpp
 uint32_t dense_blocks(uint32_t n);
 int launch_dense_compact(const pcppx_layer* fixed, const uint8_t* n_layers, uint32_t nl_stride, uint32_t n, uint32_t ml,
                          pcppx_layer* dense, uint32_t* block_sums, uint32_t* total, hipStream_t stream);
+// the compacted chains to page-locked host memory through its device mapping (dst_mapped), positions chained across the
+// chunks of a batch on the device: *cum_out = (*base_in or 0) + *count; at_base: entries at dst_mapped + base (else + 0)
+int launch_dense_push(const pcppx_layer* dense, const uint32_t* count, const uint32_t* base_in, pcppx_layer* dst_mapped,
+                      bool at_base, uint32_t* cum_out, hipStream_t stream);
 }  // namespace pcppx

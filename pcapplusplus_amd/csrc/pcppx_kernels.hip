@@ -3402,6 +3402,35 @@ __global__ __launch_bounds__(kDenseThreads) void dense_copy_kernel(const uint2* 
 		*total = pos;  // the last thread of the last block ends the batch's chains
 }
 
+// The chunk's chains (dense[0, *count)) to the caller's page-locked records through their device mapping, coalesced
+// (64 lanes store 512 contiguous bytes): no host round trip to learn the count before a copy can be sized. The chunks
+// of a host batch chain their positions on the device: *base_in (the chunks before this one, null for the first) +
+// this chunk's count -> *cum_out; `at_base` places the entries at base (the caller's array) or at 0 (a staging buffer).
+__global__ __launch_bounds__(kDenseThreads) void dense_push_kernel(const uint2* __restrict__ dense,
+                                                                   const uint32_t* __restrict__ count,
+                                                                   const uint32_t* __restrict__ base_in, uint2* dst,
+                                                                   uint32_t at_base, uint32_t* __restrict__ cum_out)
+{
+	const uint32_t cnt = *count, base = base_in != nullptr ? *base_in : 0u;
+	uint2* out = dst + (at_base ? base : 0u);
+	const uint32_t step = gridDim.x * kDenseThreads;
+	for (uint32_t j = blockIdx.x * kDenseThreads + threadIdx.x; j < cnt; j += 4 * step)
+	{
+		uint2 v[4];  // four loads in flight per lane
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u)
+			if (j + u * step < cnt)
+				v[u] = dense[j + u * step];
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u)
+			if (j + u * step < cnt)
+				out[j + u * step] = v[u];
+	}
+	__threadfence_system();  // host memory: visible to the host at the event behind this kernel, whatever its caching
+	if (blockIdx.x == 0 && threadIdx.x == 0)
+		*cum_out = base + cnt;
+}
+
 }  // namespace
 
 uint32_t dense_blocks(uint32_t n)
@@ -3421,6 +3450,14 @@ int launch_dense_compact(const pcppx_layer* fixed, const uint8_t* n_layers, uint
 	                   reinterpret_cast<const uint2*>(fixed), n_layers, nl_stride, n, ml, block_sums,
 	                   reinterpret_cast<uint2*>(dense), total);
 	return check_launch("dense_compact", stream);
+}
+
+int launch_dense_push(const pcppx_layer* dense, const uint32_t* count, const uint32_t* base_in, pcppx_layer* dst_mapped,
+                      bool at_base, uint32_t* cum_out, hipStream_t stream)
+{
+	hipLaunchKernelGGL(dense_push_kernel, dim3(128), dim3(kDenseThreads), 0, stream, reinterpret_cast<const uint2*>(dense),
+	                   count, base_in, reinterpret_cast<uint2*>(dst_mapped), at_base ? 1u : 0u, cum_out);
+	return check_launch("dense_push", stream);
 }
 
 namespace
