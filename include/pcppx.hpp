@@ -1824,7 +1824,7 @@ private:
 	uint8_t m_MaxLayers = 0;
 	const uint8_t* m_Raw = nullptr;
 	uint32_t m_Caplen = 0;
-	mutable pcppx_summary m_Full{};       // summary() of brief-backed records
+	mutable pcppx_summary m_Full;         // summary() of brief-backed records (assigned whole before any read)
 	std::shared_ptr<RawPacket> m_OwnedRaw;  // freeRawPacket
 };
 using ParsedPacket = Packet;
