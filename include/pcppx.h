@@ -144,8 +144,9 @@ typedef struct pcppx_opts {
 	uint8_t reserved[3];
 } pcppx_opts;
 #define PCPPX_WINDOW_DEFAULT 0 /* the engine's choice (ABI 7), from the traffic this context has parsed: ahead of its
-                                  parses (each until the first decision, then one in 16) about 64 tiles of the batch count
-                                  their deep stacks (a sampling kernel: after up to two VLAN tags an MPLS label, or an IP
+                                  parses (each DEFAULT one until the first decision, then one in 16, as for forced
+                                  windows) ~64 tiles of the batch count their deep stacks (a sampling kernel: after up
+                                  to two VLAN tags an MPLS label, or an IP
                                   layer not followed by TCP / UDP); when more than 1 in 256 sampled packets had one, the
                                   next launches run as DEEP (checksum launches) / with the second round (parse-only),
                                   otherwise checksum launches gather one 96-B window (5 waves/SIMD) and parse-only ones

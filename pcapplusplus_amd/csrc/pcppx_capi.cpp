@@ -258,13 +258,15 @@ pcppx_opts resolve_window(pcppx_ctx* c, const pcppx_opts* o)
 	return e;
 }
 
-// the counters a parse samples into, or null: every parse until the first decision, then one in kWinEvery
-unsigned long long* window_sample(pcppx_ctx* c)
+// the counters a parse samples into, or null: a PCPPX_WINDOW_DEFAULT parse every time until the first decision, else
+// (decided, or a window the caller forced) one parse in kWinEvery -- pcppx_window_choice follows the traffic either way
+unsigned long long* window_sample(pcppx_ctx* c, const pcppx_opts* o)
 {
 	if (!ensure_win(c))
 		return nullptr;
+	update_window(c, false);
 	const uint64_t k = c->win_launches++;
-	return (c->deep_traffic < 0 || k % kWinEvery == 0) ? c->d_win : nullptr;
+	return ((c->deep_traffic < 0 && o->window == PCPPX_WINDOW_DEFAULT) || k % kWinEvery == 0) ? c->d_win : nullptr;
 }
 
 // after a sampled parse on st (win: window_sample's counters): copy the counters out behind it on the private stream
@@ -340,7 +342,7 @@ int device_parse(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcppx_
 		ws = c->d_wave_stats;
 	}
 	const pcppx_opts eo = resolve_window(c, o);
-	unsigned long long* win = window_sample(c);
+	unsigned long long* win = window_sample(c, o);
 	int rc = info ? pcppx::launch_parse_reasm(b, &eo, r, info, st, ws, win) : pcppx::launch_parse(b, &eo, r, st, ws, win);
 	if (rc == PCPPX_OK)
 		note_window(c, st, win);
@@ -628,7 +630,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		dr.layers = ml ? s.d_lay : nullptr;
 		pcppx_opts fo = resolve_window(c, o);
 		fo.layout = PCPPX_LAYOUT_FIXED;  // DENSE is compacted from the chunk's FIXED rows below
-		unsigned long long* win = window_sample(c);
+		unsigned long long* win = window_sample(c, o);
 		rc = pcppx::launch_parse(&db, &fo, &dr, s.st, nullptr, win);
 		if (rc == PCPPX_OK)
 			note_window(c, s.st, win);
@@ -717,7 +719,7 @@ int filter_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_match_spec* 
 		dr.summary = s.d_sum;
 		dr.layers = s.d_lay;
 		const pcppx_opts eo = resolve_window(c, &o);
-		unsigned long long* win = window_sample(c);
+		unsigned long long* win = window_sample(c, &o);
 		rc = pcppx::launch_parse(&db, &eo, &dr, s.st, nullptr, win);
 		if (rc == PCPPX_OK)
 			note_window(c, s.st, win);
