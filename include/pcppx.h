@@ -143,14 +143,13 @@ typedef struct pcppx_opts {
 	uint8_t layout;              /* PCPPX_LAYOUT_*: how pcppx_records.layers is laid out */
 	uint8_t reserved[3];
 } pcppx_opts;
-#define PCPPX_WINDOW_DEFAULT 0 /* the engine's choice (ABI 7), from the traffic this context has parsed: ahead of its
-                                  parses (each DEFAULT one until the first decision, then one in 16, as for forced
-                                  windows) ~64 tiles of the batch count their deep stacks (a sampling kernel: after up
-                                  to two VLAN tags an MPLS label, or an IP
-                                  layer not followed by TCP / UDP); when more than 1 in 256 sampled packets had one, the
-                                  next launches run as DEEP (checksum launches) / with the second round (parse-only),
-                                  otherwise checksum launches gather one 96-B window (5 waves/SIMD) and parse-only ones
-                                  run as SHORT. Until 2048 packets were sampled: one 96-B window for checksum launches,
+#define PCPPX_WINDOW_DEFAULT 0 /* the engine's choice (ABI 7), from the traffic this context has parsed with it: ahead
+                                  of those parses (each until the first decision, then one in 16) ~64 tiles of the batch
+                                  count their deep stacks (a sampling kernel: after up to two VLAN tags an MPLS label,
+                                  or an IP layer not followed by TCP / UDP); when more than 1 in 256 sampled packets
+                                  had one, the next launches run as DEEP (checksum launches) / with the second round
+                                  (parse-only), otherwise checksum launches gather one 96-B window (5 waves/SIMD) and
+                                  parse-only ones run as SHORT. Until 2048 packets were sampled: one 96-B window for checksum launches,
                                   96 B + a second round up to 144 B for parse-only ones. pcppx_window_choice() */
 #define PCPPX_WINDOW_DEEP 1    /* checksum launches too gather the two-round 144-B window: deep stacks stay on the
                                   fast path instead of the generic walk; 4 waves/SIMD. Parse-only: as DEFAULT */

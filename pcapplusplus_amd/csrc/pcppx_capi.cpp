@@ -191,7 +191,7 @@ struct pcppx_ctx
 	bool win_ready = false, win_pending = false;
 	unsigned long long win_live = 0, win_deep = 0;  // the mirror at the last decision
 	int deep_traffic = -1;                            // -1: not known yet; 0: plain stacks; 1: deep stacks
-	uint64_t win_launches = 0;                        // parses since the context was made (the sampling schedule)
+	uint64_t win_launches = 0;                        // DEFAULT-window parses so far (the sampling schedule)
 };
 
 namespace
@@ -258,15 +258,15 @@ pcppx_opts resolve_window(pcppx_ctx* c, const pcppx_opts* o)
 	return e;
 }
 
-// the counters a parse samples into, or null: a PCPPX_WINDOW_DEFAULT parse every time until the first decision, else
-// (decided, or a window the caller forced) one parse in kWinEvery -- pcppx_window_choice follows the traffic either way
+// the counters a parse samples into, or null: a PCPPX_WINDOW_DEFAULT parse every time until the first decision, then
+// one in kWinEvery; a parse whose window the caller forced never (the choice follows the DEFAULT parses' traffic)
 unsigned long long* window_sample(pcppx_ctx* c, const pcppx_opts* o)
 {
-	if (!ensure_win(c))
+	if (o->window != PCPPX_WINDOW_DEFAULT || !ensure_win(c))
 		return nullptr;
 	update_window(c, false);
 	const uint64_t k = c->win_launches++;
-	return ((c->deep_traffic < 0 && o->window == PCPPX_WINDOW_DEFAULT) || k % kWinEvery == 0) ? c->d_win : nullptr;
+	return (c->deep_traffic < 0 || k % kWinEvery == 0) ? c->d_win : nullptr;
 }
 
 // after a sampled parse on st (win: window_sample's counters): copy the counters out behind it on the private stream
