@@ -281,51 +281,56 @@ int parseVecMode(const char* capture, const char* outfile, const std::string& pl
 int timeMode(const char* capture, int reps)
 {
 	using clk = std::chrono::steady_clock;
-	double acc[5] = { 0, 0, 0, 0, 0 };
+	double acc[6] = { 0, 0, 0, 0, 0, 0 };
 	size_t packets = 0;
 	for (int r = 0; r <= reps; ++r)
 	{
-		const auto t0 = clk::now();
-		pcppx::PcapFileReaderDevice reader(capture);
-		if (!reader.open())
-			return 4;
-		const auto t1 = clk::now();
-		pcppx::RawPacket raw;
+		clk::time_point t0, t1, t2, t3, t4, t5;
 		size_t n = 0, tcp = 0;
-		auto t2 = t1, t3 = t1;
-		if (reader.getNextPacket(raw))
 		{
-			t2 = clk::now();
+			t0 = clk::now();
+			pcppx::PcapFileReaderDevice reader(capture);
+			if (!reader.open())
+				return 4;
+			t1 = clk::now();
+			pcppx::RawPacket raw;
+			t2 = t3 = t1;
+			if (reader.getNextPacket(raw))
 			{
-				pcppx::Packet p(&raw, pcppx::TCP);
-				tcp += p.isPacketOfType(pcppx::TCP) ? 1 : 0;
-			}
-			t3 = clk::now();
-			++n;
-			while (reader.getNextPacket(raw))
-			{
-				pcppx::Packet p(&raw, pcppx::TCP);
-				tcp += p.isPacketOfType(pcppx::TCP) ? 1 : 0;
+				t2 = clk::now();
+				{
+					pcppx::Packet p(&raw, pcppx::TCP);
+					tcp += p.isPacketOfType(pcppx::TCP) ? 1 : 0;
+				}
+				t3 = clk::now();
 				++n;
+				while (reader.getNextPacket(raw))
+				{
+					pcppx::Packet p(&raw, pcppx::TCP);
+					tcp += p.isPacketOfType(pcppx::TCP) ? 1 : 0;
+					++n;
+				}
 			}
-		}
-		const auto t4 = clk::now();
-		reader.close();
-		const auto t5 = clk::now();
+			t4 = clk::now();
+			reader.close();
+			t5 = clk::now();
+		}  // the RawPacket and the reader go out of scope
+		const auto t6 = clk::now();
 		if (r == 0)
 			continue;  // untimed: HIP initialisation, pinned pools
 		packets = n;
-		const double d[5] = { std::chrono::duration<double, std::micro>(t1 - t0).count(),
+		const double d[6] = { std::chrono::duration<double, std::micro>(t1 - t0).count(),
 			                  std::chrono::duration<double, std::micro>(t2 - t1).count(),
 			                  std::chrono::duration<double, std::micro>(t3 - t2).count(),
 			                  std::chrono::duration<double, std::micro>(t4 - t3).count(),
-			                  std::chrono::duration<double, std::micro>(t5 - t4).count() };
-		for (int k = 0; k < 5; ++k)
+			                  std::chrono::duration<double, std::micro>(t5 - t4).count(),
+			                  std::chrono::duration<double, std::micro>(t6 - t5).count() };
+		for (int k = 0; k < 6; ++k)
 			acc[k] += d[k];
 	}
 	std::printf("{\"packets\": %zu, \"reps\": %d, \"open_us\": %.1f, \"first_packet_us\": %.1f, \"first_parse_us\": %.1f, "
-	            "\"loop_us\": %.1f, \"close_us\": %.1f}\n",
-	            packets, reps, acc[0] / reps, acc[1] / reps, acc[2] / reps, acc[3] / reps, acc[4] / reps);
+	            "\"loop_us\": %.1f, \"close_us\": %.1f, \"destroy_us\": %.1f}\n",
+	            packets, reps, acc[0] / reps, acc[1] / reps, acc[2] / reps, acc[3] / reps, acc[4] / reps, acc[5] / reps);
 	return 0;
 }
 }  // namespace

@@ -389,7 +389,11 @@ def test_gpu_host_completion_every_golden_record(built, tmp_path):
     with the reference registered as host parser: every record -- the packets the engine finishes itself and the
     flagged ones the host parser completes (their hashes, port layer, protocol mask and checksums included) -- equals
     the reference Packet++'s golden record, field for field (flags: the reference's, plus F_HOST_PARSED on the
-    completed ones)."""
+    completed ones).
+    The host parser completes exactly the packets the engine leaves to the host -- the restatement's NEEDS_HOST flags,
+    packet for packet -- so the completed records (the reference compared with itself: they test the facade's side
+    table, not the GPU) are kept apart from the engine-finished ones, which are the GPU evidence; both counts are the
+    fixtures' exact counts."""
     if not oracle.ref_available():
         pytest.skip("reference library not built")
     from conftest import golden_files
@@ -412,6 +416,13 @@ def test_gpu_host_completion_every_golden_record(built, tmp_path):
             s, lay = rec["sum"], rec["lay"]
             ml = int(opts.max_layers)
             host = (s["flags"] & F_HOST) != 0
+            # the packets the engine leaves to the host (the restatement's flags under the same options)
+            o16 = abi.Opts.from_buffer_copy(opts)
+            o16.max_layers = abi.MAX_LAYERS
+            os_, _ = oracle.oracle_parse(b, o16, threads=8)
+            left = ((os_["flags"] & abi.F_NEEDS_HOST) != 0) & ((os_["flags"] & abi.F_BAD_DESC) == 0)
+            assert (host == left).all(), f"{path.name}/{v}: host-completed packets differ from the engine's flagged ones " \
+                                         f"at {np.nonzero(host != left)[0][:5]}"
             csum = bool(opts.want_checksums)
             nl = np.minimum(s["n_layers"], ml)
             where = f"{path.name}/{v}"
@@ -436,7 +447,8 @@ def test_gpu_host_completion_every_golden_record(built, tmp_path):
                 assert len(bad) == 0, f"{where}: layers.{f} differs on {len(bad)} packets, first #{bad[0]}"
             checked += b.n
             completed += int(host.sum())
-    assert checked > 70_000 and completed > 700, (checked, completed)  # r04: 76,135 records, 798 completed
+    # the fixtures' exact counts: 75,337 records the engine finishes on the GPU + 798 the host parser completes
+    assert (checked - completed, completed) == (75_337, 798), (checked, completed)
 
 
 F_HOST = 0x4000  # pcppx::F_HOST_PARSED (include/pcppx.hpp)
