@@ -147,6 +147,54 @@ __global__ __launch_bounds__(kTile) void diag_tile_rw(const uint8_t* data, uint6
 		out[blockIdx.x] = acc;
 }
 
+// variants 120-125: diag_tile_rw with the record stores under other cache policies (round 5): 0 plain, 1 nt (as
+// diag_tile_rw), 2 sc1, 3 sc0 sc1, 4 nt sc1, 5 nt sc0 sc1 -- what the read + write mix costs per store policy
+template <int P>
+__device__ __forceinline__ void store_policy(void* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+	typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+	v4 x;
+	x.x = a; x.y = b; x.z = c; x.w = d;
+	if (P == 0)
+		*reinterpret_cast<v4*>(p) = x;
+	else if (P == 1)
+		__builtin_nontemporal_store(x, reinterpret_cast<v4*>(p));
+	else if (P == 2)
+		asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(x) : "memory");
+	else if (P == 3)
+		asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(x) : "memory");
+	else if (P == 4)
+		asm volatile("global_store_dwordx4 %0, %1, off nt sc1" : : "v"(p), "v"(x) : "memory");
+	else
+		asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" : : "v"(p), "v"(x) : "memory");
+}
+template <int P>
+__global__ __launch_bounds__(kTile) void diag_tile_rw_policy(const uint8_t* data, uint64_t len, uint32_t per_wave,
+                                                              uint8_t* wout, uint32_t w_per_wave, uint32_t* out)
+{
+	const uint64_t base = (uint64_t)blockIdx.x * per_wave;
+	uint32_t acc = 0;
+	for (uint32_t c = threadIdx.x; 16ull * c < per_wave; c += 4 * kTile)
+	{
+		uint4 v[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+		{
+			const uint64_t a = base + 16ull * (c + k * kTile);
+			v[k] = a + 16 <= len ? ld16((uintptr_t)data + a) : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) + halves(v[k].w);
+	}
+	acc = wave_incl_scan(acc);
+	uint8_t* w = wout + (uint64_t)blockIdx.x * w_per_wave;
+	for (uint32_t c = threadIdx.x; 16 * c < w_per_wave; c += kTile)
+		store_policy<P>(w + 16 * c, acc + c, acc, c, blockIdx.x);
+	if (threadIdx.x == 63)
+		out[blockIdx.x] = acc;
+}
+
 __global__ __launch_bounds__(kBlock) void diag_grid_read(const uint8_t* data, uint64_t len, uint32_t* out)
 {
 	const uint64_t nch = len / 16;
@@ -216,6 +264,29 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 			return PCPPX_E_INVAL;
 		hipLaunchKernelGGL(diag_tile_rw, dim3(blocks), dim3(kTile), 0, stream, b->data, b->data_len, per_wave,
 		                   reinterpret_cast<uint8_t*>(r->layers), w_per_wave, reinterpret_cast<uint32_t*>(r->summary));
+		break;
+	}
+	case 120:
+	case 121:
+	case 122:
+	case 123:
+	case 124:
+	case 125:
+	{
+		// diag_tile_rw under six store policies (same read + write bytes as variant 7)
+		const uint32_t per_wave = 21 * 1024, w_per_wave = 4192;
+		const uint32_t blocks = (uint32_t)((b->data_len + per_wave - 1) / per_wave);
+		if ((uint64_t)blocks * w_per_wave > (uint64_t)b->n * o->max_layers * 8)
+			return PCPPX_E_INVAL;
+		uint8_t* wo = reinterpret_cast<uint8_t*>(r->layers);
+		uint32_t* so = reinterpret_cast<uint32_t*>(r->summary);
+		const dim3 g(blocks), t(kTile);
+		if (variant == 120) hipLaunchKernelGGL(diag_tile_rw_policy<0>, g, t, 0, stream, b->data, b->data_len, per_wave, wo, w_per_wave, so);
+		if (variant == 121) hipLaunchKernelGGL(diag_tile_rw_policy<1>, g, t, 0, stream, b->data, b->data_len, per_wave, wo, w_per_wave, so);
+		if (variant == 122) hipLaunchKernelGGL(diag_tile_rw_policy<2>, g, t, 0, stream, b->data, b->data_len, per_wave, wo, w_per_wave, so);
+		if (variant == 123) hipLaunchKernelGGL(diag_tile_rw_policy<3>, g, t, 0, stream, b->data, b->data_len, per_wave, wo, w_per_wave, so);
+		if (variant == 124) hipLaunchKernelGGL(diag_tile_rw_policy<4>, g, t, 0, stream, b->data, b->data_len, per_wave, wo, w_per_wave, so);
+		if (variant == 125) hipLaunchKernelGGL(diag_tile_rw_policy<5>, g, t, 0, stream, b->data, b->data_len, per_wave, wo, w_per_wave, so);
 		break;
 	}
 	// diagnostics over the product shapes (ParseShape<NT, FillTails, TightR2, Realign, EarlyB, StreamOnly, MarkFast,

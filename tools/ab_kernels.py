@@ -41,6 +41,13 @@ cases = {
     "diag/tile-read": (abi.make_opts(0, 8, True, 0), 3),
     "diag/grid-read": (abi.make_opts(0, 8, True, 0), 4),
     "diag/tile-rw": (abi.make_opts(0, 8, True, 16), 7),
+    # the same read + write mix under other store cache policies (round 5)
+    "diag/rw-plain": (abi.make_opts(0, 8, True, 16), 120),
+    "diag/rw-nt": (abi.make_opts(0, 8, True, 16), 121),
+    "diag/rw-sc1": (abi.make_opts(0, 8, True, 16), 122),
+    "diag/rw-sc0sc1": (abi.make_opts(0, 8, True, 16), 123),
+    "diag/rw-nt-sc1": (abi.make_opts(0, 8, True, 16), 124),
+    "diag/rw-nt-sc0sc1": (abi.make_opts(0, 8, True, 16), 125),
     # parse-only instances (checksums off; configs 2 / 4 / 5): records per packet AB_ML
     "po/product": (abi.make_opts(0, 8, False, _ml), 0),
     "po/packed": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),
@@ -111,7 +118,7 @@ want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
     first = next(iter(cases.values()))[0]
     if o.max_layers != first.max_layers or o.want_checksums != want_csum_ref or o.layout != first.layout or \
-            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93, 110, 111, 112, 113) or name.endswith("+brief"):  # diagnostics / other records
+            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93, 110, 111, 112, 113, 120, 121, 122, 123, 124, 125) or name.endswith("+brief"):  # diagnostics / other records
         continue
     summ.zero_()
     lay.zero_()
