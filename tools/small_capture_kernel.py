@@ -54,7 +54,7 @@ def main() -> None:
                 # packets off the fast path: the tools-only mark (flags bit 0x8000 on fast-path packets)
                 ab.parse_device(data, offs, caps, n, b.linktype, o, summ, lay, st.cuda_stream, 30 if csum else 31)
                 torch.cuda.synchronize()
-                fl = summ.view(n, 16).view(torch.int16)[:, 6].cpu().numpy().astype(np.uint16)
+                fl = summ.view(n, 32).view(torch.int16)[:, 6].cpu().numpy().astype(np.uint16)
                 res[tag] = {"median_us": round(float(np.median(ts)), 1), "min_us": round(float(np.min(ts)), 1),
                             "generic_walk_packets": int(((fl & 0x8000) == 0).sum()),
                             "waves_with_a_generic_packet": int((((fl & 0x8000) == 0).reshape(-1)[: n // 64 * 64]
