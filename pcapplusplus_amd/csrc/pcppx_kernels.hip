@@ -109,6 +109,14 @@ __device__ __forceinline__ uint32_t rd16(const Pkt& p, uint32_t j)
 {
 	return j + 2 <= p.lim ? (lds_u32(p, j) & 0xFFFF) : le16(p, j);
 }
+// bytes j..j+3 of the packet from HBM as one unaligned dword load (gfx950 global loads take any byte alignment; the
+// compiler merges four consecutive ones into one 16-B load). Only for bytes that exist (j + 4 <= caplen).
+typedef uint32_t __attribute__((aligned(1))) u32_any;
+typedef const __attribute__((address_space(1))) u32_any* gptr32_any;
+__device__ __forceinline__ uint32_t ldu32(const Pkt& p, uint32_t j)
+{
+	return *reinterpret_cast<gptr32_any>(p.g + j);
+}
 
 // ---- validity predicates (isDataValid of each layer; cited in oracle/pcppx_oracle.c) ----
 __device__ __forceinline__ bool ipv4_ok(const Pkt& p, uint32_t o, uint32_t n)
@@ -377,45 +385,96 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t v)
 {
 	return (v - 0x01010101u) & ~v & 0x80808080u;  // the lowest flagged byte is the first zero byte
 }
-// the first '\n' in payload bytes [a, n) of the payload at o (n if none), dword-wise; *nul: the first NUL before it
+// payload bytes [j, j + 4G) at o as G dwords: from LDS where the window holds them, else as G dword loads issued
+// together (one memory round trip per 4G bytes of an HTTP header walk instead of one per dword); bytes at or past n read
+// as 0x01 (neither '\n', ' ' nor NUL). G: 2 in the checksum instance (its stream windows are live across the walk), 4 in
+// the parse-only ones.
+template <int G>
+__device__ __forceinline__ void text_group(const Pkt& p, uint32_t o, uint32_t j, uint32_t n, uint32_t (&w)[G])
+{
+	if (o + j >= p.lim && j + 4 * G <= n)
+	{
+#pragma unroll
+		for (int k = 0; k < G; ++k)
+			w[k] = ldu32(p, o + j + 4 * k);
+		return;
+	}
+#pragma unroll
+	for (int k = 0; k < G; ++k)
+	{
+		const uint32_t jj = j + 4 * k;
+		if (jj + 4 <= n)
+			w[k] = o + jj + 4 <= p.lim ? lds_u32(p, o + jj) : ldu32(p, o + jj);
+		else
+		{
+			uint32_t v = 0x01010101u;
+			for (uint32_t b = 0; jj + b < n; ++b)
+				v = (v & ~(0xFFu << (8 * b))) | (rb(p, o + jj + b) << (8 * b));
+			w[k] = v;
+		}
+	}
+}
+// the first byte equal to c in payload bytes [a, n) of the payload at o (n if none)
+template <int G>
+__device__ __forceinline__ uint32_t find_byte(const Pkt& p, uint32_t o, uint32_t a, uint32_t n, uint32_t c)
+{
+	const uint32_t cc = c * 0x01010101u;
+	for (uint32_t j = a; j < n; j += 4 * G)
+	{
+		uint32_t w[G];
+		text_group<G>(p, o, j, n, w);
+#pragma unroll
+		for (int k = 0; k < G; ++k)
+		{
+			const uint32_t m = zero_bytes(w[k] ^ cc);
+			if (m)
+			{
+				const uint32_t e = j + 4 * k + (__builtin_ctz(m) >> 3);
+				return e < n ? e : n;
+			}
+		}
+	}
+	return n;
+}
+// the first '\n' in payload bytes [a, n) of the payload at o (n if none), 4G bytes per step; *nul: the first NUL before it
+template <int G>
 __device__ uint32_t scan_nl(const Pkt& p, uint32_t o, uint32_t a, uint32_t n, uint32_t* nul)
 {
 	uint32_t z = n;
-	for (uint32_t j = a; j < n; j += 4)
+	for (uint32_t j = a; j < n; j += 4 * G)
 	{
-		uint32_t w;
-		if (j + 4 <= n)
-			w = rd32(p, o + j);
-		else
+		uint32_t w[G];
+		text_group<G>(p, o, j, n, w);
+#pragma unroll
+		for (int k = 0; k < G; ++k)
 		{
-			w = 0x01010101u;  // past the payload: neither '\n' nor NUL
-			for (uint32_t k = 0; j + k < n; ++k)
-				w = (w & ~(0xFFu << (8 * k))) | (rb(p, o + j + k) << (8 * k));
-		}
-		const uint32_t zl = zero_bytes(w ^ 0x0A0A0A0Au), z0 = zero_bytes(w);
-		if (z == n && z0)
-			z = j + (__builtin_ctz(z0) >> 3);
-		if (zl)
-		{
-			const uint32_t e = j + (__builtin_ctz(zl) >> 3);
-			*nul = z < e ? z : n;
-			return e;
+			const uint32_t zl = zero_bytes(w[k] ^ 0x0A0A0A0Au), z0 = zero_bytes(w[k]);
+			if (z == n && z0)
+				z = j + 4 * k + (__builtin_ctz(z0) >> 3);
+			if (zl)
+			{
+				const uint32_t e = j + 4 * k + (__builtin_ctz(zl) >> 3);
+				*nul = z < e ? z : n;
+				return e;
+			}
 		}
 	}
 	*nul = z;
 	return n;
 }
 // HeaderField size (TextBasedProtocol.cpp:448-461): through the first '\n', else strnlen to the end
+template <int G>
 __device__ __forceinline__ uint32_t tbp_field(const Pkt& p, uint32_t o, uint32_t a, uint32_t n)
 {
 	uint32_t nul;
-	const uint32_t e = scan_nl(p, o, a, n, &nul);
+	const uint32_t e = scan_nl<G>(p, o, a, n, &nul);
 	return e < n ? e - a + 1 : nul - a;
 }
 // TextBasedProtocolMessage::parseFields + getHeaderLen (TextBasedProtocol.cpp:87-139,436-439)
+template <int G>
 __device__ uint32_t tbp_header_len(const Pkt& p, uint32_t o, uint32_t fl, uint32_t n)
 {
-	uint32_t off = fl, s = tbp_field(p, o, off, n);
+	uint32_t off = fl, s = tbp_field<G>(p, o, off, n);
 	bool end = s == 0;
 	if (!end)
 	{
@@ -424,7 +483,7 @@ __device__ uint32_t tbp_header_len(const Pkt& p, uint32_t o, uint32_t fl, uint32
 	}
 	while (!end && off + s < n)
 	{
-		const uint32_t s2 = tbp_field(p, o, off + s, n);
+		const uint32_t s2 = tbp_field<G>(p, o, off + s, n);
 		if (s2 == 0)
 			break;
 		off += s;
@@ -436,6 +495,7 @@ __device__ uint32_t tbp_header_len(const Pkt& p, uint32_t o, uint32_t fl, uint32
 }
 // HttpRequestFirstLine's end (HttpLayer.cpp:166-213, parseVersion :287-320): the first " HTTP/" after the method's
 // space; with room for "x.y" the line ends after the next '\n', else (or with no version) at the end
+template <int G>
 __device__ uint32_t http_request_line(const Pkt& p, uint32_t o, uint32_t n)
 {
 	uint32_t sp = 0;
@@ -443,13 +503,15 @@ __device__ uint32_t http_request_line(const Pkt& p, uint32_t o, uint32_t n)
 		++sp;
 	for (uint32_t v = sp + 1; v + 6 <= n; ++v)
 	{
-		if (rb(p, o + v) != ' ' || rb(p, o + v + 1) != 'H' || rb(p, o + v + 2) != 'T' || rb(p, o + v + 3) != 'T' ||
-		    rb(p, o + v + 4) != 'P' || rb(p, o + v + 5) != '/')
+		v = find_byte<G>(p, o, v, n, ' ');  // the next space (4G bytes per step), then " HTTP/" at it
+		if (v + 6 > n)
+			break;
+		if (rd32(p, o + v + 1) != 0x50545448u || rb(p, o + v + 5) != '/')  // "HTTP" as a little-endian dword
 			continue;
 		if (v + 9 > n)
 			return n;
 		uint32_t nul;
-		const uint32_t e = scan_nl(p, o, v + 6, n, &nul);
+		const uint32_t e = scan_nl<G>(p, o, v + 6, n, &nul);
 		return e < n ? e + 1 : n;
 	}
 	return n;
@@ -466,6 +528,7 @@ __device__ __forceinline__ bool family_has(uint32_t family, uint32_t proto)
 // SSHLayer.cpp:18-40,46-56,135-170), appended at index `count`, each kept only if it passes the stop rules
 // (Packet.cpp:134-155; the first that fails is rolled back and ends the chain); stops counting once past cap_layers
 // (every further layer is another SSL record / SSH message: same mask, same DEPTH_OVERFLOW).
+template <int G>
 __device__ uint32_t l7_build(const Pkt& p, uint32_t lf, uint32_t o, uint32_t n, uint32_t dp, uint32_t count, uint32_t ml,
                              uint32_t cap_layers, uint32_t family, uint32_t until_osi, uint32_t& found,
                              uint32_t& stopped, uint64_t& mask, uint2* lay_out)
@@ -490,14 +553,14 @@ __device__ uint32_t l7_build(const Pkt& p, uint32_t lf, uint32_t o, uint32_t n, 
 		const bool req = http_port(dp) && http_request(p, o, n);  // l7_flags' order
 		uint32_t fl;
 		if (req)
-			fl = http_request_line(p, o, n);
+			fl = http_request_line<G>(p, o, n);
 		else
 		{
 			uint32_t nul;
-			const uint32_t e = scan_nl(p, o, 0, n, &nul);
+			const uint32_t e = scan_nl<G>(p, o, 0, n, &nul);
 			fl = e < n ? e + 1 : n;
 		}
-		const uint32_t h = tbp_header_len(p, o, fl, n);
+		const uint32_t h = tbp_header_len<G>(p, o, fl, n);
 		if (emit(req ? P_HTTP_REQ : P_HTTP_RESP, 7, o, h, n) && n > h)
 			emit(P_PAYLOAD, 7, o + h, n - h, n - h);
 	}
@@ -1015,6 +1078,7 @@ struct Walk
 // Packet::parsePacket (Packet.cpp:66-196): first layer by link type (createFirstLayer :827-923), the
 // parseNextLayer chain with the parse-until stop rules (:123-175), and the trailer (:178-195).
 // Layer records go straight to lay_out (uint2 per layer) when it is non-null.
+template <int G = 2>
 __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Params& prm, uint2* lay_out)
 {
 	uint32_t flags = 0;
@@ -1141,7 +1205,7 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 			}
 			// a classified HTTP / SSL / DNS layer: built here with the layers behind it; anything else is the host's
 			if (lf & kL7Built)
-				count = l7_build(p, lf, l7_end - l7_pl, l7_pl, dp, count, ml, cap_layers, prm.family, prm.until_osi,
+				count = l7_build<G>(p, lf, l7_end - l7_pl, l7_pl, dp, count, ml, cap_layers, prm.family, prm.until_osi,
 				                 found, stopped, mask, lay_out);
 			else
 				flags |= lf;
@@ -2286,7 +2350,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		else if (!SkipGeneric)
 		{
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
-			w = walk_chain(p, cap, prm, lay_out);
+			w = walk_chain<Csum ? 2 : 4>(p, cap, prm, lay_out);
 			hashes(p, w, h5, h5d, h2);
 			if (want_csum && w.v4 >= 0)
 			{
