@@ -436,15 +436,18 @@ __device__ __forceinline__ uint32_t find_byte(const Pkt& p, uint32_t o, uint32_t
 	}
 	return n;
 }
-// the first '\n' in payload bytes [a, n) of the payload at o (n if none), 4G bytes per step; *nul: the first NUL before it
+// the first '\n' in payload bytes [a, n) of the payload at o (n if none), 4G bytes per step; *nul: the first NUL before it;
+// *first: the byte at a (a < n; from the first group read, so a caller needs no read of its own)
 template <int G>
-__device__ uint32_t scan_nl(const Pkt& p, uint32_t o, uint32_t a, uint32_t n, uint32_t* nul)
+__device__ uint32_t scan_nl(const Pkt& p, uint32_t o, uint32_t a, uint32_t n, uint32_t* nul, uint32_t* first = nullptr)
 {
 	uint32_t z = n;
 	for (uint32_t j = a; j < n; j += 4 * G)
 	{
 		uint32_t w[G];
 		text_group<G>(p, o, j, n, w);
+		if (first != nullptr && j == a)
+			*first = w[0] & 0xFFu;
 #pragma unroll
 		for (int k = 0; k < G; ++k)
 		{
@@ -463,33 +466,29 @@ __device__ uint32_t scan_nl(const Pkt& p, uint32_t o, uint32_t a, uint32_t n, ui
 	return n;
 }
 // HeaderField size (TextBasedProtocol.cpp:448-461): through the first '\n', else strnlen to the end
+// (*first: the field's first byte, when the field is not empty)
 template <int G>
-__device__ __forceinline__ uint32_t tbp_field(const Pkt& p, uint32_t o, uint32_t a, uint32_t n)
+__device__ __forceinline__ uint32_t tbp_field(const Pkt& p, uint32_t o, uint32_t a, uint32_t n, uint32_t* first)
 {
 	uint32_t nul;
-	const uint32_t e = scan_nl<G>(p, o, a, n, &nul);
+	const uint32_t e = scan_nl<G>(p, o, a, n, &nul, first);
 	return e < n ? e - a + 1 : nul - a;
 }
 // TextBasedProtocolMessage::parseFields + getHeaderLen (TextBasedProtocol.cpp:87-139,436-439)
 template <int G>
 __device__ uint32_t tbp_header_len(const Pkt& p, uint32_t o, uint32_t fl, uint32_t n)
 {
-	uint32_t off = fl, s = tbp_field<G>(p, o, off, n);
-	bool end = s == 0;
-	if (!end)
-	{
-		const uint32_t c = rb(p, o + off);
-		end = c == '\r' || c == '\n';
-	}
+	uint32_t c = 0;
+	uint32_t off = fl, s = tbp_field<G>(p, o, off, n, &c);
+	bool end = s == 0 || c == '\r' || c == '\n';
 	while (!end && off + s < n)
 	{
-		const uint32_t s2 = tbp_field<G>(p, o, off + s, n);
+		const uint32_t s2 = tbp_field<G>(p, o, off + s, n, &c);
 		if (s2 == 0)
 			break;
 		off += s;
 		s = s2;
-		const uint32_t c = rb(p, o + off);
-		end = c == '\r' || c == '\n';
+		end = c == '\r' || c == '\n';  // the new field's first byte
 	}
 	return off + s;
 }
