@@ -86,6 +86,9 @@ cases = {
     "r05s/po-packed": (abi.make_opts(0, 8, False, _ml, layout=PK), -4),
     "r05s/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -4),
     "r05s/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -4),
+    # the kernel of the r05r bench lines (tools/ab/r05r), before the L7 text-walk change
+    "r05r/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -5),
+    "r05r/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -5),
     # the 16-B brief instead of the 32-B summary (ABI 7): same rows
     "tile/packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
     "po/packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),
