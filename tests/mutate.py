@@ -361,6 +361,53 @@ def crafted_l7(seed: int = 13) -> list[bytes]:
     return pk
 
 
+def crafted_http(n: int = 1500, seed: int = 29) -> list[bytes]:
+    """HTTP requests and responses whose first lines and header fields end at every offset of the engine's text-walk
+    groups (2 / 4 payload dwords per read) and far past the LDS window: random URL lengths (with spaces and near-miss
+    "HTTP" strings in them), 0-24 header fields of 0-300 bytes ending in CRLF or LF, a NUL now and then, an end of
+    header or none, a body or none; over Eth/IPv4 and VLAN/IPv6, port 80 both ways. The device's HTTP layer lengths
+    (TextBasedProtocol.cpp:87-139,448-461; HttpLayer.cpp:166-213) against the restatement and the reference."""
+    rng = np.random.default_rng(seed)
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-/._=", dtype=np.uint8)
+
+    def text(k: int) -> bytes:
+        return bytes(letters[rng.integers(0, len(letters), k)])
+
+    pk = []
+    for i in range(n):
+        nl = b"\r\n" if rng.random() < 0.7 else b"\n"
+        if rng.random() < 0.6:
+            url = bytearray(b"/" + text(int(rng.integers(0, 600))))
+            for _ in range(int(rng.integers(0, 3))):  # spaces and near-miss versions inside the URL
+                at = int(rng.integers(0, len(url) + 1))
+                url[at:at] = [b" ", b" HTTP", b" HTTP/", b" HTT", b"HTTP/"][int(rng.integers(0, 5))]
+            ver = [b" HTTP/1.1", b" HTTP/1.0", b" HTTP/1", b" HTTP/", b""][int(rng.choice(5, p=[.6, .2, .08, .06, .06]))]
+            first = [b"GET ", b"POST ", b"HEAD ", b"OPTIONS "][int(rng.integers(0, 4))] + bytes(url) + ver
+            sp, dp = 40000 + i % 1000, 80
+        else:
+            first = b"HTTP/1.1 " + [b"200 OK", b"404 Not Found", b"301 " + text(int(rng.integers(1, 80)))][
+                int(rng.integers(0, 3))]
+            sp, dp = 80, 40000 + i % 1000
+        msg = first + nl
+        for _ in range(int(rng.integers(0, 25))):
+            f = text(int(rng.integers(1, 20))) + b": " + text(int(rng.integers(0, 280)))
+            if rng.random() < 0.03:
+                at = int(rng.integers(0, len(f)))
+                f = f[:at] + b"\0" + f[at:]
+            msg += f + (nl if rng.random() < 0.97 else b"\n")
+        if rng.random() < 0.8:
+            msg += nl  # the end of the header
+            if rng.random() < 0.5:
+                msg += text(int(rng.integers(1, 300)))
+        msg = msg[:1400]
+        l4 = _tcp(sp, dp, msg)
+        if i % 2:
+            pk.append(_eth(0x0800) + _ipv4(6, len(l4)) + l4)
+        else:
+            pk.append(_eth(0x8100) + struct.pack(">HH", 7, 0x86DD) + _ipv6(6, len(l4)) + l4)
+    return pk
+
+
 def crafted_linklayers(seed: int = 23) -> dict[int, list[bytes]]:
     """First layers of the non-Ethernet link types the engine builds, per link type: Linux SLL (113), SLL2 (276)
     and Null/Loopback (0) at and around their length rules, every protocol / family encoding they dispatch on

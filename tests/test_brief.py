@@ -164,3 +164,9 @@ def test_gpu_engine_window_choice():
             hs, hl = eng.parse_host(b, abi.make_opts(0, 8, True, 8))  # the host path follows the same choice
             os_, ol = oracle.oracle_parse(b, abi.make_opts(0, 8, True, 8), threads=8)
             oracle.compare_exact(hs, hl, os_, ol)
+    # parses whose window the caller forces are not sampled: a context that only ran those has decided nothing
+    with Engine(0) as eng:
+        b = synth.config(5, 200_000)
+        for w in (abi.WINDOW_SHORT, abi.WINDOW_DEEP, abi.WINDOW_SHORT):
+            parse_on_device(eng, b, abi.make_opts(0, 8, w == abi.WINDOW_DEEP, 12, w))
+        assert eng.window_choice(True) == abi.WINDOW_DEFAULT and eng.window_choice(False) == abi.WINDOW_DEFAULT

@@ -12,7 +12,7 @@ import pytest
 
 import oracle
 from conftest import golden_files, load_golden
-from mutate import as_batch, crafted, crafted_l7, mutate
+from mutate import as_batch, crafted, crafted_http, crafted_l7, mutate
 from pcapplusplus_amd import abi, synth
 from pcapplusplus_amd.engine import parse_on_device
 from pcapplusplus_amd.pcap import from_packets
@@ -49,6 +49,24 @@ def test_gpu_crafted_deep_stacks(engine, gaps, kernel):
                  abi.make_opts(0, 8, True, 0), abi.make_opts(0, 8, False, 16),
                  abi.make_opts(0, 8, True, 16, abi.WINDOW_DEEP), abi.make_opts(4, 8, True, 16, abi.WINDOW_DEEP)):
         g = run(engine, b, opts, kernel)
+        o = oracle.oracle_parse(b, opts)
+        oracle.compare_exact(g[0], g[1], o[0], o[1])
+        if oracle.ref_available():
+            r = oracle.ref_parse(b, opts)
+            oracle.compare_engine_to_reference(g[0], g[1], r[0], r[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gaps", [False, True])
+def test_gpu_http_text_walks(engine, gaps):
+    """HTTP first lines and header fields ending at every offset of the text-walk groups and far past the LDS window
+    (mutate.crafted_http), through the checksum instance (2-dword groups) and the parse-only ones (4-dword groups, with
+    and without the second gather round): every record equal to the restatement's and the reference Packet++'s."""
+    b = as_batch(crafted_http(), gaps=gaps, seed=31)
+    for opts in (abi.make_opts(0, 8, True, 16), abi.make_opts(0, 8, False, 16),
+                 abi.make_opts(0, 8, False, 16, abi.WINDOW_SHORT), abi.make_opts(0, 8, True, 16, abi.WINDOW_DEEP),
+                 abi.make_opts(0x607, 8, False, 16), abi.make_opts(0, 7, False, 16)):
+        g = run(engine, b, opts, 0)
         o = oracle.oracle_parse(b, opts)
         oracle.compare_exact(g[0], g[1], o[0], o[1])
         if oracle.ref_available():
