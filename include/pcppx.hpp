@@ -1763,14 +1763,7 @@ private:
 	}
 	uint64_t protoMask() const
 	{
-		if (m_Sum != nullptr)
-			return m_Sum->proto_mask;
-		if (!m_MaskKnown)  // brief-backed: the OR of the recorded chain's protocols, once per Packet
-		{
-			m_Mask = pcppx_chain_proto_mask(m_Layers, (unsigned)getRecordedLayerCount());
-			m_MaskKnown = true;
-		}
-		return m_Mask;
+		return m_Sum ? m_Sum->proto_mask : pcppx_chain_proto_mask(m_Layers, (unsigned)getRecordedLayerCount());
 	}
 	/* packet i of a page's / group's records */
 	void bindRecords(const detail::Records* r, uint32_t i)
@@ -1790,7 +1783,6 @@ private:
 	}
 	void bind(RawPacket* raw, bool freeRawPacket, ProtocolTypeFamily parseUntil, OsiModelLayer parseUntilLayer)
 	{
-		m_MaskKnown = false;
 		m_Sum = emptySummary();
 		m_Brief = reinterpret_cast<const pcppx_brief*>(m_Sum);
 		m_MaxLayers = PCPPX_MAX_LAYERS;
@@ -1833,8 +1825,6 @@ private:
 	const uint8_t* m_Raw = nullptr;
 	uint32_t m_Caplen = 0;
 	mutable pcppx_summary m_Full;         // summary() of brief-backed records (assigned whole before any read)
-	mutable uint64_t m_Mask = 0;          // protoMask() of brief-backed records, once computed
-	mutable bool m_MaskKnown = false;
 	std::shared_ptr<RawPacket> m_OwnedRaw;  // freeRawPacket
 };
 using ParsedPacket = Packet;
