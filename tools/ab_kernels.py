@@ -89,6 +89,9 @@ cases = {
     # the kernel of the r05r bench lines (tools/ab/r05r), before the L7 text-walk change
     "r05r/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -5),
     "r05r/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -5),
+    # the final round-5 kernel of the r05zc bench lines (tools/ab/r05f)
+    "r05f/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -6),
+    "r05f/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -6),
     # the 16-B brief instead of the 32-B summary (ABI 7): same rows
     "tile/packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
     "po/packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),
