@@ -2346,13 +2346,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 				w.flags |= PCPPX_F_IP_CSUM | (ipc == ips ? PCPPX_F_IP_CSUM_OK : 0);
 			}
 		}
-	}
-	// the generic walk; in the parse-only instances behind a wave-uniform branch marked cold, so that the compiler lays
-	// it out away from the fast path's code (the checksum instance keeps the plain branch: the uniform one cost it SGPR
-	// and VGPR spills)
-	if (!SkipGeneric && (Csum || __builtin_expect(__ballot(live && !StreamOnly && !GatherOnly && !fast) != 0, 0)))
-	{
-		if (live && !StreamOnly && !GatherOnly && !fast)
+		else if (!SkipGeneric)
 		{
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 			w = walk_chain<Csum ? 2 : 4>(p, cap, prm, lay_out);

@@ -15,6 +15,7 @@ R04_SO = Path(__file__).resolve().parent / "r04" / "libpcppx_r04.so"
 R05S_SO = Path(__file__).resolve().parent / "r05s" / "libpcppx_r05s.so"
 R05R_SO = Path(__file__).resolve().parent / "r05r" / "libpcppx_r05r.so"
 R05F_SO = Path(__file__).resolve().parent / "r05f" / "libpcppx_r05f.so"
+R05X_SO = Path(__file__).resolve().parent / "r05x" / "libpcppx_r05x.so"
 _lib = None
 _r01 = {}
 R01 = -1  # parse_device variant: the round-1 product kernel (tools/ab/r01, rebuilt from git history)
@@ -23,6 +24,7 @@ R04 = -3  # parse_device variant: the round-4 final product kernel (tools/ab/r04
 R05S = -4  # parse_device variant: the round-5 kernel with the window sampling inside the parse (tools/ab/r05s, e4b596f)
 R05R = -5  # parse_device variant: the round-5 kernel of the r05r bench lines, before the L7 text walks (tools/ab/r05r)
 R05F = -6  # parse_device variant: the final round-5 kernel of the r05zc bench lines (tools/ab/r05f)
+R05X = -7  # parse_device variant: the cold-branch experiment, generic walk behind a wave-uniform branch (tools/ab/r05x)
 
 # pcppx_ab_parse_device variants (tools/ab/pcppx_ab.hip)
 LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ, TILE_W5_WIN256, TILE_W1_WIN128, TILE_W1_WIN256, TILE_CACHED = \
@@ -67,8 +69,8 @@ def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, 
                       abi.ptr(layers) if (layers is not None and opts.max_layers) else None, None,
                       abi.ptr(tuples) if tuples is not None else None)
     rec.brief = abi.ptr(brief) if brief is not None else None
-    if variant in (R01, PREV, R04, R05S, R05R, R05F):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
-        abi.check(r01_lib({R01: R01_SO, PREV: PREV_SO, R04: R04_SO, R05S: R05S_SO, R05R: R05R_SO, R05F: R05F_SO}[variant]).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
+    if variant in (R01, PREV, R04, R05S, R05R, R05F, R05X):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
+        abi.check(r01_lib({R01: R01_SO, PREV: PREV_SO, R04: R04_SO, R05S: R05S_SO, R05R: R05R_SO, R05F: R05F_SO, R05X: R05X_SO}[variant]).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
                   "pcppx_r01_parse_device")
         return
     abi.check(lib().pcppx_ab_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0), variant),

@@ -92,6 +92,9 @@ cases = {
     # the final round-5 kernel of the r05zc bench lines (tools/ab/r05f)
     "r05f/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -6),
     "r05f/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -6),
+    # the cold-branch experiment (tools/ab/r05x): the generic walk behind a wave-uniform branch in the parse-only instances
+    "r05x/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -7),
+    "r05x/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -7),
     # the 16-B brief instead of the 32-B summary (ABI 7): same rows
     "tile/packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
     "po/packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),
