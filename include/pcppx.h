@@ -176,7 +176,8 @@ typedef struct pcppx_opts {
  *           layers[sum_{j < i} min(n_layers_j, max_layers) + k]; pcppx_records.layers_written returns the total. The
  *           buffer must hold the total (n * max_layers entries always do; unwritten memory is never touched), and
  *           only the chains cross PCIe (config 3: 4.2 entries = 34 B per packet instead of 8 * max_layers).
- *           max_layers <= PCPPX_MAX_LAYERS. pcppx_parse_batch_host only. */
+ *           max_layers <= PCPPX_MAX_LAYERS. pcppx_parse_batch_host only. Entry positions are 32-bit: a batch with
+ *           n * max_layers > UINT32_MAX is refused with PCPPX_E_INVAL (split it; 268M packets at max_layers 16). */
 #define PCPPX_LAYOUT_DENSE 2
 
 /* The 5-tuple extract (the compact record of the bandwidth runs), 48 bytes per packet: exactly the

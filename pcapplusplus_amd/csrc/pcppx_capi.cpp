@@ -563,7 +563,9 @@ void abandon_slots(pcppx_ctx* c)
 
 // copy a finished chunk's records from pinned memory to the caller's arrays (nothing to copy when the
 // caller's arrays are pinned: the chunk's D2H wrote them directly)
-void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out, bool dense, uint64_t* written)
+// (dense_direct: the DENSE chains were pushed into the caller's array through its device mapping; otherwise they sit in
+// the slot's staging buffer -- a pinned caller array without a device mapping takes this path too)
+void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out, bool dense, bool dense_direct, uint64_t* written)
 {
 	if (dense && s.ml && out->layers)  // the chunk's chains: [batch total up to its end - its own, batch total)
 	{
@@ -577,11 +579,11 @@ void drain(CopyPool& cp, Slot& s, pcppx_records* out, bool direct_out, bool dens
 			cp.copy(out->summary + s.first, s.h_sum, (size_t)s.count * sizeof(pcppx_summary));
 		if (out->brief)
 			cp.copy(out->brief + s.first, s.h_brief, (size_t)s.count * sizeof(pcppx_brief));
-		if (s.ml && out->layers && dense)
-			cp.copy(out->layers + s.dense_first, s.h_lay, (size_t)s.dense_count * sizeof(pcppx_layer));
-		else if (s.ml && out->layers)
+		if (s.ml && out->layers && !dense)
 			cp.copy(out->layers + (size_t)s.first * s.ml, s.h_lay, (size_t)s.count * s.ml * sizeof(pcppx_layer));
 	}
+	if (s.ml && out->layers && dense && !dense_direct)
+		cp.copy(out->layers + s.dense_first, s.h_lay, (size_t)s.dense_count * sizeof(pcppx_layer));
 	if (out->flow_keys)  // the dense hash5 column, from the host copy of the summaries / briefs
 		for (uint32_t k = 0; k < s.count; ++k)
 			out->flow_keys[s.first + k] = out->summary ? out->summary[s.first + k].hash5 : out->brief[s.first + k].hash5;
@@ -603,9 +605,10 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 	// the slot's staging buffer), their positions chained on the device chunk after chunk -- no host round trip to learn
 	// a chunk's count before its copy
 	const uint32_t kTot = pcppx::dense_blocks(kChunkPackets);  // d_dsum[kTot]: the chunk's, [kTot + 1]: cumulative
-	pcppx_layer* lay_map = nullptr;
-	if (dense && direct_out && (lay_map = static_cast<pcppx_layer*>(mapped(r->layers))) == nullptr)
-		return PCPPX_E_HIP;
+	// a page-locked caller array without a device mapping (pinned by another runtime, say) is still filled: its chains
+	// are staged like a pageable array's (the FIXED rows reach such an array by DMA)
+	pcppx_layer* lay_map = dense && direct_out ? static_cast<pcppx_layer*>(mapped(r->layers)) : nullptr;
+	const bool dense_direct = lay_map != nullptr;
 	Slot* prev = nullptr;  // DENSE: the previous chunk (its cumulative count is this chunk's base)
 	uint32_t i = 0, k = 0;
 	while (i < b->n)
@@ -615,7 +618,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(c->copier, s, r, direct_out, dense, &written);
+			drain(c->copier, s, r, direct_out, dense, dense_direct, &written);
 		}
 		size_t pos = 0;
 		const uint8_t* direct = nullptr;
@@ -650,10 +653,10 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		            (!r->brief || ok(hipMemcpyAsync(hb, s.d_brief, cnt * sizeof(pcppx_brief), hipMemcpyDeviceToHost, s.st)));
 		if (dense)
 		{
-			pcppx_layer* to = direct_out ? lay_map : static_cast<pcppx_layer*>(mapped(s.h_lay));
+			pcppx_layer* to = dense_direct ? lay_map : static_cast<pcppx_layer*>(mapped(s.h_lay));
 			good = good && to != nullptr && (prev == nullptr || ok(hipStreamWaitEvent(s.st, prev->parsed, 0))) &&
 			       pcppx::launch_dense_push(s.d_dense, s.d_dsum + kTot, prev ? prev->d_dsum + kTot + 1 : nullptr, to,
-			                                direct_out, s.d_dsum + kTot + 1, s.st) == PCPPX_OK &&
+			                                dense_direct, s.d_dsum + kTot + 1, s.st) == PCPPX_OK &&
 			       ok(hipEventRecord(s.parsed, s.st)) &&
 			       ok(hipMemcpyAsync(s.h_total, s.d_dsum + kTot, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s.st)) &&
 			       ok(hipEventRecord(s.done, s.st));
@@ -678,7 +681,7 @@ int parse_host_run(pcppx_ctx* c, const pcppx_batch* b, const pcppx_opts* o, pcpp
 		{
 			if (!ok(hipEventSynchronize(s.done)))
 				return PCPPX_E_HIP;
-			drain(c->copier, s, r, direct_out, dense, &written);
+			drain(c->copier, s, r, direct_out, dense, dense_direct, &written);
 		}
 	r->layers_written = dense ? written : (rows ? (uint64_t)b->n * ml : 0);
 	return PCPPX_OK;
@@ -918,13 +921,14 @@ extern "C"
 	{
 		if (c == nullptr || b == nullptr || r == nullptr || valid_opts(o) != PCPPX_OK)
 			return PCPPX_E_INVAL;
+		r->layout = o->layout;  // set for an empty batch too: a reused records struct keeps no stale count
+		r->layers_written = 0;
 		if (b->n == 0)
 			return PCPPX_OK;
 		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr || !valid_device_records(o, r))
 			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
-		r->layout = o->layout;
 		r->layers_written = o->max_layers ? (uint64_t)b->n * o->max_layers : 0;
 		return device_parse(c, b, o, r, nullptr, static_cast<hipStream_t>(hip_stream));
 	}
@@ -933,6 +937,8 @@ extern "C"
 	{
 		if (c == nullptr || b == nullptr || r == nullptr || valid_opts(o) != PCPPX_OK)
 			return PCPPX_E_INVAL;
+		r->layout = o->layout;  // set for an empty batch too: a reused records struct keeps no stale count
+		r->layers_written = 0;
 		if (b->n == 0)
 			return PCPPX_OK;
 		if (b->data == nullptr || b->offsets == nullptr || b->caplens == nullptr ||
@@ -941,8 +947,10 @@ extern "C"
 		// device-path-only outputs
 		if (r->tuples != nullptr || r->proto_stats != nullptr || o->layout == PCPPX_LAYOUT_PACKED)
 			return PCPPX_E_INVAL;
-		r->layout = o->layout;
-		r->layers_written = 0;
+		// DENSE positions are 32-bit (the device's running totals, the facade's per-page indexes): a batch whose
+		// n * max_layers could exceed them is refused rather than wrapped
+		if (o->layout == PCPPX_LAYOUT_DENSE && (uint64_t)b->n * o->max_layers > (uint64_t)UINT32_MAX)
+			return PCPPX_E_INVAL;
 		if (!ok(hipSetDevice(c->device)))
 			return PCPPX_E_HIP;
 		int rc = init_host_path(c);

@@ -223,6 +223,51 @@ __device__ __forceinline__ bool sip_key(uint32_t k)
 	return ((kSip.valid >> h) & 1u) && kSip.key[h] == k;
 }
 
+// Round 6: the same trigger sets as register tables for the fast path (ParseShape R6 bit 2). A perfect hash of the port
+// (one 24-bit multiply and a bit-field extract; multipliers found by search, collision-freedom asserted below) picks a
+// slot; the lane holding that slot of a table register hands its entry over by ds_bpermute -- an LDS-crossbar op, no
+// memory round trip per packet. TCP: 64 slots, entry = port | 0x10000. UDP: slots 0-31 of the second register, entry =
+// port | in kUdpL7Ports << 16 | in kUdpL7DstPorts << 17; lanes 32-63 of the same register hold the SIP key slots.
+constexpr uint32_t kTcpSlotMul = 3871678u, kTcpSlotShift = 11, kUdpSlotMul = 12666738u, kUdpSlotShift = 8;
+__host__ __device__ constexpr uint32_t tcp_slot(uint32_t x)
+{
+	return ((x * kTcpSlotMul) >> kTcpSlotShift) & 63u;
+}
+__host__ __device__ constexpr uint32_t udp_slot(uint32_t x)
+{
+	return ((x * kUdpSlotMul) >> kUdpSlotShift) & 31u;
+}
+struct L7Regs
+{
+	uint32_t tcp[64], udp_sip[64];
+	bool perfect;  // every trigger port owns its slot alone
+};
+constexpr L7Regs make_l7_regs()
+{
+	L7Regs t{};
+	t.perfect = true;
+	for (uint16_t x : kTcpL7Ports)
+	{
+		t.perfect = t.perfect && t.tcp[tcp_slot(x)] == 0;
+		t.tcp[tcp_slot(x)] = x | 0x10000u;
+	}
+	auto put = [&](uint16_t x, uint32_t bit) {
+		uint32_t& e = t.udp_sip[udp_slot(x)];
+		t.perfect = t.perfect && (e == 0 || (e & 0xFFFFu) == x);
+		e = x | bit;
+	};
+	for (uint16_t x : kUdpL7Ports)
+		put(x, t.udp_sip[udp_slot(x)] | 0x10000u);
+	for (uint16_t x : kUdpL7DstPorts)
+		put(x, t.udp_sip[udp_slot(x)] | 0x20000u);
+	for (uint32_t k : kSipKeys)
+		t.udp_sip[32 + ((k * kSipMul) >> 27)] = k;
+	return t;
+}
+constexpr L7Regs kL7RegsHost = make_l7_regs();
+static_assert(kL7RegsHost.perfect, "L7 port slot hashes must be collision-free");
+__constant__ L7Regs kL7R = make_l7_regs();
+
 // ---- the first L7 layer behind TCP/UDP (restated in oracle/pcppx_oracle.c: tcp_l7 / udp_l7) ----
 // engine-internal class bits of l7_flags (never in a summary's flags: the layers are built): a MySqlLayer, SSH messages
 constexpr uint32_t kL7MySql = 0x4000u, kL7Ssh = 0x8000u;
@@ -1332,6 +1377,153 @@ __device__ __forceinline__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5
 	tuple_hashes(s, d, na, has_l4, pw, rb(p, ipo + (v4 ? 9 : 6)), h5, h5d, h2);
 }
 
+// ---- the three hashes of a whole wave (round 6, ParseShape R6 bit 1) ----
+// A packet's hash inputs, gathered by whichever walk parsed it: the first IPv4 (else first IPv6) layer's addresses (na
+// dwords each, zero past na: also the 5-tuple extract's address fields), the port layer's raw port dword (pw, whenever a
+// TCP / UDP layer exists), and meta = IP protocol / next-header byte | IPv4 << 8 | IPv6 << 9 | hashed ports << 10 (a port
+// layer, an IP layer and no ICMP, PacketUtils.cpp:141-148) | a port layer << 11.
+struct HashIn
+{
+	uint32_t s[4], d[4], pw, meta;
+};
+__device__ __forceinline__ HashIn hash_in_none()
+{
+	HashIn h;
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+		h.s[k] = h.d[k] = 0;
+	h.pw = h.meta = 0;
+	return h;
+}
+// the inputs hashes() reads, from the LDS window where staged, else HBM (a generic-walk packet)
+__device__ __forceinline__ HashIn hash_in_walk(const Pkt& p, const Walk& w)
+{
+	HashIn h = hash_in_none();
+	const bool v4 = w.v4 >= 0, ip = v4 || w.v6 >= 0;
+	const uint32_t ipo = v4 ? (uint32_t)w.v4 : (uint32_t)w.v6;
+	const uint32_t na = ip ? (v4 ? 1u : 4u) : 0u;
+	const uint32_t so = ipo + (v4 ? 12 : 8), dofs = ipo + (v4 ? 16 : 24);
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+	{
+		h.s[k] = (uint32_t)k < na ? rd32(p, so + 4 * k) : 0u;
+		h.d[k] = (uint32_t)k < na ? rd32(p, dofs + 4 * k) : 0u;
+	}
+	const bool l4 = w.l4i >= 0;
+	const bool has5 = l4 && !(w.mask & (1ull << P_ICMP));
+	h.pw = l4 ? rd32(p, w.l4o) : 0u;
+	h.meta = (ip ? (rb(p, ipo + (v4 ? 9 : 6)) | (v4 ? 0x100u : 0x200u) | (has5 ? 0x400u : 0u)) : 0u) | (l4 ? 0x800u : 0u);
+	return h;
+}
+// hash5Tuple (both directions) and hash2Tuple (PacketUtils.cpp:114-245) of every lane's packet, all 64 lanes together
+// (call with the wave converged). The byte sequences are tuple_hashes': [ports addr_a addr_b proto] and [addr_a addr_b].
+// IPv4 packets hash their 3 x 13 / 8 bytes in their own lanes. An IPv6 packet's chains are 37 / 37 / 32 bytes: run in its
+// own lane they would hold every lane of a mixed wave for them, so each IPv6 chain goes to a lane of its own instead --
+// chain k of the r-th IPv6 packet to slot k * n6 + r (k: 0 hash2Tuple, 1 hash5Tuple direction-unique, 2 hash5Tuple with
+// the pair swapped, needed only when the reference swaps it), 64 slots per round, the inputs and results moved by
+// ds_bpermute. `own`: 64 words of LDS scratch (the rank -> lane map).
+__device__ __forceinline__ void wave_tuple_hashes(const HashIn& x, uint32_t* own, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
+{
+	const uint32_t lane = threadIdx.x & 63u;
+	const bool v4 = x.meta & 0x100u, v6 = x.meta & 0x200u, l4 = x.meta & 0x400u;
+	const uint32_t proto = x.meta & 0xFFu;
+	// the address order: dst <=> src as LE u32 (IPv4) / memcmp(dst, src) (IPv6)
+	int cmp = x.d[0] < x.s[0] ? -1 : (x.d[0] > x.s[0] ? 1 : 0);
+	if (!v4)
+	{
+		cmp = 0;
+#pragma unroll
+		for (int k = 3; k >= 0; --k)
+		{
+			const uint32_t a = __builtin_bswap32(x.d[k]), b = __builtin_bswap32(x.s[k]);
+			cmp = a < b ? -1 : (a > b ? 1 : cmp);
+		}
+	}
+	const bool sw2 = cmp < 0;
+	const uint32_t sp = x.pw & 0xFFFF, dp = x.pw >> 16;  // raw network-order values, LE-loaded
+	const bool swap = dp < sp || (dp == sp && cmp < 0);
+	constexpr uint32_t iv = 2166136261u;
+	h2 = h5 = h5d = 0;
+	if (__ballot(v4))  // uniform
+	{
+		const uint32_t a = sw2 ? x.d[0] : x.s[0], b = sw2 ? x.s[0] : x.d[0];
+		const uint32_t y2 = fnv4(fnv4(iv, a), b);
+		const uint32_t yd = fnv(fnv4(fnv4(fnv4(iv, x.pw), x.s[0]), x.d[0]), proto);
+		uint32_t ys = yd;
+		if (__ballot(v4 && l4 && swap))  // uniform
+		{
+			const uint32_t t = fnv(fnv4(fnv4(fnv4(iv, (x.pw >> 16) | (x.pw << 16)), x.d[0]), x.s[0]), proto);
+			ys = swap ? t : yd;
+		}
+		h2 = v4 ? y2 : 0u;
+		h5d = v4 && l4 ? yd : 0u;
+		h5 = v4 && l4 ? ys : 0u;
+	}
+	const uint64_t m6 = __ballot(v6);
+	if (m6)  // uniform
+	{
+		const uint32_t n6 = (uint32_t)__popcll(m6);
+		const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m6 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m6, 0u));
+		if (v6)
+			own[rank] = lane;
+		__syncthreads();  // one wave per block: orders the map's writes before its reads
+		const uint32_t fl = proto | (sw2 ? 0x100u : 0u);
+		uint32_t r0 = 0, r1 = 0, r2 = 0;
+		for (uint32_t base = 0; base < 3 * n6; base += 64)  // uniform
+		{
+			const uint32_t t = base + lane;
+			const uint32_t k = t >= 2 * n6 ? 2u : (t >= n6 ? 1u : 0u);
+			const uint32_t o = own[(t - k * n6) & 63u];
+			uint32_t S[4], D[4];
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+			{
+				S[j] = __shfl(x.s[j], (int)o, 64);
+				D[j] = __shfl(x.d[j], (int)o, 64);
+			}
+			const uint32_t pw = __shfl(x.pw, (int)o, 64), of = __shfl(fl, (int)o, 64);
+			const bool dfirst = k == 2 || (k == 0 && (of & 0x100u));
+			const uint32_t yp = fnv4(iv, k == 2 ? (pw >> 16) | (pw << 16) : pw);
+			uint32_t y = k ? yp : iv;
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				y = fnv4(y, dfirst ? D[j] : S[j]);
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				y = fnv4(y, dfirst ? S[j] : D[j]);
+			const uint32_t yq = fnv(y, of & 0xFFu);
+			y = k ? yq : y;
+			// each owner takes its chains' results from the slots of this round
+			const uint32_t q0 = rank, q1 = n6 + rank, q2 = 2 * n6 + rank;
+			const uint32_t g0 = __shfl(y, (int)(q0 & 63u), 64), g1 = __shfl(y, (int)(q1 & 63u), 64),
+			               g2 = __shfl(y, (int)(q2 & 63u), 64);
+			r0 = (q0 >= base && q0 < base + 64) ? g0 : r0;
+			r1 = (q1 >= base && q1 < base + 64) ? g1 : r1;
+			r2 = (q2 >= base && q2 < base + 64) ? g2 : r2;
+		}
+		if (v6)
+		{
+			h2 = r0;
+			h5d = l4 ? r1 : 0u;
+			h5 = l4 ? (swap ? r2 : r1) : 0u;
+		}
+	}
+}
+
+// write_tuple from the inputs the hashes used (the same bytes: the fields hash5Tuple reads)
+__device__ __forceinline__ void write_tuple_in(const HashIn& x, const Walk& w, uint32_t h5, pcppx_tuple* out)
+{
+	const bool ip = (x.meta & 0x300u) != 0, l4 = (x.meta & 0x800u) != 0;
+	const uint32_t ports = swap16(x.pw) | (swap16(x.pw >> 16) << 16);  // getSrcPort / getDstPort (host order)
+	const bool has5 = (x.meta & 0x400u) != 0;
+	const uint32_t meta = (ip ? ((x.meta & 0x100u) ? 4u : 6u) : 0u) | ((x.meta & 0xFFu) << 8) |
+	                      ((l4 ? (w.is_tcp ? P_TCP : P_UDP) : 0u) << 16) | ((has5 ? 1u : 0u) << 24);
+	uint4* o = reinterpret_cast<uint4*>(out);
+	o[0] = make_uint4(x.s[0], x.s[1], x.s[2], x.s[3]);
+	o[1] = make_uint4(x.d[0], x.d[1], x.d[2], x.d[3]);
+	o[2] = make_uint4(ports, meta, h5, (w.flags & 0xFFFFu) | ((w.n_layers & 0xFFu) << 16));
+}
+
 // IPv4 header checksum (IPv4Layer.cpp:410-412): computeChecksum over min(IHL*4, dataLen) header bytes
 // with the checksum field zeroed. Returns calc; *stored gets the field.
 __device__ __forceinline__ uint32_t ipv4_checksum(const Pkt& p, const Walk& w, uint32_t* stored)
@@ -1676,6 +1868,35 @@ __device__ __forceinline__ L7Pre fast_l7_pre(const Pkt& p, const Fast& f)
 	return r;
 }
 
+// fast_l7_pre's words from the register tables (kL7R, R6 bit 2): called by every lane of the wave (ds_bpermute reads the
+// table registers of all 64 lanes), `on` for the fast-path packets with a payload behind their TCP / UDP layer. Each
+// word holds only the bit fast_l7 tests (a port's bit of its 32-port group), the SIP slot's key as kSip.key holds it.
+__device__ __forceinline__ L7Pre l7_pre_regs(const Pkt& p, const Fast& f, bool on, uint32_t rt, uint32_t rus)
+{
+	const uint32_t l4o = on ? f.l4o() : 0u;
+	const uint32_t pw = lds_u32(p, l4o);
+	const uint32_t sport = swap16(pw), dport = swap16(pw >> 16);
+	// the SIP heuristic's 4 payload bytes (read only when they lie in the window: fast_walk)
+	const bool sipw = on && !f.tcp() && f.l4dlen() - 8 >= 4;
+	const uint32_t key = __builtin_bswap32(lds_u32(p, sipw ? l4o + 8 : 0u));
+	auto bperm = [](uint32_t reg, uint32_t slot) {
+		return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(slot << 2), (int)reg);
+	};
+	const uint32_t ts = bperm(rt, tcp_slot(sport)), td = bperm(rt, tcp_slot(dport));
+	const uint32_t us = bperm(rus, udp_slot(sport)), ud = bperm(rus, udp_slot(dport));
+	const uint32_t sk = bperm(rus, 32u + ((key * kSipMul) >> 27));
+	const bool tcp = f.tcp() != 0;
+	const bool hs = tcp ? ts == (sport | 0x10000u) : (us & 0x1FFFFu) == (sport | 0x10000u);
+	const bool hd = tcp ? td == (dport | 0x10000u) : (ud & 0x1FFFFu) == (dport | 0x10000u);
+	const bool hu = !tcp && (ud & 0x2FFFFu) == (dport | 0x20000u);
+	L7Pre r;
+	r.ws = on && hs ? 1u << (sport & 31) : 0u;
+	r.wd = on && hd ? 1u << (dport & 31) : 0u;
+	r.wu = on && hu ? 1u << (dport & 31) : 0u;
+	r.sk = sipw ? sk : 0u;
+	return r;
+}
+
 // L7 dispatch of a fast-path packet (same rules as walk_chain's): an L7 payload ends the chain after the
 // L4 layer, with no Payload and no trailer. `pre`: fast_l7_pre's words (the same tests as tcp_l7 / udp_l7 / sip_key)
 __device__ __forceinline__ void fast_l7(const Pkt& p, Fast& f, uint32_t cap, const L7Pre& pre)
@@ -1727,7 +1948,9 @@ __device__ __forceinline__ bool deep_stack(const Pkt& p, uint32_t* et_out, uint3
 		et = vl ? e2 : et;
 		o = vl ? o + 4 : o;
 	}
-	const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 8 <= p.lim ? o + 8 : 0);
+	// the IPv6 next header (byte 6) under o + 8 <= lim, the IPv4 protocol (byte 9) under o + 10 <= lim: never a byte past
+	// the staged window (window_sample_kernel leaves the chunks past a short frame unwritten)
+	const uint32_t ipw = lds_u32(p, o + 8 <= p.lim ? o + 4 : 0), ipv = lds_u32(p, o + 10 <= p.lim ? o + 8 : 0);
 	const uint32_t nh = et == 0x86DD ? (ipw >> 16) & 0xFF : (ipv >> 8) & 0xFF;
 	*et_out = et;
 	*o_out = o;
@@ -1792,6 +2015,27 @@ __device__ __forceinline__ void fast_emit(const Fast& f, uint32_t cap, uint32_t 
 	const uint32_t po = l4 ? f.l4o() + f.l4hdr() : lasto + lasth, pl = l4 ? f.l4dlen() - f.l4hdr() : lastd - lasth;
 	emit(payload != 0, P_PAYLOAD, 7, po, pl, pl);
 	emit(tl != 0, P_TRAILER, 2, lasto + lastd, tl, tl);
+}
+
+// the same inputs of a fast-path packet: every byte in the LDS window
+__device__ __forceinline__ HashIn hash_in_fast(const Pkt& p, const Fast& f, const Walk& w)
+{
+	HashIn h;
+	const bool v4 = w.v4 >= 0;
+	const uint32_t ipo = v4 ? (uint32_t)w.v4 : (uint32_t)w.v6;
+	const uint32_t na = v4 ? 1 : 4;
+	const uint32_t so = ipo + (v4 ? 12 : 8), dofs = ipo + (v4 ? 16 : 24);
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+	{
+		h.s[k] = (uint32_t)k < na ? lds_u32(p, so + 4 * k) : 0u;
+		h.d[k] = (uint32_t)k < na ? lds_u32(p, dofs + 4 * k) : 0u;
+	}
+	const uint32_t proto = (lds_u32(p, ipo + (v4 ? 8 : 4)) >> (v4 ? 8 : 16)) & 0xFF;
+	const bool l4 = f.l4() != 0;  // TCP / UDP only: no ICMP on the fast path
+	h.pw = l4 ? lds_u32(p, f.l4o()) : 0u;
+	h.meta = proto | (v4 ? 0x100u : 0x200u) | (l4 ? 0xC00u : 0u);
+	return h;
 }
 
 // hash5Tuple x2 + hash2Tuple of a fast-path packet (every byte in the LDS window): the first IPv4 (else the first
@@ -1979,6 +2223,21 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 	return x;
 }
 
+// min / max / sum of one value per lane by DPP (row_shr 1/2/4/8 inside 16-lane rows, then the row broadcasts): lane 63
+// ends with the whole wave's, read into an SGPR -- no LDS round trips (the ds_bpermute butterflies of wave_min_u64 & co.
+// wait on LDS at every one of their six steps)
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce_dpp(uint32_t x, uint32_t ident, Op op)
+{
+	x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)x, 0x111, 0xF, 0xF, false));  // row_shr:1
+	x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)x, 0x112, 0xF, 0xF, false));  // row_shr:2
+	x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)x, 0x114, 0xF, 0xF, false));  // row_shr:4
+	x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)x, 0x118, 0xF, 0xF, false));  // row_shr:8
+	x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+	x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+	return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
 {
 	for (int m = 32; m >= 1; m >>= 1)
@@ -2123,15 +2382,19 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     after the hashes instead of before; bit 4: non-temporal span-stream loads (rounds 1-3) instead of default-policy
 //     ones; bit 5:
 //     the IPv6 address dwords hashed under branches instead of selects; records unchanged by bits 3-5)
+//   R6 (round 6, records unchanged by every bit): bit 0 the tile span from 32-bit DPP reductions (wave_reduce_dpp)
+//     instead of 64-bit ds_bpermute butterflies; bit 1 the three hashes taken by the whole wave after both walks
+//     (wave_tuple_hashes: IPv4 packets in their own lanes, IPv6 packets' chains spread over the wave's lanes); bit 2 the
+//     L7 trigger ports looked up in register tables by ds_bpermute (l7_pre_regs) instead of constant-memory bitmaps
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
-          int kSkip = 0>
+          int kSkip = 0, int kR6 = 7>
 struct ParseShape
 {
 	static constexpr bool NT = kNT, FillTails = kFillTails, TightR2 = kTightR2, Realign = kRealign, EarlyB = kEarlyB;
 	static constexpr bool StreamOnly = kStreamOnly, MarkFast = kMarkFast, GatherOnly = kGatherOnly,
 	                      SkipGeneric = kSkipGeneric;
-	static constexpr int Skip = kSkip;
+	static constexpr int Skip = kSkip, R6 = kR6;
 };
 
 // One wave = one 64-packet tile. MinWaves: __launch_bounds__ minimum waves per SIMD (1 = the compiler's choice).
@@ -2173,14 +2436,52 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	bool empty = true;
 	const uint32_t bad = in ? desc_flags(off, cap, prm.data_len, &empty) : 0;
 	const bool live = in && !bad && !empty;
+	// R6 bit 2: this lane's slots of the L7 register tables (one coalesced 256-B read each, issued with the descriptors)
+	uint32_t l7_rt = 0, l7_rus = 0;
+	if ((S::R6 & 4) && !S::StreamOnly && !S::GatherOnly)
+	{
+		l7_rt = kL7R.tcp[lane];
+		l7_rus = kL7R.udp_sip[lane];
+	}
 
 	// ---- tile span for the L4 checksum stream: whole packets, known before the parse, so the first
 	// stream window is issued now and lands while the headers are gathered and parsed ----
 	const uint64_t pkt_addr = (uint64_t)(uintptr_t)prm.data + off;
 	// wave reductions are uniform: moved to SGPRs so the window loop is a scalar loop
-	const uint64_t smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
-	const uint64_t emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
-	const uint64_t wire = uniform_u64(wave_sum_u64(live ? cap : 0));
+	uint64_t smin, emax, wire;
+	if (S::R6 & 1)
+	{
+		// round 6: 32-bit DPP reductions of each packet's span against one live packet's address (wave-uniform), and
+		// of the caplens (<= 65535 each: the tile's sum fits 32 bits). A span that is not within +-2 GiB of that base
+		// cannot stream anyway (emax - smin <= 2 * wire + 64 KiB), so such a tile only skips the reductions.
+		const uint64_t lm = __ballot(live);
+		smin = ~0ull;
+		emax = wire = 0;
+		if (want_csum && lm)  // uniform
+		{
+			const int first = __builtin_ctzll(lm);
+			const uint64_t base = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pkt_addr >> 32), first) << 32) |
+			                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pkt_addr, first)) & ~15ull;
+			const int64_t d0 = (int64_t)((pkt_addr & ~15ull) - base), d1 = (int64_t)(((pkt_addr + cap + 15) & ~15ull) - base);
+			const bool far = live && (d0 < INT32_MIN || d0 > INT32_MAX || d1 < INT32_MIN || d1 > INT32_MAX);
+			if (!__ballot(far))  // uniform
+			{
+				const int32_t lo = (int32_t)wave_reduce_dpp(live ? (uint32_t)(int32_t)d0 : (uint32_t)INT32_MAX, (uint32_t)INT32_MAX,
+				                                            [](uint32_t a, uint32_t b) { return (int32_t)a < (int32_t)b ? a : b; });
+				const int32_t hi = (int32_t)wave_reduce_dpp(live ? (uint32_t)(int32_t)d1 : (uint32_t)INT32_MIN, (uint32_t)INT32_MIN,
+				                                            [](uint32_t a, uint32_t b) { return (int32_t)a > (int32_t)b ? a : b; });
+				smin = base + (uint64_t)(int64_t)lo;
+				emax = base + (uint64_t)(int64_t)hi;
+				wire = wave_reduce_dpp(live ? cap : 0u, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+			}
+		}
+	}
+	else
+	{
+		smin = uniform_u64(wave_min_u64(live ? (pkt_addr & ~15ull) : ~0ull));
+		emax = uniform_u64(wave_max_u64(live ? ((pkt_addr + cap + 15) & ~15ull) : 0ull));
+		wire = uniform_u64(wave_sum_u64(live ? cap : 0));
+	}
 	const bool stream = want_csum && emax > smin && emax - smin <= 2 * wire + 65536;  // uniform
 	const uint32_t nchunks = stream ? (uint32_t)((emax - smin) >> 4) : 0;
 	uint4 va[SWin / 64], vb[SWin / 64];
@@ -2297,8 +2598,14 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			set_lim();
 		}
 	}
-	Fast f;
+	Fast f{};
 	bool fast = live && !StreamOnly && !GatherOnly && fast_walk(p, cap, prm, f);
+	constexpr bool kL7Regs = (S::R6 & 4) && !StreamOnly && !GatherOnly && !(S::Skip & 8);
+	constexpr bool kWaveHash = (S::R6 & 2) && !StreamOnly && !GatherOnly && !(S::Skip & 1);
+	// R6 bit 2: the fast path's L7 trigger words from the register tables, by the whole wave (converged here)
+	L7Pre pre_r{ 0u, 0u, 0u, 0u };
+	if (kL7Regs && __ballot(fast))  // uniform
+		pre_r = l7_pre_regs(p, f, fast && f.payload() && f.l4(), l7_rt, l7_rus);
 
 	// ---- (3) chain walk, hashes, IPv4 checksum: fast path, else the generic walk ----
 	const uint32_t ml = prm.max_layers;
@@ -2325,8 +2632,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		if (fast)
 		{
 			// the L7 table reads first: their latency hides behind the hashes
-			L7Pre pre = (S::Skip & 8) ? L7Pre{ 0u, 0u, 0u, 0u } : fast_l7_pre(p, f);
-			if (!(S::Skip & 1))
+			L7Pre pre = kL7Regs ? pre_r : ((S::Skip & 8) ? L7Pre{ 0u, 0u, 0u, 0u } : fast_l7_pre(p, f));
+			if (!(S::Skip & 1) && !kWaveHash)
 				fast_hashes<(S::Skip & 32) != 0>(p, f, fast_to_walk(f, ml), h5, h5d, h2);
 			if (S::Skip & 8)  // diagnostic: the round-3 order (table reads after the hashes)
 				pre = fast_l7_pre(p, f);
@@ -2350,7 +2657,8 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		{
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 			w = walk_chain<Csum ? 2 : 4>(p, cap, prm, lay_out);
-			hashes(p, w, h5, h5d, h2);
+			if (!kWaveHash)
+				hashes(p, w, h5, h5d, h2);
 			if (want_csum && w.v4 >= 0)
 			{
 				ipc = ipv4_checksum(p, w, &ips);
@@ -2446,6 +2754,18 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 		}
 	}
 
+	// R6 bit 1: the hashes of the whole wave, after the span stream (its two register windows are dead here), from inputs
+	// read out of the LDS window (intact until the layer rows below) or, past it, from HBM
+	HashIn hin = hash_in_none();
+	if (kWaveHash)
+	{
+		if (live && fast)
+			hin = hash_in_fast(p, f, w);
+		else if (live && !SkipGeneric)
+			hin = hash_in_walk(p, w);
+		wave_tuple_hashes(hin, m_nch, h5, h5d, h2);
+	}
+
 	if (in && NT && prm.summary != nullptr)
 	{
 		const uint32_t l4b = w.l4i >= 0 ? (uint32_t)w.l4i : 0xFFu;
@@ -2470,7 +2790,12 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 	if (in && prm.flow_keys != nullptr)
 		__builtin_nontemporal_store(h5, prm.flow_keys + i);
 	if (in && prm.tuples != nullptr)  // the LDS window is still intact here (the rows below reuse it)
-		write_tuple(p, w, h5, prm.tuples + i);
+	{
+		if (kWaveHash)
+			write_tuple_in(hin, w, h5, prm.tuples + i);
+		else
+			write_tuple(p, w, h5, prm.tuples + i);
+	}
 	if (prm.wave_stats != nullptr)  // uniform
 		wave_proto_stats(in, w.mask, w.flags, prm.wave_stats + blockIdx.x);
 	// ---- (5) layer records of fast-path packets: rows built in LDS, written with coalesced stores (whole rows,

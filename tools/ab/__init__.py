@@ -9,22 +9,10 @@ from pathlib import Path
 from pcapplusplus_amd import abi
 
 AB_SO = Path(__file__).resolve().parent / "libpcppx_ab.so"
-R01_SO = Path(__file__).resolve().parent / "r01" / "libpcppx_r01.so"
-PREV_SO = Path(__file__).resolve().parent / "prev" / "libpcppx_prev.so"
-R04_SO = Path(__file__).resolve().parent / "r04" / "libpcppx_r04.so"
-R05S_SO = Path(__file__).resolve().parent / "r05s" / "libpcppx_r05s.so"
-R05R_SO = Path(__file__).resolve().parent / "r05r" / "libpcppx_r05r.so"
-R05F_SO = Path(__file__).resolve().parent / "r05f" / "libpcppx_r05f.so"
-R05X_SO = Path(__file__).resolve().parent / "r05x" / "libpcppx_r05x.so"
+BASE_SO = Path(__file__).resolve().parent / "base" / "libpcppx_base.so"
 _lib = None
 _r01 = {}
-R01 = -1  # parse_device variant: the round-1 product kernel (tools/ab/r01, rebuilt from git history)
-PREV = -2  # parse_device variant: the r02m product kernel before device-built L7 / ICMP / tunnels (tools/ab/prev)
-R04 = -3  # parse_device variant: the round-4 final product kernel (tools/ab/r04, commit b2a062a)
-R05S = -4  # parse_device variant: the round-5 kernel with the window sampling inside the parse (tools/ab/r05s, e4b596f)
-R05R = -5  # parse_device variant: the round-5 kernel of the r05r bench lines, before the L7 text walks (tools/ab/r05r)
-R05F = -6  # parse_device variant: the final round-5 kernel of the r05zc bench lines (tools/ab/r05f)
-R05X = -7  # parse_device variant: the cold-branch experiment, generic walk behind a wave-uniform branch (tools/ab/r05x)
+BASE = -1  # parse_device variant: the final round-5 product kernel (tools/ab/base, commit afaa594, rebuilt from git)
 
 # pcppx_ab_parse_device variants (tools/ab/pcppx_ab.hip)
 LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ, TILE_W5_WIN256, TILE_W1_WIN128, TILE_W1_WIN256, TILE_CACHED = \
@@ -49,8 +37,8 @@ def lib() -> C.CDLL:
     return _lib
 
 
-def r01_lib(so: Path = R01_SO) -> C.CDLL:
-    """a product kernel rebuilt from git history (round 1, or tools/ab/prev's revision)"""
+def r01_lib(so: Path = BASE_SO) -> C.CDLL:
+    """a product kernel rebuilt from git history (tools/ab/base)"""
     if so not in _r01:
         if not so.exists():
             raise RuntimeError(f"{so} missing: run `make -C {so.parent}`")
@@ -63,14 +51,16 @@ def r01_lib(so: Path = R01_SO) -> C.CDLL:
 
 
 def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, summary, layers, stream: int,
-                 variant: int, tuples=None, brief=None) -> None:
+                 variant: int, tuples=None, brief=None, flow_keys=None) -> None:
     b = abi.Batch(abi.ptr(data), abi.ptr(offsets), abi.ptr(caplens), int(data.numel()), n, linktype, 0)
     rec = abi.Records(abi.ptr(summary) if summary is not None else None,
                       abi.ptr(layers) if (layers is not None and opts.max_layers) else None, None,
                       abi.ptr(tuples) if tuples is not None else None)
     rec.brief = abi.ptr(brief) if brief is not None else None
-    if variant in (R01, PREV, R04, R05S, R05R, R05F, R05X):  # same opts layout: the round-1 `variant` byte is today's reserved byte (0 = its product)
-        abi.check(r01_lib({R01: R01_SO, PREV: PREV_SO, R04: R04_SO, R05S: R05S_SO, R05R: R05R_SO, R05F: R05F_SO, R05X: R05X_SO}[variant]).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
+    if flow_keys is not None:
+        rec.flow_keys = abi.ptr(flow_keys)
+    if variant == BASE:  # same opts / records layout (ABI 7)
+        abi.check(r01_lib().pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
                   "pcppx_r01_parse_device")
         return
     abi.check(lib().pcppx_ab_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0), variant),

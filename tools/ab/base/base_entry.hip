@@ -1,4 +1,4 @@
-// TOOLS ONLY: the C entry point of the round-1 parse kernel (built from git history by tools/ab/r01/Makefile).
+// TOOLS ONLY: the C entry point of a product parse kernel rebuilt from git history (tools/ab/base/Makefile).
 #include "pcppx.h"
 #include "pcppx_internal.h"
 

@@ -325,6 +325,24 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 82: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, false, 10>), grid, dim3(kTile), 0, stream, prm); break;
 	// two rounds 128 B (96 + 32)
 	case 83: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 8, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
+	// round 6: the three instances under each combination of the ParseShape R6 switches (bit 0 DPP span reductions, bit 1
+	// wave-wide hashes, bit 2 L7 register tables): 200 + R6 the checksum instance, 210 + R6 the two-round parse-only
+	// instance, 220 + R6 the SHORT parse-only instance
+#define PCPPX_AB_SHAPE(r) ParseShape<true, true, true, true, true, false, false, false, false, 0, r>
+#define PCPPX_AB_R6(base, W, SW, C, CS, C1)                                                                                \
+	case base + 0: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(0)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 1: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(1)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 2: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(2)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 3: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(3)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 4: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(4)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 5: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(5)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 6: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(6)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 7: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(7)>), grid, dim3(kTile), 0, stream, prm); break;
+	PCPPX_AB_R6(200, 5, 128, 6, true, 6)
+	PCPPX_AB_R6(210, 1, 64, 9, false, 6)
+	PCPPX_AB_R6(220, 1, 64, 6, false, 6)
+#undef PCPPX_AB_SHAPE
+#undef PCPPX_AB_R6
 	default: return launch_parse(b, o, r, stream);
 	}
 	return check_launch("pcppx_ab_parse_device", stream);

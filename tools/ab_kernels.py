@@ -36,7 +36,6 @@ cases = {
     "tile/deepwin-earlyB": (abi.make_opts(0, 8, True, 8, abi.WINDOW_DEEP), 70),
     "tile/skip-generic": (abi.make_opts(0, 8, True, 8), 52),
     "lane/ml8/csum": (abi.make_opts(0, 8, True, 8), 1),
-    "r01/ml8/csum": (abi.make_opts(0, 8, True, 8), -1),
     "tile/stream-only": (abi.make_opts(0, 8, True, 0), 2),
     "diag/tile-read": (abi.make_opts(0, 8, True, 0), 3),
     "diag/grid-read": (abi.make_opts(0, 8, True, 0), 4),
@@ -78,23 +77,10 @@ cases = {
     "po/packed-no-l7": (abi.make_opts(0, 8, False, _ml, layout=PK), 91),
     "po/packed-no-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 92),
     "po/packed-no-hash-l7-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 93),
-    # the round-4 final product kernel (tools/ab/r04): round-5 changes against it in one process
-    "r04/tile-packed": (abi.make_opts(0, 8, True, 8, layout=PK), -3),
-    "r04/po-packed": (abi.make_opts(0, 8, False, _ml, layout=PK), -3),
-    # the round-5 kernel with the window sampling inside the parse (tools/ab/r05s): today's samples in its own kernel
-    "r05s/tile-packed": (abi.make_opts(0, 8, True, 8, layout=PK), -4),
-    "r05s/po-packed": (abi.make_opts(0, 8, False, _ml, layout=PK), -4),
-    "r05s/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -4),
-    "r05s/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -4),
-    # the kernel of the r05r bench lines (tools/ab/r05r), before the L7 text-walk change
-    "r05r/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -5),
-    "r05r/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -5),
-    # the final round-5 kernel of the r05zc bench lines (tools/ab/r05f)
-    "r05f/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -6),
-    "r05f/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -6),
-    # the cold-branch experiment (tools/ab/r05x): the generic walk behind a wave-uniform branch in the parse-only instances
-    "r05x/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -7),
-    "r05x/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -7),
+    # the final round-5 product kernel (tools/ab/base): round-6 changes against it in one process
+    "base/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -1),
+    "base/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -1),
+    "base/po-short+tuples": (abi.make_opts(0, 8, False, 0, abi.WINDOW_SHORT), -1),
     # the 16-B brief instead of the 32-B summary (ABI 7): same rows
     "tile/packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
     "po/packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), 0),

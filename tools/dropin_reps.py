@@ -1,4 +1,4 @@
-"""Per-run time of the drop-in benchmark (today's examples/bin/benchmark and round 4's tools/ab/r04/benchmark_r04) on
+"""Per-run time of the drop-in benchmark (examples/bin/benchmark) on
 the reference's example.pcap at several repetition counts in one process each (GPU box, repo root): a per-run cost
 that grows with the run count points at state accumulating across runs.
 
@@ -27,7 +27,7 @@ def main() -> None:
     ex, _ = load_golden(GOLDEN / "capture_example.npz")
     f = Path("/dev/shm") / f"pcppx_reps_{os.getpid()}.pcap"
     write_pcap(f, ex)
-    progs = {"engine": ROOT / "examples" / "bin" / "benchmark", "engine_r04": ROOT / "tools" / "ab" / "r04" / "benchmark_r04",
+    progs = {"engine": ROOT / "examples" / "bin" / "benchmark",
              "reference": ROOT / "oracle" / "_ref" / "benchmark_ref"}
     try:
         for trial in range(2):

@@ -46,9 +46,7 @@ def bench_pair(pcap: Path, reps: tuple[int, int], n: int, trials: int = 1) -> di
     measurements can land in a busy second)."""
     out = {"packets": n, "pcap_bytes": pcap.stat().st_size}
     progs = [(name, exe) for name, exe in (("reference_benchmark", ROOT / "oracle" / "_ref" / "benchmark_ref"),
-                                           ("engine_benchmark", ROOT / "examples" / "bin" / "benchmark"),
-                                           # the round-4 drop-in (facade + library of commit b2a062a, tools only)
-                                           ("engine_r04_benchmark", ROOT / "tools" / "ab" / "r04" / "benchmark_r04"))
+                                           ("engine_benchmark", ROOT / "examples" / "bin" / "benchmark"))
              if exe.exists()]
     per = {name: [] for name, _ in progs}
     inproc = {name: [] for name, _ in progs}

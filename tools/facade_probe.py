@@ -5,8 +5,7 @@ goes next to the reference benchmark's.
 
   python tools/facade_probe.py [reps] [trials] [imix packets]
 
-With tools/ab/r04/facade_check_r04 built (round 4's facade and library), both run, alternating trial by trial; each
-phase is the median over the trials.
+Each phase is the median over the trials.
 """
 from __future__ import annotations
 
@@ -30,10 +29,7 @@ def main() -> None:
     big = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # > 0: also config 3's IMIX pcap of that many packets
     from conftest import GOLDEN, load_golden
 
-    # today's facade, and round 4's (tools/ab/r04/facade_check_r04, commit b2a062a) where built: alternating trials
-    progs = [(name, exe) for name, exe in (("engine", ROOT / "examples" / "bin" / "facade_check"),
-                                           ("engine_r04", ROOT / "tools" / "ab" / "r04" / "facade_check_r04"))
-             if exe.exists()]
+    progs = [(name, exe) for name, exe in (("engine", ROOT / "examples" / "bin" / "facade_check"),) if exe.exists()]
     ex, _ = load_golden(GOLDEN / "capture_example.npz")
     files = {"example.pcap": (ex, reps), "config1": (synth.config(1), reps)}
     if big:

@@ -17,6 +17,8 @@
 #                                  SQ_BUSY_CYCLES -> <tag>_transient.json, <tag>_transient_pmc/, <tag>_transient.txt
 #   ab:<cfg>:<cases>               interleaved A/B of tools/ab_kernels.py cases (comma list) on config <cfg> (3s64: config 3
 #                                  at 64 B), 10M packets, 12 rounds -> <tag>_ab_cfg<cfg>.txt
+#   ab6:<cfg>:<variants>           interleaved A/B of tools/ab_r06.py variants (-1 the round-5 kernel, 0 the product,
+#                                  200+/210+/220+ R6 combinations) on bench.py's launch of <cfg> -> <tag>_ab6_cfg<cfg>.txt
 #   cmd:<shell command>            anything else, under a 600 s limit
 set -o pipefail
 TAG=$1
@@ -110,6 +112,11 @@ for step in "$@"; do
       AB_SIZES=$sz AB_ML=${AB_ML:-12} AB_CASES="$cases" timeout -k 10 400 python -u tools/ab_kernels.py 10000000 ${AB_ROUNDS:-12} "$cf" \
         > "$OUT/${TAG}_ab_cfg$c.txt" 2>&1 || { tail -20 "$OUT/${TAG}_ab_cfg$c.txt"; exit 11; }
       grep -E "median|identical" "$OUT/${TAG}_ab_cfg$c.txt" ;;
+    ab6)  # round 6: interleaved A/B of tools/ab_r06.py variants on bench.py's own launch of config <cfg>
+      c=${arg%%:*}; vs=${arg#*:}
+      timeout -k 10 400 python -u tools/ab_r06.py "$c" "" ${AB_ROUNDS:-20} "$vs" \
+        > "$OUT/${TAG}_ab6_cfg$c.txt" 2>&1 || { tail -20 "$OUT/${TAG}_ab6_cfg$c.txt"; exit 12; }
+      grep -E "median|identical" "$OUT/${TAG}_ab6_cfg$c.txt" ;;
     cmd)
       timeout -k 10 600 bash -c "$arg" || exit 8 ;;
     *)
