@@ -106,35 +106,41 @@ def test_bench_small_run_checks_its_records(cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [4, 3])
-def test_bench_two_ranks_self_launch(cfg, tmp_path):
-    """`bench.py --gpus 2` through its own launch (a child torch.distributed.run, two ranks over gloo sharing the
-    box's one card: a code-path check of the N>1 path, not a scaling number): one line from rank 0 with n_gpus 2 and
-    both ranks' times; config 4 merges the two ranks' flow tables exactly with every packet conserved and sums both
-    ranks' collectStats; the line carries rank 0's CPU baseline (measured after the timed region)."""
+@pytest.mark.parametrize("ranks,cfg", [(2, 4), (2, 3), (8, 4), (8, 3)], ids=["n2-cfg4", "n2-cfg3", "n8-cfg4", "n8-cfg3"])
+def test_bench_ranks_self_launch(ranks, cfg, tmp_path):
+    """`bench.py --gpus N` through its own launch (a child torch.distributed.run, N ranks over gloo sharing the box's
+    one card: a code-path check of the N>1 path -- the shard ranges, seeds and the host merge of N tables the driver's
+    8-GPU run uses -- not a scaling number): one line from rank 0 with n_gpus N and every rank's times; config 4 merges
+    the N ranks' flow tables exactly with every packet conserved and sums their collectStats, and the merged table
+    equals a single-pass host group-by of the restatement's hash5Tuple over the stream's first N shards; the line
+    carries rank 0's CPU baseline (measured after the timed region)."""
     import json
 
+    npk = 200_000 if ranks == 2 else 100_000
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     dump = tmp_path / "flows.npz"
-    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--config",
-                        str(cfg), "--packets", "200000", "--steps", "3", "--warmup", "1", "--no-e2e", "--no-traffic",
-                        "--cpu-sample", "20000", "--cpu-seconds", "0.5", "--dump-flows", str(dump)],
-                       capture_output=True, text=True, timeout=400, env=env)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(ranks), "--dist-backend", "gloo",
+                        "--config", str(cfg), "--packets", str(npk), "--steps", "3", "--warmup", "1", "--no-e2e",
+                        "--no-traffic", "--cpu-sample", "20000", "--cpu-seconds", "0.5", "--dump-flows", str(dump)],
+                       capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     c = line["config"]
-    assert line["n_gpus"] == 2 and c["ranks"] == 2 and c["dist_backend"] == "gloo"
-    assert len(c["per_rank_kernel_ms"]) == 2 and all(t > 0 for t in c["per_rank_kernel_ms"])
+    assert line["n_gpus"] == ranks and c["ranks"] == ranks and c["dist_backend"] == "gloo"
+    assert c["parallelism"] == f"shard{ranks} (no collective)"
+    assert len(c["per_rank_kernel_ms"]) == ranks and all(t > 0 for t in c["per_rank_kernel_ms"])
+    assert len(c["per_rank_wall_ms_per_step"]) == ranks
     assert line["value"] > 0 and c["flagged_packets"] == 0
     assert line["cpu_baseline"] is not None and line["cpu_baseline"]["value"] > 0
     if cfg == 4:
         ft = c["flow_table"]
-        assert ft["ranks_merged"] == 2 and ft["exact"] and ft["conserved"]
-        assert ft["packets_counted"] == ft["expected"] == 2 * 200000 * 4
-        assert ft["merged_within_universe"] and ft["flows_spanning_ranks"] > 1000
+        assert ft["ranks_merged"] == ranks and ft["exact"] and ft["conserved"]
+        assert ft["packets_counted"] == ft["expected"] == ranks * npk * 4
+        assert ft["merged_within_universe"] and ft["flows_spanning_ranks"] > 0
+        assert len(ft["per_rank_flows"]) == ranks
         cs = c["collect_stats"]
-        assert cs["consistent"] and cs["ranks_merged"] == 2 and cs["packet_count"] == 2 * 200000
-        # the merged table equals a single-pass map over the union of the two shards (the stream's first 400k
+        assert cs["consistent"] and cs["ranks_merged"] == ranks and cs["packet_count"] == ranks * npk
+        # the merged table equals a single-pass map over the union of the N shards (the stream's first N * npk
         # packets), key for key: the restatement's hash5Tuple grouped on the host, times the 4 launches per rank
         import numpy as np
 
@@ -142,7 +148,7 @@ def test_bench_two_ranks_self_launch(cfg, tmp_path):
         from pcapplusplus_amd import abi, shard, synth
 
         m = np.load(dump)
-        whole = synth.flow_stream(0, 400_000, 4, flows=bench.CONFIG4_FLOWS)
+        whole = synth.flow_stream(0, ranks * npk, 4, flows=bench.CONFIG4_FLOWS)
         s, _ = oracle.oracle_parse(whole, abi.make_opts(0, 8, False, 0), threads=8)
         want = shard.flow_table(s["hash5"], whole.caplens)
         launches = int(m["launches"][0])

@@ -528,26 +528,28 @@ def test_gpu_deep_window_with_checksums(engine):
             oracle.compare_exact(gs, gl, os_, ol)
 
 
-def test_gpu_config4_full_size_flow_table(engine):
-    """BASELINE config 4 at its full per-GPU size through bench.py's own path: 12.5M IMIX packets with Zipf(1.1)
-    5-tuples over 1M flows (rank 0's shard), a parse writing the summary and the dense hash5 column, then three
-    pcppx_flow_count_keys_device calls into one 2M-slot table (three bench steps). Every flow's {packets, bytes}
-    equals three times a host group-by of the device keys, key 0 goes to the stats counters, nothing is lost; the
-    keys themselves equal the restatement's hash5Tuple on every packet."""
+@pytest.mark.parametrize("shard_range", [(0, 12_500_000), (87_500_000, 100_000_000)], ids=["rank0of8", "rank7of8"])
+def test_gpu_config4_full_size_flow_table(engine, shard_range):
+    """BASELINE config 4 at its full per-GPU size on bench.py's own stream and launch: packets [lo, hi) of the one
+    config-4 stream (synth.flow_stream, seed 4, 1M flows: bench.py's rank 0 of any N, and rank 7 of 8), parsed as
+    bench.py parses them (the SHORT parse-only window, no layer records, the dense hash5 column and the collectStats
+    counters), then three pcppx_flow_count_keys_device calls into one 2M-slot table (three bench steps). Every flow's
+    {packets, bytes} equals three times a host group-by of the device keys, key 0 goes to the stats counters, nothing
+    is lost; the keys equal the restatement's hash5Tuple on every packet, and the collectStats counters its own."""
     import torch
 
-    from pcapplusplus_amd import shard
     from pcapplusplus_amd.engine import to_device
 
-    n = 12_500_000
-    b = synth.imix(n, shard.shard_seed(4, 0), flows=1_000_000, corrupt_frac=0.0)
+    lo, hi = shard_range
+    n = hi - lo
+    b = synth.flow_stream(lo, hi, 4, flows=1_000_000)
     dev = "cuda:0"
     data, offs, caps = to_device(b, dev)
     st = torch.cuda.current_stream().cuda_stream
-    summ = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     fk = torch.empty(n, dtype=torch.int32, device=dev)
-    opts = abi.make_opts(0, 8, False, 0)
-    engine.parse_device(data, offs, caps, n, b.linktype, opts, summ, None, st, fk)
+    ps = torch.zeros(abi.PROTO_STATS, dtype=torch.int64, device=dev)
+    opts = abi.make_opts(0, 8, False, 0, abi.WINDOW_SHORT)
+    engine.parse_device(data, offs, caps, n, b.linktype, opts, None, None, st, fk, None, ps)
     cap = 1 << 21
     keys = torch.zeros(cap, dtype=torch.int32, device=dev)
     pk = torch.zeros(cap, dtype=torch.int64, device=dev)
@@ -560,16 +562,18 @@ def test_gpu_config4_full_size_flow_table(engine):
     used = k != 0
     got = dict(zip(k[used].tolist(), zip(pk.cpu().numpy()[used].tolist(), by.cpu().numpy()[used].tolist())))
     hk = fk.cpu().numpy().view(np.uint32)
-    del data, offs, caps, summ, fk, keys, pk, by
+    pstats = ps.cpu().numpy()
+    del data, offs, caps, fk, keys, pk, by, ps
     uk, inv = np.unique(hk, return_inverse=True)
     cnt = np.bincount(inv)
     byt = np.bincount(inv, weights=b.caplens.astype(np.float64)).astype(np.int64)
     want = {int(x): (3 * int(c), 3 * int(y)) for x, c, y in zip(uk.tolist(), cnt.tolist(), byt.tolist()) if x != 0}
     z = int(cnt[0]) if uk[0] == 0 else 0
     zb = int(byt[0]) if uk[0] == 0 else 0
-    assert len(want) > 500_000
+    assert len(want) > 400_000
     assert got == want
     s = stt.cpu().numpy()
     assert (int(s[0]), int(s[1]), int(s[2])) == (3 * z, 3 * zb, 0)
-    o = oracle.oracle_parse(b, opts, threads=16)
+    o = oracle.oracle_parse(b, abi.make_opts(0, 8, False, 0), threads=16)
     assert np.array_equal(hk, o[0]["hash5"])
+    assert {f: int(pstats[k]) for k, f in enumerate(abi.PROTO_STATS_FIELDS)} == oracle.proto_stats(o[0])

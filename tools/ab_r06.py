@@ -89,17 +89,21 @@ for v in variants:
         if not same:
             raise SystemExit(f"variant {v}: records differ")
 del ref
+# short kernels (config 2: ~30 us) are timed as `reps` back-to-back launches per sample, so that launch gaps and the
+# clock's response to one short burst do not decide the comparison
+reps = max(1, int(2_000_000 // n))
 times = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        launch(v)
+        for _ in range(reps):
+            launch(v)
         e1.record(st)
         torch.cuda.synchronize()
         if r > 0:
-            times[v].append(e0.elapsed_time(e1))
-print(f"config {cfg_arg}: {n} packets, {rounds - 1} interleaved rounds, records {kind}", flush=True)
+            times[v].append(e0.elapsed_time(e1) / reps)
+print(f"config {cfg_arg}: {n} packets, {rounds - 1} interleaved rounds of {reps} launches, records {kind}", flush=True)
 for v, t in times.items():
     t = np.array(t)
     print(f"variant {v:4d} median {np.median(t):.4f} ms  min {t.min():.4f} ms  mean {t.mean():.4f} ms  -> "
