@@ -1300,11 +1300,16 @@ __device__ __forceinline__ uint32_t fnv4(uint32_t h, uint32_t v)
 // The address dwords past the first (IPv6) are hashed under a select, not a branch: a wave mixing IPv4 and IPv6 lanes
 // runs them either way, and the selects spare the exec-mask bookkeeping of 24 branches (kBranchy: the branches, a
 // tools-only diagnostic).
-template <bool kBranchy = false>
+// kV4Skip (R6 bit 3): the address dwords past the first are hashed only when some active lane hashes an IPv6 pair (a
+// wave-uniform branch on a ballot): a wave of IPv4 packets runs 3 x 2-3 dword steps instead of 3 x 8-9.
+template <bool kBranchy = false, bool kV4Skip = false>
 __device__ __forceinline__ void tuple_hashes(const uint32_t (&s)[4], const uint32_t (&d)[4], uint32_t na, bool has_l4,
                                              uint32_t pw, uint32_t proto, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
 {
+	const bool any6 = !kV4Skip || __ballot(na != 1) != 0;  // uniform over the active lanes
 	auto add4 = [&](uint32_t h, uint32_t k, uint32_t v) -> uint32_t {
+		if (k > 0 && !any6)
+			return h;
 		if (kBranchy)
 			return k < na ? fnv4(h, v) : h;
 		const uint32_t y = fnv4(h, v);
@@ -1356,6 +1361,7 @@ __device__ __forceinline__ void tuple_hashes(const uint32_t (&s)[4], const uint3
 // hash5Tuple / hash2Tuple of a generic-walk packet: addresses of the first IPv4 (else first IPv6) layer,
 // ports of the last TCP (else last UDP) layer, the IP layer's protocol / next-header byte. Dword reads
 // from the LDS window where the bytes are staged (rd32), else from HBM.
+template <bool kV4Skip = false>
 __device__ __forceinline__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5, uint32_t& h5d, uint32_t& h2)
 {
 	h5 = h5d = h2 = 0;
@@ -1374,7 +1380,7 @@ __device__ __forceinline__ void hashes(const Pkt& p, const Walk& w, uint32_t& h5
 	}
 	const bool has_l4 = w.l4i >= 0 && !(w.mask & (1ull << P_ICMP));  // ICMP: no 5-tuple (PacketUtils.cpp:144-145)
 	const uint32_t pw = has_l4 ? rd32(p, w.l4o) : 0;
-	tuple_hashes(s, d, na, has_l4, pw, rb(p, ipo + (v4 ? 9 : 6)), h5, h5d, h2);
+	tuple_hashes<false, kV4Skip>(s, d, na, has_l4, pw, rb(p, ipo + (v4 ? 9 : 6)), h5, h5d, h2);
 }
 
 // ---- the three hashes of a whole wave (round 6, ParseShape R6 bit 1) ----
@@ -2040,7 +2046,7 @@ __device__ __forceinline__ HashIn hash_in_fast(const Pkt& p, const Fast& f, cons
 
 // hash5Tuple x2 + hash2Tuple of a fast-path packet (every byte in the LDS window): the first IPv4 (else the first
 // IPv6) layer's addresses and protocol / next-header byte, the L4 layer's ports
-template <bool kBranchy = false>
+template <bool kBranchy = false, bool kV4Skip = false>
 __device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, const Walk& w, uint32_t& h5, uint32_t& h5d,
                                             uint32_t& h2)
 {
@@ -2056,7 +2062,7 @@ __device__ __forceinline__ void fast_hashes(const Pkt& p, const Fast& f, const W
 		d[k] = (uint32_t)k < na ? lds_u32(p, dofs + 4 * k) : 0;
 	}
 	const uint32_t proto = (lds_u32(p, ipo + (v4 ? 8 : 4)) >> (v4 ? 8 : 16)) & 0xFF;
-	tuple_hashes<kBranchy>(s, d, na, f.l4() != 0, lds_u32(p, f.l4o()), proto, h5, h5d, h2);
+	tuple_hashes<kBranchy, kV4Skip>(s, d, na, f.l4() != 0, lds_u32(p, f.l4o()), proto, h5, h5d, h2);
 }
 
 // IPv4 header checksum of the first IPv4 layer, from dword reads of the (fully staged) header
@@ -2385,10 +2391,11 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //   R6 (round 6, records unchanged by every bit): bit 0 the tile span from 32-bit DPP reductions (wave_reduce_dpp)
 //     instead of 64-bit ds_bpermute butterflies; bit 1 the three hashes taken by the whole wave after both walks
 //     (wave_tuple_hashes: IPv4 packets in their own lanes, IPv6 packets' chains spread over the wave's lanes); bit 2 the
-//     L7 trigger ports looked up in register tables by ds_bpermute (l7_pre_regs) instead of constant-memory bitmaps
+//     L7 trigger ports looked up in register tables by ds_bpermute (l7_pre_regs) instead of constant-memory bitmaps;
+//     bit 3 (with bit 1 off) the per-lane hashes skip the IPv6 address dwords in waves of IPv4 packets (tuple_hashes)
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
-          int kSkip = 0, int kR6 = 7>
+          int kSkip = 0, int kR6 = 12>
 struct ParseShape
 {
 	static constexpr bool NT = kNT, FillTails = kFillTails, TightR2 = kTightR2, Realign = kRealign, EarlyB = kEarlyB;
@@ -2634,7 +2641,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			// the L7 table reads first: their latency hides behind the hashes
 			L7Pre pre = kL7Regs ? pre_r : ((S::Skip & 8) ? L7Pre{ 0u, 0u, 0u, 0u } : fast_l7_pre(p, f));
 			if (!(S::Skip & 1) && !kWaveHash)
-				fast_hashes<(S::Skip & 32) != 0>(p, f, fast_to_walk(f, ml), h5, h5d, h2);
+				fast_hashes<(S::Skip & 32) != 0, (S::R6 & 8) != 0>(p, f, fast_to_walk(f, ml), h5, h5d, h2);
 			if (S::Skip & 8)  // diagnostic: the round-3 order (table reads after the hashes)
 				pre = fast_l7_pre(p, f);
 			if (!(S::Skip & 2))
@@ -2658,7 +2665,7 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			uint2* lay_out = stage_layers ? reinterpret_cast<uint2*>(prm.layers) + (size_t)i * ml : nullptr;
 			w = walk_chain<Csum ? 2 : 4>(p, cap, prm, lay_out);
 			if (!kWaveHash)
-				hashes(p, w, h5, h5d, h2);
+				hashes<(S::R6 & 8) != 0>(p, w, h5, h5d, h2);
 			if (want_csum && w.v4 >= 0)
 			{
 				ipc = ipv4_checksum(p, w, &ips);
@@ -3678,13 +3685,17 @@ constexpr int kParseChunks = 6;
 // packet, the rest only for the deep stacks the first window cannot hold): 99.7% of config 5's deep stacks take the
 // fast path; 16 waves/CU of LDS (144 B: 0.88 ms on config 5, 160 B: 1.00 ms at 14 waves/CU, 112 B: 1.17 ms with
 // 22% of the packets on the generic walk; gpurun_out r02l_ab_cfg5 -> profiles/r02_ab_parse_only.txt)
-constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 6;
+// Round 6: the first round holds 128 B (8 chunks) instead of 96: most deep stacks end inside it, so fewer waves take the
+// dependent second round (config 5 -2.9% in an interleaved A/B, records identical: tools/ab variant 240 against 219,
+// profiles/r06c_ab6_cfg5.txt); plain stacks take the SHORT instance, not this one
+constexpr int kParseOnlyChunks = 9, kParseOnlyChunks1 = 8;
+constexpr int kParseDeepChunks1 = 6;  // the DEEP checksum instance keeps its measured 96-B first round
 #define PCPPX_PARSE_ONLY_KERNEL parse_tile_kernel<1, 64, kParseOnlyChunks, false, kParseOnlyChunks1>
 // checksum launches with opts.window = PCPPX_WINDOW_DEEP: the parse-only instance's two-round 144-B window (tight second
 // round, dword-aligned re-gather) with the span stream; LDS 10 KiB, 4 waves/SIMD; the second stream window is issued
 // after the parse (EarlyB off: this instance's register budget)
 #define PCPPX_PARSE_DEEP_KERNEL                                                                                        \
-	parse_tile_kernel<4, kParseSWin, kParseOnlyChunks, true, kParseOnlyChunks1, ParseShape<true, true, true, true, false>>
+	parse_tile_kernel<4, kParseSWin, kParseOnlyChunks, true, kParseDeepChunks1, ParseShape<true, true, true, true, false>>
 // parse-only launches with opts.window = PCPPX_WINDOW_SHORT: one 96-B round, LDS 7 KiB (22 waves/CU, 5 waves/SIMD of
 // registers): config 4 0.464 -> 0.432 ms, config 2 43.2 -> 36.3 us, config 5 0.75 -> 1.61 ms (tools/ab variant 60,
 // profiles/r03_ab_windows_persist.txt)

@@ -325,9 +325,14 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 82: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 10, false, 10>), grid, dim3(kTile), 0, stream, prm); break;
 	// two rounds 128 B (96 + 32)
 	case 83: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 8, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	// round 6: the three instances under each combination of the ParseShape R6 switches (bit 0 DPP span reductions, bit 1
-	// wave-wide hashes, bit 2 L7 register tables): 200 + R6 the checksum instance, 210 + R6 the two-round parse-only
-	// instance, 220 + R6 the SHORT parse-only instance
+	// round 6: the 144-B parse-only window with a larger first round (128 / 112 B), the rest only for the stacks that
+	// end past it -- fewer waves with a dependent second round on deep traffic (config 5)
+	case 240: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 8>), grid, dim3(kTile), 0, stream, prm); break;
+	case 241: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 7>), grid, dim3(kTile), 0, stream, prm); break;
+	// round 6: the instances under combinations of the ParseShape R6 switches (bit 0 DPP span reductions, bit 1
+	// wave-wide hashes, bit 2 L7 register tables, bit 3 IPv4-wave hash skip): 200 + R6 (R6 < 8; 208: R6 = 8, 209: R6 = 12)
+	// the checksum instance, 210 + the two-round parse-only instance, 220 + the SHORT parse-only instance, 230 + the DEEP
+	// checksum instance (its ParseShape with EarlyB, tools/ab variant 70's)
 #define PCPPX_AB_SHAPE(r) ParseShape<true, true, true, true, true, false, false, false, false, 0, r>
 #define PCPPX_AB_R6(base, W, SW, C, CS, C1)                                                                                \
 	case base + 0: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(0)>), grid, dim3(kTile), 0, stream, prm); break; \
@@ -337,10 +342,13 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case base + 4: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(4)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 5: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(5)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 6: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(6)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 7: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(7)>), grid, dim3(kTile), 0, stream, prm); break;
+	case base + 7: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(7)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 8: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(8)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 9: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(12)>), grid, dim3(kTile), 0, stream, prm); break;
 	PCPPX_AB_R6(200, 5, 128, 6, true, 6)
 	PCPPX_AB_R6(210, 1, 64, 9, false, 6)
 	PCPPX_AB_R6(220, 1, 64, 6, false, 6)
+	PCPPX_AB_R6(230, 4, 128, 9, true, 6)
 #undef PCPPX_AB_SHAPE
 #undef PCPPX_AB_R6
 	default: return launch_parse(b, o, r, stream);

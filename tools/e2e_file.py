@@ -100,8 +100,12 @@ def google_pair(pcap: Path, args: list[str], trials: int = 1) -> dict:
             continue
         out[bm] = {}
         for name, ds in by.items():
-            ns = sorted(d["ns_per_iteration"] for d in ds)
+            # BM_PacketFirstPass: one pass over the whole file per iteration, so per packet = per iteration / packets
+            per_it = (ds[-1].get("items", ds[-1]["iterations"]) / ds[-1]["iterations"]) if bm == "BM_PacketFirstPass" else 1
+            ns = sorted(round(d["ns_per_iteration"] / per_it, 3) for d in ds)
             out[bm][name] = {"ns_per_packet": ns[len(ns) // 2], "trials_ns": ns, "iterations": ds[-1]["iterations"]}
+            if bm == "BM_PacketFirstPass":
+                out[bm][name]["packets_per_pass"] = int(per_it)
         if "reference" in out[bm] and "engine" in out[bm]:
             out[bm]["speedup"] = round(out[bm]["reference"]["ns_per_packet"] / out[bm]["engine"]["ns_per_packet"], 2)
     return out
@@ -112,9 +116,9 @@ def main() -> None:
     ap.add_argument("--packets", type=int, default=10_000_000)
     ap.add_argument("--out", default=None)
     ap.add_argument("--shm", default="/dev/shm")
-    ap.add_argument("--only", choices=("all", "google", "dropin"), default="all",
+    ap.add_argument("--only", choices=("all", "google", "dropin", "firstpass"), default="all",
                     help="google: only the benchmark-google loops (example.pcap and the IMIX pcap); dropin: only the "
-                         "drop-in benchmark.cpp runs (5 IMIX trials)")
+                         "drop-in benchmark.cpp runs (5 IMIX trials); firstpass: only the first-pass costs")
     args = ap.parse_args()
     res = {"cores": len(os.sched_getaffinity(0))}
     big = Path(args.shm) / f"pcppx_e2e_{os.getpid()}.pcap"
@@ -131,6 +135,20 @@ def main() -> None:
 
         ex, _ = load_golden(GOLDEN / "capture_example.npz")
         write_pcap(exf, ex)
+        if args.only in ("all", "google", "firstpass"):
+            # first-pass costs: BM_PacketFirstPass times the reader's open, the preload of every
+            # packet (getNextPackets) and one Packet per packet -- the engine's GPU parse of the pages included -- each
+            # repetition over a reader of its own; and the reference's BM_PacketPureParsing body run for exactly one pass
+            # (--iterations = the file's packets), whose preload is untimed in both programs
+            fp = {}
+            for tag, f, n, reps in (("example_pcap", exf, ex.n, 7), ("imix_10M", big, args.packets, 3)):
+                fp[tag] = google_pair(f, ["--benchmark", "BM_PacketFirstPass", "--iterations", "1", "--repetitions",
+                                          str(reps)], trials=3 if tag == "example_pcap" else 1)
+                fp[tag + "_pure_one_pass"] = google_pair(f, ["--benchmark", "BM_PacketPureParsing", "--iterations", str(n),
+                                                             "--repetitions", str(reps)],
+                                                         trials=3 if tag == "example_pcap" else 1)
+                print("first_pass", tag, json.dumps(fp[tag]), flush=True)
+            res["first_pass"] = fp
         if args.only in ("all", "google"):
             # benchmark-google.cpp's loops: all three on example.pcap (the library's 0.5-s runs); the two parse loops on
             # the IMIX pcap at fixed counts (the pure loop: three passes over the preloaded 10M packets)

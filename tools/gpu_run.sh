@@ -52,7 +52,7 @@ for step in "$@"; do
     e2e)
       timeout -k 10 1000 python -u tools/e2e_file.py --out "$OUT/${TAG}_e2e_file.json" $arg > "$OUT/${TAG}_e2e.log" 2>&1 \
         || { tail -20 "$OUT/${TAG}_e2e.log"; exit 3; }
-      grep -E "^map|^copy|^config1|^example|^imix|^filter|^google" "$OUT/${TAG}_e2e.log" | cut -c1-500 ;;
+      grep -E "^map|^copy|^config1|^example|^imix|^filter|^google|^first_pass" "$OUT/${TAG}_e2e.log" | cut -c1-500 ;;
     bench)
       for c in ${arg//,/ }; do
         timeout -k 10 400 python -u bench.py $(cfgargs "$c") $(tr "$c") > "$OUT/${TAG}_bench_cfg$c.json" \
