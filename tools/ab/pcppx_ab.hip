@@ -400,6 +400,12 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 13: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, false>, 1024, kFlowBatchPk, 256); break;  // two-pass flush (r04 before r04r)
 	case 14: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 4, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 4
 	case 15: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 1, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 1
+	// round 6: deferred flushes (kFlushAt): batches of 3072 / 2048 / 4096 / 6144 packets, flushed once the table holds more
+	// than 4096 / 5120 / 3584 / 1536 distinct keys
+	case 30: go(flow_count_kernel<1024, 8192, 3072, kFlowHot, true, true, true, true, 4096>, 1024, 3072, 256); break;
+	case 31: go(flow_count_kernel<1024, 8192, 2048, kFlowHot, true, true, true, true, 5120>, 1024, 2048, 256); break;
+	case 32: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, true, 3584>, 1024, 4096, 256); break;
+	case 33: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, true, 1536>, 1024, kFlowBatchPk, 256); break;
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);

@@ -16,7 +16,7 @@ from pcapplusplus_amd.engine import Engine, to_device  # noqa: E402
 from tools import ab  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-b = synth.imix(12_500_000, 4, flows=1_000_000, corrupt_frac=0.0)
+b = synth.flow_stream(0, 12_500_000, 4)  # bench.py's config-4 shard (rank 0 of the one stream)
 n = b.n
 dev = "cuda:0"
 data, offs, caps = to_device(b, dev)
@@ -24,7 +24,8 @@ st = torch.cuda.current_stream()
 eng = Engine(0)
 summ = torch.empty(n * 32, dtype=torch.uint8, device=dev)
 fk = torch.empty(n, dtype=torch.int32, device=dev)
-eng.parse_device(data, offs, caps, n, b.linktype, abi.make_opts(0, 8, False, 0), summ, None, st.cuda_stream, fk)
+eng.parse_device(data, offs, caps, n, b.linktype, abi.make_opts(0, 8, False, 0, abi.WINDOW_SHORT), summ, None,
+                 st.cuda_stream, fk)
 cap = 1 << 21
 PARTS = {6: 256, 7: 1024}  # partitions per shape (tools/ab pcppx_ab_flow_part's `want`); else 512
 queues = torch.empty(1024 * (2 * ((n + 1023) // 1024) + 4096) * 4, dtype=torch.int32, device=dev)
@@ -59,6 +60,8 @@ for s in shapes:
     if ref is None:
         ref = d
     print(f"shape {s}: table equal to shape 0: {d == ref} ({len(d)} flows)", flush=True)
+    if d != ref:
+        raise SystemExit(f"shape {s}: flow table differs")
 times = {s: [] for s in shapes}
 for r in range(rounds):
     for s in shapes:
