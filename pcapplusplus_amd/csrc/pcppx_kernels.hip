@@ -2392,7 +2392,8 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     instead of 64-bit ds_bpermute butterflies; bit 1 the three hashes taken by the whole wave after both walks
 //     (wave_tuple_hashes: IPv4 packets in their own lanes, IPv6 packets' chains spread over the wave's lanes); bit 2 the
 //     L7 trigger ports looked up in register tables by ds_bpermute (l7_pre_regs) instead of constant-memory bitmaps;
-//     bit 3 (with bit 1 off) the per-lane hashes skip the IPv6 address dwords in waves of IPv4 packets (tuple_hashes)
+//     bit 3 (with bit 1 off) the per-lane hashes skip the IPv6 address dwords in waves of IPv4 packets (tuple_hashes);
+//     bit 4 the span stream issues no window loads past the tile's last window
 template <bool kNT = true, bool kFillTails = true, bool kTightR2 = true, bool kRealign = true, bool kEarlyB = true,
           bool kStreamOnly = false, bool kMarkFast = false, bool kGatherOnly = false, bool kSkipGeneric = false,
           int kSkip = 0, int kR6 = 12>
@@ -2737,9 +2738,13 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			for (uint32_t wi = 0; wi < nwin; wi += 2)
 			{
 				process(va, wi);
-				load(va, wi + 2);
+				// R6 bit 4: no loads past the span's last window (a tile of small packets streams 2-3 windows: the padded
+				// loads of windows nwin, nwin + 1 were never consumed, yet held the wave until they returned)
+				if (!(S::R6 & 16) || wi + 2 < nwin)
+					load(va, wi + 2);
 				process(vb, wi + 1);
-				load(vb, wi + 3);
+				if (!(S::R6 & 16) || wi + 3 < nwin)
+					load(vb, wi + 3);
 			}
 			if (full)
 				fsum = p1 - p0;
@@ -3072,12 +3077,8 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
 // kOnePass (partitioned flush): the hot-flow decision is taken in the partition pass (a hot slot is kept while the kept
 // count stays within the bound, first come first kept) instead of in a pass and a barrier of its own.
-// kFlushAt (partitioned one-pass flush, round 6): 0 = flush after every batch; else a batch leaves its keys in the LDS
-// table while the table holds at most kFlushAt distinct keys (a flow met again in the next batch adds to its slot instead
-// of queueing a second record), so a block flushes -- partition pass, queue reservations, records -- every few batches.
-// The next batch always fits: kFlushAt + kFlowBatch < kFlowLds (and the kept hot flows stay below half the table).
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false, bool kOnePass = false, uint32_t kFlushAt = 0>
+          bool kPart = false, bool kDense = false, bool kOnePass = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -3088,8 +3089,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	__shared__ uint32_t s_bin[kPart ? kFlowMaxParts : 1], s_base[kPart ? kFlowMaxParts : 1];  // per-partition counts / offsets
 	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
-	__shared__ uint32_t s_kept, s_used;
-	static_assert(kFlushAt == 0 || (kPart && kOnePass && kFlushAt + kFlowBatch < kFlowLds), "flush threshold");
+	__shared__ uint32_t s_kept;
 	const uint32_t t = threadIdx.x;
 	const uint32_t m = capacity - 1;
 	unsigned long long z_pk = 0, z_by = 0, lost = 0;  // flow key 0 (PacketUtils.cpp:141-148); table full
@@ -3101,8 +3101,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	if (kPart)
 		for (uint32_t j = t; j < kFlowMaxParts; j += kFB)
 			s_bin[j] = 0;
-	if (t == 0)
-		s_used = 0;
 	__syncthreads();
 	// kPrefetch: the next batch's keys and lengths are loaded into registers before this batch's flush,
 	// so their latency overlaps the flush's HBM reads and atomics
@@ -3123,7 +3121,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		fetch((uint64_t)blockIdx.x * kFlowBatch);
 	for (uint64_t base = (uint64_t)blockIdx.x * kFlowBatch; base < n; base += (uint64_t)gridDim.x * kFlowBatch)
 	{
-		uint32_t fresh = 0;  // kFlushAt: keys this thread added to the table
 #pragma unroll
 		for (uint32_t r = 0; r < kR; ++r)
 		{
@@ -3147,7 +3144,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				if (prev == 0u || prev == key)
 				{
 					atomicAdd(&s_cnt[slot], add);
-					fresh += prev == 0u ? 1u : 0u;
 					break;
 				}
 				slot = (slot + 1) & (kFlowLds - 1);
@@ -3155,12 +3151,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		}
 		if (kPrefetch)
 			fetch(base + (uint64_t)gridDim.x * kFlowBatch);
-		if (kFlushAt)
-		{
-			const uint32_t wf = (uint32_t)wave_sum_u64(fresh);
-			if ((t & 63) == 0 && wf)
-				atomicAdd(&s_used, wf);
-		}
 		if (t == 0)
 			s_kept = 0;
 		__syncthreads();
@@ -3171,8 +3161,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 		// kept only while they fill at most half of the table, so the next batch always fits.
 		const bool last = base + (uint64_t)gridDim.x * kFlowBatch >= n;  // uniform
 		constexpr uint32_t kPer = kFlowLds / kFB;
-		if (kFlushAt && !last && s_used <= kFlushAt)  // uniform: the next batch still fits, keep every key
-			continue;
 		if constexpr (kPart && kOnePass)
 		{
 			uint32_t fk[kPer], fs[kPer], fseen[kPer];
@@ -3189,8 +3177,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				fseen[u] = fk[u] ? atomicAdd(&s_bin[fs[u]], 1u) : 0u;
 			}
 			__syncthreads();
-			if (kFlushAt && t == 0)  // the kept hot flows are the table's keys after this flush (two barriers ahead)
-				s_used = s_kept < kFlowLds / 2 - kFlowBatch / 2 ? s_kept : kFlowLds / 2 - kFlowBatch / 2;
 			for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
 			{
 				const uint32_t c = s_bin[b];

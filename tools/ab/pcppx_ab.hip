@@ -331,7 +331,7 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 241: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 7>), grid, dim3(kTile), 0, stream, prm); break;
 	// round 6: the instances under combinations of the ParseShape R6 switches (bit 0 DPP span reductions, bit 1
 	// wave-wide hashes, bit 2 L7 register tables, bit 3 IPv4-wave hash skip): 200 + R6 (R6 < 8; 208: R6 = 8, 209: R6 = 12)
-	// the checksum instance, 210 + the two-round parse-only instance, 220 + the SHORT parse-only instance, 230 + the DEEP
+	// the checksum instance (450: R6 = 28), 210 + the two-round parse-only instance, 220 + the SHORT parse-only instance, 230 + the DEEP
 	// checksum instance (its ParseShape with EarlyB, tools/ab variant 70's)
 #define PCPPX_AB_SHAPE(r) ParseShape<true, true, true, true, true, false, false, false, false, 0, r>
 #define PCPPX_AB_R6(base, W, SW, C, CS, C1)                                                                                \
@@ -344,7 +344,8 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case base + 6: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(6)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 7: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(7)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 8: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(8)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 9: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(12)>), grid, dim3(kTile), 0, stream, prm); break;
+	case base + 9: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(12)>), grid, dim3(kTile), 0, stream, prm); break; \
+	case base + 250: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(28)>), grid, dim3(kTile), 0, stream, prm); break;
 	PCPPX_AB_R6(200, 5, 128, 6, true, 6)
 	PCPPX_AB_R6(210, 1, 64, 9, false, 6)
 	PCPPX_AB_R6(220, 1, 64, 6, false, 6)
@@ -400,12 +401,6 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 13: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, false>, 1024, kFlowBatchPk, 256); break;  // two-pass flush (r04 before r04r)
 	case 14: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 4, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 4
 	case 15: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 1, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 1
-	// round 6: deferred flushes (kFlushAt): batches of 3072 / 2048 / 4096 / 6144 packets, flushed once the table holds more
-	// than 4096 / 5120 / 3584 / 1536 distinct keys
-	case 30: go(flow_count_kernel<1024, 8192, 3072, kFlowHot, true, true, true, true, 4096>, 1024, 3072, 256); break;
-	case 31: go(flow_count_kernel<1024, 8192, 2048, kFlowHot, true, true, true, true, 5120>, 1024, 2048, 256); break;
-	case 32: go(flow_count_kernel<1024, 8192, 4096, kFlowHot, true, true, true, true, 3584>, 1024, 4096, 256); break;
-	case 33: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, true, 1536>, 1024, kFlowBatchPk, 256); break;
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);
