@@ -401,6 +401,7 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 13: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, false>, 1024, kFlowBatchPk, 256); break;  // two-pass flush (r04 before r04r)
 	case 14: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 4, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 4
 	case 15: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 1, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 1
+	case 40: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // r06: 8-B records
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);
@@ -420,6 +421,9 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 6>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 19)  // 1 record per thread, 6 rounds ahead
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 1, 6>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
+	else if (shape == 40)  // round 6: 8-B queue records, the product merge shape
+		hipLaunchKernelGGL((flow_merge_kernel<kFlowMergeThreads, 4096, 2, 3, true>), dim3(1u << lp), dim3(kFlowMergeThreads), 0, stream,
+		                   fp, keys, pk, by, st);
 	else if (shape == 10)  // 256 threads x 4 records per round, 2 rounds ahead
 		hipLaunchKernelGGL((flow_merge_kernel<256, 4096, 4, 2>), dim3(1u << lp), dim3(256), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 11)  // 512 threads x 4 records, 8192-slot LDS table
