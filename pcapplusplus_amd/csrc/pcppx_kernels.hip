@@ -3050,35 +3050,6 @@ __device__ __forceinline__ uint32_t flow_part(uint32_t key, uint32_t log2p)
 {
 	return log2p ? (key * 0x9E3779B1u) >> (32 - log2p) : 0u;
 }
-// 8-B queue records (kRec8): bits [0, 32 - log2p) the low bits of key * 0x9E3779B1 (its top log2p bits are the
-// partition), then 13 bits of packets, then bytes; packets >= 1 in every record (0: none)
-constexpr uint32_t kRec8PkBits = 13, kFlowKeyMulInv = 0x0E8B2F51u;  // (0x9E3779B1)^-1 mod 2^32
-__device__ __forceinline__ uint32_t rec8_parts(unsigned long long c, uint32_t log2p)
-{
-	const uint32_t byb = 64 - (32 - log2p) - kRec8PkBits;
-	const unsigned long long pk = c >> 40, by = c & ((1ull << 40) - 1), pmax = (1ull << kRec8PkBits) - 1,
-	                         bmax = (1ull << byb) - 1;
-	const unsigned long long a = (pk + pmax - 1) / pmax, b = (by + bmax - 1) / bmax;
-	return (uint32_t)(a > b ? a : b);  // >= 1 for pk >= 1; <= pk since bmax >= 2^19 > 8 * 65535
-}
-__device__ __forceinline__ unsigned long long rec8_make(uint32_t key, unsigned long long c, uint32_t part, uint32_t parts,
-                                                        uint32_t log2p)
-{
-	const uint32_t rb = 32 - log2p;
-	const unsigned long long pk = c >> 40, by = c & ((1ull << 40) - 1);
-	const unsigned long long pki = pk / parts + (part < pk % parts ? 1u : 0u), byi = by / parts + (part < by % parts ? 1u : 0u);
-	const unsigned long long res = (unsigned long long)(key * 0x9E3779B1u) & ((1ull << rb) - 1);
-	return res | (pki << rb) | (byi << (rb + kRec8PkBits));
-}
-// -> {key, packed count} (packets << 40 | bytes); key 0: an empty record
-__device__ __forceinline__ uint32_t rec8_key(unsigned long long r, uint32_t p, uint32_t log2p, unsigned long long* c)
-{
-	const uint32_t rb = 32 - log2p;
-	const unsigned long long pk = (r >> rb) & ((1ull << kRec8PkBits) - 1), by = r >> (rb + kRec8PkBits);
-	*c = (pk << 40) | by;
-	const uint32_t h = (uint32_t)((((unsigned long long)p << rb) | (r & ((1ull << rb) - 1))) & 0xFFFFFFFFull);
-	return pk ? h * kFlowKeyMulInv : 0u;
-}
 __device__ __forceinline__ uint32_t flow_region_slot(uint32_t key, uint32_t log2r)
 {
 	return (key * 0x85EBCA6Bu) & ((1u << log2r) - 1u);
@@ -3106,11 +3077,8 @@ __device__ bool flow_region_add_atomic(uint32_t* keys, unsigned long long* packe
 // kDense: keys come from the dense column `dkeys` (pcppx_records.flow_keys) instead of the summaries' hash5.
 // kOnePass (partitioned flush): the hot-flow decision is taken in the partition pass (a hot slot is kept while the kept
 // count stays within the bound, first come first kept) instead of in a pass and a barrier of its own.
-// kRec8 (round 6): 8-B queue records instead of 16 -- the key's hash (key * 0x9E3779B1, a bijection) minus the top log2p
-// bits its partition already names, 13 bits of packets and the rest bytes; a count that does not fit goes out as several
-// records whose counts add up to it (rec8_parts)
 template <uint32_t kFB, uint32_t kFlowLds, uint32_t kFlowBatch, uint32_t kHot = kFlowHot, bool kPrefetch = false,
-          bool kPart = false, bool kDense = false, bool kOnePass = false, bool kRec8 = false>
+          bool kPart = false, bool kDense = false, bool kOnePass = false>
 __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __restrict__ sum,
                                                             const uint32_t* __restrict__ caplens, uint32_t n,
                                                             uint32_t* keys, unsigned long long* packets,
@@ -3122,7 +3090,6 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 	__shared__ uint32_t s_key[kFlowLds];
 	__shared__ unsigned long long s_cnt[kFlowLds];  // packets << 40 | bytes (launches hold < 2^24 packets)
 	__shared__ uint32_t s_kept;
-	static_assert(!kRec8 || (kPart && kOnePass), "8-B records: the partitioned one-pass flush");
 	const uint32_t t = threadIdx.x;
 	const uint32_t m = capacity - 1;
 	unsigned long long z_pk = 0, z_by = 0, lost = 0;  // flow key 0 (PacketUtils.cpp:141-148); table full
@@ -3207,7 +3174,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 				                  atomicAdd(&s_kept, 1u) < kFlowLds / 2 - kFlowBatch / 2;
 				fk[u] = keep ? 0u : key;
 				fs[u] = flow_part(fk[u], fpart.log2p);
-				fseen[u] = fk[u] ? atomicAdd(&s_bin[fs[u]], kRec8 ? rec8_parts(s_cnt[j], fpart.log2p) : 1u) : 0u;
+				fseen[u] = fk[u] ? atomicAdd(&s_bin[fs[u]], 1u) : 0u;
 			}
 			__syncthreads();
 			for (uint32_t b = t; b < (1u << fpart.log2p); b += kFB)
@@ -3226,25 +3193,7 @@ __global__ __launch_bounds__(kFB) void flow_count_kernel(const pcppx_summary* __
 					continue;
 				const uint32_t pos = s_base[fs[u]] + fseen[u];
 				const unsigned long long c = s_cnt[j];
-				if constexpr (kRec8)
-				{
-					const uint32_t parts = rec8_parts(c, fpart.log2p);
-					unsigned long long* q = reinterpret_cast<unsigned long long*>(fpart.recs) + (size_t)fs[u] * fpart.rec_cap;
-					for (uint32_t k = 0; k < parts; ++k)
-					{
-						const unsigned long long r = rec8_make(key, c, k, parts, fpart.log2p);
-						if (pos + k < fpart.rec_cap)
-							q[pos + k] = r;
-						else
-						{
-							unsigned long long ck;
-							rec8_key(r, fs[u], fpart.log2p, &ck);
-							if (!flow_region_add_atomic(keys, packets, bytes, fpart, key, ck >> 40, ck & ((1ull << 40) - 1)))
-								lost += ck >> 40;
-						}
-					}
-				}
-				else if (pos < fpart.rec_cap)
+				if (pos < fpart.rec_cap)
 					fpart.recs[(size_t)fs[u] * fpart.rec_cap + pos] = make_uint4(key, 0u, (uint32_t)c, (uint32_t)(c >> 32));
 				else if (!flow_region_add_atomic(keys, packets, bytes, fpart, key, c >> 40, c & ((1ull << 40) - 1)))
 					lost += c >> 40;
@@ -3375,7 +3324,7 @@ __global__ __launch_bounds__(kBlock) void flow_unpack_kernel(unsigned long long*
 // region -- which no other block touches, so the counts take plain loads and stores (a CAS only claims a new key's
 // slot against the block's other threads). Resets the queue length for the next launch.
 // kAhead: rounds of queue records in flight ahead of the round being inserted.
-template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT, uint32_t kAhead = 1, bool kRec8 = false>
+template <uint32_t kMB, uint32_t kMLds, uint32_t kPerT, uint32_t kAhead = 1>
 __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* keys, unsigned long long* packets,
                                                          unsigned long long* bytes, unsigned long long* stats)
 {
@@ -3386,7 +3335,6 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 	const uint32_t t = threadIdx.x, p = blockIdx.x;
 	const uint32_t cnt = fp.fill[p] < fp.rec_cap ? fp.fill[p] : fp.rec_cap;
 	const uint4* q = fp.recs + (size_t)p * fp.rec_cap;
-	const unsigned long long* q8 = reinterpret_cast<const unsigned long long*>(fp.recs) + (size_t)p * fp.rec_cap;
 	const uint32_t rbase = p << fp.log2r, rm = (1u << fp.log2r) - 1u;
 	for (uint32_t j = t; j < kMLds; j += kMB)
 	{
@@ -3405,14 +3353,7 @@ __global__ __launch_bounds__(kMB) void flow_merge_kernel(FlowPart fp, uint32_t* 
 		for (uint32_t k = 0; k < kPerT; ++k)
 		{
 			const uint32_t idx = base + k * kMB + t;
-			if constexpr (kRec8)  // unpacked to the 16-B form: {key, 0, count lo, count hi}
-			{
-				unsigned long long c = 0;
-				const uint32_t key = idx < cnt ? rec8_key(q8[idx], p, fp.log2p, &c) : 0u;
-				v[k] = make_uint4(key, 0u, (uint32_t)c, (uint32_t)(c >> 32));
-			}
-			else
-				v[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
+			v[k] = idx < cnt ? q[idx] : make_uint4(0, 0, 0, 0);
 		}
 	};
 #pragma unroll

@@ -328,6 +328,8 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	// round 6: the 144-B parse-only window with a larger first round (128 / 112 B), the rest only for the stacks that
 	// end past it -- fewer waves with a dependent second round on deep traffic (config 5)
 	case 240: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 8>), grid, dim3(kTile), 0, stream, prm); break;
+	// round 6: the SHORT parse-only instance held to 6 waves per SIMD (<= 80 VGPRs; its 7 KiB of LDS allow 22 waves per CU)
+	case 260: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 6, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 241: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 7>), grid, dim3(kTile), 0, stream, prm); break;
 	// round 6: the instances under combinations of the ParseShape R6 switches (bit 0 DPP span reductions, bit 1
 	// wave-wide hashes, bit 2 L7 register tables, bit 3 IPv4-wave hash skip): 200 + R6 (R6 < 8; 208: R6 = 8, 209: R6 = 12)
@@ -401,7 +403,6 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 	case 13: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, false>, 1024, kFlowBatchPk, 256); break;  // two-pass flush (r04 before r04r)
 	case 14: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 4, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 4
 	case 15: go(flow_count_kernel<1024, 8192, kFlowBatchPk, 1, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // + hot above 1
-	case 40: go(flow_count_kernel<1024, 8192, kFlowBatchPk, kFlowHot, true, true, true, true, true>, 1024, kFlowBatchPk, 256); break;  // r06: 8-B records
 	default: go(PCPPX_FLOW_PART_DENSE_KERNEL, 1024, kFlowBatchPk, 256); break;
 	}
 	int rc = check_launch("pcppx_ab_flow_part", stream);
@@ -421,9 +422,6 @@ PCPPX_AB_API int pcppx_ab_flow_part(const uint32_t* dkeys, const uint32_t* caple
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 2, 6>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 19)  // 1 record per thread, 6 rounds ahead
 		hipLaunchKernelGGL((flow_merge_kernel<512, 4096, 1, 6>), dim3(1u << lp), dim3(512), 0, stream, fp, keys, pk, by, st);
-	else if (shape == 40)  // round 6: 8-B queue records, the product merge shape
-		hipLaunchKernelGGL((flow_merge_kernel<kFlowMergeThreads, 4096, 2, 3, true>), dim3(1u << lp), dim3(kFlowMergeThreads), 0, stream,
-		                   fp, keys, pk, by, st);
 	else if (shape == 10)  // 256 threads x 4 records per round, 2 rounds ahead
 		hipLaunchKernelGGL((flow_merge_kernel<256, 4096, 4, 2>), dim3(1u << lp), dim3(256), 0, stream, fp, keys, pk, by, st);
 	else if (shape == 11)  // 512 threads x 4 records, 8192-slot LDS table
