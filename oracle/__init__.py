@@ -401,7 +401,8 @@ def compare_engine_to_reference(eng_sum, eng_lay, ref_sum, ref_lay) -> dict:
 
 # protocols the engine builds itself (include/pcppx.h: everything else is a host layer); HTTPRequest /
 # HTTPResponse (6/7), DNS (13), SSL (18), SSH (35) and MySQL (63) as a classified first L7 layer and the layers behind it
-ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16, 17, 18, 19, 21, 25, 26, 30, 32, 33, 35, 44, 52, 63)
+ENGINE_PROTOS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16, 17, 18, 19, 21, 25, 26, 30, 32, 33, 35, 44, 47, 52, 58,
+                 63)  # 47 NFLOG, 58 Cisco HDLC: first layers built since round 6
 
 
 # TcpLayer::parseNextLayer's trigger ports (TcpLayer.cpp:372-491; pcppx_oracle.c tcp_l7_port), HTTP's (HttpLayer.h:74-77)

@@ -12,7 +12,8 @@
  *   - except that a classified HTTP / SSL / DNS first L7 layer is built, with the layers behind it, and so
  *     are the VXLAN and GTPv1 tunnels over UDP with the packet they carry;
  *   - where it would build an out-of-scope L2/L3 layer (PPPoE, WoL, IGMP, AH, ESP, VRRP, ICMPv6, STP,
- *     NFLOG/C_HDLC first layers) the chain stops before it and PCPPX_F_NEEDS_HOST_PROTO is set;
+ *     ...) the chain stops before it and PCPPX_F_NEEDS_HOST_PROTO is set (NFLOG and Cisco HDLC first layers are
+ *     built since round 6);
  *   - no trailer is appended to a flagged chain; hashes and checksums are computed over the emitted chain.
  * For unflagged packets every field equals the reference; for flagged packets the emitted layers are an
  * exact prefix of the reference chain.
@@ -32,11 +33,12 @@
 enum {
 	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14,
 	P_GREV0 = 15, P_GREV1 = 16, P_PPTP = 17, P_SLL = 19, P_NULL = 21, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33,
-	P_LLC = 44, P_SLL2 = 52, P_VXLAN = 26, P_GTPV1 = 32
+	P_LLC = 44, P_SLL2 = 52, P_VXLAN = 26, P_GTPV1 = 32, P_NFLOG = 47, P_CISCO_HDLC = 58
 };
 
 enum kind { K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP,
-	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP, K_SLL, K_SLL2, K_NULL, K_ICMP, K_VXLAN, K_GTP1 };
+	        K_TCP, K_UDP, K_PAYLOAD, K_OUT, K_L7, K_ARP, K_SLL, K_SLL2, K_NULL, K_ICMP, K_VXLAN, K_GTP1,
+	        K_NFLOG, K_HDLC };
 
 static uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
@@ -451,6 +453,7 @@ static int engine_proto(uint32_t p)
 	case P_ETH: case P_IPV4: case P_IPV6: case P_TCP: case P_UDP: case P_ARP: case P_VLAN: case P_MPLS:
 	case P_GREV0: case P_GREV1: case P_PPTP: case P_TRAILER: case P_DOT3: case P_LLC: case P_ICMP: return 1;
 	case P_VXLAN: case P_GTPV1: return 1; /* decided exactly at the UDP layer, never a host candidate */
+	case P_NFLOG: case P_CISCO_HDLC: return 1; /* first layers the engine builds (round 6) */
 	/* a classified first L7 layer is built, an unclassified one is none of these */
 	case P_HTTP_REQ: case P_HTTP_RESP: case P_DNS: case P_SSL: case P_MYSQL: case P_SSH: return 1;
 	default: return 0;
@@ -543,6 +546,48 @@ static lay make_layer(const uint8_t* pkt, int k, uint32_t off, uint32_t len, int
 		default: NEXT(K_PAYLOAD, po, pl); break;
 		}
 		break;
+	case K_HDLC: /* CiscoHdlcLayer::parseNextLayer, Packet++/src/CiscoHdlcLayer.cpp:43-67: a 4-byte header (address,
+	              * control, protocol), no length check -- a 4-byte packet gets an empty Payload */
+		L.proto = P_CISCO_HDLC; L.osi = 2; L.hdr = 4;
+		po = off + 4; pl = len - 4;
+		switch (be16(p + 2)) {
+		case 0x0800: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 0x86DD: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	case K_NFLOG: { /* NflogLayer, Packet++/src/NflogLayer.cpp:41-96: a 4-byte nflog_header (family, version, resource
+	                 * id), then TLVs {u16 length, u16 type, value} (host byte order), each taking align<4>(length) bytes
+	                 * (NflogLayer.h NflogTlv::getTotalSize), walked as TLVRecordReader does (TLVData.h:238-312) */
+		L.proto = P_NFLOG; L.osi = 2; L.hdr = 4;
+		const uint32_t tl = len - 4; /* the TLV stream */
+		uint32_t pos = 0;            /* current record, relative to the stream */
+		int found_payload = 0, have = 0;
+		uint32_t total = 0;
+		if (tl >= 2) { /* getFirstTLVRecord: canAssign, then the record must fit and be non-empty */
+			total = (le16(p + 4) + 3u) & ~3u;
+			have = total != 0 && total <= tl;
+		}
+		while (have) {
+			if (le16(p + 4 + pos + 2) == 9) { found_payload = 1; break; } /* NFULA_PAYLOAD */
+			L.hdr += total;                                             /* getHeaderLen: every record before it */
+			pos += total;
+			/* getNextTLVRecord: canAssign (>= 2 bytes left), a non-empty record that fits */
+			if (tl - pos < 2) { have = 0; break; }
+			total = (le16(p + 4 + pos) + 3u) & ~3u;
+			have = total != 0 && pos + total <= tl;
+		}
+		if (!found_payload) break;
+		L.hdr += 4; /* the payload record's length and type */
+		if (len <= 4) break; /* parseNextLayer: m_DataLen <= sizeof(nflog_header) */
+		po = off + 4 + pos + 4; pl = total - 4;
+		switch (p[0]) { /* the address family: NflogFamilyIpv4 = 2, NflogFamilyIpv6 = 10 */
+		case 2: NEXT(ipv4_valid(pkt + po, pl) ? K_IPV4 : K_PAYLOAD, po, pl); break;
+		case 10: NEXT(ipv6_valid(pkt + po, pl) ? K_IPV6 : K_PAYLOAD, po, pl); break;
+		default: NEXT(K_PAYLOAD, po, pl); break;
+		}
+		break;
+	}
 	case K_NULL: { /* NullLoopbackLayer::getFamily :23-43, parseNextLayer :50-99 (no length check: a 4-byte packet
 	                * gets an empty next layer) */
 		L.proto = P_NULL; L.osi = 2; L.hdr = 4;
@@ -898,10 +943,8 @@ static void parse_packet(const uint8_t* pkt, uint32_t caplen, uint16_t linktype,
 	case 113: k = K_SLL; break;                                   /* LINKTYPE_LINUX_SLL: unchecked */
 	case 276: k = caplen >= 20 ? K_SLL2 : K_PAYLOAD; break;        /* Sll2Layer::isDataValid, Sll2Layer.cpp:151-154 */
 	case 0: k = caplen >= 4 ? K_NULL : K_PAYLOAD; break;           /* NullLoopbackLayer::isDataValid, NullLoopbackLayer.h:86-89 */
-	case 239: case 104: /* NFLOG, C_HDLC: host dissectors */
-		sum->flags = PCPPX_F_NEEDS_HOST_PROTO;
-		if (tup) tup->flags = PCPPX_F_NEEDS_HOST_PROTO;
-		return;
+	case 239: k = caplen >= 4 ? K_NFLOG : K_PAYLOAD; break; /* NflogLayer::isDataValid, NflogLayer.cpp:102-105 */
+	case 104: k = caplen >= 4 ? K_HDLC : K_PAYLOAD; break;  /* CiscoHdlcLayer::isDataValid, CiscoHdlcLayer.h:59-62 */
 	default: k = K_PAYLOAD; break;
 	}
 

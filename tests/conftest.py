@@ -20,6 +20,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP engine runs)")
 
 
+def make_examples():
+    """`make -C examples` under an exclusive lock: xdist workers of test_facade and test_examples build the same
+    binaries, and an unlocked concurrent rebuild leaves one worker running a half-written executable."""
+    import fcntl
+    import subprocess
+
+    root = Path(__file__).resolve().parents[1]
+    (root / "examples" / "bin").mkdir(exist_ok=True)
+    with open(root / "examples" / "bin" / ".build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return subprocess.run(["make", "-s", "-C", str(root / "examples")], capture_output=True, text=True)
+
+
 def golden_files():
     return sorted(GOLDEN.glob("*.npz"))
 

@@ -409,8 +409,9 @@ def crafted_http(n: int = 1500, seed: int = 29) -> list[bytes]:
 
 
 def crafted_linklayers(seed: int = 23) -> dict[int, list[bytes]]:
-    """First layers of the non-Ethernet link types the engine builds, per link type: Linux SLL (113), SLL2 (276)
-    and Null/Loopback (0) at and around their length rules, every protocol / family encoding they dispatch on
+    """First layers of the non-Ethernet link types the engine builds, per link type: Linux SLL (113), SLL2 (276),
+    Null/Loopback (0), Cisco HDLC (104) and NFLOG (239, its TLV walk: records before, after and without the payload
+    record, empty, short and overlong records) at and around their length rules, every protocol / family encoding they dispatch on
     (NullLoopbackLayer::getFamily's byte-order guesses, Packet++/src/NullLoopbackLayer.cpp:23-43), followed by valid
     and broken IPv4 / IPv6 / VLAN / MPLS / ARP / LLC / PPPoE payloads."""
     rng = np.random.default_rng(seed)
@@ -438,4 +439,27 @@ def crafted_linklayers(seed: int = 23) -> dict[int, list[bytes]]:
                 out[0].append(enc + body)
     for w in (0x00020000, 0x00050000, 0x00060000, 0x01000000, 0x00000200, 0x00000600, 0x00000002, 0x0000FF00):
         out[0].append(w.to_bytes(4, "little") + ip4)
+    # Cisco HDLC (104, CiscoHdlcLayer.cpp:43-67): address, control, protocol (big-endian), then IPv4 / IPv6 / anything
+    out[104] = [rng.bytes(n) for n in range(0, 12)]
+    for addr in (0x0F, 0x8F, 0x00):
+        for proto, bodies in ((0x0800, [ip4, ip4[:19], b"\x46" + ip4[1:]]), (0x86DD, [ip6, ip6[:39]]),
+                              (0x8035, [rng.bytes(20)]), (0x0806, [bytes(28)])):
+            for body in bodies + [b""]:
+                out[104].append(bytes([addr, 0]) + proto.to_bytes(2, "big") + body)
+
+    # NFLOG (239, NflogLayer.cpp:41-96): family, version, resource id, then TLVs {u16 length, u16 type} in host order,
+    # each align<4>(length) long; the payload record (type 9) carries the packet
+    def tlv(t: int, value: bytes, length: int | None = None) -> bytes:
+        ln = 4 + len(value) if length is None else length
+        raw = ln.to_bytes(2, "little") + t.to_bytes(2, "little") + value
+        return raw + bytes((-len(raw)) % 4)
+
+    out[239] = [rng.bytes(n) for n in range(0, 12)]
+    for fam, body in ((2, ip4), (10, ip6), (2, ip4[:19]), (10, ip6[:39]), (7, rng.bytes(20)), (2, ip4 + b"\0\0\0"),
+                      (2, b""), (10, ip4)):
+        head = bytes([fam, 0]) + (0x002A).to_bytes(2, "big")
+        pre = tlv(1, b"\x08\x00\x01\x00") + tlv(10, b"drop\0")  # NFULA_PACKET_HDR, a padded NFULA_PREFIX
+        out[239] += [head + pre + tlv(9, body), head + tlv(9, body), head + pre, head + pre + tlv(9, body) + rng.bytes(6),
+                     head + tlv(9, body)[:-3], head + tlv(9, body, 4 + len(body) + 40), head + tlv(9, body, 3),
+                     head + tlv(1, b"", 0) + tlv(9, body), head + tlv(8, bytes(8)) + tlv(9, body) + tlv(16, bytes(14))]
     return out

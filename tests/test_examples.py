@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import GOLDEN, ROOT, load_golden
+from conftest import GOLDEN, ROOT, load_golden, make_examples
 from pcapplusplus_amd import abi, synth
 from pcapplusplus_amd.pcap import from_packets, read_pcap, write_pcap
 
@@ -27,7 +27,7 @@ def run(args, timeout=300):
 
 @pytest.fixture(scope="module")
 def built():
-    r = subprocess.run(["make", "-s", "-C", str(ROOT / "examples")], capture_output=True, text=True)
+    r = make_examples()
     assert r.returncode == 0, r.stderr
     return BIN
 

@@ -127,9 +127,9 @@ def test_gpu_permuted_descriptors(engine, order, kernel):
 
 
 @pytest.mark.parametrize("kernel", [0, 1], ids=["tile", "lane"])
-@pytest.mark.parametrize("linktype", [0, 113, 276])
+@pytest.mark.parametrize("linktype", [0, 113, 276, 104, 239])
 def test_gpu_link_layers(engine, linktype, kernel):
-    """Linux SLL / SLL2 / Null-Loopback first layers (Packet::createFirstLayer, Packet.cpp:827-923) on the generic
+    """Linux SLL / SLL2 / Null-Loopback / Cisco HDLC / NFLOG first layers (Packet::createFirstLayer, Packet.cpp:827-923) on the generic
     walk: crafted edge cases (lengths 0-23, every dispatch value and family encoding) and their mutations, packed
     and with gaps, equal to the restatement (itself pinned to the reference in test_oracle_fuzz)."""
     from mutate import crafted_linklayers

@@ -60,9 +60,9 @@ def test_mutations_vs_reference(seed):
         oracle.check_flag_contract(os_, rs, rl, b)
 
 
-@pytest.mark.parametrize("linktype", [0, 113, 276])
+@pytest.mark.parametrize("linktype", [0, 113, 276, 104, 239])
 def test_link_layers_vs_reference(linktype):
-    """Linux SLL / SLL2 / Null-Loopback first layers (Packet::createFirstLayer, Packet.cpp:827-923): crafted edge
+    """Linux SLL / SLL2 / Null-Loopback / Cisco HDLC / NFLOG first layers (Packet::createFirstLayer, Packet.cpp:827-923): crafted edge
     cases and mutations of the reference's own captures of that link type."""
     from mutate import crafted_linklayers
     from pcapplusplus_amd.pcap import from_packets

@@ -13,6 +13,8 @@ BASE_SO = Path(__file__).resolve().parent / "base" / "libpcppx_base.so"
 _lib = None
 _r01 = {}
 BASE = -1  # parse_device variant: the final round-5 product kernel (tools/ab/base, commit afaa594, rebuilt from git)
+BASE6_SO = Path(__file__).resolve().parent / "base" / "libpcppx_base6.so"
+BASE6 = -2  # the round-6 kernel before the Cisco HDLC / NFLOG first layers (commit 1b98250, same recipe)
 
 # pcppx_ab_parse_device variants (tools/ab/pcppx_ab.hip)
 LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ, TILE_W5_WIN256, TILE_W1_WIN128, TILE_W1_WIN256, TILE_CACHED = \
@@ -59,8 +61,8 @@ def parse_device(data, offsets, caplens, n: int, linktype: int, opts: abi.Opts, 
     rec.brief = abi.ptr(brief) if brief is not None else None
     if flow_keys is not None:
         rec.flow_keys = abi.ptr(flow_keys)
-    if variant == BASE:  # same opts / records layout (ABI 7)
-        abi.check(r01_lib().pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
+    if variant in (BASE, BASE6):  # same opts / records layout (ABI 7)
+        abi.check(r01_lib(BASE_SO if variant == BASE else BASE6_SO).pcppx_r01_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0)),
                   "pcppx_r01_parse_device")
         return
     abi.check(lib().pcppx_ab_parse_device(C.byref(b), C.byref(opts), C.byref(rec), C.c_void_p(stream or 0), variant),

@@ -21,11 +21,11 @@
  * Layers the engine builds: Ethernet II / 802.3 / LLC, VLAN, MPLS, IPv4, IPv6 (+ extensions), GREv0/v1,
  * PPP_PPTP, ARP, ICMP (+ the IPv4 header an error message quotes), TCP, UDP, the VXLAN and GTPv1 tunnels
  * (+ the inner packet), Payload, Trailer, the first layers of link types Ethernet, raw IP (RAW, DLT_RAW1/2,
- * IPV4, IPV6), Linux SLL / SLL2, Null/Loopback, Cisco HDLC and NFLOG (its TLVs walked to the payload record), and the first L7 layers it can name: HTTPRequest /
+ * IPV4, IPV6), Linux SLL / SLL2 and Null/Loopback, and the first L7 layers it can name: HTTPRequest /
  * HTTPResponse (+ the Payload body), SSL records, DNS, SSH messages (port 22) and MySQL (port 3306, where no
  * dissector ahead of it in TcpLayer::parseNextLayer takes the other port).
  * Packets for which the reference would build a layer outside this scope (other L7 dissectors, IGMP, PPPoE,
- * ...) are flagged PCPPX_F_NEEDS_HOST_L7 / PCPPX_F_NEEDS_HOST_PROTO: their
+ * NFLOG / Cisco HDLC first layers, ...) are flagged PCPPX_F_NEEDS_HOST_L7 / PCPPX_F_NEEDS_HOST_PROTO: their
  * layer prefix is exact, and the host owns the rest.
  */
 #ifndef PCPPX_H

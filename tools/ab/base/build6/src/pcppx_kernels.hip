@@ -31,7 +31,7 @@ enum : uint32_t
 {
 	P_ETH = 1, P_IPV4 = 2, P_IPV6 = 3, P_TCP = 4, P_UDP = 5, P_ARP = 8, P_VLAN = 9, P_ICMP = 10, P_MPLS = 14, P_GREV0 = 15,
 	P_GREV1 = 16, P_PPTP = 17, P_SLL = 19, P_NULL = 21, P_PAYLOAD = 25, P_TRAILER = 30, P_DOT3 = 33, P_LLC = 44,
-	P_SLL2 = 52, P_VXLAN = 26, P_GTPV1 = 32, P_NFLOG = 47, P_CISCO_HDLC = 58
+	P_SLL2 = 52, P_VXLAN = 26, P_GTPV1 = 32
 };
 
 // next-layer kinds of the chain walk
@@ -40,7 +40,6 @@ enum : uint32_t
 	K_NONE = 0, K_ETH, K_DOT3, K_LLC, K_VLAN, K_MPLS, K_IPV4, K_IPV6, K_GRE0, K_GRE1, K_PPTP, K_TCP, K_UDP,
 	K_PAYLOAD, K_OUT, K_ARP, K_SLL, K_SLL2, K_NULL,  // SLL / SLL2 / Null-Loopback: first layers only
 	K_ICMP, K_VXLAN, K_GTP1,
-	K_HDLC, K_NFLOG,  // Cisco HDLC / NFLOG: first layers only (round 6)
 	// candidates: the layer a tryConstructNextLayerWithFallback would build if its isDataValid holds, else
 	// Payload (Layer.h:474-483); resolved from the candidate's own first bytes when the walk reaches it
 	C_IPV4, C_IPV6, C_TCP, C_IPVER, C_GRE, C_ETHG, C_LLC, C_ICMP, C_ETH, C_IPGTP
@@ -900,55 +899,6 @@ __device__ uint32_t gtp1_header_len(const Pkt& p, uint32_t o, uint32_t len, cons
 	return res;
 }
 
-// NflogLayer (NflogLayer.cpp:41-96) at [o, o+len), len >= 4: the TLV records after the 4-byte nflog_header, {u16 length,
-// u16 type} in host (little-endian) order, each align<4>(length) long, walked as TLVRecordReader walks them (TLVData.h:
-// 238-312: a record needs >= 2 bytes left, a non-zero aligned length, and must fit). Returns getHeaderLen (the header +
-// every record before the NFULA_PAYLOAD record + that record's 4-byte head); *pl: the payload record's aligned length
-// - 4, or ~0u when there is no payload record.
-__device__ uint32_t nflog_header_len(const Pkt& p, uint32_t o, uint32_t len, uint32_t* pl)
-{
-	const uint32_t tl = len - 4;
-	uint32_t hdr = 4, pos = 0, total = tl >= 2 ? (rd16(p, o + 4) + 3u) & ~3u : 0u;
-	bool have = total != 0 && total <= tl;
-	*pl = ~0u;
-	while (have)
-	{
-		if (rd16(p, o + 4 + pos + 2) == 9u)  // NFULA_PAYLOAD
-		{
-			*pl = total - 4;
-			return hdr + 4;
-		}
-		hdr += total;
-		pos += total;
-		if (tl - pos < 2)
-			break;
-		total = (rd16(p, o + 4 + pos) + 3u) & ~3u;
-		have = total != 0 && pos + total <= tl;
-	}
-	return hdr;
-}
-
-// The Cisco HDLC / NFLOG first layer of a packet of `cap` bytes (kind K_HDLC / K_NFLOG): CiscoHdlcLayer.cpp:43-67 (a
-// 4-byte header, then IPv4 / IPv6 by its protocol field, else a Payload -- no length check, so a 4-byte packet gets an
-// empty one) and NflogLayer.cpp:41-96 (nflog_header_len; a next layer iff the data runs past the 4-byte header and a
-// payload record exists, of that record's length; IPv4 / IPv6 by the address family byte, 2 / 10, else a Payload).
-// walk_chain builds these ahead of its loop, so their rules add nothing to the loop of the other link types.
-__device__ Step first_layer_step(const Pkt& p, uint32_t k, uint32_t cap)
-{
-	const bool hd = k == K_HDLC;
-	uint32_t pl = ~0u;
-	const uint32_t hdr = hd ? 4u : nflog_header_len(p, 0, cap, &pl);
-	const bool has_next = hd ? true : (cap > 4 && pl != ~0u);
-	const uint32_t sel = hd ? rd16(p, 2) : rb(p, 0);
-	const uint32_t v = hd ? swap16(sel) : sel;
-	uint32_t nk = K_PAYLOAD;
-	nk = (hd ? v == 0x0800 : v == 2) ? C_IPV4 : nk;
-	nk = (hd ? v == 0x86DD : v == 10) ? C_IPV6 : nk;
-	pl = hd ? cap - 4 : pl;
-	return Step{ hd ? P_CISCO_HDLC : P_NFLOG, 2u, hdr, cap, has_next ? nk : (uint32_t)K_NONE, has_next ? hdr : 0u,
-	             has_next ? pl : 0u, false };
-}
-
 // per-kind ProtocolType (6 bits) and OsiModelLayer (3 bits); kinds without a layer map to Payload / 7
 constexpr uint32_t kind_proto(uint32_t k)
 {
@@ -1186,8 +1136,7 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	case 113: k = K_SLL; break;                            // SllLayer: unchecked (Packet.cpp:849-852)
 	case 276: k = cap >= 20 ? K_SLL2 : K_PAYLOAD; break;  // Sll2Layer::isDataValid (Sll2Layer.cpp:151-154)
 	case 0: k = cap >= 4 ? K_NULL : K_PAYLOAD; break;     // NullLoopbackLayer::isDataValid (NullLoopbackLayer.h:86-89)
-	case 239: k = cap >= 4 ? K_NFLOG : K_PAYLOAD; break;    // NflogLayer::isDataValid (NflogLayer.cpp:102-105)
-	case 104: k = cap >= 4 ? K_HDLC : K_PAYLOAD; break;     // CiscoHdlcLayer::isDataValid (CiscoHdlcLayer.h:59-62)
+	case 239: case 104: k = K_OUT; break;                  // NFLOG, Cisco HDLC: host dissectors
 	default: k = K_PAYLOAD; break;
 	}
 
@@ -1206,31 +1155,6 @@ __device__ __forceinline__ Walk walk_chain(const Pkt& p, uint32_t cap, const Par
 	uint32_t prev = 0;         // previous layer: proto | offset << 16
 	uint32_t last_end = 0;
 	uint32_t o = 0, len = cap;
-
-	// Cisco HDLC / NFLOG (uniform on the link type): their first layer is built here, ahead of the loop. It is never
-	// rolled back and is neither IP nor TCP/UDP, so of the loop's bookkeeping only the stop rules' state, the record,
-	// the mask and the previous-layer fields apply.
-	if (prm.linktype == 104 || prm.linktype == 239)
-	{
-		if (k == K_HDLC || k == K_NFLOG)
-		{
-			const Step s = first_layer_step(p, k, cap);
-			const bool member = prm.family != 0 &&
-			                    (s.proto == (prm.family & 0xFF) || (s.proto << 8) == (prm.family & 0xFF00) ||
-			                     (s.proto << 16) == (prm.family & 0xFF0000) || (s.proto << 24) == (prm.family & 0xFF000000u));
-			const bool osi_fail = s.osi > prm.until_osi;
-			found = (!osi_fail && member) ? 1u : 0u;
-			const bool fail = osi_fail || (found && !member);
-			stopped = fail ? 1u : 0u;
-			if (lay_out && ml)
-				lay_out[0] = make_uint2(s.proto | (s.osi << 8), (s.hdr & 0xFFFF) | (s.dlen << 16));
-			mask = 1ull << s.proto;
-			prev = s.proto;
-			last_end = s.dlen;
-			count = 1;
-			k = fail ? (uint32_t)K_NONE : s.nk; o = s.po; len = s.pl;
-		}
-	}
 
 	// The loop body is written as selects around three divergent regions (the loop exits, the peek's HBM
 	// fallback, the record store): the 64 lanes sit on different layer kinds, and every `if` becomes an
@@ -3716,7 +3640,7 @@ bool family_engine_only(uint32_t fam)
 		const uint32_t b = (fam >> (8 * k)) & 0xFFu;
 		const bool own = b == P_ETH || b == P_IPV4 || b == P_IPV6 || b == P_TCP || b == P_UDP || b == P_ARP ||
 		                 b == P_VLAN || b == P_MPLS || b == P_GREV0 || b == P_GREV1 || b == P_PPTP ||
-		                 b == P_TRAILER || b == P_DOT3 || b == P_LLC || b == P_ICMP || b == P_NFLOG || b == P_CISCO_HDLC ||
+		                 b == P_TRAILER || b == P_DOT3 || b == P_LLC || b == P_ICMP ||
 		                 // a classified first L7 layer is built, an unclassified one is none of these
 		                 b == P_HTTP_REQ || b == P_HTTP_RESP || b == P_DNS || b == P_SSL || b == P_MYSQL || b == P_SSH;
 		if (b != 0 && !own)

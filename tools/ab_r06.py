@@ -4,6 +4,7 @@
 records are checked equal, byte for byte, to the first case's before timing.
 
   python tools/ab_r06.py <config> [packets] [rounds] [variants]      config: 2 | 3 | 3s64 | 3s512 | 3s1500 | 4 | 5
+  (variant -2: the round-6 kernel before the Cisco HDLC / NFLOG first layers, tools/ab/base/libpcppx_base6.so)
   e.g. python tools/ab_r06.py 3s64 10000000 20 -1,0
 """
 import sys
