@@ -17,8 +17,7 @@ BASE6_SO = Path(__file__).resolve().parent / "base" / "libpcppx_base6.so"
 BASE6 = -2  # the round-6 kernel before the Cisco HDLC / NFLOG first layers (commit 1b98250, same recipe)
 
 # pcppx_ab_parse_device variants (tools/ab/pcppx_ab.hip)
-LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ, TILE_W5_WIN256, TILE_W1_WIN128, TILE_W1_WIN256, TILE_CACHED = \
-    1, 2, 3, 4, 5, 6, 8, 11
+LANE, STREAM_ONLY, DIAG_TILE_READ, DIAG_GRID_READ = 1, 2, 3, 4  # (an unknown variant: PCPPX_E_INVAL)
 
 
 def lib() -> C.CDLL:

@@ -295,28 +295,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 29: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 30: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	case 31: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
-	// fast-path stage costs (config 5, parse-only): no hashes / no L7 decision / no layer rows / none of the three
-	case 90: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 1>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 91: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 2>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 92: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 4>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 93: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 7>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 94: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 8>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 95: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 8>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 96: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 16>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 97: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 98: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 32>>), grid, dim3(kTile), 0, stream, prm); break;
-	// the same stage costs in the checksum instance (the 64-B class, round 5): no hashes / no L7 / no rows / none
-	case 110: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 1>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 111: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 2>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 112: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 4>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 113: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 7>>), grid, dim3(kTile), 0, stream, prm); break;
-	// checksum-instance shapes re-tuned under the default-policy stream loads: occupancy 4 / 6, stream window 192 / 64 chunks
-	case 100: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	case 101: hipLaunchKernelGGL((parse_tile_kernel<6, 128, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	case 102: hipLaunchKernelGGL((parse_tile_kernel<5, 192, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	case 103: hipLaunchKernelGGL((parse_tile_kernel<5, 64, 6, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
-	case 44: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
-	case 52: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, true>>), grid, dim3(kTile), 0, stream, prm); break;
 	// the PCPPX_WINDOW_DEEP checksum instance with the early second stream window (the product's runs it late)
 	case 70: hipLaunchKernelGGL((parse_tile_kernel<4, 128, 9, true, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	// parse-only windows gathered in ONE round for every packet (no dependent second round): 144 B, 128 B, 160 B
@@ -332,7 +310,9 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case 260: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 6, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 241: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 7>), grid, dim3(kTile), 0, stream, prm); break;
 	// round 6: the instances under combinations of the ParseShape R6 switches (bit 0 DPP span reductions, bit 1
-	// wave-wide hashes, bit 2 L7 register tables, bit 3 IPv4-wave hash skip): 200 + R6 (R6 < 8; 208: R6 = 8, 209: R6 = 12)
+	// wave-wide hashes, bit 2 L7 register tables, bit 3 IPv4-wave hash skip): 200 + R6 for R6 = 0, 1, 2 (the rejected
+	// bits alone), 209: R6 = 12 (bits 2 + 3), 450: R6 = 28 (the product; other combinations measured in r06a-c are in git
+	// history)
 	// the checksum instance (450: R6 = 28), 210 + the two-round parse-only instance, 220 + the SHORT parse-only instance, 230 + the DEEP
 	// checksum instance (its ParseShape with EarlyB, tools/ab variant 70's)
 #define PCPPX_AB_SHAPE(r) ParseShape<true, true, true, true, true, false, false, false, false, 0, r>
@@ -340,12 +320,6 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	case base + 0: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(0)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 1: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(1)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 2: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(2)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 3: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(3)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 4: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(4)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 5: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(5)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 6: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(6)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 7: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(7)>), grid, dim3(kTile), 0, stream, prm); break; \
-	case base + 8: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(8)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 9: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(12)>), grid, dim3(kTile), 0, stream, prm); break; \
 	case base + 250: hipLaunchKernelGGL((parse_tile_kernel<W, SW, C, CS, C1, PCPPX_AB_SHAPE(28)>), grid, dim3(kTile), 0, stream, prm); break;
 	PCPPX_AB_R6(200, 5, 128, 6, true, 6)
@@ -354,7 +328,8 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	PCPPX_AB_R6(230, 4, 128, 9, true, 6)
 #undef PCPPX_AB_SHAPE
 #undef PCPPX_AB_R6
-	default: return launch_parse(b, o, r, stream);
+	case 0: return launch_parse(b, o, r, stream);
+	default: return PCPPX_E_INVAL;  // a variant this build does not hold (older ones: git history)
 	}
 	return check_launch("pcppx_ab_parse_device", stream);
 }

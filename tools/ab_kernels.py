@@ -34,7 +34,6 @@ cases = {
     "tile/packed": (abi.make_opts(0, 8, True, 8, layout=PK), 0),
     "tile/deepwin": (abi.make_opts(0, 8, True, 8, abi.WINDOW_DEEP), 0),
     "tile/deepwin-earlyB": (abi.make_opts(0, 8, True, 8, abi.WINDOW_DEEP), 70),
-    "tile/skip-generic": (abi.make_opts(0, 8, True, 8), 52),
     "lane/ml8/csum": (abi.make_opts(0, 8, True, 8), 1),
     "tile/stream-only": (abi.make_opts(0, 8, True, 0), 2),
     "diag/tile-read": (abi.make_opts(0, 8, True, 0), 3),
@@ -59,24 +58,6 @@ cases = {
     "po/packed-w8r6": (abi.make_opts(0, 8, False, _ml, layout=PK), 83),
     "po/gather-only": (abi.make_opts(0, 8, False, _ml), 29),
     "po/packed-gather-only": (abi.make_opts(0, 8, False, _ml, layout=PK), 29),
-    "po/skip-generic": (abi.make_opts(0, 8, False, _ml), 44),
-    "po/packed-l7-late": (abi.make_opts(0, 8, False, _ml, layout=PK), 94),
-    "tile/packed-l7-late": (abi.make_opts(0, 8, True, 8, layout=PK), 95),
-    "tile/packed-nt-stream": (abi.make_opts(0, 8, True, 8, layout=PK), 96),
-    "tile/packed-w4": (abi.make_opts(0, 8, True, 8, layout=PK), 100),
-    "tile/packed-w6": (abi.make_opts(0, 8, True, 8, layout=PK), 101),
-    "tile/packed-swin192": (abi.make_opts(0, 8, True, 8, layout=PK), 102),
-    "tile/packed-swin64": (abi.make_opts(0, 8, True, 8, layout=PK), 103),
-    "po/packed-hash-branchy": (abi.make_opts(0, 8, False, _ml, layout=PK), 97),
-    "tile/packed-hash-branchy": (abi.make_opts(0, 8, True, 8, layout=PK), 98),
-    "tile/packed-no-hash": (abi.make_opts(0, 8, True, 8, layout=PK), 110),
-    "tile/packed-no-l7": (abi.make_opts(0, 8, True, 8, layout=PK), 111),
-    "tile/packed-no-rows": (abi.make_opts(0, 8, True, 8, layout=PK), 112),
-    "tile/packed-no-hash-l7-rows": (abi.make_opts(0, 8, True, 8, layout=PK), 113),
-    "po/packed-no-hash": (abi.make_opts(0, 8, False, _ml, layout=PK), 90),
-    "po/packed-no-l7": (abi.make_opts(0, 8, False, _ml, layout=PK), 91),
-    "po/packed-no-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 92),
-    "po/packed-no-hash-l7-rows": (abi.make_opts(0, 8, False, _ml, layout=PK), 93),
     # the final round-5 product kernel (tools/ab/base): round-6 changes against it in one process
     "base/tile-packed+brief": (abi.make_opts(0, 8, True, 8, layout=PK), -1),
     "base/po-packed+brief": (abi.make_opts(0, 8, False, _ml, layout=PK), -1),
@@ -113,7 +94,7 @@ want_csum_ref = next(iter(cases.values()))[0].want_checksums
 for name, (o, v) in cases.items():
     first = next(iter(cases.values()))[0]
     if o.max_layers != first.max_layers or o.want_checksums != want_csum_ref or o.layout != first.layout or \
-            v in (2, 3, 4, 7, 29, 44, 52, 90, 91, 92, 93, 110, 111, 112, 113, 120, 121, 122, 123, 124, 125) or name.endswith("+brief"):  # diagnostics / other records
+            v in (2, 3, 4, 7, 29, 120, 121, 122, 123, 124, 125) or name.endswith("+brief"):  # diagnostics / other records
         continue
     summ.zero_()
     lay.zero_()
