@@ -2463,7 +2463,8 @@ constexpr uint32_t kRowMaxMl = 12;  // layer rows staged in LDS up to this max_l
 //     left out, for its cost: bit 0 the hashes, bit 1 the L7 decision, bit 2 the layer rows; bit 3: the L7 table reads
 //     after the hashes instead of before; bit 4: non-temporal span-stream loads (rounds 1-3) instead of default-policy
 //     ones; bit 5:
-//     the IPv6 address dwords hashed under branches instead of selects; records unchanged by bits 3-5)
+//     the IPv6 address dwords hashed under branches instead of selects; records unchanged by bits 3-5; bit 6: only the
+//     first half of a PACKED run stored)
 //   R6 (round 6, records unchanged by every bit): bit 0 the tile span from 32-bit DPP reductions (wave_reduce_dpp)
 //     instead of 64-bit ds_bpermute butterflies; bit 1 the three hashes taken by the whole wave after both walks
 //     (wave_tuple_hashes: IPv4 packets in their own lanes, IPv6 packets' chains spread over the wave's lanes); bit 2 the
@@ -2912,7 +2913,9 @@ __global__ __launch_bounds__(kTile, MinWaves) void parse_tile_kernel(Params prm)
 			for (uint32_t k = 0; k < cnt; ++k)  // the generic walk wrote this lane's chain at its fixed-layout slot
 				rows[excl + k] = dst[lane * ml + k];
 		__syncthreads();
-		for (uint32_t r = lane; r < total; r += kTile)
+		// (diagnostic Skip bit 6: only the first half of the run is stored -- the time's sensitivity to the row bytes)
+		const uint32_t stored = (S::Skip & 64) ? total / 2 : total;
+		for (uint32_t r = lane; r < stored; r += kTile)
 			__builtin_nontemporal_store(rows[r], &dst[r]);
 	}
 	else if (stage_layers && ml > kRowMl)  // uniform: deep records, each fast lane stores its own row

@@ -309,6 +309,10 @@ PCPPX_AB_API int pcppx_ab_parse_device(const pcppx_batch* b, const pcppx_opts* o
 	// round 6: the SHORT parse-only instance held to 6 waves per SIMD (<= 80 VGPRs; its 7 KiB of LDS allow 22 waves per CU)
 	case 260: hipLaunchKernelGGL((parse_tile_kernel<6, 64, 6, false, 6>), grid, dim3(kTile), 0, stream, prm); break;
 	case 241: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 7>), grid, dim3(kTile), 0, stream, prm); break;
+	// round 6: the write-volume sensitivity -- the product instances storing only the first half of each PACKED run
+	// (records wrong past it): 270 the checksum instance, 271 the two-round parse-only instance
+	case 270: hipLaunchKernelGGL((parse_tile_kernel<5, 128, 6, true, 6, ParseShape<true, true, true, true, true, false, false, false, false, 64>>), grid, dim3(kTile), 0, stream, prm); break;
+	case 271: hipLaunchKernelGGL((parse_tile_kernel<1, 64, 9, false, 8, ParseShape<true, true, true, true, true, false, false, false, false, 64>>), grid, dim3(kTile), 0, stream, prm); break;
 	// round 6: the instances under combinations of the ParseShape R6 switches (bit 0 DPP span reductions, bit 1
 	// wave-wide hashes, bit 2 L7 register tables, bit 3 IPv4-wave hash skip): 200 + R6 for R6 = 0, 1, 2 (the rejected
 	// bits alone), 209: R6 = 12 (bits 2 + 3), 450: R6 = 28 (the product; other combinations measured in r06a-c are in git

@@ -73,6 +73,7 @@ def records():
     return [brief.clone(), rows.clone()]
 
 
+DIAG = {270, 271}  # diagnostics whose records differ by design (half of each PACKED run stored)
 ref = None
 for v in variants:
     lay.fill_(0xAB)
@@ -82,7 +83,9 @@ for v in variants:
     launch(v)
     torch.cuda.synchronize()
     got = records()
-    if ref is None:
+    if v in DIAG:
+        print(f"variant {v}: diagnostic, records not compared", flush=True)
+    elif ref is None:
         ref = got
     else:
         same = all(torch.equal(a, c) for a, c in zip(got, ref))
