@@ -170,3 +170,24 @@ def test_gpu_engine_window_choice():
         for w in (abi.WINDOW_SHORT, abi.WINDOW_DEEP, abi.WINDOW_SHORT):
             parse_on_device(eng, b, abi.make_opts(0, 8, w == abi.WINDOW_DEEP, 12, w))
         assert eng.window_choice(True) == abi.WINDOW_DEFAULT and eng.window_choice(False) == abi.WINDOW_DEFAULT
+
+
+@pytest.mark.gpu
+def test_gpu_host_path_empty_reset_and_dense_limit(engine):
+    """pcppx_parse_batch_host: an empty batch resets a reused records struct's layout and layers_written
+    before returning OK; a DENSE batch whose n * max_layers exceeds the 32-bit entry positions is refused with
+    PCPPX_E_INVAL before any memory is touched (the 64-B buffers below stand in for a 268M-packet batch and are never
+    read)."""
+    lib = engine.lib
+    buf = np.zeros(64, dtype=np.uint8)
+    p = buf.ctypes.data
+    opts = abi.make_opts(0, 8, False, 16, layout=abi.LAYOUT_DENSE)
+    rec = abi.Records(p, p, None, None)
+    rec.layout, rec.layers_written = 0, 12345
+    empty = abi.Batch(p, p, p, 64, 0, 1, 0)
+    assert lib.pcppx_parse_batch_host(engine.ctx, C.byref(empty), C.byref(opts), C.byref(rec)) == 0
+    assert rec.layers_written == 0 and rec.layout == abi.LAYOUT_DENSE
+    huge = abi.Batch(p, p, p, 64, (1 << 32) // 16 + 1, 1, 0)  # 268,435,457 packets x 16 entries > UINT32_MAX
+    rec.layers_written = 777
+    assert lib.pcppx_parse_batch_host(engine.ctx, C.byref(huge), C.byref(opts), C.byref(rec)) == abi.E_INVAL
+    assert rec.layers_written == 0
