@@ -628,7 +628,8 @@ class ReaderCore : public std::enable_shared_from_this<ReaderCore>
 {
 public:
 	static constexpr size_t kAhead = 2;              // pages mapped ahead of the caller's
-	static constexpr uint32_t kFirstPage = 1u << 14;  // packets: small first pages (the caller starts sooner),
+	static constexpr uint32_t kFirstPage = 1u << 10;  // packets: small first pages (the caller starts sooner; 1k
+	                                                  // instead of 16k: first passes 8-9% faster, r06u_fp_*.json),
 	static constexpr uint32_t kMaxPage = 1u << 20;    // then x4 per page up to this
 
 	explicit ReaderCore(pcppx_pcap* r) : m_Map(std::make_shared<MapHandle>()) { m_Map->reader = r; }

@@ -83,7 +83,9 @@ def google_pair(pcap: Path, args: list[str], trials: int = 1) -> dict:
     (examples/bin/benchmark_google) and over the reference Packet++ built from source (oracle/_ref/benchmark_google_ref,
     one core), alternating trial by trial; per benchmark the median of the trials' ns per iteration."""
     progs = [(name, exe) for name, exe in (("reference", ROOT / "oracle" / "_ref" / "benchmark_google_ref"),
-                                           ("engine", ROOT / "examples" / "bin" / "benchmark_google")) if exe.exists()]
+                                           ("engine", ROOT / "examples" / "bin" / os.environ.get("E2E_ENGINE_GOOGLE",
+                                                                                                  "benchmark_google")))
+             if exe.exists()]
     per: dict = {}
     for _ in range(trials):
         for name, exe in progs:
