@@ -627,12 +627,20 @@ struct Page
 class ReaderCore : public std::enable_shared_from_this<ReaderCore>
 {
 public:
-	static constexpr size_t kAhead = 2;              // pages mapped ahead of the caller's
-	static constexpr uint32_t kFirstPage = 1u << 10;  // packets: small first pages (the caller starts sooner; 1k
-	                                                  // instead of 16k: first passes 8-9% faster, r06u_fp_*.json),
-	static constexpr uint32_t kMaxPage = 1u << 20;    // then x4 per page up to this
+	static constexpr size_t kAhead = 2;  // pages mapped ahead of the caller's
+	// packets in the first page, then x4 per page up to kMaxPage. A capture of kLargeCapture bytes or more starts with
+	// 1k packets, so the caller starts on a small parse while the next pages are parsed (first pass over a 1M-packet
+	// IMIX pcap 70 vs 87 ms, r06y_dropin_*.json); a smaller one with 16k, so that it takes one GPU round trip, not
+	// three (the drop-in benchmark.cpp on config 1's 10k-packet pcap 1.19 vs 1.98 ms, on example.pcap 0.86 vs 1.20 ms)
+	static constexpr uint32_t kFirstPageSmall = 1u << 14, kFirstPageLarge = 1u << 10;
+	static constexpr uint64_t kLargeCapture = 32ull << 20;
+	static constexpr uint32_t kMaxPage = 1u << 20;
 
-	explicit ReaderCore(pcppx_pcap* r) : m_Map(std::make_shared<MapHandle>()) { m_Map->reader = r; }
+	ReaderCore(pcppx_pcap* r, uint64_t fileBytes)
+	    : m_Map(std::make_shared<MapHandle>()), m_FirstPage(fileBytes >= kLargeCapture ? kFirstPageLarge : kFirstPageSmall)
+	{
+		m_Map->reader = r;
+	}
 	~ReaderCore() { stop(); }
 	ReaderCore(const ReaderCore&) = delete;
 	ReaderCore& operator=(const ReaderCore&) = delete;
@@ -691,7 +699,7 @@ public:
 private:
 	void mapLoop()
 	{
-		uint32_t size = kFirstPage;
+		uint32_t size = m_FirstPage;
 		for (;;)
 		{
 			{
@@ -755,6 +763,7 @@ private:
 	}
 
 	std::shared_ptr<MapHandle> m_Map;
+	const uint32_t m_FirstPage;
 	mutable std::mutex m_Mu;
 	std::condition_variable m_Cv;
 	std::deque<std::shared_ptr<Page>> m_Pages;   // mapped, not yet handed to the caller
@@ -1319,7 +1328,9 @@ public:
 		if (pcppx_pcap_open(m_FileName.c_str(), &r) != PCPPX_OK)
 			return false;
 		m_OpenLinkType = (LinkLayerType)pcppx_pcap_linktype(r);
-		m_Core = std::make_shared<detail::ReaderCore>(r);
+		std::ifstream f(m_FileName, std::ifstream::ate | std::ifstream::binary);
+		const std::streamoff bytes = f ? (std::streamoff)f.tellg() : 0;
+		m_Core = std::make_shared<detail::ReaderCore>(r, bytes > 0 ? (uint64_t)bytes : 0u);
 		m_Core->start();
 		return true;
 	}

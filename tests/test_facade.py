@@ -305,8 +305,9 @@ def test_gpu_packet_vector_equals_restatement(built, tmp_path, how):
             variants = len(set(plan.split(",")))
             if how == "own":  # one group (one link type) parsed once per option set
                 assert variants <= info["gpu_parses"] <= 2 * variants, (name, plan, info)
-            else:  # pages of 1k, 4k, 16k, ... packets (x4 up to 1M): each parsed once per option set (plus copies' groups)
-                pages, size, left = 0, 1024, b.n
+            else:  # pages of 16k (1k from 32 MiB of file on), then x4 up to 1M packets: each parsed once per option set
+                fbytes = 24 + 16 * b.n + int(np.asarray(b.caplens, dtype=np.int64).sum())  # (plus copies' groups)
+                pages, size, left = 0, (1024 if fbytes >= 32 << 20 else 16384), b.n
                 while left > 0:
                     pages, left, size = pages + 1, left - size, min(size * 4, 1 << 20)
                 pages = max(pages, 1) + (how == "copy")

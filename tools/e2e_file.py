@@ -46,7 +46,8 @@ def bench_pair(pcap: Path, reps: tuple[int, int], n: int, trials: int = 1) -> di
     measurements can land in a busy second)."""
     out = {"packets": n, "pcap_bytes": pcap.stat().st_size}
     progs = [(name, exe) for name, exe in (("reference_benchmark", ROOT / "oracle" / "_ref" / "benchmark_ref"),
-                                           ("engine_benchmark", ROOT / "examples" / "bin" / "benchmark"))
+                                           ("engine_benchmark", ROOT / "examples" / "bin" /
+                                            os.environ.get("E2E_ENGINE_BENCH", "benchmark")))
              if exe.exists()]
     per = {name: [] for name, _ in progs}
     inproc = {name: [] for name, _ in progs}
