@@ -623,7 +623,7 @@ struct Page
 };
 
 /* The reader's pipeline: a mapper thread indexes pages ahead of the caller, a parser thread parses them on the GPU
- * for the caller's parse options (before the first Packet: a plain Packet's). */
+ * once the caller's parse options are known. */
 class ReaderCore : public std::enable_shared_from_this<ReaderCore>
 {
 public:
@@ -750,15 +750,12 @@ private:
 			ParseKey k;
 			{
 				std::unique_lock<std::mutex> g(m_Mu);
-				// before the caller's first Packet the pages are parsed for a plain Packet(&raw) (every layer, no
-				// checksums: ParseKey{}), so the GPU works while the caller reads or preloads packets; a Packet built
-				// with other options re-parses its page for them (Page::recordsFor) and sets the key for the rest
-				m_Cv.wait(g, [&] { return m_Stop || !m_ToParse.empty(); });
+				m_Cv.wait(g, [&] { return m_Stop || (m_KeyKnown && !m_ToParse.empty()); });
 				if (m_Stop)
 					return;
 				pg = m_ToParse.front().lock();  // expired: the caller is done with the page
 				m_ToParse.pop_front();
-				k = m_KeyKnown ? m_Key : ParseKey{};
+				k = m_Key;
 			}
 			if (pg)
 				(void)pg->tryParse(k);
