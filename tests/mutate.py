@@ -462,4 +462,10 @@ def crafted_linklayers(seed: int = 23) -> dict[int, list[bytes]]:
         out[239] += [head + pre + tlv(9, body), head + tlv(9, body), head + pre, head + pre + tlv(9, body) + rng.bytes(6),
                      head + tlv(9, body)[:-3], head + tlv(9, body, 4 + len(body) + 40), head + tlv(9, body, 3),
                      head + tlv(1, b"", 0) + tlv(9, body), head + tlv(8, bytes(8)) + tlv(9, body) + tlv(16, bytes(14))]
+    # TLV walks past the gathered header window (the device reads them from HBM): 40 empty records (160 B), or one
+    # 200-B prefix, before the payload record; a record list that ends on a torn header
+    for fam, body in ((2, ip4), (10, ip6)):
+        head = bytes([fam, 0]) + (0x002A).to_bytes(2, "big")
+        out[239] += [head + tlv(11, b"") * 40 + tlv(9, body), head + tlv(10, rng.bytes(200)) + tlv(9, body),
+                     head + tlv(11, b"") * 30 + b"\x09\x00", head + tlv(11, b"") * 25 + tlv(9, body, 2000)]
     return out
