@@ -76,11 +76,6 @@ def parse_args():
                          "layer rows), the 48-B 5-tuple extract (pcppx_tuple) alone, or (config 4) only what the flow table "
                          "reads: the dense hash5 column + collectStats, no summary (auto: " + ", ".join(
                              f"config {c} {v}" for c, v in sorted(CONFIG_RECORDS.items())) + ")")
-    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="replay each timed step from a HIP graph captured once after the warmup (the same launch: "
-                         "one parse per step), for steps shorter than the host's launch path; only for a fixed window "
-                         "with no flow table or collectStats (auto: " + ", ".join(f"config {c}" for c in sorted(CONFIG_GRAPH)) +
-                         ")")
     ap.add_argument("--dump-flows", default=None,
                     help="config 4: write the merged flow table (rank 0, after the timed region) to this .npz")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -100,9 +95,6 @@ CONFIG_LAYOUT = {3: "packed", 5: "packed"}  # configs with layer records
 CONFIG_RECORDS = {2: "tuples", 3: "brief", 4: "keys", 5: "brief"}
 # plain Eth / VLAN / IP / L4 stacks (configs 2 and 4): the one-round parse-only window (PCPPX_WINDOW_SHORT)
 CONFIG_WINDOW = {2: "short", 4: "short"}
-# a ~30-us step (config 2): the Python -> ctypes -> hipLaunchKernel path per step is as long as the kernel, so the timed
-# steps replay one captured HIP graph of the step instead (the GPU, not the host loop, sets the rate)
-CONFIG_GRAPH = {2}
 KERNEL_SRC = ROOT / "pcapplusplus_amd" / "csrc" / "pcppx_kernels.hip"
 
 
@@ -331,9 +323,9 @@ def main() -> None:
         proto_stats = torch.zeros(abi.PROTO_STATS, dtype=torch.int64, device=dev)
     mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if flows else None
 
-    def step(k=None, on=None):
-        eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh if on is None else on,
-                         flow_keys, tuples, proto_stats, brief)
+    def step(k=None):
+        eng.parse_device(data, offsets, caplens, n, batch.linktype, opts, summary, layers, sh, flow_keys, tuples,
+                         proto_stats, brief)
         if flows is not None:
             if k is not None:
                 mids[k].record(stream)
@@ -343,21 +335,6 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    # HIP graph of one step (--graph): a fixed window (no per-launch window sampling), no flow table, no collectStats
-    use_graph = (args.graph == "on" or (args.graph == "auto" and cfg in CONFIG_GRAPH))
-    if use_graph and (flows is not None or proto_stats is not None or window == "default"):
-        raise SystemExit("--graph needs a fixed window and no flow table / collectStats (configs 2, 3 or 5 with "
-                         "--window short|deep)")
-    graph = None
-    if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        cs = torch.cuda.Stream(dev)
-        cs.wait_stream(stream)
-        with torch.cuda.graph(graph, stream=cs):
-            step(on=cs.cuda_stream)
-        torch.cuda.synchronize(dev)
-        graph.replay()  # one untimed replay (the graph's first launch uploads it)
-        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -366,10 +343,7 @@ def main() -> None:
     w0 = time.perf_counter()
     for k in range(args.steps):
         starts[k].record(stream)
-        if graph is not None:
-            graph.replay()
-        else:
-            step(k)
+        step(k)
         ends[k].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -552,7 +526,6 @@ def main() -> None:
                 "wire_bytes_per_gpu": wire,
                 "checksums": want_csum,
                 "window": window,
-                "graph": graph is not None,
                 "max_layers": ml,
                 "layout": layout,
                 "records": rec_kind,

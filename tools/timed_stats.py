@@ -29,8 +29,6 @@ def main() -> None:
         sys.exit(f"no kernel trace under {prof}")
     line = json.loads([ln for ln in bench.read_text().splitlines() if ln.startswith("{")][-1])
     warm, steps = int(line["warmup"]), int(line["steps"])
-    # a graph-replayed run (bench.py --graph) launches the step once more, untimed, before the timed region
-    pre = warm + (1 if line.get("config", {}).get("graph") else 0)
     launches: dict[str, list[tuple[int, int]]] = {}
     for t in traces:
         with t.open() as f:
@@ -41,11 +39,11 @@ def main() -> None:
         ls.sort()
         # the parse kernel may run once more after the timed region (bench.py's untimed check parse through the same
         # instance): launches warm+1 .. warm+steps in dispatch order are the timed ones
-        timed = len(ls) == pre + steps or ("parse_tile_kernel" in name and len(ls) > pre + steps)
-        use = ls[pre:pre + steps] if timed else ls
+        timed = len(ls) == warm + steps or ("parse_tile_kernel" in name and len(ls) > warm + steps)
+        use = ls[warm:warm + steps] if timed else ls
         d = [e - s for s, e in use]
-        label = f"timed: last {steps} of {pre}+{steps}" if len(ls) == pre + steps else \
-            f"timed: launches {pre + 1}-{pre + steps} of {len(ls)} (after them: untimed checks)"
+        label = f"timed: last {steps} of {warm}+{steps}" if len(ls) == warm + steps else \
+            f"timed: launches {warm + 1}-{warm + steps} of {len(ls)} (after them: untimed checks)"
         rows.append((name, len(d), sum(d), sum(d) / len(d), min(d), max(d), statistics.pstdev(d) if len(d) > 1 else 0.0,
                      label if timed else f"all {len(ls)}"))
     rows.sort(key=lambda r: -r[2])
