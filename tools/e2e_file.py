@@ -13,6 +13,9 @@ host memory (north_star: "the rate including the H2D/D2H copies must also be mea
    pcap, the reference's example.pcap (frozen in tests/golden/capture_example.npz) and the 10M IMIX pcap.
 
   python tools/e2e_file.py --out gpurun_out/r03_e2e_file.json
+
+E2E_ENGINE_GOOGLE / E2E_ENGINE_BENCH name another build of the engine's google-benchmark / drop-in program under
+examples/bin (an A/B of facade variants on one box, e.g. the first-page size: profiles/r06u_fp_*, r06y_dropin_*).
 """
 from __future__ import annotations
 
