@@ -122,9 +122,9 @@ def main() -> None:
     ap.add_argument("--packets", type=int, default=10_000_000)
     ap.add_argument("--out", default=None)
     ap.add_argument("--shm", default="/dev/shm")
-    ap.add_argument("--only", choices=("all", "google", "dropin", "firstpass"), default="all",
+    ap.add_argument("--only", choices=("all", "google", "dropin", "firstpass", "files"), default="all",
                     help="google: only the benchmark-google loops (example.pcap and the IMIX pcap); dropin: only the "
-                         "drop-in benchmark.cpp runs (5 IMIX trials); firstpass: only the first-pass costs")
+                         "drop-in benchmark.cpp runs (5 IMIX trials); firstpass: only the first-pass costs; files: only file -> records")
     args = ap.parse_args()
     res = {"cores": len(os.sched_getaffinity(0))}
     big = Path(args.shm) / f"pcppx_e2e_{os.getpid()}.pcap"
@@ -166,7 +166,7 @@ def main() -> None:
             res["google_imix_parsing"] = google_pair(big, ["--benchmark", "BM_PacketParsing", "--iterations",
                                                            str(args.packets)])
             print("google_imix_parsing", json.dumps(res["google_imix_parsing"]), flush=True)
-        if args.only == "all":
+        if args.only in ("all", "files"):
             runs = {}
             for tag, extra in (("map_l8_csum", []), ("copy_l8_csum", ["--copy"]),
                                ("map_summary", ["--layers", "0", "--checksums", "0"]),
